@@ -1,0 +1,170 @@
+"""TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
+
+PyTorch-CPU restatement of the reference transformer agent and mixer, written
+from scratch as functions over ``state_dict``-keyed parameter dicts.  The op
+order mirrors the reference so that the fp64 restatement equals the reference
+to rounding and the fp32 one is the "reference CPU path" timed by bench.py:
+
+* ``mha``            — transformer.py:40-84 (wide heads: every head has width
+  ``emb``; Q and K both scaled by emb**-1/4; bias-free Q/K/V projections;
+  ``unifyheads`` with bias; the mask branches are dead on this path).
+* ``block``          — transformer.py:120-140 (post-LN; returns the ORIGINAL
+  keys, so every block attends over the layer-0 input).
+* ``transformer``    — transformer.py:169-178.
+* ``agent_forward``  — transf_agent.py:54-76 (hidden token first, Q read from
+  token 0).
+* ``mixer_forward``  — n_transf_mixer.py:55-91 (w1/b1/w2/b2 from the last A+3
+  output tokens, pos_func = abs, elu hidden layer).
+"""
+import torch
+import torch.nn.functional as F
+
+
+def _lin(x, p, name, bias=True):
+    w = p[name + ".weight"]
+    b = p.get(name + ".bias") if bias else None
+    return F.linear(x, w, b)
+
+
+def mha(p, pre, q, k, heads):
+    """transformer.py:40-84 with mask=None and self.mask=False."""
+    h = heads
+    b_q, t_q, e_q = q.size()
+    b, t_k, e = k.size()
+    keys = F.linear(k, p[pre + "tokeys.weight"]).view(b, t_k, h, e)
+    values = F.linear(k, p[pre + "tovalues.weight"]).view(b, t_k, h, e)
+    queries = F.linear(q, p[pre + "toqueries.weight"]).view(b, t_q, h, e)
+    keys = keys.transpose(1, 2).contiguous().view(b * h, t_k, e)
+    values = values.transpose(1, 2).contiguous().view(b * h, t_k, e)
+    queries = queries.transpose(1, 2).contiguous().view(b * h, t_q, e)
+    queries = queries / (e ** (1 / 4))
+    keys = keys / (e ** (1 / 4))
+    dot = torch.bmm(queries, keys.transpose(1, 2))
+    dot = F.softmax(dot, dim=2)
+    out = torch.bmm(dot, values).view(b, h, t_q, e)
+    out = out.transpose(1, 2).contiguous().view(b, t_q, h * e)
+    return F.linear(out, p[pre + "unifyheads.weight"], p[pre + "unifyheads.bias"])
+
+
+def block(p, pre, q, k, heads):
+    """transformer.py:120-140 (dropout p=0 is the identity)."""
+    e = q.shape[-1]
+    attended = mha(p, pre + "attention.", q, k, heads)
+    x = F.layer_norm(attended + q, (e,), p[pre + "norm1.weight"], p[pre + "norm1.bias"])
+    ff = F.linear(x, p[pre + "ff.0.weight"], p[pre + "ff.0.bias"])
+    ff = F.relu(ff)
+    ff = F.linear(ff, p[pre + "ff.2.weight"], p[pre + "ff.2.bias"])
+    x = F.layer_norm(ff + x, (e,), p[pre + "norm2.weight"], p[pre + "norm2.bias"])
+    return x
+
+
+def transformer(p, pre, q, k, heads, depth):
+    """transformer.py:169-178: keys are never updated across blocks."""
+    x = q
+    for d in range(depth):
+        x = block(p, f"{pre}tblocks.{d}.", x, k, heads)
+    return x
+
+
+def agent_forward(p, inputs, hidden_state, *, n_entities, feat_dim, emb, heads, depth):
+    """transf_agent.py:54-76 -> (q [b,a,nA], h [b,a,E])."""
+    b, a, _ = inputs.size()
+    inputs = inputs.reshape(-1, n_entities, feat_dim)
+    hidden_state = hidden_state.reshape(-1, 1, emb)
+    embs = _lin(inputs, p, "feat_embedding")
+    x = torch.cat((hidden_state, embs), 1)
+    embs = transformer(p, "transformer.", x, x, heads, depth)
+    h = embs[:, 0:1, :]
+    q = _lin(h, p, "q_basic")
+    return q.view(b, a, -1), h.view(b, a, -1)
+
+
+def mixer_forward(p, qvals, hidden_states, hyper_weights, states, *, n_agents, n_entities,
+                  feat_dim, emb, heads, depth, pos_func="abs"):
+    """n_transf_mixer.py:55-91 (custom_space=True branch) -> (y [b,1,1], hw [b,3,E])."""
+    b, _, _ = qvals.size()
+    inputs = states.reshape(b, n_entities, feat_dim)
+    embs = _lin(inputs, p, "feat_embedding")
+    x = torch.cat((embs, hidden_states, hyper_weights), 1)
+    embs = transformer(p, "transformer.", x, x, heads, depth)
+    w1 = embs[:, -3 - n_agents:-3, :]
+    b1 = embs[:, -3, :].view(-1, 1, emb)
+    w2 = embs[:, -2, :].view(-1, emb, 1)
+    b2 = F.relu(_lin(embs[:, -1, :], p, "hyper_b2")).view(-1, 1, 1)
+    if pos_func == "abs":
+        w1, w2 = torch.abs(w1), torch.abs(w2)
+    elif pos_func == "quadratic":
+        w1, w2 = 0.5 * w1 ** 2, 0.5 * w2 ** 2
+    hidden = F.elu(torch.matmul(qvals, w1) + b1)
+    y = torch.matmul(hidden, w2) + b2
+    return y, embs[:, -3:, :]
+
+
+def agent_unroll(p, obs, h0, *, cfg):
+    """Unroll the agent over obs [b, T, A, n_ent*F] from hidden h0 [b, A, E].
+
+    Returns q [b, T, A, nA] and h [b, T, A, E] (h[:, t] = hidden after step t)."""
+    qs, hs = [], []
+    h = h0
+    for t in range(obs.shape[1]):
+        q, h = agent_forward(p, obs[:, t].contiguous(), h, n_entities=cfg["n_entities"],
+                             feat_dim=cfg["obs_entity_feats"], emb=cfg["emb"],
+                             heads=cfg["heads"], depth=cfg["depth"])
+        qs.append(q)
+        hs.append(h)
+    return torch.stack(qs, 1), torch.stack(hs, 1)
+
+
+def mixer_unroll(p, qvals, hidden, states, hw0, *, cfg):
+    """Unroll the mixer over qvals [b,T,A], hidden [b,T,A,E], states [b,T,S].
+
+    The 3 hyper-weight tokens are recurrent (n_transf_mixer.py:69,91).
+    Returns y [b, T] and hw [b, T, 3, E] (hw[:, t] = hyper tokens after step t)."""
+    ys, hws = [], []
+    hw = hw0
+    for t in range(qvals.shape[1]):
+        y, hw = mixer_forward(p, qvals[:, t:t + 1], hidden[:, t], hw, states[:, t],
+                              n_agents=cfg["n_agents"], n_entities=cfg["n_entities"],
+                              feat_dim=cfg["state_entity_feats"], emb=cfg["mixer_emb"],
+                              heads=cfg["mixer_heads"], depth=cfg["mixer_depth"])
+        ys.append(y.view(-1))
+        hws.append(hw)
+    return torch.stack(ys, 1), torch.stack(hws, 1)
+
+
+def init_params(kind, cfg, seed, dtype=torch.float32):
+    """torch-default-initialised parameters with the reference state_dict keys
+    (SURVEY.md §8 b).  Uses nn.Linear/nn.LayerNorm constructors so the init
+    distribution equals the reference modules' own."""
+    g = torch.Generator().manual_seed(seed)
+    E = cfg["emb"] if kind == "agent" else cfg["mixer_emb"]
+    H = cfg["heads"] if kind == "agent" else cfg["mixer_heads"]
+    D = cfg["depth"] if kind == "agent" else cfg["mixer_depth"]
+    Fd = cfg["obs_entity_feats"] if kind == "agent" else cfg["state_entity_feats"]
+    FF = cfg.get("ff_hidden_mult", 4) * E
+    shapes = [("feat_embedding", (E, Fd), True)]
+    for d in range(D):
+        pre = f"transformer.tblocks.{d}."
+        shapes += [(pre + "attention.tokeys", (H * E, E), False),
+                   (pre + "attention.toqueries", (H * E, E), False),
+                   (pre + "attention.tovalues", (H * E, E), False),
+                   (pre + "attention.unifyheads", (E, H * E), True),
+                   (pre + "norm1", None, "ln"), (pre + "norm2", None, "ln"),
+                   (pre + "ff.0", (FF, E), True), (pre + "ff.2", (E, FF), True)]
+    if kind == "agent":
+        shapes.append(("q_basic", (cfg["n_actions"], E), True))
+    else:
+        shapes.append(("hyper_b2", (1, E), True))
+    p = {}
+    for name, shp, bias in shapes:
+        if bias == "ln":
+            # LayerNorm defaults are ones/zeros; perturb so LN affine is exercised.
+            p[name + ".weight"] = (1.0 + 0.1 * torch.randn(E, generator=g)).to(dtype)
+            p[name + ".bias"] = (0.1 * torch.randn(E, generator=g)).to(dtype)
+            continue
+        fan_in = shp[1]
+        bound = 1.0 / (fan_in ** 0.5)
+        p[name + ".weight"] = ((torch.rand(shp, generator=g) * 2 - 1) * bound).to(dtype)
+        if bias:
+            p[name + ".bias"] = ((torch.rand(shp[0], generator=g) * 2 - 1) * bound).to(dtype)
+    return p
