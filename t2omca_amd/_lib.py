@@ -1,0 +1,78 @@
+"""ctypes binding of the C-ABI library (include/t2omca.h).
+
+The library is the product: there is no CPU or eager-PyTorch fallback.  If
+libt2omca.so is missing, importing the compute entry points raises.
+"""
+import ctypes
+import os
+
+import torch
+
+from .build import LIB
+
+MAX_DEPTH = 4
+_I64x = ctypes.c_int64 * MAX_DEPTH
+
+
+class Layout(ctypes.Structure):
+    _fields_ = ([(n, ctypes.c_int32) for n in ("kind", "E", "H", "D", "F", "NA", "FF", "n_ent")] +
+                [(n, ctypes.c_int64) for n in ("WeT", "We", "be", "Wo", "bo", "WoT")] +
+                [(n, _I64x) for n in ("M", "MT", "N", "NT", "bu", "g1", "n1", "W1", "W1T", "c1",
+                                      "W2", "W2T", "c2", "g2", "n2")] +
+                [("total", ctypes.c_int64), ("grad_total", ctypes.c_int64)])
+
+
+EXPORTS = {
+    # name: (restype, argtypes)
+    "t2o_layout_init": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_int] * 8),
+    "t2o_param_count": (ctypes.c_int64, [ctypes.c_int] * 7),
+    "t2o_pack_params": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_void_p, ctypes.c_void_p,
+                                       ctypes.c_void_p]),
+    "t2o_unpack_grads": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p]),
+    "t2o_reduce_slabs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
+                                        ctypes.c_void_p, ctypes.c_void_p]),
+    "t2o_agent_unroll_fwd": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_void_p] * 3 +
+                             [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 6 + [ctypes.c_int] * 3 +
+                             [ctypes.c_void_p]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libt2omca.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise RuntimeError(f"t2omca_amd: {LIB} not built; run `python -m t2omca_amd.build` "
+                               "(there is no CPU fallback)")
+        h = ctypes.CDLL(LIB)
+        for name, (res, args) in EXPORTS.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = h
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"t2omca_amd: {what} failed with status {rc}")
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def make_layout(kind, E, H, D, F, NA, FF, n_ent):
+    L = Layout()
+    check(lib().t2o_layout_init(ctypes.byref(L), kind, E, H, D, F, NA, FF, n_ent), "t2o_layout_init")
+    return L

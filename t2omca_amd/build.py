@@ -1,0 +1,50 @@
+"""Build the in-tree HIP library t2omca_amd/lib/libt2omca.so for gfx950.
+
+    python -m t2omca_amd.build        (or __graft_entry__.build())
+
+One hipcc invocation compiles every csrc/*.hip translation unit into a single
+C-ABI shared library (declared in include/t2omca.h).  The .so is git-ignored
+but travels to the GPU box inside the repo snapshot.
+"""
+import glob
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIBDIR = os.path.join(HERE, "lib")
+LIB = os.path.join(LIBDIR, "libt2omca.so")
+ARCH = os.environ.get("T2O_OFFLOAD_ARCH", "gfx950")
+
+
+def sources():
+    return sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+
+
+def _stale():
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = sources() + glob.glob(os.path.join(CSRC, "*.hpp"))
+    deps.append(os.path.join(os.path.dirname(HERE), "include", "t2omca.h"))
+    return any(os.path.getmtime(p) > t for p in deps)
+
+
+def build(force=False, verbose=False):
+    if not force and not _stale():
+        return LIB
+    os.makedirs(LIBDIR, exist_ok=True)
+    hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
+    tmp = LIB + ".tmp"
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wno-unused-result", "-o", tmp] + sources()
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,135 @@
+// t2o_common.hpp — CDNA4 (gfx950) building blocks shared by the T2OMCA kernels.
+//
+// Register layout ("T-layout").  A wave owns a tile of 16 ROWS (agent: one
+// (episode, agent) sequence per row; mixer: one query token per row).  Lane
+// l = 16*g + c holds row c; its lane group g (0..3) holds features
+// 16*t + 4*g + r (r = 0..3) of every 16-feature tile t, i.e. an activation
+// vector of 16*T features is `f4 v[T]`.  This is exactly the D layout of
+// v_mfma_f32_16x16x4_f32 when the MFMA computes   y^T = W · x^T
+// (out-features on the MFMA M axis, rows on the N axis), and — because the
+// contraction order is free — the same registers are directly the B operand
+// of the next MFMA: step s of a 16-wide K tile feeds register r = s, so a
+// chain of projections never moves activations between lanes or through LDS.
+// Weights are the A operand: lane (g, c) of step s needs W[16o+c][16i+4g+s],
+// i.e. ONE 16-byte load of 4 consecutive in-features of a row-major W.
+//
+// All arithmetic here is fp32; v_mfma_f32_16x16x4_f32 is an exact fp32 FMA
+// chain (MI355X_MICROARCH.md §Matrix cores), so results track the reference's
+// fp32 CPU path to rounding.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/t2omca.h"
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+#define T2O_DEV __device__ __forceinline__
+
+namespace t2o {
+
+T2O_DEV int lane_c() { return threadIdx.x & 15; }
+T2O_DEV int lane_g() { return (threadIdx.x >> 4) & 3; }
+T2O_DEV int wave_id() { return threadIdx.x >> 6; }
+
+T2O_DEV f4 zero4() { return f4{0.f, 0.f, 0.f, 0.f}; }
+
+T2O_DEV f4 mfma4(float a, float b, f4 acc) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+}
+
+T2O_DEV f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+T2O_DEV void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
+
+// acc += W[16o.. , 16i..] (16x16 tile of row-major W, leading dim ldw) · x_tile
+T2O_DEV f4 mma_tile(const float* __restrict__ W, int ldw, int o, int i, f4 x, f4 acc) {
+  const f4 w = ld4(W + (size_t)(16 * o + lane_c()) * ldw + 16 * i + 4 * lane_g());
+  acc = mfma4(w[0], x[0], acc);
+  acc = mfma4(w[1], x[1], acc);
+  acc = mfma4(w[2], x[2], acc);
+  acc = mfma4(w[3], x[3], acc);
+  return acc;
+}
+
+// y[0..OT) = W[16*OT x 16*IT] · x[0..IT)  (T-layout in, T-layout out)
+template <int OT, int IT>
+T2O_DEV void matvec(const float* __restrict__ W, int ldw, const f4* x, f4* y) {
+#pragma unroll
+  for (int o = 0; o < OT; ++o) {
+    f4 acc = zero4();
+#pragma unroll
+    for (int i = 0; i < IT; ++i) acc = mma_tile(W, ldw, o, i, x[i], acc);
+    y[o] = acc;
+  }
+}
+
+// T-layout slice of a bias / gamma vector: elements 16t+4g .. 16t+4g+3
+T2O_DEV f4 vec_t(const float* __restrict__ v, int t) { return ld4(v + 16 * t + 4 * lane_g()); }
+
+// ---- cross-lane reductions -------------------------------------------------
+// Sum over the 4 lanes holding one row (c, c+16, c+32, c+48).  Additions are
+// commutative pairings, so all four lanes get bit-identical results.
+T2O_DEV float allsum4(float v) {
+  v += __shfl_xor(v, 16);
+  v += __shfl_xor(v, 32);
+  return v;
+}
+T2O_DEV float allmax4(float v) {
+  v = fmaxf(v, __shfl_xor(v, 16));
+  v = fmaxf(v, __shfl_xor(v, 32));
+  return v;
+}
+// Sum over the 16 rows of a lane group (lanes 16g .. 16g+15).
+T2O_DEV float rowsum16(float v) {
+  v += __shfl_xor(v, 1);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 8);
+  return v;
+}
+
+// ---- LayerNorm over E = 16*ET features of each row (eps 1e-5, biased var) --
+template <int ET>
+T2O_DEV void layernorm_fwd(const f4* r, const float* __restrict__ gamma,
+                           const float* __restrict__ beta, f4* out, f4* xhat, float& rstd) {
+  constexpr float inv_e = 1.0f / (16 * ET);
+  float s = 0.f;
+#pragma unroll
+  for (int t = 0; t < ET; ++t) s += (r[t][0] + r[t][1]) + (r[t][2] + r[t][3]);
+  const float mean = allsum4(s) * inv_e;
+  float v = 0.f;
+#pragma unroll
+  for (int t = 0; t < ET; ++t) {
+    const f4 d = r[t] - mean;
+    v += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
+  }
+  const float var = allsum4(v) * inv_e;
+  rstd = 1.0f / sqrtf(var + 1e-5f);
+#pragma unroll
+  for (int t = 0; t < ET; ++t) {
+    xhat[t] = (r[t] - mean) * rstd;
+    out[t] = xhat[t] * vec_t(gamma, t) + vec_t(beta, t);
+  }
+}
+
+// grad wrt LN input given grad wrt LN output (gamma applied inside)
+template <int ET>
+T2O_DEV void layernorm_bwd(const f4* gout, const f4* xhat, float rstd,
+                           const float* __restrict__ gamma, f4* gin) {
+  constexpr float inv_e = 1.0f / (16 * ET);
+  f4 gx[ET];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int t = 0; t < ET; ++t) {
+    gx[t] = gout[t] * vec_t(gamma, t);
+    s1 += (gx[t][0] + gx[t][1]) + (gx[t][2] + gx[t][3]);
+    const f4 p = gx[t] * xhat[t];
+    s2 += (p[0] + p[1]) + (p[2] + p[3]);
+  }
+  const float m1 = allsum4(s1) * inv_e;
+  const float m2 = allsum4(s2) * inv_e;
+#pragma unroll
+  for (int t = 0; t < ET; ++t) gin[t] = (gx[t] - m1 - xhat[t] * m2) * rstd;
+}
+
+}  // namespace t2o
