@@ -99,19 +99,21 @@ int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, const float*
                          int B, int T, int A, void* stream);
 
 /* Agent BPTT over steps T-1..0 of one network.  h_seq = forward h output
- * [b][T][a][E], h0 as in the forward.  External grads: gq[b][t][a][NA] (may be
- * NULL) plus, if actions != NULL, gchosen[b][t][a] routed to q[action]
- * (actions int64 [b][t][a] with strides act_sb, act_st); gh[b][t][a][E] (may
- * be NULL).  Outputs: gpack_slabs[nslab][grad_total] per-workgroup partial
- * gradients (compact layout, overwritten); gh0[b][a][E] (may be NULL).
- * Returns the number of slabs written via *nslab. */
+ * [b][h_ts][a][E] (h_ts >= T), h0 as in the forward (NULL = zeros).  External
+ * grads of the T steps: gq[b][t][a][NA] (may be NULL) plus, if gchosen != NULL,
+ * gchosen[b][t][a] routed to q[action] (actions int64 [b][t][a] with element
+ * strides act_sb, act_st, a-stride 1); gh[b][t][a][E] (may be NULL).
+ * Outputs: gslabs[nslab][grad_total] per-workgroup partial gradients (compact
+ * layout, overwritten; *nslab = number written, at most max_slabs =
+ * t2o_agent_bwd_max_slabs(B, A)); gh0[b][a][E] = dL/dh0 (may be NULL). */
 int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack,
                          const float* obs, int64_t obs_sb, int64_t obs_st,
-                         const float* h0, const float* h_seq,
+                         const float* h0, const float* h_seq, int h_ts,
                          const float* gq, const float* gchosen, const int64_t* actions,
                          int64_t act_sb, int64_t act_st, const float* gh,
                          float* gslabs, int max_slabs, int* nslab, float* gh0,
                          int B, int T, int A, void* stream);
+int t2o_agent_bwd_max_slabs(int B, int A);
 
 /* Sum nslab partial gradient slabs [nslab][n] into out[n] (out = sum, overwritten). */
 int t2o_reduce_slabs(const float* slabs, int nslab, int64_t n, float* out, void* stream);

@@ -35,6 +35,12 @@ EXPORTS = {
     "t2o_agent_unroll_fwd": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_void_p] * 3 +
                              [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 6 + [ctypes.c_int] * 3 +
                              [ctypes.c_void_p]),
+    "t2o_agent_unroll_bwd": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_void_p] * 2 +
+                             [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 2 + [ctypes.c_int] +
+                             [ctypes.c_void_p] * 3 + [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 2 +
+                             [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_void_p] +
+                             [ctypes.c_int] * 3 + [ctypes.c_void_p]),
+    "t2o_agent_bwd_max_slabs": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
 }
 
 _lib = None

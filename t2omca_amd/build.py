@@ -41,7 +41,12 @@ def build(force=False, verbose=False):
            "-Wno-unused-result", "-o", tmp] + sources()
     if verbose:
         print(" ".join(cmd))
-    subprocess.run(cmd, check=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError("hipcc failed building libt2omca.so")
+    if verbose and r.stderr.strip():
+        sys.stderr.write(r.stderr)
     os.replace(tmp, LIB)
     return LIB
 

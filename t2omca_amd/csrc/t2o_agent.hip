@@ -9,6 +9,7 @@
 // run in the same launch on the same observations (blockIdx.y).
 #include "t2o_agent_block.hpp"
 #include "t2o_dispatch.hpp"
+#include "t2o_layout.hpp"
 
 using namespace t2o;
 
@@ -92,6 +93,165 @@ int launch_fwd(const AgentFwdArgs& args, int nnet, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------
+// BPTT.  One workgroup = 4 waves = 64 sequences; each wave walks its 16
+// sequences backwards over t.  Per step it recomputes the step's forward from
+// the stored h_{t-1} (blocks 0..D-2 plain, then each block again with its
+// cache right before its backward), back-propagates the incoming grads
+// (dL/dq_t, dL/dh_t from the mixer and from step t+1) and produces dL/dh_{t-1}.
+// Weight grads go to an LDS gradient block shared by the 4 waves (ds_add_f32);
+// at the end the workgroup writes it as one slab.
+struct AgentBwdArgs {
+  t2o_layout L, G;
+  const float* pack;
+  const float* obs;
+  int64_t obs_sb, obs_st;
+  const float* h0;
+  const float* h_seq;
+  int h_ts;
+  const float* gq;
+  const float* gchosen;
+  const int64_t* actions;
+  int64_t act_sb, act_st;
+  const float* gh;
+  float* slabs;
+  float* gh0;
+  int B, T, A, F;
+  int lds_grad;  // floats reserved for the gradient block (>= G.grad_total)
+};
+
+template <int E, int H, int D, int NE, int FF>
+__global__ __launch_bounds__(256) void agent_bwd_kernel(AgentBwdArgs args) {
+  constexpr int ET = E / 16;
+  constexpr int STAGE = StageDims<ET>::FLOATS;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const t2o_layout& L = args.L;
+  const t2o_layout& G = args.G;
+  float* lg = smem;
+  float* stage = smem + args.lds_grad + wave_id() * STAGE;
+  for (int i = threadIdx.x; i < args.lds_grad; i += 256) lg[i] = 0.f;
+  __syncthreads();
+
+  const int A = args.A, F = args.F, T = args.T;
+  const int R = args.B * A;
+  const int rt = blockIdx.x * 4 + wave_id();
+  const int c = lane_c(), g = lane_g();
+  const int row_raw = rt * 16 + c;
+  const bool valid = row_raw < R;
+  const int row = valid ? row_raw : R - 1;
+  const int b = row / A, a = row % A;
+  const float* __restrict__ P = args.pack;
+
+  if (rt * 16 < R) {
+    f4 gh_rec[ET];
+#pragma unroll
+    for (int t = 0; t < ET; ++t) gh_rec[t] = zero4();
+    for (int step = T - 1; step >= 0; --step) {
+      f4 h[ET];
+      const float* hp = step == 0 ? args.h0 : args.h_seq + (((size_t)b * args.h_ts + step - 1) * A + a) * E;
+      if (step == 0 && args.h0) hp = args.h0 + (size_t)row * E;
+#pragma unroll
+      for (int t = 0; t < ET; ++t) h[t] = hp ? ld4(hp + 16 * t + 4 * g) : zero4();
+      const float* ob = args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * NE * F;
+      f4 o[NE];
+#pragma unroll
+      for (int j = 0; j < NE; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int f = 4 * g + r;
+          o[j][r] = f < F ? ob[j * F + f] : 0.f;
+        }
+      // external grads of this step
+      const size_t sidx = ((size_t)b * T + step) * A + a;
+      f4 gq = zero4();
+      if (args.gq) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * g + r < L.NA) gq[r] = args.gq[sidx * L.NA + 4 * g + r];
+      }
+      if (args.gchosen) {
+        const int64_t act = args.actions[b * args.act_sb + step * args.act_st + a];
+        const float gc = args.gchosen[sidx];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * g + r == act) gq[r] += gc;
+      }
+      f4 gx[ET];
+#pragma unroll
+      for (int t = 0; t < ET; ++t) {
+        gx[t] = gh_rec[t];
+        if (args.gh) gx[t] += ld4(args.gh + sidx * E + 16 * t + 4 * g);
+      }
+      if (!valid) {
+        gq = zero4();
+#pragma unroll
+        for (int t = 0; t < ET; ++t) gx[t] = zero4();
+      }
+      // forward recompute of blocks 0..D-2 (inputs kept)
+      f4 xs[D][ET];
+#pragma unroll
+      for (int t = 0; t < ET; ++t) xs[0][t] = h[t];
+#pragma unroll
+      for (int d = 0; d + 1 < D; ++d) {
+        f4 x[ET];
+#pragma unroll
+        for (int t = 0; t < ET; ++t) x[t] = xs[d][t];
+        agent_block_fwd<E, H, NE, FF, false>(P, L, d, h, o, x, nullptr);
+#pragma unroll
+        for (int t = 0; t < ET; ++t) xs[d + 1][t] = x[t];
+      }
+      f4 gh_in[ET], gbe[ET];
+#pragma unroll
+      for (int t = 0; t < ET; ++t) gh_in[t] = gbe[t] = zero4();
+#pragma unroll
+      for (int d = D - 1; d >= 0; --d) {
+        AgentCache<E, H, NE, FF> cache;
+        f4 x[ET];
+#pragma unroll
+        for (int t = 0; t < ET; ++t) x[t] = xs[d][t];
+        agent_block_fwd<E, H, NE, FF, true>(P, L, d, h, o, x, &cache);
+        if (d == D - 1) {  // q = Wo x + bo
+          dw_accumulate<1, ET>(lg + G.Wo, E, &gq, x, stage);
+          vec_accumulate<1>(lg + G.bo, &gq);
+          f4 t1[ET];
+          matvec<ET, 1>(P + L.WoT, 16, &gq, t1);
+#pragma unroll
+          for (int t = 0; t < ET; ++t) gx[t] += t1[t];
+        }
+        agent_block_bwd<E, H, NE, FF>(P, L, G, lg, stage, d, h, o, cache, gx, gh_in, gbe);
+      }
+      vec_accumulate<ET>(lg + G.be, gbe);
+#pragma unroll
+      for (int t = 0; t < ET; ++t) gh_rec[t] = gx[t] + gh_in[t];
+    }
+    if (args.gh0 && valid) {
+#pragma unroll
+      for (int t = 0; t < ET; ++t) st4(args.gh0 + (size_t)row * E + 16 * t + 4 * g, gh_rec[t]);
+    }
+  }
+  __syncthreads();
+  float* slab = args.slabs + (size_t)blockIdx.x * G.grad_total;
+  for (int i = threadIdx.x; i < G.grad_total; i += 256) slab[i] = lg[i];
+}
+
+template <int E, int H, int D, int NE, int FF>
+int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
+  constexpr int ET = E / 16;
+  const int R = args.B * args.A;
+  const int tiles = (R + 15) / 16;
+  const int grid = (tiles + 3) / 4;
+  if (grid > max_slabs) return T2O_EINVAL;
+  args.lds_grad = (int)((args.G.grad_total + 15) / 16 * 16);
+  const size_t lds = sizeof(float) * ((size_t)args.lds_grad + 4 * StageDims<ET>::FLOATS);
+  auto kern = agent_bwd_kernel<E, H, D, NE, FF>;
+  if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, stream, args);
+  *nslab = grid;
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, const float* pack_tg,
@@ -120,4 +280,46 @@ extern "C" int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, c
   int rc = T2O_EUNSUPPORTED;
   T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF, rc = (launch_fwd<E_, H_, D_, NE_, FF_>(args, nnet, (hipStream_t)stream)));
   return rc;
+}
+
+extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, const float* obs, int64_t obs_sb,
+                                    int64_t obs_st, const float* h0, const float* h_seq, int h_ts,
+                                    const float* gq, const float* gchosen, const int64_t* actions,
+                                    int64_t act_sb, int64_t act_st, const float* gh, float* gslabs,
+                                    int max_slabs, int* nslab, float* gh0, int B, int T, int A,
+                                    void* stream) {
+  if (!L || L->kind != 0 || !pack || !obs || !h_seq || !gslabs || !nslab || B < 1 || T < 1 || A < 1 ||
+      L->n_ent != A || h_ts < T || (gchosen && !actions))
+    return T2O_EINVAL;
+  AgentBwdArgs args{};
+  args.L = *L;
+  grad_layout(*L, args.G);
+  args.pack = pack;
+  args.obs = obs;
+  args.obs_sb = obs_sb;
+  args.obs_st = obs_st;
+  args.h0 = h0;
+  args.h_seq = h_seq;
+  args.h_ts = h_ts;
+  args.gq = gq;
+  args.gchosen = gchosen;
+  args.actions = actions;
+  args.act_sb = act_sb;
+  args.act_st = act_st;
+  args.gh = gh;
+  args.slabs = gslabs;
+  args.gh0 = gh0;
+  args.B = B;
+  args.T = T;
+  args.A = A;
+  args.F = L->F;
+  int rc = T2O_EUNSUPPORTED;
+  T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
+               rc = (launch_bwd<E_, H_, D_, NE_, FF_>(args, max_slabs, nslab, (hipStream_t)stream)));
+  return rc;
+}
+
+extern "C" int t2o_agent_bwd_max_slabs(int B, int A) {
+  const int tiles = (B * A + 15) / 16;
+  return (tiles + 3) / 4;
 }

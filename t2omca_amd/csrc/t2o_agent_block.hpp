@@ -146,4 +146,123 @@ T2O_DEV void agent_block_fwd(const float* __restrict__ P, const t2o_layout& L, i
   }
 }
 
+
+// Backward of block d.  gx: in = grad wrt block output, out = grad wrt block
+// input (query path).  gh_in accumulates the grad wrt h through the key/value
+// path (token 0).  Weight grads are accumulated into the LDS gradient block G
+// (compact layout, t2o_layout.hpp) over the wave's 16 rows.
+template <int E, int H, int NE, int FF>
+T2O_DEV void agent_block_bwd(const float* __restrict__ P, const t2o_layout& L, const t2o_layout& G,
+                             float* __restrict__ lg, float* __restrict__ stage, int d, const f4* h,
+                             const f4 (&o)[NE], const AgentCache<E, H, NE, FF>& c, f4* gx, f4* gh_in,
+                             f4* gbe) {
+  constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
+  const float* be = P + L.be;
+  // ---- LN2: x' = xh2*g2 + n2
+  {
+    f4 t0[ET];
+#pragma unroll
+    for (int t = 0; t < ET; ++t) t0[t] = gx[t] * c.xh2[t];
+    vec_accumulate<ET>(lg + G.g2[d], t0);
+    vec_accumulate<ET>(lg + G.n2[d], gx);
+  }
+  f4 gr2[ET];
+  layernorm_bwd<ET>(gx, c.xh2, c.rs2, P + L.g2[d], gr2);
+  // ---- FFN: r2 = W2 relu(f1) + c2 + y
+  {
+    f4 f1r[FT];
+#pragma unroll
+    for (int t = 0; t < FT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) f1r[t][r] = fmaxf(c.f1[t][r], 0.f);
+    dw_accumulate<ET, FT>(lg + G.W2[d], FF, gr2, f1r, stage);
+  }
+  vec_accumulate<ET>(lg + G.c2[d], gr2);
+  f4 gf1[FT];
+  matvec<FT, ET>(P + L.W2T[d], E, gr2, gf1);
+#pragma unroll
+  for (int t = 0; t < FT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gf1[t][r] = c.f1[t][r] > 0.f ? gf1[t][r] : 0.f;
+  dw_accumulate<FT, ET>(lg + G.W1[d], E, gf1, c.y, stage);
+  vec_accumulate<FT>(lg + G.c1[d], gf1);
+  f4 gy[ET];
+  matvec<ET, FT>(P + L.W1T[d], FF, gf1, gy);
+#pragma unroll
+  for (int t = 0; t < ET; ++t) gy[t] += gr2[t];
+  // ---- LN1: y = xh1*g1 + n1
+  {
+    f4 t0[ET];
+#pragma unroll
+    for (int t = 0; t < ET; ++t) t0[t] = gy[t] * c.xh1[t];
+    vec_accumulate<ET>(lg + G.g1[d], t0);
+    vec_accumulate<ET>(lg + G.n1[d], gy);
+  }
+  f4 gr1[ET];
+  layernorm_bwd<ET>(gy, c.xh1, c.rs1, P + L.g1[d], gr1);
+  // ---- r1 = N z + b_U + x
+  dw_accumulate<ET, HET>(lg + G.N[d], H * E, gr1, c.z, stage);
+  vec_accumulate<ET>(lg + G.bu[d], gr1);
+  f4 gz[HET];
+  matvec<HET, ET>(P + L.NT[d], E, gr1, gz);
+  f4 gu[HET];
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh) {
+    const f4* gzh = &gz[hh * ET];
+    const f4* uh = &c.u[hh * ET];
+    const float p0 = c.p[hh][0];
+    // z_h = p0 h + We oh + Ps be
+    float gp0p = 0.f, gPp = 0.f;
+#pragma unroll
+    for (int t = 0; t < ET; ++t) {
+      const f4 bt = vec_t(be, t);
+      gp0p += (gzh[t][0] * h[t][0] + gzh[t][1] * h[t][1]) + (gzh[t][2] * h[t][2] + gzh[t][3] * h[t][3]);
+      gPp += (gzh[t][0] * bt[0] + gzh[t][1] * bt[1]) + (gzh[t][2] * bt[2] + gzh[t][3] * bt[3]);
+      gh_in[t] += p0 * gzh[t];
+      gbe[t] += c.Ps[hh] * gzh[t];
+    }
+    const float gp0 = allsum4(gp0p);
+    const float gP = allsum4(gPp);
+    f4 goh;
+    matvec<1, ET>(P + L.WeT, E, gzh, &goh);
+    dw_accumulate<ET, 1>(lg + G.We, 16, gzh, &c.oh[hh], stage);
+    // softmax backward over [token 0, entities]
+    float gp[NE + 1];
+    gp[0] = gp0;
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const float sp = (goh[0] * o[j][0] + goh[1] * o[j][1]) + (goh[2] * o[j][2] + goh[3] * o[j][3]);
+      gp[j + 1] = allsum4(sp) + gP;
+    }
+    float dot = 0.f;
+#pragma unroll
+    for (int j = 0; j <= NE; ++j) dot += c.p[hh][j] * gp[j];
+    const float gs0 = p0 * (gp[0] - dot);
+    f4 gw = zero4();
+    float gc = 0.f;
+#pragma unroll
+    for (int j = 0; j < NE; ++j) {
+      const float gsj = c.p[hh][j + 1] * (gp[j + 1] - dot);
+      gw += gsj * o[j];
+      gc += gsj;
+    }
+    // s_h0 = u_h·h ; s_hj = (WeT u_h)·o_j + u_h·be
+    f4 t1[ET];
+    matvec<ET, 1>(P + L.We, 16, &gw, t1);
+#pragma unroll
+    for (int t = 0; t < ET; ++t) {
+      gu[hh * ET + t] = t1[t] + gs0 * h[t] + gc * vec_t(be, t);
+      gh_in[t] += gs0 * uh[t];
+      gbe[t] += gc * uh[t];
+    }
+    dw_accumulate<ET, 1>(lg + G.We, 16, uh, &gw, stage);
+  }
+  // ---- u = M x
+  dw_accumulate<HET, ET>(lg + G.M[d], E, gu, c.x, stage);
+  f4 gxp[ET];
+  matvec<ET, HET>(P + L.MT[d], H * E, gu, gxp);
+#pragma unroll
+  for (int t = 0; t < ET; ++t) gx[t] = gxp[t] + gr1[t];
+}
+
 }  // namespace t2o

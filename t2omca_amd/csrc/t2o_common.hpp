@@ -133,3 +133,84 @@ T2O_DEV void layernorm_bwd(const f4* gout, const f4* xhat, float rstd,
 }
 
 }  // namespace t2o
+
+namespace t2o {
+
+// ---- weight-gradient accumulation -------------------------------------------
+// dW[16*OT x 16*IT] += Σ_rows dY[row]ᵀ ⊗ X[row] over the wave's 16 rows, added
+// into an LDS accumulator (row-major, leading dim ldw) with ds_add_f32.
+// The contraction runs over ROWS, which the T-layout keeps on the lane axis,
+// so both operands are transposed through a per-wave LDS staging area: the
+// operand with fewer tiles is staged whole (row stride ≡ 16 mod 32 floats so
+// the two 32-lane halves hit disjoint banks), the other is streamed one 16x16
+// tile at a time.  MFMA step s consumes rows 4s..4s+3 (k = lane group g).
+template <int NT>
+struct StageDims {
+  static constexpr int LD = 16 * NT + ((16 * NT) % 32 == 16 ? 0 : 16);  // ≡ 16 (mod 32)
+  static constexpr int FLOATS = 16 * LD + 16 * 16;
+};
+
+T2O_DEV void stage_tile(float* st, int ld, int col0, f4 v) {
+  *reinterpret_cast<f4*>(st + lane_c() * ld + col0 + 4 * lane_g()) = v;
+}
+
+template <int OT, int IT>
+T2O_DEV void dw_accumulate(float* __restrict__ ldsW, int ldw, const f4* dY, const f4* X, float* stage) {
+  constexpr int NS = OT < IT ? OT : IT;  // tiles staged whole
+  constexpr int LD = StageDims<NS>::LD;
+  float* st_full = stage;
+  float* st_tile = stage + 16 * LD;
+  const int c = lane_c(), g = lane_g();
+  if constexpr (IT <= OT) {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) stage_tile(st_full, LD, 16 * i, X[i]);
+#pragma unroll
+    for (int o = 0; o < OT; ++o) {
+      stage_tile(st_tile, 16, 0, dY[o]);
+      float a[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) a[s] = st_tile[(4 * s + g) * 16 + c];
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {
+        f4 acc = zero4();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = mfma4(a[s], st_full[(4 * s + g) * LD + 16 * i + c], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) atomicAdd(ldsW + (16 * o + 4 * g + r) * ldw + 16 * i + c, acc[r]);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int o = 0; o < OT; ++o) stage_tile(st_full, LD, 16 * o, dY[o]);
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      stage_tile(st_tile, 16, 0, X[i]);
+      float bv[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) bv[s] = st_tile[(4 * s + g) * 16 + c];
+#pragma unroll
+      for (int o = 0; o < OT; ++o) {
+        f4 acc = zero4();
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = mfma4(st_full[(4 * s + g) * LD + 16 * o + c], bv[s], acc);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) atomicAdd(ldsW + (16 * o + 4 * g + r) * ldw + 16 * i + c, acc[r]);
+      }
+    }
+  }
+}
+
+// vec[16*NT] += Σ_rows v[row]  (T-layout input; one lane per group adds)
+template <int NT>
+T2O_DEV void vec_accumulate(float* __restrict__ ldsv, const f4* v) {
+  const int c = lane_c(), g = lane_g();
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float s = rowsum16(v[t][r]);
+      if (c == 0) atomicAdd(ldsv + 16 * t + 4 * g + r, s);
+    }
+}
+
+}  // namespace t2o

@@ -108,3 +108,36 @@ def agent_unroll_fwd(shape: NetShape, pack_on, obs, h0_on=None, pack_tg=None, h0
     if pack_tg is not None:
         return q_on, h_on, q_tg, h_tg
     return q_on, h_on
+
+
+def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchosen=None, actions=None,
+                     gh=None, want_gh0=False, slabs=None):
+    """BPTT of agent_unroll_fwd over the first T = len(grads) steps.
+
+    obs [B, >=T, A, nF]; h_seq [B, Ts>=T, A, E] (forward output); gq [B,T,A,NA],
+    gchosen [B,T,A] + actions (int64 [B, >=T, A], a-stride 1), gh [B,T,A,E].
+    Returns (gpack, gh0) with gpack the compact weight-gradient block."""
+    _dev(pack, obs, h_seq, h0, gq, gchosen, actions, gh)
+    B, _, A, _ = obs.shape
+    T = next(t.shape[1] for t in (gq, gchosen, gh) if t is not None)
+    L = shape.layout()
+    for t in (gq, gchosen, gh):
+        assert t is None or t.is_contiguous()
+    assert h_seq.is_contiguous() and h_seq.shape[1] >= T
+    act_sb = act_st = 0
+    if gchosen is not None:
+        assert actions is not None and actions.dtype == torch.int64 and actions.stride(2) == 1
+        act_sb, act_st = actions.stride(0), actions.stride(1)
+    nmax = int(lib().t2o_agent_bwd_max_slabs(B, A))
+    if slabs is None or slabs.numel() < nmax * L.grad_total:
+        slabs = torch.empty(nmax * L.grad_total, device=obs.device)
+    gh0 = torch.empty(B, A, shape.E, device=obs.device) if want_gh0 else None
+    nslab = ctypes.c_int(0)
+    check(lib().t2o_agent_unroll_bwd(ctypes.byref(L), ptr(pack), ptr(obs), obs.stride(0), obs.stride(1),
+                                     ptr(h0), ptr(h_seq), h_seq.shape[1], ptr(gq), ptr(gchosen),
+                                     ptr(actions), act_sb, act_st, ptr(gh), ptr(slabs), nmax,
+                                     ctypes.byref(nslab), ptr(gh0), B, T, A, stream_ptr()),
+          "agent_unroll_bwd")
+    gpack = torch.empty(L.grad_total, device=obs.device)
+    reduce_slabs(slabs, nslab.value, gpack)
+    return gpack, gh0
