@@ -115,6 +115,63 @@ int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack,
                          int B, int T, int A, void* stream);
 int t2o_agent_bwd_max_slabs(int B, int A);
 
+/* Mixer unroll forward for up to two networks (online + target) in one
+ * launch; one wave per episode.  states[b][t][n_ent*F] (element strides
+ * st_sb, st_st); hid_*[b][t][a][E] agent hidden states (strides hid_sb,
+ * hid_st, a-stride E); hw0 [B][3][E] initial hyper tokens (NULL = zeros).
+ * qmode: 0 = qvals given (qv_* [B][T][A]); 1 = chosen-action gather from the
+ * network's Q array (q_on / q_tg [b][q_ts][a][n_actions], actions int64
+ * [b][t][a] with strides act_sb, act_st); 2 = double-Q: the network's Q
+ * array at argmax_a' of q_on masked by avail (int32 [b][t][a][n_actions],
+ * strides av_sb, av_st; NULL = all available), ties -> lowest index.
+ * Outputs per network: y[B][T], hw[B][T][3][E] (hyper tokens after step t),
+ * qvo[B][T][A] (qvals used, may be NULL), xout[B][T][A+3][E] (final query
+ * rows, may be NULL; required by the backward). */
+int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, const float* pack_tg,
+                         const float* states, int64_t st_sb, int64_t st_st,
+                         const float* hid_on, const float* hid_tg, int64_t hid_sb, int64_t hid_st,
+                         const float* hw0_on, const float* hw0_tg, int qmode_on, int qmode_tg,
+                         const float* qv_on, const float* qv_tg, const float* q_on, const float* q_tg,
+                         int q_ts, int n_actions, const int64_t* actions, int64_t act_sb, int64_t act_st,
+                         const int32_t* avail, int64_t av_sb, int64_t av_st,
+                         float* y_on, float* hw_on, float* qvo_on, float* xout_on,
+                         float* y_tg, float* hw_tg, float* qvo_tg, float* xout_tg,
+                         int B, int T_on, int T_tg, void* stream);
+
+/* Mixer BPTT over steps T-1..0 of one network.  qv = forward qvo [B][T][A],
+ * hw / xout = forward outputs.  gy[B][T] = dL/dy; ghw_ext [B][T][3][E] optional
+ * extra grad on the hyper outputs.  Outputs: gqv[B][T][A] (dL/dqvals),
+ * ghid[B][T][A][E] (dL/dhidden states), ghw0[B][3][E] (may be NULL), partial
+ * weight-grad slabs as for the agent (max_slabs = t2o_mixer_bwd_max_slabs(B)). */
+int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, const float* states,
+                         int64_t st_sb, int64_t st_st, const float* hid, int64_t hid_sb,
+                         int64_t hid_st, const float* hw0, const float* qv, const float* hw,
+                         const float* xout, const float* gy, const float* ghw_ext, float* gqv,
+                         float* ghid, float* ghw0, float* gslabs, int max_slabs, int* nslab,
+                         int B, int T, void* stream);
+int t2o_mixer_bwd_max_slabs(int B);
+
+/* TD(λ) targets, masked PER-weighted loss, dL/dQtot and priorities
+ * (PyMARL2 NQLearner semantics; see t2o_learner.hip).  qtot [B][T] (online
+ * mixer), qtot_tgt [B][T+1] (target mixer), reward/term/filled [b][t] with
+ * element strides (term/filled may be NULL), per_weight [B] (NULL = 1);
+ * mask_sum > 0 overrides the local Σ mask (data parallel).  Outputs gq[B][T],
+ * targets[B][T] (may be NULL), prio[B], loss[2] = {loss, local Σ mask}. */
+int t2o_td_loss(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
+                int64_t rw_st, const float* term, int64_t tm_sb, int64_t tm_st,
+                const float* filled, int64_t fl_sb, int64_t fl_st, const float* per_weight,
+                float gamma, float td_lambda, float mask_sum, float* gq, float* targets,
+                float* prio, float* loss, int B, int T, void* stream);
+
+/* clip_grad_norm_(max_grad_norm) + Adam (torch.optim.Adam semantics, L2
+ * weight decay) over n floats.  workspace: t2o_adam_workspace_floats() floats
+ * (needed when max_grad_norm > 0).  grad_norm_out [1] may be NULL. */
+int t2o_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
+                  float* workspace, int64_t n, double lr, double beta1, double beta2, float eps,
+                  float weight_decay, float max_grad_norm, int64_t step, float* grad_norm_out,
+                  void* stream);
+int t2o_adam_workspace_floats(void);
+
 /* Sum nslab partial gradient slabs [nslab][n] into out[n] (out = sum, overwritten). */
 int t2o_reduce_slabs(const float* slabs, int nslab, int64_t n, float* out, void* stream);
 

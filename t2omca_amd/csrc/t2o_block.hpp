@@ -1,0 +1,126 @@
+// t2o_block.hpp — the attention-independent half of a transformer block
+// (transformer.py:82-84 unifyheads, :130-136 residual/LN1/FFN/residual/LN2),
+// forward with optional cache and backward, for one 16-row T-layout tile.
+//
+// With folded weights the block's attended vector is  a = Σ_h N_h z_h + b_U,
+// where z_h is the head's attention-weighted average of the (original) key
+// tokens.  This half maps (z, x) -> x' and is shared by the agent (per-row
+// keys, observation-space attention) and the mixer (per-episode keys in LDS).
+#pragma once
+#include "t2o_common.hpp"
+
+namespace t2o {
+
+template <int E, int H, int FF>
+struct PostCache {
+  static constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
+  f4 x[ET];    // block input (query path)
+  f4 z[HET];   // per-head attention outputs
+  f4 xh1[ET];
+  float rs1;
+  f4 y[ET];
+  f4 f1[FT];   // W1 y + c1 (pre-ReLU)
+  f4 xh2[ET];
+  float rs2;
+};
+
+// x: in = block input, out = block output.
+template <int E, int H, int FF, bool CACHE>
+T2O_DEV void post_fwd(const float* __restrict__ P, const t2o_layout& L, int d, const f4* z, f4* x,
+                      PostCache<E, H, FF>* c) {
+  constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
+  f4 r1[ET];
+  matvec<ET, HET>(P + L.N[d], H * E, z, r1);
+#pragma unroll
+  for (int t = 0; t < ET; ++t) r1[t] += vec_t(P + L.bu[d], t) + x[t];
+  f4 y[ET], xh1[ET];
+  float rs1;
+  layernorm_fwd<ET>(r1, P + L.g1[d], P + L.n1[d], y, xh1, rs1);
+  f4 f1[FT], f1r[FT];
+  matvec<FT, ET>(P + L.W1[d], E, y, f1);
+#pragma unroll
+  for (int t = 0; t < FT; ++t) {
+    f1[t] += vec_t(P + L.c1[d], t);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) f1r[t][r] = fmaxf(f1[t][r], 0.f);
+  }
+  f4 r2[ET];
+  matvec<ET, FT>(P + L.W2[d], FF, f1r, r2);
+#pragma unroll
+  for (int t = 0; t < ET; ++t) r2[t] += vec_t(P + L.c2[d], t) + y[t];
+  if constexpr (CACHE) {
+#pragma unroll
+    for (int t = 0; t < ET; ++t) {
+      c->x[t] = x[t];
+      c->xh1[t] = xh1[t];
+      c->y[t] = y[t];
+    }
+#pragma unroll
+    for (int t = 0; t < HET; ++t) c->z[t] = z[t];
+#pragma unroll
+    for (int t = 0; t < FT; ++t) c->f1[t] = f1[t];
+    c->rs1 = rs1;
+  }
+  f4 xh2[ET];
+  float rs2;
+  layernorm_fwd<ET>(r2, P + L.g2[d], P + L.n2[d], x, xh2, rs2);
+  if constexpr (CACHE) {
+#pragma unroll
+    for (int t = 0; t < ET; ++t) c->xh2[t] = xh2[t];
+    c->rs2 = rs2;
+  }
+}
+
+// gx: grad wrt block output.  Produces gz (grad wrt z, HET tiles) and gres
+// (grad wrt the block input through the LN1 residual).  Weight / vector grads
+// go to the LDS gradient block lg (compact layout G).
+template <int E, int H, int FF>
+T2O_DEV void post_bwd(const float* __restrict__ P, const t2o_layout& L, const t2o_layout& G,
+                      float* __restrict__ lg, float* __restrict__ stage, int d, const PostCache<E, H, FF>& c,
+                      const f4* gx, f4* gz, f4* gres) {
+  constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
+  {  // LN2: x' = xh2*g2 + n2
+    f4 t0[ET];
+#pragma unroll
+    for (int t = 0; t < ET; ++t) t0[t] = gx[t] * c.xh2[t];
+    vec_accumulate<ET>(lg + G.g2[d], t0);
+    vec_accumulate<ET>(lg + G.n2[d], gx);
+  }
+  f4 gr2[ET];
+  layernorm_bwd<ET>(gx, c.xh2, c.rs2, P + L.g2[d], gr2);
+  {  // r2 = W2 relu(f1) + c2 + y
+    f4 f1r[FT];
+#pragma unroll
+    for (int t = 0; t < FT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) f1r[t][r] = fmaxf(c.f1[t][r], 0.f);
+    dw_accumulate<ET, FT>(lg + G.W2[d], FF, gr2, f1r, stage);
+  }
+  vec_accumulate<ET>(lg + G.c2[d], gr2);
+  f4 gf1[FT];
+  matvec<FT, ET>(P + L.W2T[d], E, gr2, gf1);
+#pragma unroll
+  for (int t = 0; t < FT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gf1[t][r] = c.f1[t][r] > 0.f ? gf1[t][r] : 0.f;
+  dw_accumulate<FT, ET>(lg + G.W1[d], E, gf1, c.y, stage);
+  vec_accumulate<FT>(lg + G.c1[d], gf1);
+  f4 gy[ET];
+  matvec<ET, FT>(P + L.W1T[d], FF, gf1, gy);
+#pragma unroll
+  for (int t = 0; t < ET; ++t) gy[t] += gr2[t];
+  {  // LN1: y = xh1*g1 + n1
+    f4 t0[ET];
+#pragma unroll
+    for (int t = 0; t < ET; ++t) t0[t] = gy[t] * c.xh1[t];
+    vec_accumulate<ET>(lg + G.g1[d], t0);
+    vec_accumulate<ET>(lg + G.n1[d], gy);
+  }
+  layernorm_bwd<ET>(gy, c.xh1, c.rs1, P + L.g1[d], gres);
+  // r1 = N z + b_U + x
+  dw_accumulate<ET, HET>(lg + G.N[d], H * E, gres, c.z, stage);
+  vec_accumulate<ET>(lg + G.bu[d], gres);
+  matvec<HET, ET>(P + L.NT[d], E, gres, gz);
+}
+
+}  // namespace t2o

@@ -1,0 +1,497 @@
+// t2o_mixer.hip — TransformerMixer unrolled over a replay batch on MI355X.
+//
+// Reference: n_transf_mixer.py:55-91 driven by the learner once per timestep
+// with the recurrent hyper-weight tokens (n_transf_mixer.py:69,91).  One wave
+// owns one episode for the whole unroll (episodes are independent; the
+// recurrence is only over the 3 hyper tokens), so a launch needs no
+// inter-workgroup synchronisation.  The learner's Q selection is fused into
+// the mixer's input read:
+//   qmode 0  qvals given directly                      [b][t][a]
+//   qmode 1  chosen-action Q  gather(Q[:, t], actions)  (online mixer)
+//   qmode 2  double-Q         Q_tgt[argmax(Q_on masked by avail)] (target mixer)
+#include "t2o_dispatch.hpp"
+#include "t2o_layout.hpp"
+#include "t2o_mixer_block.hpp"
+
+using namespace t2o;
+
+namespace {
+
+struct MixerNet {
+  const float* pack;
+  const float* hw0;   // [B][3][E] or null (zeros)
+  const float* hid;   // [b][t][a][E] (a-stride E)
+  int64_t hid_sb, hid_st;
+  const float* qsel;  // Q values for qmode 1/2: [b][t][a][NA], time extent q_ts
+  const float* qv_in; // qmode 0: [B][T][A]
+  int qmode, T;
+  float* y;           // [B][T]
+  float* hw;          // [B][T][3][E]
+  float* qv;          // [B][T][A] (may be null)
+  float* xout;        // [B][T][A+3][E] final query outputs (may be null)
+};
+
+struct MixerFwdArgs {
+  t2o_layout L;
+  MixerNet net[2];
+  const float* states;  // [b][t][ns*Fs]
+  int64_t st_sb, st_st;
+  const float* qarg;    // online-agent Q for the double-Q argmax, [b][t][a][NA]
+  int q_ts, n_actions;
+  const int64_t* actions;
+  int64_t act_sb, act_st;
+  const int32_t* avail;  // [b][t][a][NA]
+  int64_t av_sb, av_st;
+  int B, Fs;
+};
+
+template <int E, int A>
+struct MixDims {
+  static constexpr int NS = A;              // state entities (n_entities = n_agents)
+  static constexpr int Q = A + 3;           // query rows read out
+  static constexpr int LK = 2 * A + 3;      // keys
+  static constexpr int KT = (LK + 15) / 16;
+  static constexpr int QT = (Q + 15) / 16;
+  static constexpr int ST = (NS + 15) / 16;
+  static constexpr int LDX = E + 4;
+  static constexpr int X0F = KT * 16 * LDX;
+  static constexpr int OUTF = QT * 16 * E;
+  static constexpr int GX0F = KT * 16 * E;
+};
+
+T2O_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+T2O_DEV float elu1(float x) { return x > 0.f ? x : expm1f(x); }
+
+// qvals of step t for all A agents (every lane computes the same values)
+template <int A>
+T2O_DEV void load_qv(const MixerFwdArgs& a, const MixerNet& n, int b, int t, float (&qv)[A]) {
+  const int NA = a.n_actions;
+#pragma unroll
+  for (int ag = 0; ag < A; ++ag) {
+    if (n.qmode == 0) {
+      qv[ag] = n.qv_in[((size_t)b * n.T + t) * A + ag];
+    } else {
+      const size_t qrow = (((size_t)b * a.q_ts + t) * A + ag) * NA;
+      int act;
+      if (n.qmode == 1) {
+        act = (int)a.actions[b * a.act_sb + t * a.act_st + ag];
+      } else {
+        float best = -INFINITY;
+        act = 0;
+        const int32_t* av = a.avail ? a.avail + b * a.av_sb + t * a.av_st + ag * NA : nullptr;
+        for (int k = 0; k < NA; ++k) {
+          const float v = (av && av[k] == 0) ? -9999999.0f : a.qarg[qrow + k];
+          if (v > best) { best = v; act = k; }
+        }
+      }
+      qv[ag] = n.qsel[qrow + act];
+    }
+  }
+}
+
+// Build the key block X0 rows for step t: state-entity embeddings and agent
+// hidden tokens (the hyper-token rows are carried separately).
+template <int E, int A>
+T2O_DEV void build_keys(const float* __restrict__ P, const t2o_layout& L, const MixerFwdArgs& a,
+                        const MixerNet& n, int b, int t, float* X0) {
+  using Dm = MixDims<E, A>;
+  constexpr int ET = E / 16;
+  const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
+  const float* st = a.states + b * a.st_sb + t * a.st_st;
+#pragma unroll
+  for (int s = 0; s < Dm::ST; ++s) {
+    const int j = 16 * s + c;
+    f4 sv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 4 * g + r;
+      sv[r] = (j < Dm::NS && f < a.Fs) ? st[j * a.Fs + f] : 0.f;
+    }
+    f4 emb[ET];
+    matvec<ET, 1>(P + L.We, 16, &sv, emb);
+    if (j < Dm::NS) {
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft) st4(X0 + j * Dm::LDX + 16 * ft + 4 * g, emb[ft] + vec_t(P + L.be, ft));
+    }
+  }
+  const float* hd = n.hid + b * n.hid_sb + t * n.hid_st;
+  for (int i = lane; i < A * E / 4; i += 64) {
+    const int ag = (4 * i) / E, f = (4 * i) % E;
+    st4(X0 + (Dm::NS + ag) * Dm::LDX + f, ld4(hd + 4 * i));
+  }
+}
+
+// Mixing head (n_transf_mixer.py:75-89) on the final query rows OUT[q][f],
+// lanes = features.  Returns y; writes hyper tokens back into X0.
+template <int E, int A>
+T2O_DEV float mixer_head(const float* __restrict__ P, const t2o_layout& L, const float* OUT,
+                         const float (&qv)[A], float& pre_h, float& pre2) {
+  const int f = threadIdx.x & 63;
+  const bool fv = f < E;
+  const int fc = fv ? f : 0;
+  float ph = OUT[A * E + fc];
+#pragma unroll
+  for (int ag = 0; ag < A; ++ag) ph += qv[ag] * fabsf(OUT[ag * E + fc]);
+  pre_h = ph;
+  const float hidden = elu1(ph);
+  const float w2 = fabsf(OUT[(A + 1) * E + fc]);
+  const float yv = wave_sum(fv ? hidden * w2 : 0.f);
+  const float p2 = wave_sum(fv ? P[L.Wo + fc] * OUT[(A + 2) * E + fc] : 0.f) + P[L.bo];
+  pre2 = p2;
+  return yv + fmaxf(p2, 0.f);
+}
+
+template <int E, int H, int D, int A, int FF>
+__global__ __launch_bounds__(256) void mixer_fwd_kernel(MixerFwdArgs args) {
+  using Dm = MixDims<E, A>;
+  constexpr int ET = E / 16;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int w = wave_id();
+  const int b = blockIdx.x * 4 + w;
+  if (b >= args.B) return;  // wave-uniform; no block barriers in this kernel
+  const MixerNet n = args.net[blockIdx.y];
+  const t2o_layout& L = args.L;
+  const float* __restrict__ P = n.pack;
+  float* X0 = smem + w * (Dm::X0F + Dm::OUTF);
+  float* OUT = X0 + Dm::X0F;
+  const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
+  for (int i = lane; i < Dm::X0F; i += 64) X0[i] = 0.f;
+  for (int i = lane; i < 3 * E; i += 64) {
+    const int k = i / E, f = i % E;
+    X0[(Dm::NS + A + k) * Dm::LDX + f] = n.hw0 ? n.hw0[(size_t)b * 3 * E + i] : 0.f;
+  }
+  for (int t = 0; t < n.T; ++t) {
+    build_keys<E, A>(P, L, args, n, b, t, X0);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int qt = 0; qt < Dm::QT; ++qt) {
+      const int q = 16 * qt + c;
+      f4 x[ET];
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft)
+        x[ft] = q < Dm::Q ? ld4(X0 + (Dm::NS + q) * Dm::LDX + 16 * ft + 4 * g) : zero4();
+#pragma unroll
+      for (int d = 0; d < D; ++d)
+        mixer_block_fwd<E, H, Dm::KT, FF, Dm::LDX, false>(P, L, d, X0, Dm::LK, x, nullptr);
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft) st4(OUT + q * E + 16 * ft + 4 * g, x[ft]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    float qv[A];
+    load_qv<A>(args, n, b, t, qv);
+    float pre_h, pre2;
+    const float y = mixer_head<E, A>(P, L, OUT, qv, pre_h, pre2);
+    const size_t bt = (size_t)b * n.T + t;
+    if (lane == 0) n.y[bt] = y;
+    if (n.qv && lane < A) {
+#pragma unroll
+      for (int ag = 0; ag < A; ++ag)
+        if (lane == ag) n.qv[bt * A + ag] = qv[ag];
+    }
+    for (int i = lane; i < 3 * E; i += 64) {
+      const int k = i / E, f = i % E;
+      const float v = OUT[(A + k) * E + f];
+      n.hw[bt * 3 * E + i] = v;
+      X0[(Dm::NS + A + k) * Dm::LDX + f] = v;
+    }
+    if (n.xout) {
+      for (int i = lane; i < Dm::Q * E; i += 64) n.xout[bt * Dm::Q * E + i] = OUT[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+template <int E, int H, int D, int A, int FF>
+int launch_mixer_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
+  using Dm = MixDims<E, A>;
+  const size_t lds = sizeof(float) * 4 * (Dm::X0F + Dm::OUTF);
+  auto kern = mixer_fwd_kernel<E, H, D, A, FF>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  dim3 grid((args.B + 3) / 4, nnet);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, args);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// BPTT.  One wave per episode, 2 waves per workgroup (the shared LDS gradient
+// block + per-wave key/staging buffers fill one CU's 160 KiB).  Per step t
+// (backwards): rebuild X0 from the stored inputs and hyper tokens, run the
+// mixing-head backward on the stored final query rows, then per query tile
+// recompute the blocks with cache and back-propagate.  Outputs per step: grad
+// wrt the qvals (-> the agent's chosen-Q grad) and wrt the agent hidden
+// tokens; the hyper-token grad is carried to step t-1.
+struct MixerBwdArgs {
+  MixerFwdArgs f;     // net[0] = the network (qmode 0: qv_in = forward qv output)
+  t2o_layout G;
+  const float* hw;    // forward hw output [B][T][3][E]
+  const float* xout;  // forward final query rows [B][T][A+3][E]
+  const float* gy;    // [B][T]
+  const float* ghw_ext;  // [B][T][3][E] extra grad on the hyper outputs (may be null)
+  float* gqv;         // [B][T][A]
+  float* ghid;        // [B][T][A][E]
+  float* ghw0;        // [B][3][E] (may be null)
+  float* slabs;
+  int lds_grad;
+  int waves;          // episodes (waves) per workgroup: 2, or 1 when 2 do not fit in LDS
+};
+
+constexpr int MIX_BWD_WAVES = 2;
+
+template <int E, int H, int D, int A, int FF>
+__global__ __launch_bounds__(128) void mixer_bwd_kernel(MixerBwdArgs args) {
+  using Dm = MixDims<E, A>;
+  constexpr int ET = E / 16, KT = Dm::KT;
+  constexpr int STAGE = StageDims<(KT < ET ? KT : ET) < 2 ? 2 : (KT < ET ? KT : ET)>::FLOATS;
+  constexpr int PERW = Dm::X0F + Dm::OUTF + Dm::GX0F + STAGE;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const MixerFwdArgs& fa = args.f;
+  const MixerNet& n = fa.net[0];
+  const t2o_layout& L = fa.L;
+  const t2o_layout& G = args.G;
+  float* lg = smem;
+  const int w = wave_id();
+  float* X0 = smem + args.lds_grad + w * PERW;
+  float* OUT = X0 + Dm::X0F;
+  float* GX0 = OUT + Dm::OUTF;
+  float* stage = GX0 + Dm::GX0F;
+  for (int i = threadIdx.x; i < args.lds_grad; i += blockDim.x) lg[i] = 0.f;
+  __syncthreads();
+  const int b = blockIdx.x * args.waves + w;
+  const float* __restrict__ P = n.pack;
+  const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
+  if (b < fa.B) {
+    for (int i = lane; i < Dm::X0F; i += 64) X0[i] = 0.f;
+    for (int i = lane; i < Dm::GX0F; i += 64) GX0[i] = 0.f;
+    float ghw[3] = {0.f, 0.f, 0.f};  // grad wrt this step's hyper outputs, lane = feature
+    const int f = lane < E ? lane : 0;
+    const bool fv = lane < E;
+    for (int t = n.T - 1; t >= 0; --t) {
+      const size_t bt = (size_t)b * n.T + t;
+      build_keys<E, A>(P, L, fa, n, b, t, X0);
+      for (int i = lane; i < 3 * E; i += 64) {
+        const int k = i / E, ff = i % E;
+        const float v = t > 0 ? args.hw[(bt - 1) * 3 * E + i] : (n.hw0 ? n.hw0[(size_t)b * 3 * E + i] : 0.f);
+        X0[(Dm::NS + A + k) * Dm::LDX + ff] = v;
+      }
+      for (int i = lane; i < Dm::Q * E; i += 64) OUT[i] = args.xout[bt * Dm::Q * E + i];
+      __builtin_amdgcn_wave_barrier();
+      // ---- mixing head backward (lanes = features)
+      float qv[A];
+      load_qv<A>(fa, n, b, t, qv);
+      float pre_h, pre2;
+      (void)mixer_head<E, A>(P, L, OUT, qv, pre_h, pre2);
+      const float gyv = args.gy[bt];
+      const float hidden = elu1(pre_h);
+      const float xw2 = OUT[(A + 1) * E + f];
+      const float sgn_w2 = (xw2 > 0.f) - (xw2 < 0.f);
+      const float gpre = gyv * fabsf(xw2) * (pre_h > 0.f ? 1.f : expf(pre_h));
+      const float gpre2 = pre2 > 0.f ? gyv : 0.f;
+      float gout[A + 3];
+#pragma unroll
+      for (int ag = 0; ag < A; ++ag) {
+        const float xa = OUT[ag * E + f];
+        gout[ag] = qv[ag] * gpre * ((xa > 0.f) - (xa < 0.f));
+        const float gq = wave_sum(fv ? gpre * fabsf(xa) : 0.f);
+        if (lane == 0) args.gqv[bt * A + ag] = gq;
+      }
+      if (args.ghw_ext) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ghw[k] += args.ghw_ext[(bt * 3 + k) * E + f];
+      }
+      gout[A] = gpre + ghw[0];
+      gout[A + 1] = gyv * hidden * sgn_w2 + ghw[1];
+      gout[A + 2] = gpre2 * P[L.Wo + f] + ghw[2];
+      if (fv) {
+        atomicAdd(lg + G.Wo + f, gpre2 * OUT[(A + 2) * E + f]);
+        if (lane == 0) atomicAdd(lg + G.bo, gpre2);
+      }
+      __builtin_amdgcn_wave_barrier();
+      // gOUT rows -> OUT buffer (the forward rows are no longer needed)
+      if (fv) {
+#pragma unroll
+        for (int q = 0; q < A + 3; ++q) OUT[q * E + f] = gout[q];
+      }
+      for (int i = Dm::Q * E + lane; i < Dm::OUTF; i += 64) OUT[i] = 0.f;
+      __builtin_amdgcn_wave_barrier();
+      // ---- blocks backward per query tile
+#pragma unroll
+      for (int qt = 0; qt < Dm::QT; ++qt) {
+        const int q = 16 * qt + c;
+        f4 gx[ET];
+        f4 xs[D][ET];
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft) {
+          gx[ft] = ld4(OUT + q * E + 16 * ft + 4 * g);
+          xs[0][ft] = q < Dm::Q ? ld4(X0 + (Dm::NS + q) * Dm::LDX + 16 * ft + 4 * g) : zero4();
+        }
+#pragma unroll
+        for (int d = 0; d + 1 < D; ++d) {
+          f4 x[ET];
+#pragma unroll
+          for (int ft = 0; ft < ET; ++ft) x[ft] = xs[d][ft];
+          mixer_block_fwd<E, H, KT, FF, Dm::LDX, false>(P, L, d, X0, Dm::LK, x, nullptr);
+#pragma unroll
+          for (int ft = 0; ft < ET; ++ft) xs[d + 1][ft] = x[ft];
+        }
+#pragma unroll
+        for (int d = D - 1; d >= 0; --d) {
+          MixerCache<E, H, KT, FF> cache;
+          f4 x[ET];
+#pragma unroll
+          for (int ft = 0; ft < ET; ++ft) x[ft] = xs[d][ft];
+          mixer_block_fwd<E, H, KT, FF, Dm::LDX, true>(P, L, d, X0, Dm::LK, x, &cache);
+          mixer_block_bwd<E, H, KT, FF, Dm::LDX>(P, L, G, lg, stage, d, X0, GX0, cache, gx);
+        }
+        // query path: the block-0 input rows are key tokens NS+q
+        if (q < Dm::Q) {
+#pragma unroll
+          for (int ft = 0; ft < ET; ++ft)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) atomicAdd(GX0 + (Dm::NS + q) * E + 16 * ft + 4 * g + r, gx[ft][r]);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      // ---- key-token grads: agent hidden tokens out, hyper tokens carried,
+      // state embeddings -> We / be
+      for (int i = lane; i < A * E; i += 64) args.ghid[bt * A * E + i] = GX0[(Dm::NS) * E + i];
+      if (fv) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ghw[k] = GX0[(Dm::NS + A + k) * E + f];
+        const float* st = fa.states + b * fa.st_sb + t * fa.st_st;
+        float gbe = 0.f;
+        for (int fs = 0; fs < fa.Fs; ++fs) {
+          float acc = 0.f;
+          for (int j = 0; j < Dm::NS; ++j) acc += GX0[j * E + f] * st[j * fa.Fs + fs];
+          atomicAdd(lg + G.We + f * 16 + fs, acc);
+        }
+        for (int j = 0; j < Dm::NS; ++j) gbe += GX0[j * E + f];
+        atomicAdd(lg + G.be + f, gbe);
+      }
+      __builtin_amdgcn_wave_barrier();
+      for (int i = lane; i < Dm::GX0F; i += 64) GX0[i] = 0.f;
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (args.ghw0 && fv) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) args.ghw0[((size_t)b * 3 + k) * E + f] = ghw[k];
+    }
+  }
+  __syncthreads();
+  float* slab = args.slabs + (size_t)blockIdx.x * G.grad_total;
+  for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) slab[i] = lg[i];
+}
+
+template <int E, int H, int D, int A, int FF>
+int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
+  using Dm = MixDims<E, A>;
+  constexpr int ET = E / 16, KT = Dm::KT;
+  constexpr int STAGE = StageDims<(KT < ET ? KT : ET) < 2 ? 2 : (KT < ET ? KT : ET)>::FLOATS;
+  constexpr int PERW = Dm::X0F + Dm::OUTF + Dm::GX0F + STAGE;
+  args.lds_grad = (int)((args.G.grad_total + 15) / 16 * 16);
+  args.waves = MIX_BWD_WAVES;
+  size_t lds = sizeof(float) * ((size_t)args.lds_grad + args.waves * PERW);
+  if (lds > 160 * 1024) {
+    args.waves = 1;
+    lds = sizeof(float) * ((size_t)args.lds_grad + PERW);
+  }
+  if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
+  const int grid = (args.f.B + args.waves - 1) / args.waves;
+  if (grid > max_slabs) return T2O_EINVAL;
+  auto kern = mixer_bwd_kernel<E, H, D, A, FF>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * args.waves), lds, stream, args);
+  *nslab = grid;
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, const float* pack_tg,
+                                    const float* states, int64_t st_sb, int64_t st_st,
+                                    const float* hid_on, const float* hid_tg, int64_t hid_sb, int64_t hid_st,
+                                    const float* hw0_on, const float* hw0_tg, int qmode_on, int qmode_tg,
+                                    const float* qv_on, const float* qv_tg, const float* q_on,
+                                    const float* q_tg, int q_ts, int n_actions, const int64_t* actions,
+                                    int64_t act_sb, int64_t act_st, const int32_t* avail, int64_t av_sb,
+                                    int64_t av_st, float* y_on, float* hw_on, float* qvo_on, float* xout_on,
+                                    float* y_tg, float* hw_tg, float* qvo_tg, float* xout_tg, int B, int T_on,
+                                    int T_tg, void* stream) {
+  if (!L || L->kind != 1 || !pack_on || !states || !hid_on || !y_on || !hw_on || B < 1 || T_on < 1 ||
+      L->E > 64)
+    return T2O_EINVAL;
+  MixerFwdArgs a{};
+  a.L = *L;
+  a.states = states;
+  a.st_sb = st_sb;
+  a.st_st = st_st;
+  a.qarg = q_on;
+  a.q_ts = q_ts;
+  a.n_actions = n_actions;
+  a.actions = actions;
+  a.act_sb = act_sb;
+  a.act_st = act_st;
+  a.avail = avail;
+  a.av_sb = av_sb;
+  a.av_st = av_st;
+  a.B = B;
+  a.Fs = L->F;
+  auto check_mode = [&](int mode, const float* qv, const float* qsel) {
+    if (mode == 0) return qv != nullptr;
+    if (mode == 1) return qsel && actions;
+    if (mode == 2) return qsel && q_on != nullptr;
+    return false;
+  };
+  if (!check_mode(qmode_on, qv_on, q_on)) return T2O_EINVAL;
+  a.net[0] = MixerNet{pack_on, hw0_on, hid_on, hid_sb, hid_st, q_on, qv_on, qmode_on, T_on,
+                      y_on, hw_on, qvo_on, xout_on};
+  int nnet = 1;
+  if (pack_tg) {
+    if (!hid_tg || !y_tg || !hw_tg || T_tg < 1 || !check_mode(qmode_tg, qv_tg, q_tg)) return T2O_EINVAL;
+    a.net[1] = MixerNet{pack_tg, hw0_tg, hid_tg, hid_sb, hid_st, q_tg, qv_tg, qmode_tg, T_tg,
+                        y_tg, hw_tg, qvo_tg, xout_tg};
+    nnet = 2;
+  }
+  int rc = T2O_EUNSUPPORTED;
+  T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
+               rc = (launch_mixer_fwd<E_, H_, D_, NE_, FF_>(a, nnet, (hipStream_t)stream)));
+  return rc;
+}
+
+extern "C" int t2o_mixer_bwd_max_slabs(int B) { return B; }  // worst case: 1 episode per workgroup
+
+extern "C" int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, const float* states, int64_t st_sb,
+                                    int64_t st_st, const float* hid, int64_t hid_sb, int64_t hid_st,
+                                    const float* hw0, const float* qv, const float* hw, const float* xout,
+                                    const float* gy, const float* ghw_ext, float* gqv, float* ghid, float* ghw0,
+                                    float* gslabs,
+                                    int max_slabs, int* nslab, int B, int T, void* stream) {
+  if (!L || L->kind != 1 || !pack || !states || !hid || !qv || !hw || !xout || !gy || !gqv || !ghid ||
+      !gslabs || !nslab || B < 1 || T < 1 || L->E > 64)
+    return T2O_EINVAL;
+  MixerBwdArgs a{};
+  a.f.L = *L;
+  a.f.states = states;
+  a.f.st_sb = st_sb;
+  a.f.st_st = st_st;
+  a.f.B = B;
+  a.f.Fs = L->F;
+  a.f.net[0] = MixerNet{pack, hw0, hid, hid_sb, hid_st, nullptr, qv, 0, T, nullptr, nullptr, nullptr, nullptr};
+  grad_layout(*L, a.G);
+  a.hw = hw;
+  a.xout = xout;
+  a.gy = gy;
+  a.ghw_ext = ghw_ext;
+  a.gqv = gqv;
+  a.ghid = ghid;
+  a.ghw0 = ghw0;
+  a.slabs = gslabs;
+  int rc = T2O_EUNSUPPORTED;
+  T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
+               rc = (launch_mixer_bwd<E_, H_, D_, NE_, FF_>(a, max_slabs, nslab, (hipStream_t)stream)));
+  return rc;
+}

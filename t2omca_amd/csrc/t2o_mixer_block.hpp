@@ -1,0 +1,145 @@
+// t2o_mixer_block.hpp — one transformer block of the mixer for a 16-query tile.
+//
+// Reference: n_transf_mixer.py:55-91 -> transformer.py:40-140.  The mixer's
+// tokens for one (episode, t) are X0 = [We·s_j + b_e (A state entities),
+// agent hidden states (A), hyper-weight tokens (3)]; only the last A+3 rows
+// are read out (w1, b1, w2, b2 — n_transf_mixer.py:75-85), and keys never
+// change across blocks (transformer.py:140), so only those A+3 query rows are
+// propagated.  A wave owns ONE episode: queries sit on the MFMA N axis (lanes),
+// the key block X0 [keys x E] is wave-private LDS, and per head
+//   Sᵀ = X0 · u_h        (u_h = M_h x, scores for all keys of all queries)
+//   Zᵀ = X0ᵀ · softmax(S)ᵀ
+// are two MFMA products whose outputs are already in the T-layout the next
+// step consumes (keys on the register axis for S, features for Z).
+#pragma once
+#include "t2o_block.hpp"
+
+namespace t2o {
+
+template <int E, int H, int KT, int FF>
+struct MixerCache {
+  static constexpr int ET = E / 16, HET = H * ET;
+  PostCache<E, H, FF> post;
+  f4 u[HET];
+  f4 p[H][KT];
+};
+
+// Sᵀ-style product: out[kt] (keys 16kt+4g+r, query c) = Σ_f X0[key][f] v[f]
+template <int E, int KT, int LDX>
+T2O_DEV void keys_dot(const float* __restrict__ X0, const f4* v, f4* out) {
+  constexpr int ET = E / 16;
+  const int c = lane_c(), g = lane_g();
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    f4 acc = zero4();
+#pragma unroll
+    for (int ft = 0; ft < ET; ++ft) {
+      const f4 a = ld4(X0 + (16 * kt + c) * LDX + 16 * ft + 4 * g);
+      acc = mfma4(a[0], v[ft][0], acc);
+      acc = mfma4(a[1], v[ft][1], acc);
+      acc = mfma4(a[2], v[ft][2], acc);
+      acc = mfma4(a[3], v[ft][3], acc);
+    }
+    out[kt] = acc;
+  }
+}
+
+// Zᵀ-style product: out[ft] (features 16ft+4g+r, query c) = Σ_key X0[key][f] w[key]
+template <int E, int KT, int LDX>
+T2O_DEV void keys_combine(const float* __restrict__ X0, const f4* w, f4* out) {
+  constexpr int ET = E / 16;
+  const int c = lane_c(), g = lane_g();
+#pragma unroll
+  for (int ft = 0; ft < ET; ++ft) {
+    f4 acc = zero4();
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+        acc = mfma4(X0[(16 * kt + 4 * g + s) * LDX + 16 * ft + c], w[kt][s], acc);
+    out[ft] = acc;
+  }
+}
+
+template <int E, int H, int KT, int FF, int LDX, bool CACHE>
+T2O_DEV void mixer_block_fwd(const float* __restrict__ P, const t2o_layout& L, int d,
+                             const float* __restrict__ X0, int Lk, f4* x, MixerCache<E, H, KT, FF>* cache) {
+  constexpr int ET = E / 16, HET = H * ET;
+  const int g = lane_g();
+  f4 u[HET];
+  matvec<HET, ET>(P + L.M[d], E, x, u);
+  f4 z[HET];
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh) {
+    f4 s[KT];
+    keys_dot<E, KT, LDX>(X0, &u[hh * ET], s);
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (16 * kt + 4 * g + r >= Lk) s[kt][r] = -INFINITY;
+        m = fmaxf(m, s[kt][r]);
+      }
+    m = allmax4(m);
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s[kt][r] = expf(s[kt][r] - m);
+        l += s[kt][r];
+      }
+    const float il = 1.0f / allsum4(l);
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) s[kt] *= il;
+    keys_combine<E, KT, LDX>(X0, s, &z[hh * ET]);
+    if constexpr (CACHE) {
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) cache->p[hh][kt] = s[kt];
+    }
+  }
+  if constexpr (CACHE) {
+#pragma unroll
+    for (int t = 0; t < HET; ++t) cache->u[t] = u[t];
+  }
+  post_fwd<E, H, FF, CACHE>(P, L, d, z, x, CACHE ? &cache->post : nullptr);
+}
+
+// Backward of block d for one query tile.  gx: in = grad wrt block output,
+// out = grad wrt block input.  gX0 (wave-private LDS [KT*16][E]) accumulates
+// the grad wrt the key tokens (contraction over queries = rows).
+template <int E, int H, int KT, int FF, int LDX>
+T2O_DEV void mixer_block_bwd(const float* __restrict__ P, const t2o_layout& L, const t2o_layout& G,
+                             float* __restrict__ lg, float* __restrict__ stage, int d,
+                             const float* __restrict__ X0, float* __restrict__ gX0,
+                             const MixerCache<E, H, KT, FF>& c, f4* gx) {
+  constexpr int ET = E / 16, HET = H * ET;
+  f4 gz[HET], gres[ET];
+  post_bwd<E, H, FF>(P, L, G, lg, stage, d, c.post, gx, gz, gres);
+  f4 gu[HET];
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh) {
+    f4 gp[KT];
+    keys_dot<E, KT, LDX>(X0, &gz[hh * ET], gp);
+    float dot = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dot += c.p[hh][kt][r] * gp[kt][r];
+    dot = allsum4(dot);
+    f4 gs[KT];
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) gs[kt] = c.p[hh][kt] * (gp[kt] - dot);
+    keys_combine<E, KT, LDX>(X0, gs, &gu[hh * ET]);
+    dw_accumulate<KT, ET>(gX0, E, c.p[hh], &gz[hh * ET], stage);
+    dw_accumulate<KT, ET>(gX0, E, gs, &c.u[hh * ET], stage);
+  }
+  dw_accumulate<HET, ET>(lg + G.M[d], E, gu, c.post.x, stage);
+  f4 gxp[ET];
+  matvec<ET, HET>(P + L.MT[d], H * E, gu, gxp);
+#pragma unroll
+  for (int t = 0; t < ET; ++t) gx[t] = gxp[t] + gres[t];
+}
+
+}  // namespace t2o

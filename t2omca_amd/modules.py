@@ -1,0 +1,184 @@
+"""Drop-in replacements for the reference's hot-path modules.
+
+``TransformerAgent`` and ``TransformerMixer`` keep the reference constructor
+signatures, the args fields they read, ``init_hidden`` and the forward
+signatures (transf_agent.py:9-76, n_transf_mixer.py:13-91) and register
+exactly the reference parameter tree, so ``state_dict`` keys/shapes match
+(SURVEY.md §8 b) and checkpoints move between the two frameworks.
+
+The forward passes run the HIP kernels (one-step unrolls of
+t2o_agent_unroll_fwd / t2o_mixer_unroll_fwd); autograd is supported through
+the BPTT kernels with T = 1.  The TD update itself does not go through these
+per-step forwards: ``t2omca_amd.learner.TDLearner`` runs whole-unroll kernels
+on the same parameters.  CPU tensors raise — there is no CPU fallback.
+"""
+import torch
+import torch.nn as nn
+
+from . import ops
+
+
+class MultiHeadAttention(nn.Module):
+    """Parameter container with the reference names (transformer.py:34-38)."""
+
+    def __init__(self, emb, heads=8, mask=False):
+        super().__init__()
+        self.emb, self.heads, self.mask = emb, heads, mask
+        self.tokeys = nn.Linear(emb, emb * heads, bias=False)
+        self.toqueries = nn.Linear(emb, emb * heads, bias=False)
+        self.tovalues = nn.Linear(emb, emb * heads, bias=False)
+        self.unifyheads = nn.Linear(heads * emb, emb)
+
+
+class TransformerBlock(nn.Module):
+    """Parameter container (transformer.py:103-118)."""
+
+    def __init__(self, emb, heads, mask, ff_hidden_mult=4, dropout=0.0):
+        super().__init__()
+        self.attention = MultiHeadAttention(emb, heads=heads, mask=mask)
+        self.mask = mask
+        self.norm1 = nn.LayerNorm(emb)
+        self.norm2 = nn.LayerNorm(emb)
+        self.ff = nn.Sequential(nn.Linear(emb, ff_hidden_mult * emb), nn.ReLU(),
+                                nn.Linear(ff_hidden_mult * emb, emb))
+        self.do = nn.Dropout(dropout)
+
+
+class Transformer(nn.Module):
+    """Parameter container (transformer.py:143-167); the compute is fused in HIP."""
+
+    def __init__(self, emb, heads, depth, ff_hidden_mult=4, dropout=0.0):
+        super().__init__()
+        if dropout != 0.0:
+            raise ValueError("t2omca_amd: dropout > 0 is not supported (the reference path uses 0)")
+        self.tblocks = nn.Sequential(*[TransformerBlock(emb=emb, heads=heads, mask=False,
+                                                        ff_hidden_mult=ff_hidden_mult, dropout=dropout)
+                                       for _ in range(depth)])
+
+
+def _flat(module):
+    return torch.cat([p.reshape(-1) for p in module.parameters()])
+
+
+class _AgentStep(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, flat, inputs, hidden, shape):
+        b, a, nf = inputs.shape
+        pack = ops.pack_params(shape, flat.detach().contiguous())
+        obs = inputs.detach().contiguous().view(b, 1, a, nf)
+        h0 = hidden.detach().reshape(b * a, shape.E).contiguous()
+        q, h = ops.agent_unroll_fwd(shape, pack, obs, h0_on=h0)
+        ctx.save_for_backward(flat, obs, h0, h)
+        ctx.shape = shape
+        return q[:, 0], h[:, 0]
+
+    @staticmethod
+    def backward(ctx, gq, gh):
+        flat, obs, h0, h = ctx.saved_tensors
+        shape = ctx.shape
+        pack = ops.pack_params(shape, flat.detach().contiguous())
+        b, _, a, _ = obs.shape
+        gq = (gq if gq is not None else torch.zeros_like(h[:, 0, :, :0])).contiguous().view(b, 1, a, -1)
+        gh = (gh if gh is not None else torch.zeros_like(h[:, 0])).contiguous().view(b, 1, a, shape.E)
+        gpack, gh0 = ops.agent_unroll_bwd(shape, pack, obs, h, h0=h0, gq=gq, gh=gh, want_gh0=True)
+        gflat = torch.zeros_like(flat)
+        ops.unpack_grads(shape, flat.detach().contiguous(), gpack, gflat)
+        return gflat, None, gh0.view(b, a, shape.E), None
+
+
+class TransformerAgent(nn.Module):
+    """transf_agent.py:8-76 drop-in (HIP forward/backward)."""
+
+    def __init__(self, input_shape, args):
+        super().__init__()
+        self.args = args
+        self.n_agents = args.n_agents
+        self.n_entities = getattr(self.args, "n_entities_obs", self.args.n_entities)
+        self.feat_dim = args.obs_entity_feats
+        self.emb_dim = args.emb
+        self.feat_embedding = nn.Linear(self.feat_dim, self.emb_dim)
+        self.transformer = Transformer(args.emb, args.heads, args.depth, args.ff_hidden_mult, args.dropout)
+        if getattr(self.args, "action_selector", None) == "noisy-new":
+            raise NotImplementedError("t2omca_amd: the NoisyLinear head (transf_agent.py:37-39) is not on "
+                                      "the fused path")
+        self.q_basic = nn.Linear(args.emb, args.n_actions)
+        self.shape = ops.NetShape(ops.AGENT, args.emb, args.heads, args.depth, self.feat_dim, args.n_actions,
+                                  args.ff_hidden_mult * args.emb, self.n_entities)
+
+    def init_hidden(self):
+        return torch.zeros(1, self.args.emb, device=self.args.device)
+
+    def forward(self, inputs, hidden_state):
+        b, a, _ = inputs.size()
+        if b * a * self.emb_dim != hidden_state.numel():
+            hidden_state = hidden_state.expand(b, a, self.emb_dim)
+        q, h = _AgentStep.apply(_flat(self), inputs, hidden_state, self.shape)
+        return q.view(b, a, -1), h.view(b, a, -1)
+
+
+class _MixerStep(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, flat, qvals, hidden_states, hyper_weights, states, shape):
+        b = qvals.shape[0]
+        A, E = shape.n_ent, shape.E
+        pack = ops.pack_params(shape, flat.detach().contiguous())
+        qv = qvals.detach().reshape(b, 1, A).contiguous()
+        hid = hidden_states.detach().reshape(b, 1, A, E).contiguous()
+        hw0 = hyper_weights.detach().reshape(b, 3, E).contiguous()
+        st = states.detach().reshape(b, 1, -1).contiguous()
+        out = ops.mixer_unroll_fwd(shape, pack, st, hid, qmode_on=0, qv_on=qv, hw0_on=hw0)
+        ctx.save_for_backward(flat, qv, hid, hw0, st, out["y"], out["hw"], out["qv"], out["xout"])
+        ctx.shape = shape
+        return out["y"].view(b, 1, 1), out["hw"][:, 0]
+
+    @staticmethod
+    def backward(ctx, gy, ghw):
+        flat, qv, hid, hw0, st, y, hw, qvo, xout = ctx.saved_tensors
+        shape = ctx.shape
+        b = qv.shape[0]
+        pack = ops.pack_params(shape, flat.detach().contiguous())
+        gy = (gy if gy is not None else torch.zeros_like(y)).reshape(b, 1).contiguous()
+        ghw = ghw.reshape(b, 1, 3, shape.E).contiguous() if ghw is not None else None
+        fwd = dict(y=y, hw=hw, qv=qvo, xout=xout)
+        gpack, gqv, ghid, ghw0 = ops.mixer_unroll_bwd(shape, pack, st, hid, fwd, gy, hw0=hw0, ghw_ext=ghw,
+                                                      want_ghw0=True)
+        gflat = torch.zeros_like(flat)
+        ops.unpack_grads(shape, flat.detach().contiguous(), gpack, gflat)
+        return gflat, gqv.view(b, 1, -1), ghid.view(b, -1, shape.E), ghw0, None, None
+
+
+class TransformerMixer(nn.Module):
+    """n_transf_mixer.py:12-102 drop-in (HIP forward/backward, pos_func abs)."""
+
+    def __init__(self, args, abs=True):
+        super().__init__()
+        self.args = args
+        self.n_agents = args.n_agents
+        self.n_entities = getattr(self.args, "n_entities_state", self.args.n_entities)
+        self.feat_dim = args.state_entity_feats
+        self.emb_dim = args.mixer_emb
+        self.feat_embedding = nn.Linear(self.feat_dim, self.emb_dim)
+        self.transformer = Transformer(args.mixer_emb, args.mixer_heads, args.mixer_depth,
+                                       args.ff_hidden_mult, args.dropout)
+        self.qmix_pos_func = getattr(self.args, "qmix_pos_func", "abs")
+        self.custom_space = args.env_args.get("state_entity_mode", True)
+        if self.qmix_pos_func != "abs" or not self.custom_space:
+            raise NotImplementedError("t2omca_amd: only qmix_pos_func='abs' with state_entity_mode=True "
+                                      "(the reference defaults, n_transf_mixer.py:42-43) are fused")
+        if self.n_entities != self.n_agents:
+            raise NotImplementedError("t2omca_amd: n_entities_state must equal n_agents "
+                                      "(environment_multi_mec.py:429)")
+        self.hyper_b2 = nn.Linear(self.emb_dim, 1)
+        if getattr(args, "use_orthogonal", False):
+            raise NotImplementedError("t2omca_amd: use_orthogonal init is not supported")
+        self.shape = ops.NetShape(ops.MIXER, args.mixer_emb, args.mixer_heads, args.mixer_depth, self.feat_dim, 1,
+                                  args.ff_hidden_mult * args.mixer_emb, self.n_agents)
+
+    def init_hidden(self):
+        # n_transf_mixer.py:52-53 (shape [1, A, E] as in the reference)
+        return torch.zeros(1, self.n_agents, self.args.emb, device=self.args.device)
+
+    def forward(self, qvals, hidden_states, hyper_weights, states, obs):
+        b = qvals.size(0)
+        hyper_weights = hyper_weights.expand(b, 3, self.emb_dim)
+        return _MixerStep.apply(_flat(self), qvals, hidden_states, hyper_weights, states, self.shape)

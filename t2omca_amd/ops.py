@@ -141,3 +141,116 @@ def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchose
     gpack = torch.empty(L.grad_total, device=obs.device)
     reduce_slabs(slabs, nslab.value, gpack)
     return gpack, gh0
+
+
+def _mstrides(t):
+    return (t.stride(0), t.stride(1)) if t is not None else (0, 0)
+
+
+def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv_on=None, q_on=None,
+                     actions=None, avail=None, hw0_on=None, T_on=None,
+                     pack_tg=None, hid_tg=None, qmode_tg=2, qv_tg=None, q_tg=None, hw0_tg=None,
+                     T_tg=None, want_xout=True):
+    """Mixer unroll (see include/t2omca.h).  states [B, >=T, n_ent*F];
+    hid_* [B, >=T, A, E] (contiguous inner [A, E]); q_on/q_tg [B, q_ts, A, NA]
+    contiguous; actions int64 [B, >=T, A]; avail int32 [B, >=T, A, NA].
+    Returns dict of outputs per network: y [B,T], hw [B,T,3,E], qv [B,T,A], xout."""
+    _dev(pack_on, states, hid_on, qv_on, q_on, hw0_on, pack_tg, hid_tg, qv_tg, q_tg, hw0_tg)
+    B = states.shape[0]
+    A, E = hid_on.shape[2], shape.E
+    L = shape.layout()
+    dev = states.device
+    T_on = T_on or (qv_on.shape[1] if qv_on is not None else hid_on.shape[1])
+    assert hid_on.stride(3) == 1 and hid_on.stride(2) == E and states.stride(2) == 1
+    if hid_tg is not None:
+        assert hid_tg.stride(0) == hid_on.stride(0) and hid_tg.stride(1) == hid_on.stride(1)
+    q_ts = q_on.shape[1] if q_on is not None else 0
+    for q in (q_on, q_tg):
+        assert q is None or (q.is_contiguous() and q.shape[1] == q_ts)
+    if actions is not None:
+        assert actions.dtype == torch.int64 and actions.stride(2) == 1
+    if avail is not None:
+        assert avail.dtype == torch.int32 and avail.stride(3) == 1 and avail.stride(2) == avail.shape[3]
+
+    def outs(T):
+        return dict(y=torch.empty(B, T, device=dev), hw=torch.empty(B, T, 3, E, device=dev),
+                    qv=torch.empty(B, T, A, device=dev),
+                    xout=torch.empty(B, T, A + 3, E, device=dev) if want_xout else None)
+
+    o_on = outs(T_on)
+    o_tg = None
+    if pack_tg is not None:
+        T_tg = T_tg or hid_tg.shape[1]
+        o_tg = outs(T_tg)
+    n_actions = q_on.shape[3] if q_on is not None else 0
+    act_sb, act_st = _mstrides(actions)
+    av_sb, av_st = _mstrides(avail)
+    g = lambda d, k: ptr(d[k]) if d is not None else None  # noqa: E731
+    check(lib().t2o_mixer_unroll_fwd(
+        ctypes.byref(L), ptr(pack_on), ptr(pack_tg), ptr(states), states.stride(0), states.stride(1),
+        ptr(hid_on), ptr(hid_tg), hid_on.stride(0), hid_on.stride(1), ptr(hw0_on), ptr(hw0_tg),
+        qmode_on, qmode_tg, ptr(qv_on), ptr(qv_tg), ptr(q_on), ptr(q_tg), q_ts, n_actions,
+        ptr(actions), act_sb, act_st, ptr(avail), av_sb, av_st,
+        g(o_on, "y"), g(o_on, "hw"), g(o_on, "qv"), g(o_on, "xout"),
+        g(o_tg, "y"), g(o_tg, "hw"), g(o_tg, "qv"), g(o_tg, "xout"),
+        B, T_on, T_tg or 0, stream_ptr()), "mixer_unroll_fwd")
+    return (o_on, o_tg) if pack_tg is not None else o_on
+
+
+def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_ext=None,
+                     want_ghw0=False, slabs=None):
+    """BPTT of mixer_unroll_fwd (one network, `fwd` = its output dict).
+    Returns (gpack, gqv [B,T,A], ghid [B,T,A,E], ghw0 or None)."""
+    _dev(pack, states, hid, gy, hw0, ghw_ext)
+    B, T = gy.shape
+    A, E = hid.shape[2], shape.E
+    L = shape.layout()
+    dev = gy.device
+    assert gy.is_contiguous() and fwd["xout"] is not None
+    nmax = int(lib().t2o_mixer_bwd_max_slabs(B))
+    if slabs is None or slabs.numel() < nmax * L.grad_total:
+        slabs = torch.empty(nmax * L.grad_total, device=dev)
+    gqv = torch.empty(B, T, A, device=dev)
+    ghid = torch.empty(B, T, A, E, device=dev)
+    ghw0 = torch.empty(B, 3, E, device=dev) if want_ghw0 else None
+    nslab = ctypes.c_int(0)
+    check(lib().t2o_mixer_unroll_bwd(
+        ctypes.byref(L), ptr(pack), ptr(states), states.stride(0), states.stride(1), ptr(hid),
+        hid.stride(0), hid.stride(1), ptr(hw0), ptr(fwd["qv"]), ptr(fwd["hw"]), ptr(fwd["xout"]),
+        ptr(gy), ptr(ghw_ext), ptr(gqv), ptr(ghid), ptr(ghw0), ptr(slabs), nmax, ctypes.byref(nslab),
+        B, T, stream_ptr()), "mixer_unroll_bwd")
+    gpack = torch.empty(L.grad_total, device=dev)
+    reduce_slabs(slabs, nslab.value, gpack)
+    return gpack, gqv, ghid, ghw0
+
+
+def td_loss(qtot, qtot_tgt, reward, terminated=None, filled=None, per_weight=None, gamma=0.99,
+            td_lambda=0.6, mask_sum=0.0):
+    """TD(λ) targets / loss / grads / priorities (PyMARL2 NQLearner contract).
+    qtot [B,T], qtot_tgt [B,T+1]; reward/terminated/filled [B, >=T] float views.
+    Returns dict(gq [B,T], targets [B,T], prio [B], loss [2])."""
+    _dev(qtot, qtot_tgt, reward, terminated, filled, per_weight)
+    B, T = qtot.shape
+    dev = qtot.device
+    assert qtot.is_contiguous() and qtot_tgt.is_contiguous() and qtot_tgt.shape[1] == T + 1
+    out = dict(gq=torch.empty(B, T, device=dev), targets=torch.empty(B, T, device=dev),
+               prio=torch.empty(B, device=dev), loss=torch.empty(2, device=dev))
+    rs, ts, fs = _mstrides(reward), _mstrides(terminated), _mstrides(filled)
+    check(lib().t2o_td_loss(ptr(qtot), ptr(qtot_tgt), ptr(reward), rs[0], rs[1], ptr(terminated),
+                            ts[0], ts[1], ptr(filled), fs[0], fs[1], ptr(per_weight), float(gamma),
+                            float(td_lambda), float(mask_sum), ptr(out["gq"]), ptr(out["targets"]),
+                            ptr(out["prio"]), ptr(out["loss"]), B, T, stream_ptr()), "td_loss")
+    return out
+
+
+def adam_step(params, grads, exp_avg, exp_avg_sq, step, *, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
+              weight_decay=0.0, max_grad_norm=10.0, workspace=None, grad_norm_out=None):
+    """In-place clip_grad_norm_ + Adam on flat fp32 buffers."""
+    _dev(params, grads, exp_avg, exp_avg_sq, workspace, grad_norm_out)
+    n = params.numel()
+    if workspace is None:
+        workspace = torch.empty(int(lib().t2o_adam_workspace_floats()), device=params.device)
+    check(lib().t2o_adam_step(ptr(params), ptr(grads), ptr(exp_avg), ptr(exp_avg_sq), ptr(workspace), n,
+                              float(lr), float(betas[0]), float(betas[1]), float(eps),
+                              float(weight_decay), float(max_grad_norm), int(step), ptr(grad_norm_out),
+                              stream_ptr()), "adam_step")
