@@ -1,0 +1,177 @@
+#!/usr/bin/env python3
+"""Benchmark: agent-transitions/sec of a full TD update (fwd + bwd + Adam).
+
+BASELINE.json metric, configs[2]: 8 AGVs x 4 MEC servers, replay batch 1024
+episodes x T = 60, emb 32 / 3 heads / depth 2 (SURVEY.md §8 defaults), one
+TD update = t2omca_amd.learner.TDLearner.train on a synthetic batch resident
+in HBM (t2omca_amd.synthetic, SURVEY.md §8 d).  One agent-transition = one
+(episode, timestep, agent) of the sampled batch, so an update is B*T*A.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Data parallel (weak scaling): every rank trains on its own 1024-episode shard
+and the flat gradient (+ Σ mask) is all-reduced over RCCL once per update.
+Rank 0 prints ONE JSON line.  Per-kernel times come from HIP events recorded
+on the launch stream inside the timed region; the CPU baseline is the
+oracle's PyTorch-CPU TD update (oracle/ref_learner.py) on a bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix = vector peak (dense)
+PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E spec peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=1024, help="episodes per GPU")
+    ap.add_argument("--T", type=int, default=60)
+    ap.add_argument("--agents", type=int, default=8)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=16, help="episodes in the CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    return ap.parse_args()
+
+
+class KernelTimer:
+    """HIP events around each phase of TDLearner.train (same stream as the launches)."""
+
+    def __init__(self):
+        self.events = []
+
+    def __call__(self, name):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self.events.append((name, ev))
+
+    def durations(self):
+        out = {}
+        for (n0, e0), (n1, e1) in zip(self.events, self.events[1:]):
+            if n0.startswith("begin:") and n1 == "end:" + n0[6:]:
+                out.setdefault(n0[6:], []).append(e0.elapsed_time(e1))
+        return out
+
+
+def cpu_baseline(args):
+    """The oracle's PyTorch-CPU TD update on a bounded sample of the same workload."""
+    from oracle import ref_learner, ref_model
+    A, T, B = args.agents, args.T, args.cpu_sample
+    cfg = dict(n_agents=A, n_entities=A, obs_entity_feats=9, emb=32, heads=3, depth=2, ff_hidden_mult=4,
+               n_actions=5, state_entity_feats=8, mixer_emb=32, mixer_heads=3, mixer_depth=2)
+    from t2omca_amd.synthetic import make_batch
+    batch, w = make_batch(B, T, A, seed=7, device="cpu")
+    learner = ref_learner.RefLearner(ref_model.init_params("agent", cfg, 0), ref_model.init_params("mixer", cfg, 1),
+                                     cfg)
+    threads = torch.get_num_threads()
+    learner.train(batch, 0, 0, per_weight=w)  # warm-up
+    times = []
+    t_start = time.perf_counter()
+    while len(times) < 3 or (time.perf_counter() - t_start < args.cpu_seconds and len(times) < 20):
+        t0 = time.perf_counter()
+        learner.train(batch, 0, 0, per_weight=w)
+        times.append(time.perf_counter() - t0)
+    best = min(times)
+    return {"value": B * T * A / best, "unit": "agent-transitions/s", "cores": threads, "kind": "port",
+            "sample": f"{B} episodes x T={T} x A={A} (one TD update = {B * T * A} agent-transitions), "
+                      f"min of {len(times)} updates after 1 warm-up, torch CPU fp32, {threads} threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    from t2omca_amd.learner import TDLearner
+    from t2omca_amd.modules import TransformerAgent, TransformerMixer
+    from t2omca_amd.perfmodel import ref_order_flops_per_transition, td_update_bytes, td_update_flops
+    from t2omca_amd.synthetic import make_args, make_batch
+
+    A, T, B = args.agents, args.T, args.batch
+    torch.manual_seed(0)
+    margs = make_args(A, device=str(dev))
+    agent = TransformerAgent(None, margs).to(dev)
+    mixer = TransformerMixer(margs).to(dev)
+    learner = TDLearner(agent, mixer, target_update_interval=10 ** 9)
+    batch, w = make_batch(B, T, A, seed=1 + rank, device=dev)
+    for i in range(args.warmup):
+        learner.train(batch, 0, i, per_weight=w)
+    timer = KernelTimer()
+    learner.timer = timer
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        learner.train(batch, 0, i, per_weight=w)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    learner.timer = None
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    transitions = world * B * T * A * args.steps
+    value = transitions / elapsed
+    kern = {k: sum(v) / len(v) for k, v in timer.durations().items()}
+    flops = td_update_flops(B, T, A)
+    bytes_ = td_update_bytes(B, T, A)
+    dom = max((k for k in flops), key=lambda k: kern.get(k, 0.0))
+    dom_ms = kern.get(dom, float("nan"))
+    achieved = flops[dom] / (dom_ms * 1e-3) / 1e12
+    out = {
+        "metric": "agent-transitions/sec for TD update fwd+bwd (whole node)",
+        "value": value,
+        "unit": "agent-transitions/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (SURVEY.md §8 d distributions, seeded per rank, resident in HBM)",
+        "config": {"workload": "configs[2]: full TD update fwd+bwd+Adam, 8 AGVs x 4 MEC, "
+                               f"batch {B} episodes/GPU x T={T}",
+                   "global_batch": B * world, "seq_len": T, "agents": A, "emb": 32, "heads": 3, "depth": 2,
+                   "parallelism": f"dp{world}"},
+        "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": PEAK_FP32_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
+                     "algorithmic_flops_per_launch": flops[dom],
+                     "algorithmic_bytes_per_launch": bytes_[dom],
+                     "avg_launch_ms": dom_ms},
+        "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items())},
+        "flops_per_transition": {"executed_algorithm": sum(flops.values()) / (B * T * A),
+                                 "reference_order": ref_order_flops_per_transition(A)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

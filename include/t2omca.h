@@ -165,11 +165,13 @@ int t2o_td_loss(const float* qtot, const float* qtot_tgt, const float* reward, i
 
 /* clip_grad_norm_(max_grad_norm) + Adam (torch.optim.Adam semantics, L2
  * weight decay) over n floats.  workspace: t2o_adam_workspace_floats() floats
- * (needed when max_grad_norm > 0).  grad_norm_out [1] may be NULL. */
+ * (needed when max_grad_norm > 0).  grad_div [1] (may be NULL): device scalar
+ * every grad is divided by first (the global Σ mask under data parallelism).
+ * grad_norm_out [1] may be NULL. */
 int t2o_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
                   float* workspace, int64_t n, double lr, double beta1, double beta2, float eps,
-                  float weight_decay, float max_grad_norm, int64_t step, float* grad_norm_out,
-                  void* stream);
+                  float weight_decay, float max_grad_norm, int64_t step, const float* grad_div,
+                  float* grad_norm_out, void* stream);
 int t2o_adam_workspace_floats(void);
 
 /* Sum nslab partial gradient slabs [nslab][n] into out[n] (out = sum, overwritten). */

@@ -111,6 +111,7 @@ struct AdamArgs {
   float* m;
   float* v;
   const float* part;  // NORM_BLOCKS partial Σ g² (null: no clipping)
+  const float* gdiv;  // [1] optional device divisor applied to every grad (data-parallel Σ mask)
   float* norm_out;    // [1] grad norm before clipping (may be null)
   int64_t n;
   float omb1, beta2, omb2, eps, weight_decay, max_norm;  // 1-β1, β2, 1-β2 (rounded from double)
@@ -119,12 +120,13 @@ struct AdamArgs {
 };
 
 __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
-  float coef = 1.f;
+  const float inv = a.gdiv ? 1.0f / a.gdiv[0] : 1.0f;
+  float coef = inv;
   if (a.part) {
     float s = 0.f;
     for (int i = 0; i < NORM_BLOCKS; ++i) s += a.part[i];
-    const float norm = sqrtf(s);
-    coef = fminf(a.max_norm / (norm + 1e-6f), 1.0f);
+    const float norm = sqrtf(s) * inv;
+    coef = inv * fminf(a.max_norm / (norm + 1e-6f), 1.0f);
     if (a.norm_out && blockIdx.x == 0 && threadIdx.x == 0) a.norm_out[0] = norm;
   }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -157,8 +159,8 @@ extern "C" int t2o_td_loss(const float* qtot, const float* qtot_tgt, const float
 
 extern "C" int t2o_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,
                              float* workspace, int64_t n, double lr, double beta1, double beta2, float eps,
-                             float weight_decay, float max_grad_norm, int64_t step, float* grad_norm_out,
-                             void* stream) {
+                             float weight_decay, float max_grad_norm, int64_t step, const float* grad_div,
+                             float* grad_norm_out, void* stream) {
   if (!params || !grads || !exp_avg || !exp_avg_sq || n < 1 || step < 1) return T2O_EINVAL;
   if (max_grad_norm > 0.f && !workspace) return T2O_EINVAL;
   AdamArgs a{};
@@ -178,6 +180,7 @@ extern "C" int t2o_adam_step(float* params, const float* grads, float* exp_avg, 
   a.step_size = (float)(lr / bc1);
   a.bc2_sqrt = (float)sqrt(bc2);
   a.norm_out = grad_norm_out;
+  a.gdiv = grad_div;
   hipStream_t s = (hipStream_t)stream;
   if (max_grad_norm > 0.f) {
     hipLaunchKernelGGL(sqnorm_partials, dim3(NORM_BLOCKS), dim3(256), 0, s, grads, n, workspace);

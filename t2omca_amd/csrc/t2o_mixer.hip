@@ -318,8 +318,8 @@ __global__ __launch_bounds__(128) void mixer_bwd_kernel(MixerBwdArgs args) {
       }
       for (int i = Dm::Q * E + lane; i < Dm::OUTF; i += 64) OUT[i] = 0.f;
       __builtin_amdgcn_wave_barrier();
-      // ---- blocks backward per query tile
-#pragma unroll
+      // ---- blocks backward per query tile (body too large to unroll; qt only moves addresses)
+#pragma unroll 1
       for (int qt = 0; qt < Dm::QT; ++qt) {
         const int q = 16 * qt + c;
         f4 gx[ET];

@@ -1,0 +1,184 @@
+"""GPU TD update with the reference driver's learner contract.
+
+per_run.py:224-238 calls
+
+    info = learner.train(episode_sample, runner.t_env, episode, weights)
+    buffer.update_priorities(idx, (info["td_errors_abs"].flatten() + 1e-6).numpy().tolist())
+
+The reference's learner module is absent, so the semantics are
+the PyMARL2 NQLearner ones (oracle/ref_learner.py restates them on the CPU;
+parity-unpinned beyond the agent/mixer arithmetic).  One ``train`` call is a
+fixed sequence of HIP launches on the current stream (no host sync until the
+priorities are copied out):
+
+  pack(online agent, online mixer)                 t2o_pack_params x2
+  agent unroll fwd, online + target, t = 0..T      t2o_agent_unroll_fwd (1 launch)
+  mixer unroll fwd, online (chosen Q, t < T) +
+        target (double-Q, t <= T)                  t2o_mixer_unroll_fwd (1 launch)
+  TD(λ) targets, loss, dL/dQtot, priorities        t2o_td_loss
+  mixer BPTT -> dL/dq_chosen, dL/dhidden           t2o_mixer_unroll_bwd + slab reduce
+  agent BPTT                                       t2o_agent_unroll_bwd + slab reduce
+  unfold grads into the reference parameter order  t2o_unpack_grads x2
+  [data parallel: one all_reduce of the flat grad + Σ mask over RCCL]
+  clip_grad_norm_ + Adam                           t2o_adam_step
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from . import ops
+
+
+def _bind_flat(modules, device):
+    """Move the modules' parameters into one flat fp32 buffer (views)."""
+    params = [p for m in modules for p in m.parameters()]
+    n = sum(p.numel() for p in params)
+    flat = torch.empty(n, device=device, dtype=torch.float32)
+    off = 0
+    for p in params:
+        k = p.numel()
+        flat[off:off + k].copy_(p.detach().reshape(-1))
+        p.data = flat[off:off + k].view_as(p)
+        off += k
+    return flat
+
+
+class TDLearner:
+    def __init__(self, agent, mixer, *, lr=1e-3, gamma=0.99, td_lambda=0.6, grad_norm_clip=10.0,
+                 target_update_interval=200, optim_betas=(0.9, 0.999), optim_eps=1e-8, weight_decay=0.0,
+                 detach_mixer_hidden=False, process_group=None, priorities_to_cpu=True):
+        dev = next(agent.parameters()).device
+        if dev.type != "cuda":
+            raise RuntimeError("TDLearner needs the modules on a HIP device (no CPU fallback)")
+        self.agent, self.mixer = agent, mixer
+        self.sa, self.sm = agent.shape, mixer.shape
+        self.na, self.nm = self.sa.n_params, self.sm.n_params
+        assert self.na == sum(p.numel() for p in agent.parameters())
+        assert self.nm == sum(p.numel() for p in mixer.parameters())
+        self.device = dev
+        self.params = _bind_flat([agent, mixer], dev)
+        self.grad = torch.zeros(self.na + self.nm + 1, device=dev)  # last slot: Σ mask
+        self.exp_avg = torch.zeros_like(self.params)
+        self.exp_avg_sq = torch.zeros_like(self.params)
+        self.target_params = self.params.clone()
+        self.adam_ws = torch.empty(int(ops.lib().t2o_adam_workspace_floats()), device=dev)
+        self.grad_norm = torch.zeros(1, device=dev)
+        self.lr, self.betas, self.eps, self.wd = lr, optim_betas, optim_eps, weight_decay
+        self.gamma, self.td_lambda, self.clip = gamma, td_lambda, grad_norm_clip
+        self.target_update_interval = target_update_interval
+        self.detach_mixer_hidden = detach_mixer_hidden
+        self.pg = process_group
+        self.priorities_to_cpu = priorities_to_cpu
+        self.step_count = 0
+        self.last_target_update_episode = 0
+        self.timer = None   # optional callable(tag) recording HIP events around the big kernels
+        self.pack_a = torch.empty(self.sa.layout().total, device=dev)
+        self.pack_m = torch.empty(self.sm.layout().total, device=dev)
+        self.pack_at = torch.empty_like(self.pack_a)
+        self.pack_mt = torch.empty_like(self.pack_m)
+        self._pack_targets()
+        self._slabs = {}
+
+    # -- parameters --------------------------------------------------------
+    def agent_params(self, target=False):
+        src = self.target_params if target else self.params
+        return src[:self.na]
+
+    def mixer_params(self, target=False):
+        src = self.target_params if target else self.params
+        return src[self.na:]
+
+    def _pack_targets(self):
+        ops.pack_params(self.sa, self.target_params[:self.na], self.pack_at)
+        ops.pack_params(self.sm, self.target_params[self.na:], self.pack_mt)
+
+    def update_targets(self):
+        self.target_params.copy_(self.params)
+        self._pack_targets()
+
+    def _world(self):
+        if self.pg is not None or (dist.is_available() and dist.is_initialized()):
+            return dist.get_world_size(self.pg)
+        return 1
+
+    def _slab(self, key, n):
+        t = self._slabs.get(key)
+        if t is None or t.numel() < n:
+            t = torch.empty(n, device=self.device)
+            self._slabs[key] = t
+        return t
+
+    # -- the TD update -------------------------------------------------------
+    def train(self, batch, t_env=0, episode_num=0, per_weight=None):
+        obs = batch["obs"]
+        state = batch["state"]
+        actions = batch["actions"]
+        avail = batch["avail_actions"]
+        B, T1, A, _ = obs.shape
+        T = T1 - 1
+        dev = self.device
+        if avail.dtype != torch.int32:
+            avail = avail.int()
+        act = actions[..., 0] if actions.dim() == 4 else actions
+        if act.dtype != torch.int64:
+            act = act.long()
+        if act.stride(2) != 1:
+            act = act.contiguous()
+        reward = batch["reward"][:, :, 0]
+        term = batch["terminated"][:, :, 0].float()
+        filled = batch["filled"][:, :, 0].float() if "filled" in _keys(batch) else None
+        w = None
+        if per_weight is not None:
+            w = torch.as_tensor(np.asarray(per_weight) if not torch.is_tensor(per_weight) else per_weight,
+                                dtype=torch.float32).to(dev).reshape(B).contiguous()
+
+        ops.pack_params(self.sa, self.params[:self.na], self.pack_a)
+        ops.pack_params(self.sm, self.params[self.na:], self.pack_m)
+        # 1. agents: online + target over t = 0..T
+        q_on, h_on, q_tg, h_tg = ops.agent_unroll_fwd(self.sa, self.pack_a, obs, pack_tg=self.pack_at,
+                                                      timer=self.timer)
+        # 2. mixers: online on chosen Q (t < T), target on double-Q (t <= T)
+        o_on, o_tg = ops.mixer_unroll_fwd(self.sm, self.pack_m, state, h_on, qmode_on=1, q_on=q_on,
+                                          actions=act, avail=avail, T_on=T, pack_tg=self.pack_mt,
+                                          hid_tg=h_tg, qmode_tg=2, q_tg=q_tg, T_tg=T1,
+                                          timer=self.timer)
+        # 3. TD(λ) targets / loss (un-normalised: Σ mask is applied in Adam so the
+        #    data-parallel sum over ranks divides by the GLOBAL Σ mask)
+        td = ops.td_loss(o_on["y"], o_tg["y"], reward, term, filled, w, gamma=self.gamma,
+                         td_lambda=self.td_lambda, mask_sum=1.0)
+        # 4. mixer BPTT
+        slabs_m = self._slab("m", int(ops.lib().t2o_mixer_bwd_max_slabs(B)) * self.sm.layout().grad_total)
+        gm, gqv, ghid, _ = ops.mixer_unroll_bwd(self.sm, self.pack_m, state, h_on, o_on, td["gq"], slabs=slabs_m,
+                                                timer=self.timer)
+        # 5. agent BPTT (grads of the chosen Q and, unless detached, of the hidden states)
+        slabs_a = self._slab("a", int(ops.lib().t2o_agent_bwd_max_slabs(B, A)) * self.sa.layout().grad_total)
+        ga, _ = ops.agent_unroll_bwd(self.sa, self.pack_a, obs, h_on, gchosen=gqv, actions=act,
+                                     gh=None if self.detach_mixer_hidden else ghid, slabs=slabs_a,
+                                     timer=self.timer)
+        # 6. grads in reference parameter order
+        self.grad.zero_()
+        ops.unpack_grads(self.sa, self.params[:self.na], ga, self.grad[:self.na])
+        ops.unpack_grads(self.sm, self.params[self.na:], gm, self.grad[self.na:self.na + self.nm])
+        self.grad[-1:].copy_(td["loss"][1:2])
+        if self._world() > 1:
+            dist.all_reduce(self.grad, group=self.pg)
+        # 7. clip + Adam
+        self.step_count += 1
+        ops.adam_step(self.params, self.grad[:-1], self.exp_avg, self.exp_avg_sq, self.step_count, lr=self.lr,
+                      betas=self.betas, eps=self.eps, weight_decay=self.wd, max_grad_norm=self.clip,
+                      workspace=self.adam_ws, grad_div=self.grad[-1:], grad_norm_out=self.grad_norm)
+        if (episode_num - self.last_target_update_episode) / self.target_update_interval >= 1.0:
+            self.update_targets()
+            self.last_target_update_episode = episode_num
+        prio = td["prio"]
+        info = {"td_errors_abs": prio.cpu() if self.priorities_to_cpu else prio,
+                "loss_sum": td["loss"][0:1], "mask_sum": td["loss"][1:2], "grad_norm": self.grad_norm,
+                "qtot": o_on["y"], "targets": td["targets"]}
+        return info
+
+
+def _keys(batch):
+    try:
+        return batch.keys()
+    except AttributeError:
+        return getattr(batch, "scheme", {}).keys()

@@ -82,7 +82,12 @@ def reduce_slabs(slabs, nslab, out):
     return out
 
 
-def agent_unroll_fwd(shape: NetShape, pack_on, obs, h0_on=None, pack_tg=None, h0_tg=None):
+def _mark(timer, tag):
+    if timer is not None:
+        timer(tag)
+
+
+def agent_unroll_fwd(shape: NetShape, pack_on, obs, h0_on=None, pack_tg=None, h0_tg=None, timer=None):
     """Unroll the agent over obs [B, T, A, n_ent*F] (any stride over B, T; inner
     [A, n_ent*F] contiguous).  Returns (q_on, h_on[, q_tg, h_tg]) with
     q [B, T, A, NA], h [B, T, A, E]."""
@@ -101,17 +106,19 @@ def agent_unroll_fwd(shape: NetShape, pack_on, obs, h0_on=None, pack_tg=None, h0
     for h0 in (h0_on, h0_tg):
         if h0 is not None:
             assert h0.is_contiguous() and h0.numel() == B * A * shape.E
+    _mark(timer, "begin:agent_fwd")
     check(lib().t2o_agent_unroll_fwd(ctypes.byref(L), ptr(pack_on), ptr(pack_tg), ptr(obs),
                                      obs.stride(0), obs.stride(1), ptr(h0_on), ptr(h0_tg),
                                      ptr(q_on), ptr(h_on), ptr(q_tg), ptr(h_tg), B, T, A,
                                      stream_ptr()), "agent_unroll_fwd")
+    _mark(timer, "end:agent_fwd")
     if pack_tg is not None:
         return q_on, h_on, q_tg, h_tg
     return q_on, h_on
 
 
 def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchosen=None, actions=None,
-                     gh=None, want_gh0=False, slabs=None):
+                     gh=None, want_gh0=False, slabs=None, timer=None):
     """BPTT of agent_unroll_fwd over the first T = len(grads) steps.
 
     obs [B, >=T, A, nF]; h_seq [B, Ts>=T, A, E] (forward output); gq [B,T,A,NA],
@@ -133,11 +140,13 @@ def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchose
         slabs = torch.empty(nmax * L.grad_total, device=obs.device)
     gh0 = torch.empty(B, A, shape.E, device=obs.device) if want_gh0 else None
     nslab = ctypes.c_int(0)
+    _mark(timer, "begin:agent_bwd")
     check(lib().t2o_agent_unroll_bwd(ctypes.byref(L), ptr(pack), ptr(obs), obs.stride(0), obs.stride(1),
                                      ptr(h0), ptr(h_seq), h_seq.shape[1], ptr(gq), ptr(gchosen),
                                      ptr(actions), act_sb, act_st, ptr(gh), ptr(slabs), nmax,
                                      ctypes.byref(nslab), ptr(gh0), B, T, A, stream_ptr()),
           "agent_unroll_bwd")
+    _mark(timer, "end:agent_bwd")
     gpack = torch.empty(L.grad_total, device=obs.device)
     reduce_slabs(slabs, nslab.value, gpack)
     return gpack, gh0
@@ -150,7 +159,7 @@ def _mstrides(t):
 def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv_on=None, q_on=None,
                      actions=None, avail=None, hw0_on=None, T_on=None,
                      pack_tg=None, hid_tg=None, qmode_tg=2, qv_tg=None, q_tg=None, hw0_tg=None,
-                     T_tg=None, want_xout=True):
+                     T_tg=None, want_xout=True, timer=None):
     """Mixer unroll (see include/t2omca.h).  states [B, >=T, n_ent*F];
     hid_* [B, >=T, A, E] (contiguous inner [A, E]); q_on/q_tg [B, q_ts, A, NA]
     contiguous; actions int64 [B, >=T, A]; avail int32 [B, >=T, A, NA].
@@ -186,6 +195,7 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
     act_sb, act_st = _mstrides(actions)
     av_sb, av_st = _mstrides(avail)
     g = lambda d, k: ptr(d[k]) if d is not None else None  # noqa: E731
+    _mark(timer, "begin:mixer_fwd")
     check(lib().t2o_mixer_unroll_fwd(
         ctypes.byref(L), ptr(pack_on), ptr(pack_tg), ptr(states), states.stride(0), states.stride(1),
         ptr(hid_on), ptr(hid_tg), hid_on.stride(0), hid_on.stride(1), ptr(hw0_on), ptr(hw0_tg),
@@ -194,11 +204,12 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
         g(o_on, "y"), g(o_on, "hw"), g(o_on, "qv"), g(o_on, "xout"),
         g(o_tg, "y"), g(o_tg, "hw"), g(o_tg, "qv"), g(o_tg, "xout"),
         B, T_on, T_tg or 0, stream_ptr()), "mixer_unroll_fwd")
+    _mark(timer, "end:mixer_fwd")
     return (o_on, o_tg) if pack_tg is not None else o_on
 
 
 def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_ext=None,
-                     want_ghw0=False, slabs=None):
+                     want_ghw0=False, slabs=None, timer=None):
     """BPTT of mixer_unroll_fwd (one network, `fwd` = its output dict).
     Returns (gpack, gqv [B,T,A], ghid [B,T,A,E], ghw0 or None)."""
     _dev(pack, states, hid, gy, hw0, ghw_ext)
@@ -214,11 +225,13 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
     ghid = torch.empty(B, T, A, E, device=dev)
     ghw0 = torch.empty(B, 3, E, device=dev) if want_ghw0 else None
     nslab = ctypes.c_int(0)
+    _mark(timer, "begin:mixer_bwd")
     check(lib().t2o_mixer_unroll_bwd(
         ctypes.byref(L), ptr(pack), ptr(states), states.stride(0), states.stride(1), ptr(hid),
         hid.stride(0), hid.stride(1), ptr(hw0), ptr(fwd["qv"]), ptr(fwd["hw"]), ptr(fwd["xout"]),
         ptr(gy), ptr(ghw_ext), ptr(gqv), ptr(ghid), ptr(ghw0), ptr(slabs), nmax, ctypes.byref(nslab),
         B, T, stream_ptr()), "mixer_unroll_bwd")
+    _mark(timer, "end:mixer_bwd")
     gpack = torch.empty(L.grad_total, device=dev)
     reduce_slabs(slabs, nslab.value, gpack)
     return gpack, gqv, ghid, ghw0
@@ -244,13 +257,15 @@ def td_loss(qtot, qtot_tgt, reward, terminated=None, filled=None, per_weight=Non
 
 
 def adam_step(params, grads, exp_avg, exp_avg_sq, step, *, lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
-              weight_decay=0.0, max_grad_norm=10.0, workspace=None, grad_norm_out=None):
-    """In-place clip_grad_norm_ + Adam on flat fp32 buffers."""
-    _dev(params, grads, exp_avg, exp_avg_sq, workspace, grad_norm_out)
+              weight_decay=0.0, max_grad_norm=10.0, workspace=None, grad_div=None, grad_norm_out=None):
+    """In-place clip_grad_norm_ + Adam on flat fp32 buffers (grads divided by the
+    device scalar grad_div first, if given)."""
+    _dev(params, grads, exp_avg, exp_avg_sq, workspace, grad_div, grad_norm_out)
     n = params.numel()
     if workspace is None:
         workspace = torch.empty(int(lib().t2o_adam_workspace_floats()), device=params.device)
     check(lib().t2o_adam_step(ptr(params), ptr(grads), ptr(exp_avg), ptr(exp_avg_sq), ptr(workspace), n,
                               float(lr), float(betas[0]), float(betas[1]), float(eps),
-                              float(weight_decay), float(max_grad_norm), int(step), ptr(grad_norm_out),
+                              float(weight_decay), float(max_grad_norm), int(step), ptr(grad_div),
+                              ptr(grad_norm_out),
                               stream_ptr()), "adam_step")

@@ -1,0 +1,76 @@
+"""Algorithmic FLOP / byte counts of the kernels' algorithm (for roofline lines).
+
+Counts the arithmetic the fused kernels are required to do by their algorithm
+(token-pruned, folded projections, observation-space agent attention; see
+DESIGN.md §3), not what the MFMA tiles pad it to, and excluding the backward's
+forward recompute.  A multiply-add is 2 FLOPs; softmax exp/div and LayerNorm
+count ~5 FLOPs per element.
+
+SURVEY.md §8(d) also quotes the reference-association-order counts
+(1.793 / 2.608 / 7.833 MFLOP per agent-transition at A = 8 / 16 / 64);
+``ref_order_flops_per_transition`` reproduces that formula so bench.py can
+report both.  Rooflines are always priced against the executed algorithm.
+"""
+
+
+def agent_row_step_flops(E=32, H=3, D=2, F=9, n=8, NA=5, FF=None):
+    FF = FF or 4 * E
+    HE = H * E
+    blk = (2 * HE * E            # u = M x
+           + H * 2 * F * E       # w_h = We^T u_h
+           + H * 4 * E           # c_h, s_h0
+           + H * n * 2 * F       # entity scores
+           + H * (n + 1) * 5     # softmax
+           + H * n * 2 * F       # ô_h
+           + H * (2 * E * F + 4 * E)  # z_h
+           + 2 * E * HE          # N z
+           + 2 * 2 * FF * E      # FFN
+           + 2 * 8 * E)          # residuals + 2 LayerNorms
+    return D * blk + 2 * NA * E
+
+
+def mixer_episode_step_flops(E=32, H=3, D=2, A=8, Fs=8, FF=None):
+    FF = FF or 4 * E
+    HE = H * E
+    Lk, Q = 2 * A + 3, A + 3
+    row_blk = (2 * HE * E + H * 2 * Lk * E + H * Lk * 5 + H * 2 * Lk * E + 2 * E * HE + 2 * 2 * FF * E + 2 * 8 * E)
+    embed = A * 2 * Fs * E
+    head = A * 3 * E + 6 * E
+    return D * Q * row_blk + embed + head
+
+
+def td_update_flops(B, T, A, E=32, H=3, D=2, F=9, Fs=8, NA=5):
+    """Per-kernel algorithmic FLOPs of one TD update (fwd online+target, bwd = 2x fwd)."""
+    fa = agent_row_step_flops(E, H, D, F, A, NA)
+    fm = mixer_episode_step_flops(E, H, D, A, Fs)
+    return {
+        "agent_fwd": 2 * B * (T + 1) * A * fa,
+        "mixer_fwd": (B * T + B * (T + 1)) * fm,
+        "mixer_bwd": 2 * B * T * fm,
+        "agent_bwd": 2 * B * T * A * fa,
+    }
+
+
+def td_update_bytes(B, T, A, E=32, F=9, Fs=8, NA=5):
+    """Compulsory HBM bytes per kernel (fp32 inputs read / outputs written once)."""
+    obs = B * (T + 1) * A * A * F * 4
+    st = B * (T + 1) * A * Fs * 4
+    qh = B * (T + 1) * A * (NA + E) * 4
+    return {
+        "agent_fwd": obs + 2 * qh,
+        "mixer_fwd": st + 2 * qh + 2 * B * (T + 1) * ((A + 3) * E + 3 * E + A + 1) * 4,
+        "mixer_bwd": st + B * T * ((A + 3) * E + 3 * E + 2 * A + A * E + 2) * 4,
+        "agent_bwd": obs + B * T * A * (2 * E + 2) * 4,
+    }
+
+
+def ref_order_flops_per_transition(A, E=32, H=3, D=2, F=9, Fs=8, NA=5, FF=None):
+    """SURVEY.md §8(d) formula: 4*F_agent + 4*F_mixer/A (reference association order)."""
+    FF = FF or 4 * E
+    HE = H * E
+    La, Lm, Lq = A + 1, 2 * A + 3, A + 3
+    f_agent = 2 * A * F * E + D * (4 * La * E * HE + 2 * E * HE + 4 * H * La * E + 2 * HE * E + 4 * E * FF) \
+        + 2 * E * NA
+    f_mixer = 2 * A * Fs * E + D * (4 * Lm * E * HE + 2 * Lq * E * HE + 4 * H * Lq * Lm * E
+                                    + 2 * Lq * HE * E + 4 * Lq * E * FF)
+    return 4 * f_agent + 4 * f_mixer / A
