@@ -90,16 +90,18 @@ int t2o_unpack_grads(const t2o_layout* L, const float* params, const float* gpac
 /* Agent unroll forward over T steps for up to two networks sharing the
  * observations (online + target).  obs[b][t][a][n_ent*F] with element strides
  * obs_sb, obs_st (a-stride = n_ent*F).  h0 may be NULL (zeros, init_hidden).
- * Outputs q[b][t][a][NA], h[b][t][a][E] (h after step t).  pack_tg/q_tg/h_tg
- * may be NULL to run one network. */
+ * Outputs q[b][t][a][NA], h[b][t][a][E] (h after step t) and, if non-NULL,
+ * hmid[b][t][D-1][a][E] (inputs of blocks 1..D-1, lets the backward skip
+ * recomputing them).  pack_tg/q_tg/h_tg/hmid_tg may be NULL to run one network. */
 int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, const float* pack_tg,
                          const float* obs, int64_t obs_sb, int64_t obs_st,
                          const float* h0_on, const float* h0_tg,
-                         float* q_on, float* h_on, float* q_tg, float* h_tg,
-                         int B, int T, int A, void* stream);
+                         float* q_on, float* h_on, float* hmid_on, float* q_tg, float* h_tg,
+                         float* hmid_tg, int B, int T, int A, void* stream);
 
 /* Agent BPTT over steps T-1..0 of one network.  h_seq = forward h output
- * [b][h_ts][a][E] (h_ts >= T), h0 as in the forward (NULL = zeros).  External
+ * [b][h_ts][a][E] (h_ts >= T), hmid = forward hmid [b][h_ts][D-1][a][E] or
+ * NULL, h0 as in the forward (NULL = zeros).  External
  * grads of the T steps: gq[b][t][a][NA] (may be NULL) plus, if gchosen != NULL,
  * gchosen[b][t][a] routed to q[action] (actions int64 [b][t][a] with element
  * strides act_sb, act_st, a-stride 1); gh[b][t][a][E] (may be NULL).
@@ -108,7 +110,7 @@ int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, const float*
  * t2o_agent_bwd_max_slabs(B, A)); gh0[b][a][E] = dL/dh0 (may be NULL). */
 int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack,
                          const float* obs, int64_t obs_sb, int64_t obs_st,
-                         const float* h0, const float* h_seq, int h_ts,
+                         const float* h0, const float* h_seq, const float* hmid, int h_ts,
                          const float* gq, const float* gchosen, const int64_t* actions,
                          int64_t act_sb, int64_t act_st, const float* gh,
                          float* gslabs, int max_slabs, int* nslab, float* gh0,
@@ -126,7 +128,9 @@ int t2o_agent_bwd_max_slabs(int B, int A);
  * strides av_sb, av_st; NULL = all available), ties -> lowest index.
  * Outputs per network: y[B][T], hw[B][T][3][E] (hyper tokens after step t),
  * qvo[B][T][A] (qvals used, may be NULL), xout[B][T][A+3][E] (final query
- * rows, may be NULL; required by the backward). */
+ * rows, may be NULL; required by the backward), xmid[B][T][D-1][A+3][E]
+ * (inputs of blocks 1..D-1, may be NULL; lets the backward skip recomputing
+ * them). */
 int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, const float* pack_tg,
                          const float* states, int64_t st_sb, int64_t st_st,
                          const float* hid_on, const float* hid_tg, int64_t hid_sb, int64_t hid_st,
@@ -134,19 +138,19 @@ int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, const float*
                          const float* qv_on, const float* qv_tg, const float* q_on, const float* q_tg,
                          int q_ts, int n_actions, const int64_t* actions, int64_t act_sb, int64_t act_st,
                          const int32_t* avail, int64_t av_sb, int64_t av_st,
-                         float* y_on, float* hw_on, float* qvo_on, float* xout_on,
-                         float* y_tg, float* hw_tg, float* qvo_tg, float* xout_tg,
+                         float* y_on, float* hw_on, float* qvo_on, float* xout_on, float* xmid_on,
+                         float* y_tg, float* hw_tg, float* qvo_tg, float* xout_tg, float* xmid_tg,
                          int B, int T_on, int T_tg, void* stream);
 
 /* Mixer BPTT over steps T-1..0 of one network.  qv = forward qvo [B][T][A],
- * hw / xout = forward outputs.  gy[B][T] = dL/dy; ghw_ext [B][T][3][E] optional
+ * hw / xout / xmid = forward outputs (xmid may be NULL).  gy[B][T] = dL/dy; ghw_ext [B][T][3][E] optional
  * extra grad on the hyper outputs.  Outputs: gqv[B][T][A] (dL/dqvals),
  * ghid[B][T][A][E] (dL/dhidden states), ghw0[B][3][E] (may be NULL), partial
  * weight-grad slabs as for the agent (max_slabs = t2o_mixer_bwd_max_slabs(B)). */
 int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, const float* states,
                          int64_t st_sb, int64_t st_st, const float* hid, int64_t hid_sb,
                          int64_t hid_st, const float* hw0, const float* qv, const float* hw,
-                         const float* xout, const float* gy, const float* ghw_ext, float* gqv,
+                         const float* xout, const float* xmid, const float* gy, const float* ghw_ext, float* gqv,
                          float* ghid, float* ghw0, float* gslabs, int max_slabs, int* nslab,
                          int B, int T, void* stream);
 int t2o_mixer_bwd_max_slabs(int B);

@@ -33,10 +33,10 @@ EXPORTS = {
     "t2o_reduce_slabs": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
                                         ctypes.c_void_p, ctypes.c_void_p]),
     "t2o_agent_unroll_fwd": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_void_p] * 3 +
-                             [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 6 + [ctypes.c_int] * 3 +
+                             [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 8 + [ctypes.c_int] * 3 +
                              [ctypes.c_void_p]),
     "t2o_agent_unroll_bwd": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_void_p] * 2 +
-                             [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 2 + [ctypes.c_int] +
+                             [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 3 + [ctypes.c_int] +
                              [ctypes.c_void_p] * 3 + [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 2 +
                              [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_void_p] +
                              [ctypes.c_int] * 3 + [ctypes.c_void_p]),
@@ -45,11 +45,11 @@ EXPORTS = {
                              [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 2 + [ctypes.c_int64] * 2 +
                              [ctypes.c_void_p] * 2 + [ctypes.c_int] * 2 + [ctypes.c_void_p] * 4 +
                              [ctypes.c_int] * 2 + [ctypes.c_void_p] + [ctypes.c_int64] * 2 +
-                             [ctypes.c_void_p] + [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 8 +
+                             [ctypes.c_void_p] + [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 10 +
                              [ctypes.c_int] * 3 + [ctypes.c_void_p]),
     "t2o_mixer_unroll_bwd": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_void_p] * 2 +
                              [ctypes.c_int64] * 2 + [ctypes.c_void_p] + [ctypes.c_int64] * 2 +
-                             [ctypes.c_void_p] * 10 + [ctypes.c_int, ctypes.POINTER(ctypes.c_int)] +
+                             [ctypes.c_void_p] * 11 + [ctypes.c_int, ctypes.POINTER(ctypes.c_int)] +
                              [ctypes.c_int] * 2 + [ctypes.c_void_p]),
     "t2o_mixer_bwd_max_slabs": (ctypes.c_int, [ctypes.c_int]),
     "t2o_td_loss": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_int64] * 2 + [ctypes.c_void_p] +
@@ -59,6 +59,7 @@ EXPORTS = {
     "t2o_adam_step": (ctypes.c_int, [ctypes.c_void_p] * 5 + [ctypes.c_int64] + [ctypes.c_double] * 3 +
                       [ctypes.c_float] * 3 + [ctypes.c_int64] + [ctypes.c_void_p] * 3),
     "t2o_adam_workspace_floats": (ctypes.c_int, []),
+    "t2o_probe_lane_ops": (ctypes.c_int, [ctypes.c_void_p] * 3),
 }
 
 _lib = None

@@ -20,6 +20,7 @@ struct AgentNet {
   const float* h0;
   float* q;
   float* h;
+  float* hmid;  // [B][T][D-1][A][E] inputs of blocks 1..D-1 (may be null)
 };
 
 struct AgentFwdArgs {
@@ -64,7 +65,14 @@ __global__ __launch_bounds__(256) void agent_fwd_kernel(AgentFwdArgs args) {
 #pragma unroll
     for (int t = 0; t < ET; ++t) x[t] = h[t];
 #pragma unroll
-    for (int d = 0; d < D; ++d) agent_block_fwd<E, H, NE, FF, false>(P, L, d, h, o, x, nullptr);
+    for (int d = 0; d < D; ++d) {
+      if (d > 0 && net.hmid && valid) {
+        float* hm = net.hmid + ((((size_t)b * args.T + step) * (D - 1) + d - 1) * A + a) * E;
+#pragma unroll
+        for (int t = 0; t < ET; ++t) st4(hm + 16 * t + 4 * g, x[t]);
+      }
+      agent_block_fwd<E, H, NE, FF, false>(P, L, d, h, o, x, nullptr);
+    }
     f4 q = zero4();
 #pragma unroll
     for (int i = 0; i < ET; ++i) q = mma_tile(P + L.Wo, E, 0, i, x[i], q);
@@ -109,6 +117,7 @@ struct AgentBwdArgs {
   int64_t obs_sb, obs_st;
   const float* h0;
   const float* h_seq;
+  const float* hmid;  // forward hmid [B][h_ts][D-1][A][E] (may be null)
   int h_ts;
   const float* gq;
   const float* gchosen;
@@ -121,8 +130,10 @@ struct AgentBwdArgs {
   int lds_grad;  // floats reserved for the gradient block (>= G.grad_total)
 };
 
+constexpr int AG_BWD_WAVES = 2;  // 32 sequences per workgroup: B*A/32 workgroups cover every CU
+
 template <int E, int H, int D, int NE, int FF>
-__global__ __launch_bounds__(256) void agent_bwd_kernel(AgentBwdArgs args) {
+__global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdArgs args) {
   constexpr int ET = E / 16;
   constexpr int STAGE = StageDims<ET>::FLOATS;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -130,12 +141,12 @@ __global__ __launch_bounds__(256) void agent_bwd_kernel(AgentBwdArgs args) {
   const t2o_layout& G = args.G;
   float* lg = smem;
   float* stage = smem + args.lds_grad + wave_id() * STAGE;
-  for (int i = threadIdx.x; i < args.lds_grad; i += 256) lg[i] = 0.f;
+  for (int i = threadIdx.x; i < args.lds_grad; i += blockDim.x) lg[i] = 0.f;
   __syncthreads();
 
   const int A = args.A, F = args.F, T = args.T;
   const int R = args.B * A;
-  const int rt = blockIdx.x * 4 + wave_id();
+  const int rt = blockIdx.x * AG_BWD_WAVES + wave_id();
   const int c = lane_c(), g = lane_g();
   const int row_raw = rt * 16 + c;
   const bool valid = row_raw < R;
@@ -188,18 +199,27 @@ __global__ __launch_bounds__(256) void agent_bwd_kernel(AgentBwdArgs args) {
 #pragma unroll
         for (int t = 0; t < ET; ++t) gx[t] = zero4();
       }
-      // forward recompute of blocks 0..D-2 (inputs kept)
+      // inputs of every block: stored by the forward, else recomputed
       f4 xs[D][ET];
 #pragma unroll
       for (int t = 0; t < ET; ++t) xs[0][t] = h[t];
+      if (args.hmid) {
 #pragma unroll
-      for (int d = 0; d + 1 < D; ++d) {
-        f4 x[ET];
+        for (int d = 1; d < D; ++d) {
+          const float* hm = args.hmid + ((((size_t)b * args.h_ts + step) * (D - 1) + d - 1) * A + a) * E;
 #pragma unroll
-        for (int t = 0; t < ET; ++t) x[t] = xs[d][t];
-        agent_block_fwd<E, H, NE, FF, false>(P, L, d, h, o, x, nullptr);
+          for (int t = 0; t < ET; ++t) xs[d][t] = ld4(hm + 16 * t + 4 * g);
+        }
+      } else {
 #pragma unroll
-        for (int t = 0; t < ET; ++t) xs[d + 1][t] = x[t];
+        for (int d = 0; d + 1 < D; ++d) {
+          f4 x[ET];
+#pragma unroll
+          for (int t = 0; t < ET; ++t) x[t] = xs[d][t];
+          agent_block_fwd<E, H, NE, FF, false>(P, L, d, h, o, x, nullptr);
+#pragma unroll
+          for (int t = 0; t < ET; ++t) xs[d + 1][t] = x[t];
+        }
       }
       f4 gh_in[ET], gbe[ET];
 #pragma unroll
@@ -211,6 +231,7 @@ __global__ __launch_bounds__(256) void agent_bwd_kernel(AgentBwdArgs args) {
 #pragma unroll
         for (int t = 0; t < ET; ++t) x[t] = xs[d][t];
         agent_block_fwd<E, H, NE, FF, true>(P, L, d, h, o, x, &cache);
+        T2O_FENCE();
         if (d == D - 1) {  // q = Wo x + bo
           dw_accumulate<1, ET>(lg + G.Wo, E, &gq, x, stage);
           vec_accumulate<1>(lg + G.bo, &gq);
@@ -219,7 +240,9 @@ __global__ __launch_bounds__(256) void agent_bwd_kernel(AgentBwdArgs args) {
 #pragma unroll
           for (int t = 0; t < ET; ++t) gx[t] += t1[t];
         }
+        T2O_FENCE();
         agent_block_bwd<E, H, NE, FF>(P, L, G, lg, stage, d, h, o, cache, gx, gh_in, gbe);
+        T2O_FENCE();
       }
       vec_accumulate<ET>(lg + G.be, gbe);
 #pragma unroll
@@ -232,7 +255,7 @@ __global__ __launch_bounds__(256) void agent_bwd_kernel(AgentBwdArgs args) {
   }
   __syncthreads();
   float* slab = args.slabs + (size_t)blockIdx.x * G.grad_total;
-  for (int i = threadIdx.x; i < G.grad_total; i += 256) slab[i] = lg[i];
+  for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) slab[i] = lg[i];
 }
 
 template <int E, int H, int D, int NE, int FF>
@@ -240,14 +263,14 @@ int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream
   constexpr int ET = E / 16;
   const int R = args.B * args.A;
   const int tiles = (R + 15) / 16;
-  const int grid = (tiles + 3) / 4;
+  const int grid = (tiles + AG_BWD_WAVES - 1) / AG_BWD_WAVES;
   if (grid > max_slabs) return T2O_EINVAL;
   args.lds_grad = (int)((args.G.grad_total + 15) / 16 * 16);
-  const size_t lds = sizeof(float) * ((size_t)args.lds_grad + 4 * StageDims<ET>::FLOATS);
+  const size_t lds = sizeof(float) * ((size_t)args.lds_grad + AG_BWD_WAVES * StageDims<ET>::FLOATS);
   auto kern = agent_bwd_kernel<E, H, D, NE, FF>;
   if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(256), lds, stream, args);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * AG_BWD_WAVES), lds, stream, args);
   *nslab = grid;
   return (int)hipGetLastError();
 }
@@ -256,18 +279,18 @@ int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream
 
 extern "C" int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, const float* pack_tg,
                                     const float* obs, int64_t obs_sb, int64_t obs_st, const float* h0_on,
-                                    const float* h0_tg, float* q_on, float* h_on, float* q_tg, float* h_tg,
-                                    int B, int T, int A, void* stream) {
+                                    const float* h0_tg, float* q_on, float* h_on, float* hmid_on, float* q_tg,
+                                    float* h_tg, float* hmid_tg, int B, int T, int A, void* stream) {
   if (!L || L->kind != 0 || !pack_on || !obs || !q_on || !h_on || B < 1 || T < 1 || A < 1 ||
       L->n_ent != A)
     return T2O_EINVAL;
   AgentFwdArgs args{};
   args.L = *L;
-  args.net[0] = AgentNet{pack_on, h0_on, q_on, h_on};
+  args.net[0] = AgentNet{pack_on, h0_on, q_on, h_on, hmid_on};
   int nnet = 1;
   if (pack_tg) {
     if (!q_tg || !h_tg) return T2O_EINVAL;
-    args.net[1] = AgentNet{pack_tg, h0_tg, q_tg, h_tg};
+    args.net[1] = AgentNet{pack_tg, h0_tg, q_tg, h_tg, hmid_tg};
     nnet = 2;
   }
   args.obs = obs;
@@ -283,7 +306,7 @@ extern "C" int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, c
 }
 
 extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, const float* obs, int64_t obs_sb,
-                                    int64_t obs_st, const float* h0, const float* h_seq, int h_ts,
+                                    int64_t obs_st, const float* h0, const float* h_seq, const float* hmid, int h_ts,
                                     const float* gq, const float* gchosen, const int64_t* actions,
                                     int64_t act_sb, int64_t act_st, const float* gh, float* gslabs,
                                     int max_slabs, int* nslab, float* gh0, int B, int T, int A,
@@ -300,6 +323,7 @@ extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, cons
   args.obs_st = obs_st;
   args.h0 = h0;
   args.h_seq = h_seq;
+  args.hmid = hmid;
   args.h_ts = h_ts;
   args.gq = gq;
   args.gchosen = gchosen;
@@ -321,5 +345,5 @@ extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, cons
 
 extern "C" int t2o_agent_bwd_max_slabs(int B, int A) {
   const int tiles = (B * A + 15) / 16;
-  return (tiles + 3) / 4;
+  return (tiles + AG_BWD_WAVES - 1) / AG_BWD_WAVES;
 }

@@ -161,9 +161,11 @@ T2O_DEV void agent_block_bwd(const float* __restrict__ P, const t2o_layout& L, c
       gbe[t] += gc * uh[t];
     }
     dw_accumulate<ET, 1>(lg + G.We, 16, uh, &gw, stage);
+    T2O_FENCE();
   }
   // u = M x
   dw_accumulate<HET, ET>(lg + G.M[d], E, gu, c.post.x, stage);
+  T2O_FENCE();
   f4 gxp[ET];
   matvec<ET, HET>(P + L.MT[d], H * E, gu, gxp);
 #pragma unroll

@@ -19,7 +19,7 @@ struct PostCache {
   f4 xh1[ET];
   float rs1;
   f4 y[ET];
-  f4 f1[FT];   // W1 y + c1 (pre-ReLU)
+  f4 f1r[FT];  // relu(W1 y + c1); the ReLU mask is f1r > 0
   f4 xh2[ET];
   float rs2;
 };
@@ -58,7 +58,7 @@ T2O_DEV void post_fwd(const float* __restrict__ P, const t2o_layout& L, int d, c
 #pragma unroll
     for (int t = 0; t < HET; ++t) c->z[t] = z[t];
 #pragma unroll
-    for (int t = 0; t < FT; ++t) c->f1[t] = f1[t];
+    for (int t = 0; t < FT; ++t) c->f1r[t] = f1r[t];
     c->rs1 = rs1;
   }
   f4 xh2[ET];
@@ -88,23 +88,21 @@ T2O_DEV void post_bwd(const float* __restrict__ P, const t2o_layout& L, const t2
   }
   f4 gr2[ET];
   layernorm_bwd<ET>(gx, c.xh2, c.rs2, P + L.g2[d], gr2);
-  {  // r2 = W2 relu(f1) + c2 + y
-    f4 f1r[FT];
-#pragma unroll
-    for (int t = 0; t < FT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) f1r[t][r] = fmaxf(c.f1[t][r], 0.f);
-    dw_accumulate<ET, FT>(lg + G.W2[d], FF, gr2, f1r, stage);
-  }
+  T2O_FENCE();
+  // r2 = W2 relu(f1) + c2 + y
+  dw_accumulate<ET, FT>(lg + G.W2[d], FF, gr2, c.f1r, stage);
   vec_accumulate<ET>(lg + G.c2[d], gr2);
+  T2O_FENCE();
   f4 gf1[FT];
   matvec<FT, ET>(P + L.W2T[d], E, gr2, gf1);
 #pragma unroll
   for (int t = 0; t < FT; ++t)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) gf1[t][r] = c.f1[t][r] > 0.f ? gf1[t][r] : 0.f;
+    for (int r = 0; r < 4; ++r) gf1[t][r] = c.f1r[t][r] > 0.f ? gf1[t][r] : 0.f;
+  T2O_FENCE();
   dw_accumulate<FT, ET>(lg + G.W1[d], E, gf1, c.y, stage);
   vec_accumulate<FT>(lg + G.c1[d], gf1);
+  T2O_FENCE();
   f4 gy[ET];
   matvec<ET, FT>(P + L.W1T[d], FF, gf1, gy);
 #pragma unroll
@@ -117,10 +115,13 @@ T2O_DEV void post_bwd(const float* __restrict__ P, const t2o_layout& L, const t2
     vec_accumulate<ET>(lg + G.n1[d], gy);
   }
   layernorm_bwd<ET>(gy, c.xh1, c.rs1, P + L.g1[d], gres);
+  T2O_FENCE();
   // r1 = N z + b_U + x
   dw_accumulate<ET, HET>(lg + G.N[d], H * E, gres, c.z, stage);
   vec_accumulate<ET>(lg + G.bu[d], gres);
+  T2O_FENCE();
   matvec<HET, ET>(P + L.NT[d], E, gres, gz);
+  T2O_FENCE();
 }
 
 }  // namespace t2o

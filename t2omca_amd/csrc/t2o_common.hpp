@@ -34,6 +34,11 @@ T2O_DEV int wave_id() { return threadIdx.x >> 6; }
 
 T2O_DEV f4 zero4() { return f4{0.f, 0.f, 0.f, 0.f}; }
 
+// Scheduling fence: stops the machine scheduler from hoisting the (activation-
+// independent) weight loads of later stages above the current one, which
+// otherwise keeps every layer's weight fragments live at once and spills.
+#define T2O_FENCE() __builtin_amdgcn_sched_barrier(0)
+
 T2O_DEV f4 mfma4(float a, float b, f4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
 }
@@ -69,12 +74,12 @@ T2O_DEV f4 vec_t(const float* __restrict__ v, int t) { return ld4(v + 16 * t + 4
 // ---- cross-lane reductions -------------------------------------------------
 // Sum over the 4 lanes holding one row (c, c+16, c+32, c+48).  Additions are
 // commutative pairings, so all four lanes get bit-identical results.
-T2O_DEV float allsum4(float v) {
+T2O_DEV float allsum4_shfl(float v) {
   v += __shfl_xor(v, 16);
   v += __shfl_xor(v, 32);
   return v;
 }
-T2O_DEV float allmax4(float v) {
+T2O_DEV float allmax4_shfl(float v) {
   v = fmaxf(v, __shfl_xor(v, 16));
   v = fmaxf(v, __shfl_xor(v, 32));
   return v;
@@ -85,6 +90,47 @@ T2O_DEV float rowsum16(float v) {
   v += __shfl_xor(v, 2);
   v += __shfl_xor(v, 4);
   v += __shfl_xor(v, 8);
+  return v;
+}
+
+// gfx950 VALU cross-lane forms (no LDS crossbar round trip).
+// v_permlane16_swap: swaps rows 1,3 of the first operand with rows 0,2 of the
+// second; with both operands = v the two results hold (v[l], v[l^16]) in some
+// order, so their sum is the xor-16 pair sum.  permlane32_swap likewise for
+// the two 32-lane halves.
+T2O_DEV float xor16_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+T2O_DEV float xor32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+T2O_DEV float xor16_max(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+T2O_DEV float xor32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+T2O_DEV float allsum4_fast(float v) { return xor32_sum(xor16_sum(v)); }
+T2O_DEV float allmax4_fast(float v) { return xor32_max(xor16_max(v)); }
+// the kernels' 4-lane all-reduces (bit-identical in the 4 lanes of a row)
+T2O_DEV float allsum4(float v) { return allsum4_fast(v); }
+T2O_DEV float allmax4(float v) { return allmax4_fast(v); }
+
+// Sum over the 16 lanes of a row with DPP (VALU only); the total lands in the
+// row's last lane (c == 15) — other lanes hold partial sums.
+template <int CTRL, int BANK>
+T2O_DEV float dpp_shr(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, BANK, true));
+}
+T2O_DEV float rowsum16_fast(float v) {
+  v += dpp_shr<0x111, 0xF>(v);   // row_shr:1
+  v += dpp_shr<0x112, 0xF>(v);   // row_shr:2
+  v += dpp_shr<0x114, 0xE>(v);   // row_shr:4, banks 1..3
+  v += dpp_shr<0x118, 0xC>(v);   // row_shr:8, banks 2..3
   return v;
 }
 
@@ -200,17 +246,61 @@ T2O_DEV void dw_accumulate(float* __restrict__ ldsW, int ldw, const f4* dY, cons
   }
 }
 
+// Same contraction, accumulated into MFMA accumulator registers acc[o][i]
+// (a wave-private gradient block that stays in registers across calls).
+template <int OT, int IT>
+T2O_DEV void dw_accumulate_regs(f4 (&acc)[OT][IT], const f4* dY, const f4* X, float* stage) {
+  constexpr int NS = OT < IT ? OT : IT;
+  constexpr int LD = StageDims<NS>::LD;
+  float* st_full = stage;
+  float* st_tile = stage + 16 * LD;
+  const int c = lane_c(), g = lane_g();
+  if constexpr (IT <= OT) {
+#pragma unroll
+    for (int i = 0; i < IT; ++i) stage_tile(st_full, LD, 16 * i, X[i]);
+#pragma unroll
+    for (int o = 0; o < OT; ++o) {
+      stage_tile(st_tile, 16, 0, dY[o]);
+      float a[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) a[s] = st_tile[(4 * s + g) * 16 + c];
+#pragma unroll
+      for (int i = 0; i < IT; ++i)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[o][i] = mfma4(a[s], st_full[(4 * s + g) * LD + 16 * i + c], acc[o][i]);
+    }
+  } else {
+#pragma unroll
+    for (int o = 0; o < OT; ++o) stage_tile(st_full, LD, 16 * o, dY[o]);
+#pragma unroll
+    for (int i = 0; i < IT; ++i) {
+      stage_tile(st_tile, 16, 0, X[i]);
+      float bv[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) bv[s] = st_tile[(4 * s + g) * 16 + c];
+#pragma unroll
+      for (int o = 0; o < OT; ++o)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[o][i] = mfma4(st_full[(4 * s + g) * LD + 16 * o + c], bv[s], acc[o][i]);
+    }
+  }
+}
+
 // vec[16*NT] += Σ_rows v[row]  (T-layout input; one lane per group adds)
 template <int NT>
 T2O_DEV void vec_accumulate(float* __restrict__ ldsv, const f4* v) {
   const int c = lane_c(), g = lane_g();
+  float s[NT][4];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float s = rowsum16(v[t][r]);
-      if (c == 0) atomicAdd(ldsv + 16 * t + 4 * g + r, s);
-    }
+    for (int r = 0; r < 4; ++r) s[t][r] = rowsum16_fast(v[t][r]);  // total in lane c == 15
+  if (c == 15) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) atomicAdd(ldsv + 16 * t + 4 * g + r, s[t][r]);
+  }
 }
 
 }  // namespace t2o

@@ -29,6 +29,7 @@ struct MixerNet {
   float* hw;          // [B][T][3][E]
   float* qv;          // [B][T][A] (may be null)
   float* xout;        // [B][T][A+3][E] final query outputs (may be null)
+  float* xmid;        // [B][T][D-1][A+3][E] inputs of blocks 1..D-1 (may be null)
 };
 
 struct MixerFwdArgs {
@@ -176,8 +177,14 @@ __global__ __launch_bounds__(256) void mixer_fwd_kernel(MixerFwdArgs args) {
       for (int ft = 0; ft < ET; ++ft)
         x[ft] = q < Dm::Q ? ld4(X0 + (Dm::NS + q) * Dm::LDX + 16 * ft + 4 * g) : zero4();
 #pragma unroll
-      for (int d = 0; d < D; ++d)
+      for (int d = 0; d < D; ++d) {
+        if (d > 0 && n.xmid && q < Dm::Q) {
+          float* xm = n.xmid + ((((size_t)b * n.T + t) * (D - 1) + d - 1) * Dm::Q + q) * E;
+#pragma unroll
+          for (int ft = 0; ft < ET; ++ft) st4(xm + 16 * ft + 4 * g, x[ft]);
+        }
         mixer_block_fwd<E, H, Dm::KT, FF, Dm::LDX, false>(P, L, d, X0, Dm::LK, x, nullptr);
+      }
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) st4(OUT + q * E + 16 * ft + 4 * g, x[ft]);
     }
@@ -235,19 +242,34 @@ struct MixerBwdArgs {
   float* gqv;         // [B][T][A]
   float* ghid;        // [B][T][A][E]
   float* ghw0;        // [B][3][E] (may be null)
+  const float* xmid;  // forward block inputs of blocks 1..D-1 [B][T][D-1][A+3][E] (may be null)
   float* slabs;
   int lds_grad;
-  int waves;          // episodes (waves) per workgroup: 2, or 1 when 2 do not fit in LDS
+  int waves;          // episodes (waves) per workgroup: 4, 2 or 1, whatever fits in LDS
 };
 
-constexpr int MIX_BWD_WAVES = 2;
+
+template <int E, int A>
+struct MixBwdDims {
+  using Dm = MixDims<E, A>;
+  static constexpr int ET = E / 16, KT = Dm::KT;
+  static constexpr int NSTAGE = (KT < ET ? KT : ET) < 2 ? 2 : (KT < ET ? KT : ET);
+  static constexpr int STAGE = StageDims<NSTAGE>::FLOATS;
+  // WORK holds, in turn: the final query rows (head forward), their grads, the
+  // dW staging area (blocks), and the key-token grad block gX0 [KT*16][E].
+  // With one query tile the grads are in registers before staging starts, so
+  // the three uses can alias; otherwise the grads keep their own region.
+  static constexpr int GOUT = Dm::QT == 1 ? 0 : Dm::OUTF;
+  static constexpr int W0 = Dm::OUTF > STAGE ? Dm::OUTF : STAGE;
+  static constexpr int WORK = GOUT + (W0 > Dm::GX0F ? W0 : Dm::GX0F);
+  static constexpr int PERW = Dm::X0F + WORK;
+};
 
 template <int E, int H, int D, int A, int FF>
-__global__ __launch_bounds__(128) void mixer_bwd_kernel(MixerBwdArgs args) {
+__global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   using Dm = MixDims<E, A>;
+  using Bd = MixBwdDims<E, A>;
   constexpr int ET = E / 16, KT = Dm::KT;
-  constexpr int STAGE = StageDims<(KT < ET ? KT : ET) < 2 ? 2 : (KT < ET ? KT : ET)>::FLOATS;
-  constexpr int PERW = Dm::X0F + Dm::OUTF + Dm::GX0F + STAGE;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const MixerFwdArgs& fa = args.f;
   const MixerNet& n = fa.net[0];
@@ -255,10 +277,10 @@ __global__ __launch_bounds__(128) void mixer_bwd_kernel(MixerBwdArgs args) {
   const t2o_layout& G = args.G;
   float* lg = smem;
   const int w = wave_id();
-  float* X0 = smem + args.lds_grad + w * PERW;
-  float* OUT = X0 + Dm::X0F;
-  float* GX0 = OUT + Dm::OUTF;
-  float* stage = GX0 + Dm::GX0F;
+  float* X0 = smem + args.lds_grad + w * Bd::PERW;
+  float* WORK = X0 + Dm::X0F;
+  float* GOUTB = Bd::GOUT ? WORK : WORK;        // head grads (rows of OUT layout)
+  float* stage = WORK + Bd::GOUT;               // staging / gX0 region
   for (int i = threadIdx.x; i < args.lds_grad; i += blockDim.x) lg[i] = 0.f;
   __syncthreads();
   const int b = blockIdx.x * args.waves + w;
@@ -266,7 +288,6 @@ __global__ __launch_bounds__(128) void mixer_bwd_kernel(MixerBwdArgs args) {
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
   if (b < fa.B) {
     for (int i = lane; i < Dm::X0F; i += 64) X0[i] = 0.f;
-    for (int i = lane; i < Dm::GX0F; i += 64) GX0[i] = 0.f;
     float ghw[3] = {0.f, 0.f, 0.f};  // grad wrt this step's hyper outputs, lane = feature
     const int f = lane < E ? lane : 0;
     const bool fv = lane < E;
@@ -278,6 +299,7 @@ __global__ __launch_bounds__(128) void mixer_bwd_kernel(MixerBwdArgs args) {
         const float v = t > 0 ? args.hw[(bt - 1) * 3 * E + i] : (n.hw0 ? n.hw0[(size_t)b * 3 * E + i] : 0.f);
         X0[(Dm::NS + A + k) * Dm::LDX + ff] = v;
       }
+      float* OUT = stage;  // forward final query rows
       for (int i = lane; i < Dm::Q * E; i += 64) OUT[i] = args.xout[bt * Dm::Q * E + i];
       __builtin_amdgcn_wave_barrier();
       // ---- mixing head backward (lanes = features)
@@ -305,38 +327,59 @@ __global__ __launch_bounds__(128) void mixer_bwd_kernel(MixerBwdArgs args) {
       }
       gout[A] = gpre + ghw[0];
       gout[A + 1] = gyv * hidden * sgn_w2 + ghw[1];
+      const float x2 = OUT[(A + 2) * E + f];
       gout[A + 2] = gpre2 * P[L.Wo + f] + ghw[2];
       if (fv) {
-        atomicAdd(lg + G.Wo + f, gpre2 * OUT[(A + 2) * E + f]);
+        atomicAdd(lg + G.Wo + f, gpre2 * x2);
         if (lane == 0) atomicAdd(lg + G.bo, gpre2);
       }
       __builtin_amdgcn_wave_barrier();
-      // gOUT rows -> OUT buffer (the forward rows are no longer needed)
+      float* GOUT = Bd::GOUT ? GOUTB : stage;
       if (fv) {
 #pragma unroll
-        for (int q = 0; q < A + 3; ++q) OUT[q * E + f] = gout[q];
+        for (int q = 0; q < A + 3; ++q) GOUT[q * E + f] = gout[q];
       }
-      for (int i = Dm::Q * E + lane; i < Dm::OUTF; i += 64) OUT[i] = 0.f;
+      for (int i = Dm::Q * E + lane; i < Dm::OUTF; i += 64) GOUT[i] = 0.f;
       __builtin_amdgcn_wave_barrier();
-      // ---- blocks backward per query tile (body too large to unroll; qt only moves addresses)
-#pragma unroll 1
+      // ---- blocks backward per query tile; gX0 accumulates in registers
+      f4 gX0[KT][ET];
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft) gX0[kt][ft] = zero4();
+      f4 gq0[Dm::QT][ET];
+#pragma unroll
+      for (int qt = 0; qt < Dm::QT; ++qt)
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft) gq0[qt][ft] = ld4(GOUT + (16 * qt + c) * E + 16 * ft + 4 * g);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
       for (int qt = 0; qt < Dm::QT; ++qt) {
         const int q = 16 * qt + c;
         f4 gx[ET];
         f4 xs[D][ET];
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft) {
-          gx[ft] = ld4(OUT + q * E + 16 * ft + 4 * g);
+          gx[ft] = gq0[qt][ft];
           xs[0][ft] = q < Dm::Q ? ld4(X0 + (Dm::NS + q) * Dm::LDX + 16 * ft + 4 * g) : zero4();
         }
+        if (args.xmid) {  // stored block inputs of blocks 1..D-1 (no plain recompute)
 #pragma unroll
-        for (int d = 0; d + 1 < D; ++d) {
-          f4 x[ET];
+          for (int d = 1; d < D; ++d)
 #pragma unroll
-          for (int ft = 0; ft < ET; ++ft) x[ft] = xs[d][ft];
-          mixer_block_fwd<E, H, KT, FF, Dm::LDX, false>(P, L, d, X0, Dm::LK, x, nullptr);
+            for (int ft = 0; ft < ET; ++ft)
+              xs[d][ft] = q < Dm::Q ? ld4(args.xmid + ((bt * (D - 1) + d - 1) * Dm::Q + q) * E + 16 * ft + 4 * g)
+                                    : zero4();
+        } else {
 #pragma unroll
-          for (int ft = 0; ft < ET; ++ft) xs[d + 1][ft] = x[ft];
+          for (int d = 0; d + 1 < D; ++d) {
+            f4 x[ET];
+#pragma unroll
+            for (int ft = 0; ft < ET; ++ft) x[ft] = xs[d][ft];
+            mixer_block_fwd<E, H, KT, FF, Dm::LDX, false>(P, L, d, X0, Dm::LK, x, nullptr);
+#pragma unroll
+            for (int ft = 0; ft < ET; ++ft) xs[d + 1][ft] = x[ft];
+          }
         }
 #pragma unroll
         for (int d = D - 1; d >= 0; --d) {
@@ -345,14 +388,32 @@ __global__ __launch_bounds__(128) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft) x[ft] = xs[d][ft];
           mixer_block_fwd<E, H, KT, FF, Dm::LDX, true>(P, L, d, X0, Dm::LK, x, &cache);
-          mixer_block_bwd<E, H, KT, FF, Dm::LDX>(P, L, G, lg, stage, d, X0, GX0, cache, gx);
+          T2O_FENCE();
+          mixer_block_bwd<E, H, KT, FF, Dm::LDX>(P, L, G, lg, stage, d, X0, gX0, cache, gx);
+          T2O_FENCE();
         }
-        // query path: the block-0 input rows are key tokens NS+q
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft) gq0[qt][ft] = q < Dm::Q ? gx[ft] : zero4();
+      }
+      __builtin_amdgcn_wave_barrier();
+      // ---- gX0 registers -> LDS rows [key][feature], plus the query path
+      float* GX0 = stage;
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) GX0[(16 * kt + 4 * g + r) * E + 16 * ft + c] = gX0[kt][ft][r];
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int qt = 0; qt < Dm::QT; ++qt) {
+        const int q = 16 * qt + c;
         if (q < Dm::Q) {
 #pragma unroll
-          for (int ft = 0; ft < ET; ++ft)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) atomicAdd(GX0 + (Dm::NS + q) * E + 16 * ft + 4 * g + r, gx[ft][r]);
+          for (int ft = 0; ft < ET; ++ft) {
+            float* dst = GX0 + (Dm::NS + q) * E + 16 * ft + 4 * g;
+            st4(dst, ld4(dst) + gq0[qt][ft]);
+          }
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -373,8 +434,6 @@ __global__ __launch_bounds__(128) void mixer_bwd_kernel(MixerBwdArgs args) {
         atomicAdd(lg + G.be + f, gbe);
       }
       __builtin_amdgcn_wave_barrier();
-      for (int i = lane; i < Dm::GX0F; i += 64) GX0[i] = 0.f;
-      __builtin_amdgcn_wave_barrier();
     }
     if (args.ghw0 && fv) {
 #pragma unroll
@@ -388,18 +447,14 @@ __global__ __launch_bounds__(128) void mixer_bwd_kernel(MixerBwdArgs args) {
 
 template <int E, int H, int D, int A, int FF>
 int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
-  using Dm = MixDims<E, A>;
-  constexpr int ET = E / 16, KT = Dm::KT;
-  constexpr int STAGE = StageDims<(KT < ET ? KT : ET) < 2 ? 2 : (KT < ET ? KT : ET)>::FLOATS;
-  constexpr int PERW = Dm::X0F + Dm::OUTF + Dm::GX0F + STAGE;
+  constexpr int PERW = MixBwdDims<E, A>::PERW;
   args.lds_grad = (int)((args.G.grad_total + 15) / 16 * 16);
-  args.waves = MIX_BWD_WAVES;
-  size_t lds = sizeof(float) * ((size_t)args.lds_grad + args.waves * PERW);
-  if (lds > 160 * 1024) {
-    args.waves = 1;
-    lds = sizeof(float) * ((size_t)args.lds_grad + PERW);
+  size_t lds = 0;
+  for (args.waves = 4; args.waves >= 1; args.waves >>= 1) {
+    lds = sizeof(float) * ((size_t)args.lds_grad + args.waves * PERW);
+    if (lds <= 160 * 1024) break;
   }
-  if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
+  if (args.waves < 1) return T2O_EUNSUPPORTED;
   const int grid = (args.f.B + args.waves - 1) / args.waves;
   if (grid > max_slabs) return T2O_EINVAL;
   auto kern = mixer_bwd_kernel<E, H, D, A, FF>;
@@ -419,8 +474,8 @@ extern "C" int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, c
                                     const float* q_tg, int q_ts, int n_actions, const int64_t* actions,
                                     int64_t act_sb, int64_t act_st, const int32_t* avail, int64_t av_sb,
                                     int64_t av_st, float* y_on, float* hw_on, float* qvo_on, float* xout_on,
-                                    float* y_tg, float* hw_tg, float* qvo_tg, float* xout_tg, int B, int T_on,
-                                    int T_tg, void* stream) {
+                                    float* xmid_on, float* y_tg, float* hw_tg, float* qvo_tg, float* xout_tg,
+                                    float* xmid_tg, int B, int T_on, int T_tg, void* stream) {
   if (!L || L->kind != 1 || !pack_on || !states || !hid_on || !y_on || !hw_on || B < 1 || T_on < 1 ||
       L->E > 64)
     return T2O_EINVAL;
@@ -448,12 +503,12 @@ extern "C" int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, c
   };
   if (!check_mode(qmode_on, qv_on, q_on)) return T2O_EINVAL;
   a.net[0] = MixerNet{pack_on, hw0_on, hid_on, hid_sb, hid_st, q_on, qv_on, qmode_on, T_on,
-                      y_on, hw_on, qvo_on, xout_on};
+                      y_on, hw_on, qvo_on, xout_on, xmid_on};
   int nnet = 1;
   if (pack_tg) {
     if (!hid_tg || !y_tg || !hw_tg || T_tg < 1 || !check_mode(qmode_tg, qv_tg, q_tg)) return T2O_EINVAL;
     a.net[1] = MixerNet{pack_tg, hw0_tg, hid_tg, hid_sb, hid_st, q_tg, qv_tg, qmode_tg, T_tg,
-                        y_tg, hw_tg, qvo_tg, xout_tg};
+                        y_tg, hw_tg, qvo_tg, xout_tg, xmid_tg};
     nnet = 2;
   }
   int rc = T2O_EUNSUPPORTED;
@@ -467,8 +522,8 @@ extern "C" int t2o_mixer_bwd_max_slabs(int B) { return B; }  // worst case: 1 ep
 extern "C" int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, const float* states, int64_t st_sb,
                                     int64_t st_st, const float* hid, int64_t hid_sb, int64_t hid_st,
                                     const float* hw0, const float* qv, const float* hw, const float* xout,
-                                    const float* gy, const float* ghw_ext, float* gqv, float* ghid, float* ghw0,
-                                    float* gslabs,
+                                    const float* xmid, const float* gy, const float* ghw_ext, float* gqv,
+                                    float* ghid, float* ghw0, float* gslabs,
                                     int max_slabs, int* nslab, int B, int T, void* stream) {
   if (!L || L->kind != 1 || !pack || !states || !hid || !qv || !hw || !xout || !gy || !gqv || !ghid ||
       !gslabs || !nslab || B < 1 || T < 1 || L->E > 64)
@@ -480,7 +535,9 @@ extern "C" int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, cons
   a.f.st_st = st_st;
   a.f.B = B;
   a.f.Fs = L->F;
-  a.f.net[0] = MixerNet{pack, hw0, hid, hid_sb, hid_st, nullptr, qv, 0, T, nullptr, nullptr, nullptr, nullptr};
+  a.f.net[0] = MixerNet{pack, hw0, hid, hid_sb, hid_st, nullptr, qv, 0, T, nullptr, nullptr, nullptr, nullptr,
+                        nullptr};
+  a.xmid = xmid;
   grad_layout(*L, a.G);
   a.hw = hw;
   a.xout = xout;

@@ -107,12 +107,13 @@ T2O_DEV void mixer_block_fwd(const float* __restrict__ P, const t2o_layout& L, i
 }
 
 // Backward of block d for one query tile.  gx: in = grad wrt block output,
-// out = grad wrt block input.  gX0 (wave-private LDS [KT*16][E]) accumulates
-// the grad wrt the key tokens (contraction over queries = rows).
+// out = grad wrt block input.  gX0 — MFMA accumulator registers, tile [kt][ft]
+// holds gX0[key 16kt+4g+r][feature 16ft+c] — accumulates the grad wrt the key
+// tokens (a contraction over queries = rows, via the staging transposes).
 template <int E, int H, int KT, int FF, int LDX>
 T2O_DEV void mixer_block_bwd(const float* __restrict__ P, const t2o_layout& L, const t2o_layout& G,
                              float* __restrict__ lg, float* __restrict__ stage, int d,
-                             const float* __restrict__ X0, float* __restrict__ gX0,
+                             const float* __restrict__ X0, f4 (&gX0)[KT][E / 16],
                              const MixerCache<E, H, KT, FF>& c, f4* gx) {
   constexpr int ET = E / 16, HET = H * ET;
   f4 gz[HET], gres[ET];
@@ -132,10 +133,12 @@ T2O_DEV void mixer_block_bwd(const float* __restrict__ P, const t2o_layout& L, c
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) gs[kt] = c.p[hh][kt] * (gp[kt] - dot);
     keys_combine<E, KT, LDX>(X0, gs, &gu[hh * ET]);
-    dw_accumulate<KT, ET>(gX0, E, c.p[hh], &gz[hh * ET], stage);
-    dw_accumulate<KT, ET>(gX0, E, gs, &c.u[hh * ET], stage);
+    dw_accumulate_regs<KT, ET>(gX0, c.p[hh], &gz[hh * ET], stage);
+    dw_accumulate_regs<KT, ET>(gX0, gs, &c.u[hh * ET], stage);
+    T2O_FENCE();
   }
   dw_accumulate<HET, ET>(lg + G.M[d], E, gu, c.post.x, stage);
+  T2O_FENCE();
   f4 gxp[ET];
   matvec<ET, HET>(P + L.MT[d], H * E, gu, gxp);
 #pragma unroll

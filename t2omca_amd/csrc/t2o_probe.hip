@@ -1,0 +1,24 @@
+// t2o_probe.hip — on-device checks of the cross-lane primitives the kernels use
+// (semantics of DPP row reductions and gfx950 permlane swaps are verified by
+// tests/test_gpu_primitives.py against host-computed expectations).
+#include "t2o_common.hpp"
+
+using namespace t2o;
+
+namespace {
+__global__ void probe_kernel(const float* __restrict__ in, float* __restrict__ out) {
+  const int l = threadIdx.x;
+  const float v = in[l];
+  out[0 * 64 + l] = allsum4_shfl(v);
+  out[1 * 64 + l] = allsum4_fast(v);
+  out[2 * 64 + l] = rowsum16(v);
+  out[3 * 64 + l] = rowsum16_fast(v);
+  out[4 * 64 + l] = allmax4_shfl(v);
+  out[5 * 64 + l] = allmax4_fast(v);
+}
+}  // namespace
+
+extern "C" int t2o_probe_lane_ops(const float* in, float* out, void* stream) {
+  hipLaunchKernelGGL(probe_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, in, out);
+  return (int)hipGetLastError();
+}

@@ -101,6 +101,16 @@ class TDLearner:
             return dist.get_world_size(self.pg)
         return 1
 
+    def _buf(self, key, shape):
+        t = self._slabs.get(key)
+        n = 1
+        for d in shape:
+            n *= d
+        if t is None or t.numel() < n:
+            t = torch.empty(n, device=self.device)
+            self._slabs[key] = t
+        return t[:n].view(shape)
+
     def _slab(self, key, n):
         t = self._slabs.get(key)
         if t is None or t.numel() < n:
@@ -135,8 +145,9 @@ class TDLearner:
         ops.pack_params(self.sa, self.params[:self.na], self.pack_a)
         ops.pack_params(self.sm, self.params[self.na:], self.pack_m)
         # 1. agents: online + target over t = 0..T
+        hmid = self._buf("hmid", (B, T1, self.sa.D - 1, A, self.sa.E)) if self.sa.D > 1 else None
         q_on, h_on, q_tg, h_tg = ops.agent_unroll_fwd(self.sa, self.pack_a, obs, pack_tg=self.pack_at,
-                                                      timer=self.timer)
+                                                      timer=self.timer, hmid_on=hmid)
         # 2. mixers: online on chosen Q (t < T), target on double-Q (t <= T)
         o_on, o_tg = ops.mixer_unroll_fwd(self.sm, self.pack_m, state, h_on, qmode_on=1, q_on=q_on,
                                           actions=act, avail=avail, T_on=T, pack_tg=self.pack_mt,
@@ -154,7 +165,7 @@ class TDLearner:
         slabs_a = self._slab("a", int(ops.lib().t2o_agent_bwd_max_slabs(B, A)) * self.sa.layout().grad_total)
         ga, _ = ops.agent_unroll_bwd(self.sa, self.pack_a, obs, h_on, gchosen=gqv, actions=act,
                                      gh=None if self.detach_mixer_hidden else ghid, slabs=slabs_a,
-                                     timer=self.timer)
+                                     timer=self.timer, hmid=hmid)
         # 6. grads in reference parameter order
         self.grad.zero_()
         ops.unpack_grads(self.sa, self.params[:self.na], ga, self.grad[:self.na])

@@ -128,6 +128,7 @@ class _MixerStep(torch.autograd.Function):
         st = states.detach().reshape(b, 1, -1).contiguous()
         out = ops.mixer_unroll_fwd(shape, pack, st, hid, qmode_on=0, qv_on=qv, hw0_on=hw0)
         ctx.save_for_backward(flat, qv, hid, hw0, st, out["y"], out["hw"], out["qv"], out["xout"])
+        ctx.xmid = out["xmid"]
         ctx.shape = shape
         return out["y"].view(b, 1, 1), out["hw"][:, 0]
 
@@ -139,7 +140,7 @@ class _MixerStep(torch.autograd.Function):
         pack = ops.pack_params(shape, flat.detach().contiguous())
         gy = (gy if gy is not None else torch.zeros_like(y)).reshape(b, 1).contiguous()
         ghw = ghw.reshape(b, 1, 3, shape.E).contiguous() if ghw is not None else None
-        fwd = dict(y=y, hw=hw, qv=qvo, xout=xout)
+        fwd = dict(y=y, hw=hw, qv=qvo, xout=xout, xmid=ctx.xmid)
         gpack, gqv, ghid, ghw0 = ops.mixer_unroll_bwd(shape, pack, st, hid, fwd, gy, hw0=hw0, ghw_ext=ghw,
                                                       want_ghw0=True)
         gflat = torch.zeros_like(flat)

@@ -87,10 +87,12 @@ def _mark(timer, tag):
         timer(tag)
 
 
-def agent_unroll_fwd(shape: NetShape, pack_on, obs, h0_on=None, pack_tg=None, h0_tg=None, timer=None):
+def agent_unroll_fwd(shape: NetShape, pack_on, obs, h0_on=None, pack_tg=None, h0_tg=None, timer=None,
+                     hmid_on=None):
     """Unroll the agent over obs [B, T, A, n_ent*F] (any stride over B, T; inner
     [A, n_ent*F] contiguous).  Returns (q_on, h_on[, q_tg, h_tg]) with
-    q [B, T, A, NA], h [B, T, A, E]."""
+    q [B, T, A, NA], h [B, T, A, E].  hmid_on: optional [B, T, D-1, A, E]
+    output buffer for the inter-block activations (used by the backward)."""
     _dev(pack_on, obs, h0_on, pack_tg, h0_tg)
     B, T, A, nf = obs.shape
     assert obs.dtype == torch.float32 and nf == shape.n_ent * shape.F
@@ -109,8 +111,8 @@ def agent_unroll_fwd(shape: NetShape, pack_on, obs, h0_on=None, pack_tg=None, h0
     _mark(timer, "begin:agent_fwd")
     check(lib().t2o_agent_unroll_fwd(ctypes.byref(L), ptr(pack_on), ptr(pack_tg), ptr(obs),
                                      obs.stride(0), obs.stride(1), ptr(h0_on), ptr(h0_tg),
-                                     ptr(q_on), ptr(h_on), ptr(q_tg), ptr(h_tg), B, T, A,
-                                     stream_ptr()), "agent_unroll_fwd")
+                                     ptr(q_on), ptr(h_on), ptr(hmid_on), ptr(q_tg), ptr(h_tg), None,
+                                     B, T, A, stream_ptr()), "agent_unroll_fwd")
     _mark(timer, "end:agent_fwd")
     if pack_tg is not None:
         return q_on, h_on, q_tg, h_tg
@@ -118,7 +120,7 @@ def agent_unroll_fwd(shape: NetShape, pack_on, obs, h0_on=None, pack_tg=None, h0
 
 
 def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchosen=None, actions=None,
-                     gh=None, want_gh0=False, slabs=None, timer=None):
+                     gh=None, want_gh0=False, slabs=None, timer=None, hmid=None):
     """BPTT of agent_unroll_fwd over the first T = len(grads) steps.
 
     obs [B, >=T, A, nF]; h_seq [B, Ts>=T, A, E] (forward output); gq [B,T,A,NA],
@@ -142,7 +144,7 @@ def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchose
     nslab = ctypes.c_int(0)
     _mark(timer, "begin:agent_bwd")
     check(lib().t2o_agent_unroll_bwd(ctypes.byref(L), ptr(pack), ptr(obs), obs.stride(0), obs.stride(1),
-                                     ptr(h0), ptr(h_seq), h_seq.shape[1], ptr(gq), ptr(gchosen),
+                                     ptr(h0), ptr(h_seq), ptr(hmid), h_seq.shape[1], ptr(gq), ptr(gchosen),
                                      ptr(actions), act_sb, act_st, ptr(gh), ptr(slabs), nmax,
                                      ctypes.byref(nslab), ptr(gh0), B, T, A, stream_ptr()),
           "agent_unroll_bwd")
@@ -184,7 +186,9 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
     def outs(T):
         return dict(y=torch.empty(B, T, device=dev), hw=torch.empty(B, T, 3, E, device=dev),
                     qv=torch.empty(B, T, A, device=dev),
-                    xout=torch.empty(B, T, A + 3, E, device=dev) if want_xout else None)
+                    xout=torch.empty(B, T, A + 3, E, device=dev) if want_xout else None,
+                    xmid=torch.empty(B, T, shape.D - 1, A + 3, E, device=dev)
+                    if (want_xout and shape.D > 1) else None)
 
     o_on = outs(T_on)
     o_tg = None
@@ -201,8 +205,8 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
         ptr(hid_on), ptr(hid_tg), hid_on.stride(0), hid_on.stride(1), ptr(hw0_on), ptr(hw0_tg),
         qmode_on, qmode_tg, ptr(qv_on), ptr(qv_tg), ptr(q_on), ptr(q_tg), q_ts, n_actions,
         ptr(actions), act_sb, act_st, ptr(avail), av_sb, av_st,
-        g(o_on, "y"), g(o_on, "hw"), g(o_on, "qv"), g(o_on, "xout"),
-        g(o_tg, "y"), g(o_tg, "hw"), g(o_tg, "qv"), g(o_tg, "xout"),
+        g(o_on, "y"), g(o_on, "hw"), g(o_on, "qv"), g(o_on, "xout"), g(o_on, "xmid"),
+        g(o_tg, "y"), g(o_tg, "hw"), g(o_tg, "qv"), g(o_tg, "xout"), g(o_tg, "xmid"),
         B, T_on, T_tg or 0, stream_ptr()), "mixer_unroll_fwd")
     _mark(timer, "end:mixer_fwd")
     return (o_on, o_tg) if pack_tg is not None else o_on
@@ -229,7 +233,7 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
     check(lib().t2o_mixer_unroll_bwd(
         ctypes.byref(L), ptr(pack), ptr(states), states.stride(0), states.stride(1), ptr(hid),
         hid.stride(0), hid.stride(1), ptr(hw0), ptr(fwd["qv"]), ptr(fwd["hw"]), ptr(fwd["xout"]),
-        ptr(gy), ptr(ghw_ext), ptr(gqv), ptr(ghid), ptr(ghw0), ptr(slabs), nmax, ctypes.byref(nslab),
+        ptr(fwd.get("xmid")), ptr(gy), ptr(ghw_ext), ptr(gqv), ptr(ghid), ptr(ghw0), ptr(slabs), nmax, ctypes.byref(nslab),
         B, T, stream_ptr()), "mixer_unroll_bwd")
     _mark(timer, "end:mixer_bwd")
     gpack = torch.empty(L.grad_total, device=dev)
