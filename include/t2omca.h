@@ -62,6 +62,7 @@ typedef struct {
   int64_t W1[T2O_MAX_DEPTH], W1T[T2O_MAX_DEPTH], c1[T2O_MAX_DEPTH]; /* [FF][E],[E][FF],[FF] */
   int64_t W2[T2O_MAX_DEPTH], W2T[T2O_MAX_DEPTH], c2[T2O_MAX_DEPTH]; /* [E][FF],[FF][E],[E] */
   int64_t g2[T2O_MAX_DEPTH], n2[T2O_MAX_DEPTH];
+  int64_t fwd_total;          /* floats [0, fwd_total) = every tensor the forward reads */
   int64_t total;              /* pack size in floats */
   int64_t grad_total;         /* size of the compact gradient block (no transposes) */
 } t2o_layout;
@@ -177,6 +178,11 @@ int t2o_adam_step(float* params, const float* grads, float* exp_avg, float* exp_
                   float weight_decay, float max_grad_norm, int64_t step, const float* grad_div,
                   float* grad_norm_out, void* stream);
 int t2o_adam_workspace_floats(void);
+
+/* Diagnostic: runs the cross-lane primitives the kernels rely on (4-lane
+ * all-reduces via ds_bpermute and via gfx950 permlane swaps, 16-lane DPP row
+ * sums) on in[64]; writes 6 x 64 results (tests/test_gpu_primitives.py). */
+int t2o_probe_lane_ops(const float* in, float* out, void* stream);
 
 /* Sum nslab partial gradient slabs [nslab][n] into out[n] (out = sum, overwritten). */
 int t2o_reduce_slabs(const float* slabs, int nslab, int64_t n, float* out, void* stream);

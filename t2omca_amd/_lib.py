@@ -19,7 +19,7 @@ class Layout(ctypes.Structure):
                 [(n, ctypes.c_int64) for n in ("WeT", "We", "be", "Wo", "bo", "WoT")] +
                 [(n, _I64x) for n in ("M", "MT", "N", "NT", "bu", "g1", "n1", "W1", "W1T", "c1",
                                       "W2", "W2T", "c2", "g2", "n2")] +
-                [("total", ctypes.c_int64), ("grad_total", ctypes.c_int64)])
+                [("fwd_total", ctypes.c_int64), ("total", ctypes.c_int64), ("grad_total", ctypes.c_int64)])
 
 
 EXPORTS = {

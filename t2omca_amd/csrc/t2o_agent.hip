@@ -34,18 +34,22 @@ struct AgentFwdArgs {
 template <int E, int H, int D, int NE, int FF>
 __global__ __launch_bounds__(256) void agent_fwd_kernel(AgentFwdArgs args) {
   constexpr int ET = E / 16;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
   const AgentNet net = args.net[blockIdx.y];
   const t2o_layout& L = args.L;
+  // the forward section of the pack lives in LDS for the whole unroll
+  copy_to_lds(smem, net.pack, L.fwd_total);
+  __syncthreads();
   const int A = args.A, F = args.F;
   const int R = args.B * A;
   const int rt = blockIdx.x * 4 + wave_id();
-  if (rt * 16 >= R) return;  // wave-uniform: this kernel has no barriers
+  if (rt * 16 >= R) return;  // wave-uniform: no barriers after this point
   const int c = lane_c(), g = lane_g();
   const int row_raw = rt * 16 + c;
   const bool valid = row_raw < R;
   const int row = valid ? row_raw : R - 1;
   const int b = row / A, a = row % A;
-  const float* __restrict__ P = net.pack;
+  const float* __restrict__ P = smem;
 
   f4 h[ET];
 #pragma unroll
@@ -97,7 +101,11 @@ int launch_fwd(const AgentFwdArgs& args, int nnet, hipStream_t stream) {
   const int R = args.B * args.A;
   const int tiles = (R + 15) / 16;
   dim3 grid((tiles + 3) / 4, nnet);
-  hipLaunchKernelGGL((agent_fwd_kernel<E, H, D, NE, FF>), grid, dim3(256), 0, stream, args);
+  const size_t lds = sizeof(float) * (size_t)args.L.fwd_total;
+  if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
+  auto kern = agent_fwd_kernel<E, H, D, NE, FF>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, args);
   return (int)hipGetLastError();
 }
 

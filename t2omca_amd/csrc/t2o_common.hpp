@@ -182,6 +182,11 @@ T2O_DEV void layernorm_bwd(const f4* gout, const f4* xhat, float rstd,
 
 namespace t2o {
 
+// Cooperative copy of n floats (n % 4 == 0, 16-B aligned) global -> LDS by the whole block.
+T2O_DEV void copy_to_lds(float* __restrict__ dst, const float* __restrict__ src, int64_t n) {
+  for (int64_t i = 4 * (int64_t)threadIdx.x; i < n; i += 4 * (int64_t)blockDim.x) st4(dst + i, ld4(src + i));
+}
+
 // ---- weight-gradient accumulation -------------------------------------------
 // dW[16*OT x 16*IT] += Σ_rows dY[row]ᵀ ⊗ X[row] over the wave's 16 rows, added
 // into an LDS accumulator (row-major, leading dim ldw) with ds_add_f32.

@@ -71,7 +71,7 @@ inline void grad_layout(const t2o_layout& L, t2o_layout& G) {
     G.g2[d] = o; o += E;
     G.n2[d] = o; o += E;
   }
-  G.total = G.grad_total = o;
+  G.total = G.grad_total = G.fwd_total = o;
 }
 
 }  // namespace t2o

@@ -153,12 +153,15 @@ __global__ __launch_bounds__(256) void mixer_fwd_kernel(MixerFwdArgs args) {
   constexpr int ET = E / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int w = wave_id();
-  const int b = blockIdx.x * 4 + w;
-  if (b >= args.B) return;  // wave-uniform; no block barriers in this kernel
   const MixerNet n = args.net[blockIdx.y];
   const t2o_layout& L = args.L;
-  const float* __restrict__ P = n.pack;
-  float* X0 = smem + w * (Dm::X0F + Dm::OUTF);
+  const int lds_w = (int)((L.fwd_total + 15) / 16 * 16);
+  copy_to_lds(smem, n.pack, L.fwd_total);  // forward weights in LDS for the unroll
+  __syncthreads();
+  const int b = blockIdx.x * 4 + w;
+  if (b >= args.B) return;  // wave-uniform; no block barriers after this point
+  const float* __restrict__ P = smem;
+  float* X0 = smem + lds_w + w * (Dm::X0F + Dm::OUTF);
   float* OUT = X0 + Dm::X0F;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
   for (int i = lane; i < Dm::X0F; i += 64) X0[i] = 0.f;
@@ -216,7 +219,8 @@ __global__ __launch_bounds__(256) void mixer_fwd_kernel(MixerFwdArgs args) {
 template <int E, int H, int D, int A, int FF>
 int launch_mixer_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
   using Dm = MixDims<E, A>;
-  const size_t lds = sizeof(float) * 4 * (Dm::X0F + Dm::OUTF);
+  const size_t lds = sizeof(float) * ((args.L.fwd_total + 15) / 16 * 16 + 4 * (Dm::X0F + Dm::OUTF));
+  if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
   auto kern = mixer_fwd_kernel<E, H, D, A, FF>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid((args.B + 3) / 4, nnet);

@@ -167,29 +167,33 @@ extern "C" int t2o_layout_init(t2o_layout* L, int kind, int E, int H, int D, int
   L->kind = kind; L->E = E; L->H = H; L->D = D; L->F = F; L->NA = NA; L->FF = FF; L->n_ent = n_ent;
   int64_t o = 0;
   const int64_t HE = (int64_t)H * E;
+  // forward section first (one contiguous copy into LDS), backward extras after
   L->WeT = o; o += 16 * (int64_t)E;
   L->We = o; o += (int64_t)E * 16;
   L->be = o; o += E;
   L->Wo = o; o += 16 * (int64_t)E;
   L->bo = o; o += 16;
-  L->WoT = o; o += (int64_t)E * 16;
   for (int d = 0; d < T2O_MAX_DEPTH; ++d) {
     if (d >= D) { L->M[d] = L->MT[d] = L->N[d] = L->NT[d] = L->bu[d] = L->g1[d] = L->n1[d] = L->W1[d] = L->W1T[d] = L->c1[d] = L->W2[d] = L->W2T[d] = L->c2[d] = L->g2[d] = L->n2[d] = -1; continue; }
     L->M[d] = o; o += HE * E;
-    L->MT[d] = o; o += E * HE;
     L->N[d] = o; o += E * HE;
-    L->NT[d] = o; o += HE * E;
     L->bu[d] = o; o += E;
     L->g1[d] = o; o += E;
     L->n1[d] = o; o += E;
     L->W1[d] = o; o += (int64_t)FF * E;
-    L->W1T[d] = o; o += (int64_t)E * FF;
     L->c1[d] = o; o += FF;
     L->W2[d] = o; o += (int64_t)E * FF;
-    L->W2T[d] = o; o += (int64_t)FF * E;
     L->c2[d] = o; o += E;
     L->g2[d] = o; o += E;
     L->n2[d] = o; o += E;
+  }
+  L->fwd_total = o;
+  L->WoT = o; o += (int64_t)E * 16;
+  for (int d = 0; d < D; ++d) {
+    L->MT[d] = o; o += E * HE;
+    L->NT[d] = o; o += HE * E;
+    L->W1T[d] = o; o += (int64_t)E * FF;
+    L->W2T[d] = o; o += (int64_t)FF * E;
   }
   L->total = o;
   t2o_layout G;

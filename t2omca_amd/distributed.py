@@ -1,0 +1,35 @@
+"""Data parallelism for the TD update (one process per GPU, RCCL over xGMI).
+
+Episodes of a replay batch are independent (the recurrence is over t inside
+an episode), so each rank trains on its own episode shard and the only
+collective is ONE all-reduce per update of a flat fp32 buffer
+[Σ_shard grad (un-normalised) ..., Σ_shard mask].  Dividing by the summed
+mask afterwards (inside the Adam kernel, t2o_adam_step's grad_div) makes the
+DP update equal to the full-batch update:
+
+    loss = Σ_b w_b Σ_t ½ td² m / Σ_all m   ->   grad = Σ_r g_r / Σ_r M_r
+
+At E = 32 that buffer is 84,007 floats (336 KB): latency-bound over xGMI, so
+no bucketing or overlap machinery is warranted.
+"""
+import torch.distributed as dist
+
+
+def world_size(group=None):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group)
+    return 1
+
+
+def allreduce_grad_and_mask(buf, group=None):
+    """In-place SUM all-reduce of [grad..., mask_sum]; returns buf."""
+    if world_size(group) > 1:
+        dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
+    return buf
+
+
+def shard_bounds(n, rank, world):
+    """Contiguous episode shard [lo, hi) of rank (weak scaling uses a full batch per rank)."""
+    per = (n + world - 1) // world
+    lo = min(n, rank * per)
+    return lo, min(n, lo + per)

@@ -27,6 +27,7 @@ import torch
 import torch.distributed as dist
 
 from . import ops
+from .distributed import allreduce_grad_and_mask
 
 
 def _bind_flat(modules, device):
@@ -171,8 +172,7 @@ class TDLearner:
         ops.unpack_grads(self.sa, self.params[:self.na], ga, self.grad[:self.na])
         ops.unpack_grads(self.sm, self.params[self.na:], gm, self.grad[self.na:self.na + self.nm])
         self.grad[-1:].copy_(td["loss"][1:2])
-        if self._world() > 1:
-            dist.all_reduce(self.grad, group=self.pg)
+        allreduce_grad_and_mask(self.grad, self.pg)
         # 7. clip + Adam
         self.step_count += 1
         ops.adam_step(self.params, self.grad[:-1], self.exp_avg, self.exp_avg_sq, self.step_count, lr=self.lr,

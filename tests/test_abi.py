@@ -1,0 +1,77 @@
+"""CPU: the C-ABI library builds/loads and exports every entry point include/t2omca.h declares,
+and the host-side layout logic (no device compute)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    txt = open(os.path.join(REPO, "include", "t2omca.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(t2o_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    from t2omca_amd import build
+    build.build()
+    lib = ctypes.CDLL(build.LIB)
+    names = _declared()
+    assert len(names) >= 15
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_ctypes_bindings_cover_header():
+    from t2omca_amd import _lib
+    names = set(_declared())
+    assert names <= set(_lib.EXPORTS), names - set(_lib.EXPORTS)
+
+
+@pytest.mark.parametrize("kind,F,NA", [(0, 9, 5), (1, 8, 1)])
+def test_layout_and_param_count(kind, F, NA):
+    """Host-side layout init and the reference parameter counts (SURVEY.md §8 b)."""
+    from t2omca_amd import _lib
+    L = _lib.make_layout(kind, 32, 3, 2, F, NA, 128, 8)
+    n = _lib.lib().t2o_param_count(kind, 32, 3, 2, F, NA, 128)
+    assert n == (42085 if kind == 0 else 41921)
+    assert L.total > L.grad_total > 0
+    offs = [L.WeT, L.We, L.be, L.Wo, L.bo, L.WoT] + [getattr(L, k)[d] for k in
+                                                   ("M", "MT", "N", "NT", "W1", "W1T", "W2", "W2T") for d in range(2)]
+    assert all(o % 16 == 0 for o in offs), "every pack tensor must be 64-byte aligned"
+    assert L.M[2] == -1
+
+
+def test_layout_rejects_bad_shapes():
+    from t2omca_amd import _lib
+    L = _lib.Layout()
+    assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 30, 3, 2, 9, 5, 128, 8) != 0  # E % 16
+    assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 32, 3, 9, 9, 5, 128, 8) != 0  # depth > 4
+    assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 32, 3, 2, 20, 5, 128, 8) != 0  # F > 16
+
+
+def test_product_path_refuses_cpu_tensors():
+    import torch
+    from t2omca_amd import ops
+    shape = ops.NetShape(0, 32, 3, 2, 9, 5, 128, 8)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        ops.pack_params(shape, torch.zeros(shape.n_params))
+
+
+def test_dropin_modules_state_dict_matches_reference_keys():
+    """state_dict keys/shapes equal the reference modules' (checked against the golden fixture)."""
+    import glob
+
+    import numpy as np
+    from t2omca_amd.modules import TransformerAgent, TransformerMixer
+    from t2omca_amd.synthetic import make_args
+    args = make_args(8, device="cpu")
+    for cls, pat in ((TransformerAgent, "agent_a8*.npz"), (TransformerMixer, "mixer_a8*.npz")):
+        m = cls(None, args) if cls is TransformerAgent else cls(args)
+        z = np.load(glob.glob(os.path.join(REPO, "tests", "golden", pat))[0])
+        ref = {k[6:]: z[k].shape for k in z.files if k.startswith("param/")}
+        mine = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+        assert list(mine) == list(ref) and mine == ref
