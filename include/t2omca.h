@@ -187,6 +187,38 @@ int t2o_probe_lane_ops(const float* in, float* out, void* stream);
 /* Sum nslab partial gradient slabs [nslab][n] into out[n] (out = sum, overwritten). */
 int t2o_reduce_slabs(const float* slabs, int nslab, int64_t n, float* out, void* stream);
 
+/* ---- vectorised MEC-offloading environment -------------
+ * Replaces MultiAgvOffloadingEnv (environment_multi_mec.py:12-439) driven by
+ * parallel_runner.py's env_worker (:224-270): NE envs advance in lock-step, one
+ * wave per env, state resident in HBM.  All arrays are device pointers.
+ *
+ * mode 0  construction (:12-59: mec_index + positions, zeroed queues/normaliser)
+ * mode 1  worker 'reset'  (:257-263 -> reset() :219-227, get_state, get_avail_actions, get_obs)
+ * mode 2  worker 'step'   (:239-256 -> step() :309-366, get_state, get_avail_actions, get_obs)
+ * mode 3  get_env_info's two get_obs calls (:421-439; normaliser updates only)
+ *
+ * spec[15] (fp64): mec_radius, computation_cycles, bandwidth, noise_power,
+ *   path_loss, channel_gain_linear, mec_compute_cap, agv_transmit_power,
+ *   agv_compute_cap, latency_max, t_length, job_size_min, job_size_max,
+ *   job_arrival_p, edge_only (0/1)  (t2omca_amd/env_spec.py).
+ * state[17]: mec_index i32[NE][A], x f64[NE][A], y f64[NE][A],
+ *   q_size i32[NE][A][QMAX], q_thr i32[NE][A][QMAX], q_head i32[NE][A],
+ *   q_len i32[NE][A], task_num i32[NE][A], task_success i32[NE][A],
+ *   remain_delay f64[NE][A], last_ack i32[NE][A], time_slot i32[NE],
+ *   draw i64[NE], nrm_n i64[NE], nrm_mean f64[NE][9A], nrm_S f64[NE][9A],
+ *   nrm_std f64[NE][9A].
+ * out[8] (any entry may be NULL except reward/terminated/info in mode 2):
+ *   obs f32[NE][A][9A], obs f64[NE][A][9A], state f32[NE][8A],
+ *   avail i32[NE][A][C+1], reward f64[NE], terminated u8[NE],
+ *   info f64[NE][6] = delay_reward, overtime_penalty, channel_utilization_rate,
+ *   conflict_ratio, task_completion_rate, task_completion_delay (NaN unless terminal),
+ *   ack i32[NE][A].
+ * actions: i64, env e's agent a at actions[e*act_se + a] (values in 0..C).
+ * Limits: A <= 64, M <= 16, C <= 16.  Random draws: env_spec.uniforms(seed, env, draw). */
+int t2o_env_run(int mode, const double* spec, void* const* state, void* const* out,
+                const int64_t* actions, int64_t act_se, int NE, int A, int M, int C, int QMAX, int T,
+                uint64_t seed, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

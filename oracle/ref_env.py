@@ -28,8 +28,9 @@ ACK_ONEHOT = {-1: (1.0, 0.0, 0.0), 0: (0.0, 1.0, 0.0), 1: (0.0, 0.0, 1.0)}
 
 
 class RefEnv:
-    def __init__(self, M, A, T, seed, env_id, num_channels=4):
+    def __init__(self, M, A, T, seed, env_id, num_channels=4, edge_only=False):
         self.M, self.A, self.T, self.C = M, A, T, num_channels
+        self.edge_only = edge_only
         self.nA = num_channels + 1
         self.seed, self.env_id = seed, env_id
         self.draw = 0
@@ -124,7 +125,9 @@ class RefEnv:
         return np.concatenate((ack.flatten(), inf.flatten()))
 
     def get_avail_actions(self):
-        return np.array([[1] * self.nA if self.queue[a] else [1] + [0] * (self.nA - 1) for a in range(self.A)])
+        """get_avail_agent_actions (:61-74), incl. the edge_only variant."""
+        busy = [0] + [1] * (self.nA - 1) if self.edge_only else [1] * self.nA
+        return np.array([busy if self.queue[a] else [1] + [0] * (self.nA - 1) for a in range(self.A)])
 
     def get_env_info(self):
         """get_env_info (:421-439): two get_obs calls (normaliser updates)."""

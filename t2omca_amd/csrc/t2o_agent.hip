@@ -29,6 +29,7 @@ struct AgentFwdArgs {
   const float* obs;
   int64_t obs_sb, obs_st;
   int B, T, A, F;
+  int wlds;  // weights staged in LDS (set by the launcher)
 };
 
 template <int E, int H, int D, int NE, int FF>
@@ -37,9 +38,11 @@ __global__ __launch_bounds__(256) void agent_fwd_kernel(AgentFwdArgs args) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const AgentNet net = args.net[blockIdx.y];
   const t2o_layout& L = args.L;
-  // the forward section of the pack lives in LDS for the whole unroll
-  copy_to_lds(smem, net.pack, L.fwd_total);
-  __syncthreads();
+  // the forward section of the pack lives in LDS for the whole unroll (when it fits)
+  if (args.wlds) {
+    copy_to_lds(smem, net.pack, L.fwd_total);
+    __syncthreads();
+  }
   const int A = args.A, F = args.F;
   const int R = args.B * A;
   const int rt = blockIdx.x * 4 + wave_id();
@@ -49,7 +52,7 @@ __global__ __launch_bounds__(256) void agent_fwd_kernel(AgentFwdArgs args) {
   const bool valid = row_raw < R;
   const int row = valid ? row_raw : R - 1;
   const int b = row / A, a = row % A;
-  const float* __restrict__ P = smem;
+  const float* __restrict__ P = args.wlds ? smem : net.pack;
 
   f4 h[ET];
 #pragma unroll
@@ -101,11 +104,13 @@ int launch_fwd(const AgentFwdArgs& args, int nnet, hipStream_t stream) {
   const int R = args.B * args.A;
   const int tiles = (R + 15) / 16;
   dim3 grid((tiles + 3) / 4, nnet);
-  const size_t lds = sizeof(float) * (size_t)args.L.fwd_total;
-  if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
+  AgentFwdArgs a = args;
+  size_t lds = sizeof(float) * (size_t)args.L.fwd_total;
+  a.wlds = lds <= 160 * 1024;
+  if (!a.wlds) lds = 0;
   auto kern = agent_fwd_kernel<E, H, D, NE, FF>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, args);
+  hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, a);
   return (int)hipGetLastError();
 }
 

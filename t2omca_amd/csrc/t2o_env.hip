@@ -1,0 +1,491 @@
+// t2o_env.hip — vectorised MultiAgvOffloadingEnv on MI355X (one wave per env).
+//
+// Reference: environment_multi_mec.py (step :309-366, get_reward :229-293,
+// calculate_offload_delay :106-121, get_agent_inf :123-146, get_obs_agent
+// :148-182, get_obs :184-186, get_state :188-204, reset/reset_user
+// :206-227, update_users :295-307, get_avail_agent_actions :61-74) and
+// normalization.py:4-35, driven with parallel_runner.py's worker protocol
+// (:239-263).  Stand-in constants and the counter-based draw stream:
+// t2omca_amd/env_spec.py (mirrored in EnvSpec below).
+//
+// Exactness.  Decisions (bincount collisions, acks, avail masks, job queues,
+// indices) are integer work and bit-exact.  The float path is IEEE fp64 with
+// FMA contraction OFF so every +,-,*,/,sqrt rounds as numpy/CPython do; the
+// reference's two rounding flavours are reproduced exactly:
+//   numpy   round(np.float64, 2) = rint(x*100)/100
+//   CPython round(float, 2)      = correctly rounded decimal (exact x*100 via fma)
+// Only log10/log2/pow come from the device libm (ocml) instead of glibc; their
+// results pass through a 2-decimal rounding before anything observable, and
+// tests/test_gpu_env.py measures agreement with the numpy oracle.
+#pragma clang fp contract(off)
+#include <math.h>
+
+#include "t2o_common.hpp"
+
+namespace {
+
+struct EnvSpec {
+  double mec_radius, comp_cycles, bandwidth, noise, path_loss, cgl, mec_cap, tx_power, user_cap;
+  int latency_max, t_length, size_min, size_max;
+  double arrival_p;
+  int edge_only;  // get_avail_agent_actions' edge_only variant (:63-68)
+};
+
+struct EnvState {
+  int32_t* mec_index;   // [NE][A]
+  double* x;            // [NE][A]
+  double* y;
+  int32_t* q_size;      // [NE][A][QMAX]
+  int32_t* q_thr;       // [NE][A][QMAX]
+  int32_t* q_head;      // [NE][A]
+  int32_t* q_len;       // [NE][A]
+  int32_t* task_num;    // [NE][A]
+  int32_t* task_success;
+  double* remain_delay;
+  int32_t* last_ack;    // [NE][A]
+  int32_t* time_slot;   // [NE]
+  int64_t* draw;        // [NE]
+  int64_t* nrm_n;       // [NE]
+  double* nrm_mean;     // [NE][9A]
+  double* nrm_S;
+  double* nrm_std;
+};
+
+struct EnvOut {
+  float* obs;           // [NE][A][9A] (may be null)
+  double* obs64;        // [NE][A][9A] (may be null)
+  float* state;         // [NE][8A] (may be null)
+  int32_t* avail;       // [NE][A][nA] (may be null)
+  double* reward;       // [NE]
+  uint8_t* terminated;  // [NE]
+  double* info;         // [NE][6]: delay_reward, overtime, utilization, conflict_ratio,
+                        //          task_completion_rate, task_completion_delay (NaN if not terminal)
+  int32_t* ack;         // [NE][A]
+};
+
+struct EnvArgs {
+  EnvSpec sp;
+  EnvState s;
+  EnvOut o;
+  const int64_t* actions;  // [NE][A] (step)
+  int64_t act_se;          // element stride between envs
+  int NE, A, M, C, QMAX, T;
+  uint64_t seed;
+  int mode;                // 0 init, 1 reset, 2 step, 3 env_info
+};
+
+constexpr int MAXA = 64;
+
+// ---- counter-based uniforms (env_spec.uniforms) -----------------------------
+__device__ double uniform(uint64_t seed, int env, int64_t idx) {
+  uint64_t x = ((uint64_t)env << 40) | (uint64_t)idx;
+  x ^= seed * 0xD1B54A32D192ED03ull;
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z = z ^ (z >> 31);
+  return (double)(z >> 11) * 0x1.0p-53;
+}
+
+__device__ double round2_numpy(double x) { return rint(x * 100.0) / 100.0; }
+
+// CPython round(x, 2): round-half-even of the EXACT value x*100, then /100.
+__device__ double round2_python(double x) {
+  const double p = x * 100.0;
+  const double e = fma(x, 100.0, -p);  // exact: x*100 = p + e
+  double r = rint(p);
+  const double fl = floor(p);
+  if (p - fl == 0.5) {  // p is a half-integer: the exact value decides
+    if (e > 0.0) r = fl + 1.0;
+    else if (e < 0.0) r = fl;
+  }
+  return r / 100.0;
+}
+
+__device__ void mec_pos(const EnvArgs& a, int m, double& mx, double& my) {
+  mx = (double)m * (a.sp.mec_radius * 2) + a.sp.mec_radius;
+  my = a.sp.mec_radius;
+}
+
+__device__ void position(const EnvArgs& a, int m, double u1, double u2, double& x, double& y) {
+  double mx, my;
+  mec_pos(a, m, mx, my);
+  const double aa = 2.0 * u1 - 1.0;
+  const double bb = 2.0 * u2 - 1.0;
+  x = mx + a.sp.mec_radius * aa;
+  y = my + (a.sp.mec_radius * bb) * sqrt(1.0 - aa * aa);
+}
+
+// calculate_offload_delay (:106-121)
+__device__ double offload_delay(const EnvArgs& a, int mec, double x, double y, int size) {
+  double mx, my;
+  mec_pos(a, mec, mx, my);
+  const double dx = x - mx, dy = y - my;
+  const double d = sqrt(dx * dx + dy * dy);
+  const double pl_db = 128.1 + 37.6 * log10(d + 0.1);
+  const double pl = pow(a.sp.path_loss, -pl_db / 10.0);
+  const double rate = a.sp.bandwidth * log2(1.0 + (a.sp.cgl * a.sp.tx_power * pl) / a.sp.noise);
+  const double tx = (double)size / rate * 1000.0;
+  const double cmp = ((double)(a.sp.comp_cycles * size) / a.sp.mec_cap) * 1000.0;
+  return round2_numpy(tx + cmp);
+}
+
+struct AgentView {
+  int mec, len, size, thr, ack;
+  double x, y;
+};
+
+__device__ void load_agent(const EnvArgs& a, int e, int ag, AgentView& v) {
+  const int i = e * a.A + ag;
+  v.mec = a.s.mec_index[i];
+  v.x = a.s.x[i];
+  v.y = a.s.y[i];
+  v.len = a.s.q_len[i];
+  const int h = a.s.q_head[i];
+  v.size = v.len ? a.s.q_size[(size_t)i * a.QMAX + h] : 0;
+  v.thr = v.len ? a.s.q_thr[(size_t)i * a.QMAX + h] : 0;
+  v.ack = a.s.last_ack[i];
+}
+
+// get_agent_inf (:123-146) -> inf[5]
+__device__ void agent_inf(const EnvArgs& a, const AgentView& v, double* inf) {
+  if (v.len) {
+    inf[0] = (double)v.size;
+    inf[1] = rint(((double)(v.size * (int64_t)a.sp.comp_cycles) / a.sp.user_cap) * 1000.0);
+    inf[2] = offload_delay(a, v.mec, v.x, v.y, v.size);
+    inf[3] = (double)v.thr;
+    inf[4] = (double)v.len;
+  } else {
+    inf[0] = inf[1] = inf[2] = inf[3] = inf[4] = 0.0;
+  }
+}
+
+// LDS scratch of one env (one wave)
+struct EnvLds {
+  double inf[MAXA][5];
+  int mec[MAXA];
+  int ack[MAXA];
+  int freq[16][17];
+  double dr[MAXA];
+  double rd[MAXA];
+  int tn[MAXA], ts[MAXA];
+};
+
+// get_obs (:184-186) = A sequential normaliser updates; writes outputs if out != 0.
+// The update count n is kept in a register by every lane (the caller loads and
+// stores it once), so no lane ever reads another lane's global store.
+__device__ void get_obs(const EnvArgs& a, int e, EnvLds& L, bool out, int64_t& n) {
+  const int A = a.A, n9 = 9 * A, lane = threadIdx.x & 63;
+  double* mean = a.s.nrm_mean + (size_t)e * n9;
+  double* S = a.s.nrm_S + (size_t)e * n9;
+  double* sd = a.s.nrm_std + (size_t)e * n9;
+  for (int i = 0; i < A; ++i) {
+    ++n;
+    for (int p = lane; p < n9; p += 64) {
+      const int j = p / 9, f = p % 9;
+      double x = 0.0;
+      if (L.mec[i] == L.mec[j]) {
+        if (f < 3) x = (f == L.ack[j] + 1) ? 1.0 : 0.0;  // ack_mapping: -1 -> [1,0,0], 0 -> [0,1,0], 1 -> [0,0,1]
+        else if (f < 8) x = L.inf[j][f - 3];
+        else x = (i == j) ? 1.0 : 0.0;
+      }
+      double m, s, d;
+      if (n == 1) {
+        m = x;
+        s = S[p];
+        d = x;
+      } else {
+        const double old = mean[p];
+        m = old + (x - old) / (double)n;
+        s = S[p] + (x - old) * (x - m);
+        d = sqrt(s / (double)n);
+      }
+      mean[p] = m;
+      S[p] = s;
+      sd[p] = d;
+      if (out) {
+        const double v = (x - m) / (d + 1e-8);
+        const size_t o = ((size_t)e * A + i) * n9 + p;
+        if (a.o.obs) a.o.obs[o] = (float)v;
+        if (a.o.obs64) a.o.obs64[o] = v;
+      }
+    }
+  }
+}
+
+__device__ void fill_lds(const EnvArgs& a, int e, EnvLds& L) {
+  const int lane = threadIdx.x & 63;
+  if (lane < a.A) {
+    AgentView v;
+    load_agent(a, e, lane, v);
+    L.mec[lane] = v.mec;
+    L.ack[lane] = v.ack;
+    agent_inf(a, v, L.inf[lane]);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __syncthreads();
+}
+
+__device__ void write_state_avail(const EnvArgs& a, int e, const EnvLds& L) {
+  const int A = a.A, lane = threadIdx.x & 63, nA = a.C + 1;
+  if (a.o.state) {
+    for (int p = lane; p < 8 * A; p += 64) {
+      float v;
+      if (p < 3 * A) {
+        const int j = p / 3, f = p % 3;
+        v = (f == L.ack[j] + 1) ? 1.f : 0.f;
+      } else {
+        const int q = p - 3 * A;
+        v = (float)L.inf[q / 5][q % 5];
+      }
+      a.o.state[(size_t)e * 8 * A + p] = v;
+    }
+  }
+  if (a.o.avail && lane < A) {
+    const bool has = a.s.q_len[e * A + lane] > 0;
+    for (int k = 0; k < nA; ++k)
+      a.o.avail[((size_t)e * A + lane) * nA + k] = has ? (a.sp.edge_only ? k != 0 : 1) : k == 0;
+  }
+}
+
+__device__ void generate_job(const EnvArgs& a, int i, double u1, double u2) {
+  if (u1 < a.sp.arrival_p) {
+    const int len = a.s.q_len[i];
+    const int slot = (a.s.q_head[i] + len) % a.QMAX;
+    a.s.q_size[(size_t)i * a.QMAX + slot] = a.sp.size_min + (int)(u2 * (double)(a.sp.size_max - a.sp.size_min + 1));
+    a.s.q_thr[(size_t)i * a.QMAX + slot] = a.sp.latency_max;
+    a.s.q_len[i] = len + 1;
+    a.s.task_num[i] += 1;
+  }
+}
+
+__global__ __launch_bounds__(64) void env_kernel(EnvArgs a) {
+  __shared__ EnvLds L;
+  const int e = blockIdx.x;
+  const int A = a.A, M = a.M, C = a.C, lane = threadIdx.x;
+  if (e >= a.NE) return;
+  const int64_t base = a.mode == 0 ? 0 : a.s.draw[e];
+  if (a.mode == 0) {  // construction (:25-40): mec_index + position per agent
+    if (lane < A) {
+      const int i = e * A + lane;
+      const double u0 = uniform(a.seed, e, base + 3 * lane), u1 = uniform(a.seed, e, base + 3 * lane + 1),
+                   u2 = uniform(a.seed, e, base + 3 * lane + 2);
+      const int m = (int)(u0 * (double)M);
+      a.s.mec_index[i] = m;
+      position(a, m, u1, u2, a.s.x[i], a.s.y[i]);
+      a.s.q_head[i] = a.s.q_len[i] = 0;
+      a.s.task_num[i] = a.s.task_success[i] = 0;
+      a.s.remain_delay[i] = 0.0;
+      a.s.last_ack[i] = 0;
+    }
+    for (int p = lane; p < 9 * A; p += 64) {
+      const size_t q = (size_t)e * 9 * A + p;
+      a.s.nrm_mean[q] = a.s.nrm_S[q] = a.s.nrm_std[q] = 0.0;
+    }
+    if (lane == 0) {
+      a.s.nrm_n[e] = 0;
+      a.s.time_slot[e] = 0;
+      a.s.draw[e] = base + 3 * A;
+    }
+    return;
+  }
+  if (a.mode == 3) {  // get_env_info (:421-439): two get_obs calls
+    int64_t n = a.s.nrm_n[e];
+    fill_lds(a, e, L);
+    get_obs(a, e, L, false, n);
+    get_obs(a, e, L, false, n);
+    if (lane == 0) a.s.nrm_n[e] = n;
+    return;
+  }
+  if (a.mode == 1) {  // reset (:219-227), then the worker's get_state/get_avail/get_obs
+    if (lane < A) {
+      const int i = e * A + lane;
+      const int64_t b = base + 5 * lane;
+      const int m = (int)(uniform(a.seed, e, b) * (double)M);
+      position(a, m, uniform(a.seed, e, b + 1), uniform(a.seed, e, b + 2), a.s.x[i], a.s.y[i]);
+      a.s.q_head[i] = a.s.q_len[i] = 0;
+      a.s.task_num[i] = a.s.task_success[i] = 0;
+      a.s.remain_delay[i] = 0.0;
+      generate_job(a, i, uniform(a.seed, e, b + 3), uniform(a.seed, e, b + 4));
+      a.s.last_ack[i] = 0;
+    }
+    if (lane == 0) {
+      a.s.time_slot[e] = 0;
+      a.s.draw[e] = base + 5 * A;
+    }
+    __syncthreads();
+    int64_t n = a.s.nrm_n[e];
+    fill_lds(a, e, L);
+    get_obs(a, e, L, false, n);  // reset()'s own get_obs
+    write_state_avail(a, e, L);
+    get_obs(a, e, L, true, n);   // the worker's get_obs
+    if (lane == 0) a.s.nrm_n[e] = n;
+    return;
+  }
+  // ---- step (:309-366)
+  for (int k = lane; k < 16 * 17; k += 64) (&L.freq[0][0])[k] = 0;
+  __syncthreads();
+  AgentView v;
+  int act = 0;
+  if (lane < A) {
+    load_agent(a, e, lane, v);
+    act = (int)a.actions[(int64_t)e * a.act_se + lane];
+    act = act < 0 ? 0 : (act > C ? C : act);  // actions come from avail-masked selection; clamp keeps LDS in bounds
+    atomicAdd(&L.freq[v.mec][act], 1);
+  }
+  __syncthreads();
+  int ack = 0;
+  if (lane < A) {
+    if (act == 0) ack = 0;
+    else ack = (L.freq[v.mec][act] == 1) ? 1 : -1;
+  }
+  const unsigned long long confl = __ballot(lane < A && ack == -1);
+  // get_reward (:229-293): per-agent terms, summed in agent order below
+  double dr = 0.0, rd_inc = 0.0;
+  int over = 0, succ = 0;
+  bool has_dr = false;
+  if (lane < A && v.len) {
+    const double local = round2_python(((double)(a.sp.comp_cycles * v.size) / a.sp.user_cap) * 1000.0);
+    if (ack == 0) {
+      if ((double)v.thr - local > 0) {
+        succ = 1;
+        rd_inc = (double)(a.sp.latency_max - v.thr) + local;
+      } else {
+        over = a.sp.latency_max;
+      }
+    } else if (ack == -1) {
+      if (v.thr - a.sp.t_length <= 0) over = a.sp.latency_max;
+    } else {
+      const double off = offload_delay(a, v.mec, v.x, v.y, v.size);
+      dr = local - off;
+      has_dr = true;
+      if ((double)v.thr - off > 0) {
+        succ = 1;
+        rd_inc = (double)(a.sp.latency_max - v.thr) + off;
+      } else {
+        over = a.sp.latency_max;
+      }
+    }
+  }
+  if (lane < A) {
+    L.dr[lane] = has_dr ? dr : NAN;
+    L.ack[lane] = ack;
+    L.mec[lane] = v.mec;
+    L.tn[lane] = over;
+  }
+  __syncthreads();
+  if (lane == 0) {
+    // channel utilisation (:321-329): counts > 1 zeroed, Python sums in order
+    double util = 0.0;
+    for (int m = 0; m < M; ++m) {
+      double s = 0.0;
+      for (int c = 0; c <= C; ++c) {
+        const int f = L.freq[m][c] > 1 ? 0 : L.freq[m][c];
+        s = s + (double)f / (double)C;
+      }
+      util = util + s;
+    }
+    util = util / (double)M;
+    double delay_reward = 0.0;
+    int overtime = 0;
+    for (int ag = 0; ag < A; ++ag) {
+      if (!isnan(L.dr[ag])) delay_reward = delay_reward + L.dr[ag];
+      overtime += L.tn[ag];
+    }
+    a.o.reward[e] = delay_reward - (double)overtime;
+    double* info = a.o.info + (size_t)e * 6;
+    info[0] = delay_reward;
+    info[1] = (double)overtime;
+    info[2] = util;
+    info[3] = (double)__popcll(confl) / (double)A;
+    info[4] = info[5] = NAN;
+  }
+  __syncthreads();
+  // update_users (:295-307) after the reward, agent by agent (independent)
+  if (lane < A) {
+    const int i = e * A + lane;
+    a.s.last_ack[i] = ack;
+    if (a.o.ack) a.o.ack[i] = ack;
+    a.s.task_success[i] += succ;
+    a.s.remain_delay[i] = a.s.remain_delay[i] + rd_inc;
+    const int64_t b = base + 5 * lane;
+    const int m = (int)(uniform(a.seed, e, b) * (double)M);
+    position(a, m, uniform(a.seed, e, b + 1), uniform(a.seed, e, b + 2), a.s.x[i], a.s.y[i]);
+    int head = a.s.q_head[i], len = a.s.q_len[i];
+    if (ack != -1 && len > 0) {
+      head = (head + 1) % a.QMAX;
+      --len;
+    }
+    for (int k = 0; k < len; ++k) a.s.q_thr[(size_t)i * a.QMAX + (head + k) % a.QMAX] -= 5;
+    while (len > 0 && a.s.q_thr[(size_t)i * a.QMAX + head] <= 0) {  // expired jobs are a FIFO prefix
+      head = (head + 1) % a.QMAX;
+      --len;
+    }
+    a.s.q_head[i] = head;
+    a.s.q_len[i] = len;
+    generate_job(a, i, uniform(a.seed, e, b + 3), uniform(a.seed, e, b + 4));
+    L.tn[lane] = a.s.task_num[i];
+    L.ts[lane] = a.s.task_success[i];
+    L.rd[lane] = a.s.remain_delay[i];
+  }
+  __syncthreads();
+  if (lane == 0) {
+    a.s.draw[e] = base + 5 * A;
+    const int ts = a.s.time_slot[e] + 1;
+    a.s.time_slot[e] = ts;
+    const bool term = ts == a.T;
+    a.o.terminated[e] = term ? 1 : 0;
+    if (term) {  // get_task_num (:368-415)
+      int tn = 0, tsu = 0;
+      double rd = 0.0;
+      for (int ag = 0; ag < A; ++ag) {
+        tn += L.tn[ag];
+        tsu += L.ts[ag];
+        rd = rd + L.rd[ag];
+      }
+      double* info = a.o.info + (size_t)e * 6;
+      info[4] = (double)tsu / (double)tn;
+      info[5] = tsu != 0 ? rd / (double)tsu : 0.0;
+    }
+  }
+  __syncthreads();
+  // the worker's get_state / get_avail_actions / get_obs on the new state
+  int64_t n = a.s.nrm_n[e];
+  fill_lds(a, e, L);
+  write_state_avail(a, e, L);
+  get_obs(a, e, L, true, n);
+  if (lane == 0) a.s.nrm_n[e] = n;
+}
+
+}  // namespace
+
+extern "C" int t2o_env_run(int mode, const double* spec, void* const* state, void* const* out,
+                           const int64_t* actions, int64_t act_se, int NE, int A, int M, int C, int QMAX, int T,
+                           uint64_t seed, void* stream) {
+  if (NE < 1 || A < 1 || A > MAXA || M < 1 || M > 16 || C < 1 || C > 16 || QMAX < 1 || !spec || !state ||
+      (mode == 2 && (!actions || !out)) || (mode == 1 && !out) || mode < 0 || mode > 3)
+    return T2O_EINVAL;
+  EnvArgs a{};
+  a.sp = EnvSpec{spec[0], spec[1], spec[2], spec[3], spec[4], spec[5], spec[6], spec[7], spec[8],
+                 (int)spec[9], (int)spec[10], (int)spec[11], (int)spec[12], spec[13], spec[14] != 0.0};
+  a.s = EnvState{(int32_t*)state[0], (double*)state[1], (double*)state[2], (int32_t*)state[3],
+                 (int32_t*)state[4], (int32_t*)state[5], (int32_t*)state[6], (int32_t*)state[7],
+                 (int32_t*)state[8], (double*)state[9], (int32_t*)state[10], (int32_t*)state[11],
+                 (int64_t*)state[12], (int64_t*)state[13], (double*)state[14], (double*)state[15],
+                 (double*)state[16]};
+  if (out)
+    a.o = EnvOut{(float*)out[0], (double*)out[1], (float*)out[2], (int32_t*)out[3], (double*)out[4],
+                 (uint8_t*)out[5], (double*)out[6], (int32_t*)out[7]};
+  a.actions = actions;
+  a.act_se = act_se;
+  a.NE = NE;
+  a.A = A;
+  a.M = M;
+  a.C = C;
+  a.QMAX = QMAX;
+  a.T = T;
+  a.seed = seed;
+  a.mode = mode;
+  hipLaunchKernelGGL(env_kernel, dim3(NE), dim3(64), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}

@@ -44,6 +44,7 @@ struct MixerFwdArgs {
   const int32_t* avail;  // [b][t][a][NA]
   int64_t av_sb, av_st;
   int B, Fs;
+  int waves, wlds;  // set by the launcher
 };
 
 template <int E, int A>
@@ -155,12 +156,15 @@ __global__ __launch_bounds__(256) void mixer_fwd_kernel(MixerFwdArgs args) {
   const int w = wave_id();
   const MixerNet n = args.net[blockIdx.y];
   const t2o_layout& L = args.L;
-  const int lds_w = (int)((L.fwd_total + 15) / 16 * 16);
-  copy_to_lds(smem, n.pack, L.fwd_total);  // forward weights in LDS for the unroll
-  __syncthreads();
-  const int b = blockIdx.x * 4 + w;
+  // forward weights in LDS for the unroll when they fit beside the per-wave buffers
+  const int lds_w = args.wlds ? (int)((L.fwd_total + 15) / 16 * 16) : 0;
+  if (args.wlds) {
+    copy_to_lds(smem, n.pack, L.fwd_total);
+    __syncthreads();
+  }
+  const int b = blockIdx.x * args.waves + w;
   if (b >= args.B) return;  // wave-uniform; no block barriers after this point
-  const float* __restrict__ P = smem;
+  const float* __restrict__ P = args.wlds ? smem : n.pack;
   float* X0 = smem + lds_w + w * (Dm::X0F + Dm::OUTF);
   float* OUT = X0 + Dm::X0F;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
@@ -219,12 +223,24 @@ __global__ __launch_bounds__(256) void mixer_fwd_kernel(MixerFwdArgs args) {
 template <int E, int H, int D, int A, int FF>
 int launch_mixer_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
   using Dm = MixDims<E, A>;
-  const size_t lds = sizeof(float) * ((args.L.fwd_total + 15) / 16 * 16 + 4 * (Dm::X0F + Dm::OUTF));
-  if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
+  MixerFwdArgs a = args;
+  const size_t wfl = (args.L.fwd_total + 15) / 16 * 16, perw = Dm::X0F + Dm::OUTF;
+  size_t lds = 0;
+  // 4 waves with LDS weights, else 2, else 4 waves reading weights from HBM/L2
+  for (a.waves = 4, a.wlds = 1; a.waves >= 2; a.waves >>= 1) {
+    lds = sizeof(float) * (wfl + a.waves * perw);
+    if (lds <= 160 * 1024) break;
+  }
+  if (a.waves < 2) {
+    a.waves = 4;
+    a.wlds = 0;
+    lds = sizeof(float) * 4 * perw;
+    if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
+  }
   auto kern = mixer_fwd_kernel<E, H, D, A, FF>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  dim3 grid((args.B + 3) / 4, nnet);
-  hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, args);
+  dim3 grid((args.B + a.waves - 1) / a.waves, nnet);
+  hipLaunchKernelGGL(kern, grid, dim3(64 * a.waves), lds, stream, a);
   return (int)hipGetLastError();
 }
 

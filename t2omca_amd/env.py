@@ -1,0 +1,129 @@
+"""Vectorised MEC-offloading environment on the HIP device.
+
+``VecEnv`` advances ``n_envs`` copies of ``MultiAgvOffloadingEnv``
+(environment_multi_mec.py:9-439) in lock-step through ``t2o_env_run``
+(include/t2omca.h), with the per-env state resident in device memory.  The
+methods are the batched form of parallel_runner.py's env-worker protocol
+(:224-270):
+
+    get_env_info()     -> dict            ('get_env_info', env 0 only, :34)
+    reset()            -> state, avail, obs                       (:257-263)
+    step(actions)      -> reward, terminated, info, state, avail, obs (:239-256)
+
+Shapes: obs [n_envs, A, 9A] f32, state [n_envs, 8A] f32, avail
+[n_envs, A, nA] i32, reward [n_envs] f64, terminated [n_envs] bool, info a dict
+of [n_envs] f64 tensors (task_completion_* are NaN except on the terminal step).
+Every launch goes on the current HIP stream; nothing synchronises with the host.
+
+Random draws are env_spec.uniforms(seed, env, draw) instead of the reference's
+unseeded global numpy RNG; the stand-in constants are env_spec's.
+"""
+import ctypes
+
+import torch
+
+from . import env_spec as S
+from ._lib import check, lib, stream_ptr
+
+INFO_KEYS = ("delay_reward", "overtime_penalty", "channel_utilization_rate", "conflict_ratio",
+             "task_completion_rate", "task_completion_delay")
+
+
+def spec_vector(edge_only=False):
+    """The fp64 spec[15] of t2o_env_run from env_spec's constants."""
+    return [S.MEC_RADIUS, float(S.COMPUTATION_CYCLES), S.BANDWIDTH, S.NOISE_POWER, float(S.PATH_LOSS),
+            10 ** (S.CHANNEL_GAIN / 10), S.MEC_COMPUTE_CAP, S.AGV_TRANSMIT_POWER, S.AGV_COMPUTE_CAP,
+            float(S.LATENCY_MAX), float(S.T_LENGTH), float(S.JOB_SIZE_MIN), float(S.JOB_SIZE_MAX),
+            S.JOB_ARRIVAL_P, 1.0 if edge_only else 0.0]
+
+
+class VecEnv:
+    def __init__(self, n_envs, mec_num=2, agv_num=16, num_channels=4, episode_limit=150, seed=0,
+                 edge_only=False, device="cuda", keep_obs64=False):
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise RuntimeError("VecEnv runs on the HIP device only (the numpy restatement in oracle/ is test-only)")
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        if not (1 <= agv_num <= 64 and 1 <= mec_num <= 16 and 1 <= num_channels <= 16):
+            raise ValueError("VecEnv supports agv_num <= 64, mec_num <= 16, num_channels <= 16")
+        self.n_envs, self.M, self.A, self.C = n_envs, mec_num, agv_num, num_channels
+        self.T, self.seed, self.device = episode_limit, int(seed), device
+        self.n_actions = num_channels + 1
+        self.qmax = S.QMAX
+        NE, A, Q = n_envs, agv_num, S.QMAX
+        i32 = dict(dtype=torch.int32, device=device)
+        f64 = dict(dtype=torch.float64, device=device)
+        self._state = [
+            torch.zeros(NE, A, **i32), torch.zeros(NE, A, **f64), torch.zeros(NE, A, **f64),
+            torch.zeros(NE, A, Q, **i32), torch.zeros(NE, A, Q, **i32), torch.zeros(NE, A, **i32),
+            torch.zeros(NE, A, **i32), torch.zeros(NE, A, **i32), torch.zeros(NE, A, **i32),
+            torch.zeros(NE, A, **f64), torch.zeros(NE, A, **i32), torch.zeros(NE, **i32),
+            torch.zeros(NE, dtype=torch.int64, device=device), torch.zeros(NE, dtype=torch.int64, device=device),
+            torch.zeros(NE, 9 * A, **f64), torch.zeros(NE, 9 * A, **f64), torch.zeros(NE, 9 * A, **f64),
+        ]
+        self._spec = torch.tensor(spec_vector(edge_only), dtype=torch.float64, device=device)
+        self.obs = torch.empty(NE, A, 9 * A, dtype=torch.float32, device=device)
+        self.obs64 = torch.empty(NE, A, 9 * A, **f64) if keep_obs64 else None
+        self.state = torch.empty(NE, 8 * A, dtype=torch.float32, device=device)
+        self.avail = torch.empty(NE, A, self.n_actions, **i32)
+        self.reward = torch.empty(NE, **f64)
+        self.terminated = torch.empty(NE, dtype=torch.uint8, device=device)
+        self.info = torch.empty(NE, 6, **f64)
+        self.ack = torch.empty(NE, A, **i32)
+        self._run(0)  # construction
+
+    # -- raw launches --------------------------------------------------------------
+    def _ptrs(self, ts):
+        arr = (ctypes.c_void_p * len(ts))()
+        for i, t in enumerate(ts):
+            arr[i] = None if t is None else t.data_ptr()
+        return arr
+
+    def _run(self, mode, actions=None, n_envs=None):
+        out = self._ptrs([self.obs, self.obs64, self.state, self.avail, self.reward, self.terminated,
+                          self.info, self.ack])
+        act_p, act_se = None, 0
+        if actions is not None:
+            act_p, act_se = ctypes.c_void_p(actions.data_ptr()), actions.stride(0)
+        rc = lib().t2o_env_run(mode, ctypes.c_void_p(self._spec.data_ptr()), self._ptrs(self._state), out,
+                               act_p, act_se, n_envs or self.n_envs, self.A, self.M, self.C, self.qmax,
+                               self.T, ctypes.c_uint64(self.seed & ((1 << 64) - 1)),
+                               stream_ptr(self.device))
+        check(rc, "env_run")
+
+    # -- worker protocol, batched ------------------------------------------------------
+    def get_env_info(self, all_envs=False):
+        """get_env_info (:421-439) on env 0, as the runner does once at start-up (:34);
+        all_envs=True calls it on every env (as a standalone env object per env would)."""
+        self._run(3, n_envs=None if all_envs else 1)
+        return dict(state_shape=8 * self.A, obs_shape=9 * self.A, n_actions=self.n_actions,
+                    n_agents=self.A, episode_limit=self.T, n_entities=self.A, obs_entity_feats=9,
+                    state_entity_feats=8)
+
+    def reset(self):
+        self._run(1)
+        return self.state, self.avail, self.obs
+
+    def step(self, actions):
+        """actions: int64 [n_envs, A] on the device (rows may be strided views)."""
+        if actions.dtype != torch.int64 or actions.device != self.device or actions.dim() != 2:
+            raise TypeError("actions must be an int64 [n_envs, A] device tensor")
+        if actions.shape != (self.n_envs, self.A) or actions.stride(1) != 1:
+            raise ValueError(f"actions must be [{self.n_envs}, {self.A}] with unit agent stride")
+        self._run(2, actions=actions)
+        info = {k: self.info[:, i] for i, k in enumerate(INFO_KEYS)}
+        return self.reward, self.terminated.bool(), info, self.state, self.avail, self.obs
+
+    # -- state views (tests / diagnostics) ----------------------------------------------
+    @property
+    def mec_index(self):
+        return self._state[0]
+
+    @property
+    def queue_len(self):
+        return self._state[6]
+
+    @property
+    def draws(self):
+        return self._state[12]

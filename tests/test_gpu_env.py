@@ -1,0 +1,120 @@
+"""GPU: the HIP env (t2o_env.hip via t2omca_amd.env.VecEnv) against the reference env's own
+trajectories (tests/golden/env_*.npz) and against the numpy restatement (oracle/ref_env.py) on
+larger random rollouts.  Bar: bit-exact -- integer/decision outputs equal, fp64 outputs equal
+to the last bit, f32 outputs equal to the f32 cast of the fp64 reference values."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.ref_env import RefEnv
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+INFO = {"delay_reward": "delay_reward", "overtime_penalty": "overtime_penalty",
+        "channel_utilization_rate": "utilization", "conflict_ratio": "conflict_ratio",
+        "task_completion_rate": "task_completion_rate", "task_completion_delay": "task_completion_delay"}
+
+
+def _eq(got, ref, what):
+    got = np.asarray(got)
+    ref = np.asarray(ref)
+    assert got.shape == ref.shape, (what, got.shape, ref.shape)
+    if got.dtype.kind == "f" or ref.dtype.kind == "f":
+        g, r = np.asarray(got, np.float64), np.asarray(ref, np.float64)
+        bad = ~((g == r) | (np.isnan(g) & np.isnan(r)))
+        assert not bad.any(), f"{what}: {bad.sum()} mismatches, e.g. {g[bad][:4]} vs {r[bad][:4]}"
+    else:
+        assert np.array_equal(got, ref), what
+
+
+def _check_obs(env, ref_obs64, what):
+    _eq(env.obs64.cpu().numpy(), ref_obs64, what + "/obs64")
+    _eq(env.obs.cpu().numpy(), np.asarray(ref_obs64, np.float32), what + "/obs")
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "env_*.npz"))))
+def test_env_matches_reference_trajectories(path):
+    from t2omca_amd.env import VecEnv
+    z = np.load(path)
+    M, A, T, eps, seed = (int(z[k]) for k in ("M", "A", "T", "episodes", "seed"))
+    NE = len({k.split("/")[0] for k in z.files if k.startswith("env")})
+    env = VecEnv(NE, mec_num=M, agv_num=A, episode_limit=T, seed=seed, keep_obs64=True)
+    _eq(env.mec_index.cpu().numpy(), np.stack([z[f"env{e}/mec_index"] for e in range(NE)]), "mec_index")
+    env.get_env_info(all_envs=True)
+    gold = {k: np.stack([z[f"env{e}/{k}"] for e in range(NE)]) for k in
+            ("obs", "state", "avail", "actions", "reward", "ack", "terminated", "utilization", "conflict_ratio",
+             "delay_reward", "overtime_penalty", "task_completion_rate", "task_completion_delay", "draws")}
+    k = j = 0
+    for _ in range(eps):
+        st, av, _ = env.reset()
+        _eq(st.cpu().numpy(), gold["state"][:, j].astype(np.float32), "reset/state")
+        _eq(av.cpu().numpy(), gold["avail"][:, j], "reset/avail")
+        _check_obs(env, gold["obs"][:, j], "reset")
+        j += 1
+        for _ in range(T):
+            acts = torch.from_numpy(gold["actions"][:, k].astype(np.int64)).cuda()
+            r, d, info, st, av, _ = env.step(acts)
+            _eq(r.cpu().numpy(), gold["reward"][:, k], "reward")
+            _eq(d.cpu().numpy(), gold["terminated"][:, k], "terminated")
+            _eq(env.ack.cpu().numpy(), gold["ack"][:, k], "ack")
+            for key, g in INFO.items():
+                _eq(info[key].cpu().numpy(), gold[g][:, k], key)
+            _eq(st.cpu().numpy(), gold["state"][:, j].astype(np.float32), "state")
+            _eq(av.cpu().numpy(), gold["avail"][:, j], "avail")
+            _check_obs(env, gold["obs"][:, j], f"step{k}")
+            k += 1
+            j += 1
+    _eq(env.draws.cpu().numpy(), gold["draws"], "draws")
+
+
+def _rollout_vs_oracle(NE, M, A, T, eps, seed, edge_only=False, runner_info=True):
+    from t2omca_amd.env import VecEnv
+    env = VecEnv(NE, mec_num=M, agv_num=A, episode_limit=T, seed=seed, edge_only=edge_only, keep_obs64=True)
+    refs = [RefEnv(M, A, T, seed, e, edge_only=edge_only) for e in range(NE)]
+    if runner_info:  # the runner's get_env_info touches env 0 only (parallel_runner.py:34)
+        env.get_env_info()
+        refs[0].get_env_info()
+    rng = np.random.default_rng(seed)
+    for _ in range(eps):
+        st, av, _ = env.reset()
+        outs = [r.worker_reset() for r in refs]
+        _eq(st.cpu().numpy(), np.stack([o[0] for o in outs]).astype(np.float32), "reset/state")
+        _eq(av.cpu().numpy(), np.stack([o[1] for o in outs]), "reset/avail")
+        _check_obs(env, np.stack([o[2] for o in outs]), "reset")
+        for t in range(T):
+            avn = av.cpu().numpy()
+            acts = np.array([[rng.choice(np.nonzero(avn[e, i])[0]) for i in range(A)] for e in range(NE)])
+            r, d, info, st, av, _ = env.step(torch.from_numpy(acts).cuda())
+            outs = [ref.worker_step(acts[e]) for e, ref in enumerate(refs)]
+            _eq(r.cpu().numpy(), np.array([o[0] for o in outs], np.float64), "reward")
+            _eq(d.cpu().numpy(), np.array([o[1] for o in outs]), "terminated")
+            _eq(env.ack.cpu().numpy(), np.stack([ref.last_ack for ref in refs]), "ack")
+            for key in INFO:
+                _eq(info[key].cpu().numpy(), np.array([o[2].get(key, np.nan) for o in outs], np.float64), key)
+            _eq(st.cpu().numpy(), np.stack([o[3] for o in outs]).astype(np.float32), "state")
+            _eq(av.cpu().numpy(), np.stack([o[4] for o in outs]), "avail")
+            _check_obs(env, np.stack([o[5] for o in outs]), f"t{t}")
+            ql = env.queue_len.cpu().numpy()
+            assert np.array_equal(ql, np.array([[len(q) for q in ref.queue] for ref in refs]))
+            assert ql.max() <= env.qmax
+    _eq(env.draws.cpu().numpy(), np.array([ref.draw for ref in refs]), "draws")
+
+
+def test_env_rollout_config3_shape_vs_oracle():
+    _rollout_vs_oracle(NE=24, M=4, A=8, T=14, eps=2, seed=99)
+
+
+def test_env_rollout_config4_shape_vs_oracle():
+    _rollout_vs_oracle(NE=3, M=16, A=64, T=6, eps=1, seed=5)
+
+
+def test_env_rollout_edge_only_vs_oracle():
+    _rollout_vs_oracle(NE=8, M=2, A=16, T=8, eps=1, seed=3, edge_only=True, runner_info=False)
+
+
+def test_env_single_agent_and_channel_extremes():
+    _rollout_vs_oracle(NE=4, M=1, A=1, T=12, eps=2, seed=11)
+    _rollout_vs_oracle(NE=4, M=3, A=5, T=12, eps=1, seed=12)
