@@ -108,13 +108,16 @@ int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, const float*
  * strides act_sb, act_st, a-stride 1); gh[b][t][a][E] (may be NULL).
  * Outputs: gslabs[nslab][grad_total] per-workgroup partial gradients (compact
  * layout, overwritten; *nslab = number written, at most max_slabs =
- * t2o_agent_bwd_max_slabs(B, A)); gh0[b][a][E] = dL/dh0 (may be NULL). */
+ * t2o_agent_bwd_max_slabs(B, A)); gh0[b][a][E] = dL/dh0 (may be NULL).
+ * Workspace: tape, t2o_bwd_tape_floats(L, T*B*A) floats — the per-record
+ * operand pairs of the M/N/W1/W2 weight grads, contracted by a second launch
+ * (t2o_dwgemm.hpp) on the same stream before this call returns. */
 int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack,
                          const float* obs, int64_t obs_sb, int64_t obs_st,
                          const float* h0, const float* h_seq, const float* hmid, int h_ts,
                          const float* gq, const float* gchosen, const int64_t* actions,
                          int64_t act_sb, int64_t act_st, const float* gh,
-                         float* gslabs, int max_slabs, int* nslab, float* gh0,
+                         float* gslabs, int max_slabs, int* nslab, float* tape, float* gh0,
                          int B, int T, int A, void* stream);
 int t2o_agent_bwd_max_slabs(int B, int A);
 
@@ -147,14 +150,18 @@ int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, const float*
  * hw / xout / xmid = forward outputs (xmid may be NULL).  gy[B][T] = dL/dy; ghw_ext [B][T][3][E] optional
  * extra grad on the hyper outputs.  Outputs: gqv[B][T][A] (dL/dqvals),
  * ghid[B][T][A][E] (dL/dhidden states), ghw0[B][3][E] (may be NULL), partial
- * weight-grad slabs as for the agent (max_slabs = t2o_mixer_bwd_max_slabs(B)). */
+ * weight-grad slabs as for the agent (max_slabs = t2o_mixer_bwd_max_slabs(B)),
+ * tape workspace of t2o_bwd_tape_floats(L, B*T*(A+3)) floats. */
 int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, const float* states,
                          int64_t st_sb, int64_t st_st, const float* hid, int64_t hid_sb,
                          int64_t hid_st, const float* hw0, const float* qv, const float* hw,
                          const float* xout, const float* xmid, const float* gy, const float* ghw_ext, float* gqv,
-                         float* ghid, float* ghw0, float* gslabs, int max_slabs, int* nslab,
+                         float* ghid, float* ghw0, float* gslabs, int max_slabs, int* nslab, float* tape,
                          int B, int T, void* stream);
 int t2o_mixer_bwd_max_slabs(int B);
+
+/* Floats of backward tape workspace for `records` records (D * records * (4E + 2HE + 2FF)). */
+int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t records);
 
 /* TD(λ) targets, masked PER-weighted loss, dL/dQtot and priorities
  * (PyMARL2 NQLearner semantics; see t2o_learner.hip).  qtot [B][T] (online

@@ -9,6 +9,7 @@
 // run in the same launch on the same observations (blockIdx.y).
 #include "t2o_agent_block.hpp"
 #include "t2o_dispatch.hpp"
+#include "t2o_dwgemm.hpp"
 #include "t2o_layout.hpp"
 
 using namespace t2o;
@@ -116,13 +117,16 @@ int launch_fwd(const AgentFwdArgs& args, int nnet, hipStream_t stream) {
 
 
 // ---------------------------------------------------------------------------
-// BPTT.  One workgroup = 4 waves = 64 sequences; each wave walks its 16
-// sequences backwards over t.  Per step it recomputes the step's forward from
-// the stored h_{t-1} (blocks 0..D-2 plain, then each block again with its
-// cache right before its backward), back-propagates the incoming grads
-// (dL/dq_t, dL/dh_t from the mixer and from step t+1) and produces dL/dh_{t-1}.
-// Weight grads go to an LDS gradient block shared by the 4 waves (ds_add_f32);
-// at the end the workgroup writes it as one slab.
+// BPTT.  One wave walks 16 sequences backwards over t; a workgroup holds
+// AG_BWD_WAVES waves and one LDS copy of the forward weights (the forward
+// section of the pack; transposed products read it with matvec_t).  Per step
+// it recomputes the step's forward from the stored h_{t-1} and block inputs
+// (hmid), then back-propagates the incoming grads (dL/dq_t, dL/dh_t from the
+// mixer and from step t+1) and produces dL/dh_{t-1}.  Weight grads:
+//   M, N, W1, W2   operand pairs -> tape record (step*R + row, per block);
+//                  t2o_dwgemm.hpp contracts them into slab k afterwards
+//   We, Wo         MFMA register blocks for the whole unroll, flushed once
+//   vectors        DPP row sums + float atomics into the workgroup's slab
 struct AgentBwdArgs {
   t2o_layout L, G;
   const float* pack;
@@ -138,9 +142,9 @@ struct AgentBwdArgs {
   int64_t act_sb, act_st;
   const float* gh;
   float* slabs;
+  float* tape;  // [D][T*B*A][TapeRec::SIZE]
   float* gh0;
   int B, T, A, F;
-  int lds_grad;  // floats reserved for the gradient block (>= G.grad_total)
 };
 
 constexpr int AG_BWD_WAVES = 2;  // 32 sequences per workgroup: B*A/32 workgroups cover every CU
@@ -148,13 +152,16 @@ constexpr int AG_BWD_WAVES = 2;  // 32 sequences per workgroup: B*A/32 workgroup
 template <int E, int H, int D, int NE, int FF>
 __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdArgs args) {
   constexpr int ET = E / 16;
-  constexpr int STAGE = StageDims<ET>::FLOATS;
+  constexpr int STAGE = StageDims<1>::FLOATS;
+  using Rec = TapeRec<E, H, FF>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const t2o_layout& L = args.L;
   const t2o_layout& G = args.G;
-  float* lg = smem;
-  float* stage = smem + args.lds_grad + wave_id() * STAGE;
-  for (int i = threadIdx.x; i < args.lds_grad; i += blockDim.x) lg[i] = 0.f;
+  const int lds_w = (int)((L.fwd_total + 15) / 16 * 16);
+  float* stage = smem + lds_w + wave_id() * STAGE;
+  float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
+  copy_to_lds(smem, args.pack, L.fwd_total);
+  for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) gs[i] = 0.f;
   __syncthreads();
 
   const int A = args.A, F = args.F, T = args.T;
@@ -165,9 +172,13 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
   const bool valid = row_raw < R;
   const int row = valid ? row_raw : R - 1;
   const int b = row / A, a = row % A;
-  const float* __restrict__ P = args.pack;
+  const float* __restrict__ P = smem;
+  const size_t nrec = (size_t)T * R;
 
   if (rt * 16 < R) {
+    f4 gWe[ET][1], gWo[1][ET];
+#pragma unroll
+    for (int t = 0; t < ET; ++t) gWe[t][0] = gWo[0][t] = zero4();
     f4 gh_rec[ET];
 #pragma unroll
     for (int t = 0; t < ET; ++t) gh_rec[t] = zero4();
@@ -244,20 +255,18 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
 #pragma unroll
         for (int t = 0; t < ET; ++t) x[t] = xs[d][t];
         agent_block_fwd<E, H, NE, FF, true>(P, L, d, h, o, x, &cache);
-        T2O_FENCE();
         if (d == D - 1) {  // q = Wo x + bo
-          dw_accumulate<1, ET>(lg + G.Wo, E, &gq, x, stage);
-          vec_accumulate<1>(lg + G.bo, &gq);
+          dw_accumulate_regs<1, ET>(gWo, &gq, x, stage);
+          vec_accumulate_g<1>(gs + G.bo, &gq);
           f4 t1[ET];
-          matvec<ET, 1>(P + L.WoT, 16, &gq, t1);
+          matvec_t<ET, 1>(P + L.Wo, E, &gq, t1);
 #pragma unroll
           for (int t = 0; t < ET; ++t) gx[t] += t1[t];
         }
-        T2O_FENCE();
-        agent_block_bwd<E, H, NE, FF>(P, L, G, lg, stage, d, h, o, cache, gx, gh_in, gbe);
-        T2O_FENCE();
+        float* rec = valid ? args.tape + ((size_t)d * nrec + (size_t)step * R + row) * Rec::SIZE : nullptr;
+        agent_block_bwd<E, H, NE, FF>(P, L, G, gs, rec, stage, d, h, o, cache, gx, gh_in, gbe, gWe);
       }
-      vec_accumulate<ET>(lg + G.be, gbe);
+      vec_accumulate_g<ET>(gs + G.be, gbe);
 #pragma unroll
       for (int t = 0; t < ET; ++t) gh_rec[t] = gx[t] + gh_in[t];
     }
@@ -265,27 +274,27 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
 #pragma unroll
       for (int t = 0; t < ET; ++t) st4(args.gh0 + (size_t)row * E + 16 * t + 4 * g, gh_rec[t]);
     }
+    flush_tiles_g<ET, 1>(gs + G.We, 16, gWe);
+    flush_tiles_g<1, ET>(gs + G.Wo, E, gWo);
   }
-  __syncthreads();
-  float* slab = args.slabs + (size_t)blockIdx.x * G.grad_total;
-  for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) slab[i] = lg[i];
 }
 
 template <int E, int H, int D, int NE, int FF>
 int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
-  constexpr int ET = E / 16;
   const int R = args.B * args.A;
   const int tiles = (R + 15) / 16;
   const int grid = (tiles + AG_BWD_WAVES - 1) / AG_BWD_WAVES;
   if (grid > max_slabs) return T2O_EINVAL;
-  args.lds_grad = (int)((args.G.grad_total + 15) / 16 * 16);
-  const size_t lds = sizeof(float) * ((size_t)args.lds_grad + AG_BWD_WAVES * StageDims<ET>::FLOATS);
+  const size_t lds = sizeof(float) * ((size_t)(args.L.fwd_total + 15) / 16 * 16 + AG_BWD_WAVES * StageDims<1>::FLOATS);
   auto kern = agent_bwd_kernel<E, H, D, NE, FF>;
   if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * AG_BWD_WAVES), lds, stream, args);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
   *nslab = grid;
-  return (int)hipGetLastError();
+  return launch_dw_gemm<E, H, FF>(args.tape, (int64_t)args.T * R, D, args.slabs, args.G.grad_total, args.G, grid,
+                                  stream);
 }
 
 }  // namespace
@@ -322,9 +331,9 @@ extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, cons
                                     int64_t obs_st, const float* h0, const float* h_seq, const float* hmid, int h_ts,
                                     const float* gq, const float* gchosen, const int64_t* actions,
                                     int64_t act_sb, int64_t act_st, const float* gh, float* gslabs,
-                                    int max_slabs, int* nslab, float* gh0, int B, int T, int A,
+                                    int max_slabs, int* nslab, float* tape, float* gh0, int B, int T, int A,
                                     void* stream) {
-  if (!L || L->kind != 0 || !pack || !obs || !h_seq || !gslabs || !nslab || B < 1 || T < 1 || A < 1 ||
+  if (!L || L->kind != 0 || !pack || !obs || !h_seq || !gslabs || !nslab || !tape || B < 1 || T < 1 || A < 1 ||
       L->n_ent != A || h_ts < T || (gchosen && !actions))
     return T2O_EINVAL;
   AgentBwdArgs args{};
@@ -345,6 +354,7 @@ extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, cons
   args.act_st = act_st;
   args.gh = gh;
   args.slabs = gslabs;
+  args.tape = tape;
   args.gh0 = gh0;
   args.B = B;
   args.T = T;
@@ -354,6 +364,11 @@ extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, cons
   T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
                rc = (launch_bwd<E_, H_, D_, NE_, FF_>(args, max_slabs, nslab, (hipStream_t)stream)));
   return rc;
+}
+
+extern "C" int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t records) {
+  if (!L || records < 0) return -1;
+  return (int64_t)L->D * records * (4 * L->E + 2 * L->H * L->E + 2 * L->FF);
 }
 
 extern "C" int t2o_agent_bwd_max_slabs(int B, int A) {

@@ -99,17 +99,18 @@ T2O_DEV void agent_block_fwd(const float* __restrict__ P, const t2o_layout& L, i
 
 // Backward of block d.  gx: in = grad wrt block output, out = grad wrt block
 // input (query path).  gh_in accumulates the grad wrt h through the key/value
-// path (token 0); gbe the grad wrt the embedding bias.  Weight grads are
-// accumulated into the LDS gradient block (compact layout G).
+// path (token 0); gbe the grad wrt the embedding bias; gWe (MFMA register
+// block, [E][16] as ET x 1 tiles) the grad wrt the embedding weight.  M's
+// operand pair goes to the tape record (t2o_common.hpp TapeRec).
 template <int E, int H, int NE, int FF>
 T2O_DEV void agent_block_bwd(const float* __restrict__ P, const t2o_layout& L, const t2o_layout& G,
-                             float* __restrict__ lg, float* __restrict__ stage, int d, const f4* h,
-                             const f4 (&o)[NE], const AgentCache<E, H, NE, FF>& c, f4* gx, f4* gh_in,
-                             f4* gbe) {
+                             float* __restrict__ gs, float* __restrict__ rec, float* __restrict__ stage, int d,
+                             const f4* h, const f4 (&o)[NE], const AgentCache<E, H, NE, FF>& c, f4* gx,
+                             f4* gh_in, f4* gbe, f4 (&gWe)[E / 16][1]) {
   constexpr int ET = E / 16, HET = H * ET;
   const float* be = P + L.be;
   f4 gz[HET], gres[ET];
-  post_bwd<E, H, FF>(P, L, G, lg, stage, d, c.post, gx, gz, gres);
+  post_bwd<E, H, FF>(P, L, G, gs, rec, d, c.post, gx, gz, gres);
   f4 gu[HET];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
@@ -129,8 +130,8 @@ T2O_DEV void agent_block_bwd(const float* __restrict__ P, const t2o_layout& L, c
     const float gp0 = allsum4(gp0p);
     const float gP = allsum4(gPp);
     f4 goh;
-    matvec<1, ET>(P + L.WeT, E, gzh, &goh);
-    dw_accumulate<ET, 1>(lg + G.We, 16, gzh, &c.oh[hh], stage);
+    matvec_t<1, ET>(P + L.We, 16, gzh, &goh);
+    dw_accumulate_regs<ET, 1>(gWe, gzh, &c.oh[hh], stage);
     // softmax backward over [token 0, entities]
     float gp[NE + 1];
     gp[0] = gp0;
@@ -160,14 +161,15 @@ T2O_DEV void agent_block_bwd(const float* __restrict__ P, const t2o_layout& L, c
       gh_in[t] += gs0 * uh[t];
       gbe[t] += gc * uh[t];
     }
-    dw_accumulate<ET, 1>(lg + G.We, 16, uh, &gw, stage);
-    T2O_FENCE();
+    dw_accumulate_regs<ET, 1>(gWe, uh, &gw, stage);
   }
   // u = M x
-  dw_accumulate<HET, ET>(lg + G.M[d], E, gu, c.post.x, stage);
-  T2O_FENCE();
+  if (rec) {
+    rec_store<HET>(rec, TapeRec<E, H, FF>::GU, gu);
+    rec_store<ET>(rec, TapeRec<E, H, FF>::X, c.post.x);
+  }
   f4 gxp[ET];
-  matvec<ET, HET>(P + L.MT[d], H * E, gu, gxp);
+  matvec_t<ET, HET>(P + L.M[d], E, gu, gxp);
 #pragma unroll
   for (int t = 0; t < ET; ++t) gx[t] = gxp[t] + gres[t];
 }

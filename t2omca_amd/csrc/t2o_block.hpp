@@ -72,56 +72,61 @@ T2O_DEV void post_fwd(const float* __restrict__ P, const t2o_layout& L, int d, c
 }
 
 // gx: grad wrt block output.  Produces gz (grad wrt z, HET tiles) and gres
-// (grad wrt the block input through the LN1 residual).  Weight / vector grads
-// go to the LDS gradient block lg (compact layout G).
+// (grad wrt the block input through the LN1 residual).  The operand pairs of
+// the big weight grads (N, W1, W2) go to this row's tape record `rec` (null for
+// padding rows); vector grads go to the workgroup's global slab gs (layout G).
+// Weights are read from P (LDS); transposed products use matvec_t.
 template <int E, int H, int FF>
 T2O_DEV void post_bwd(const float* __restrict__ P, const t2o_layout& L, const t2o_layout& G,
-                      float* __restrict__ lg, float* __restrict__ stage, int d, const PostCache<E, H, FF>& c,
+                      float* __restrict__ gs, float* __restrict__ rec, int d, const PostCache<E, H, FF>& c,
                       const f4* gx, f4* gz, f4* gres) {
   constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
+  using R = TapeRec<E, H, FF>;
   {  // LN2: x' = xh2*g2 + n2
     f4 t0[ET];
 #pragma unroll
     for (int t = 0; t < ET; ++t) t0[t] = gx[t] * c.xh2[t];
-    vec_accumulate<ET>(lg + G.g2[d], t0);
-    vec_accumulate<ET>(lg + G.n2[d], gx);
+    vec_accumulate_g<ET>(gs + G.g2[d], t0);
+    vec_accumulate_g<ET>(gs + G.n2[d], gx);
   }
   f4 gr2[ET];
   layernorm_bwd<ET>(gx, c.xh2, c.rs2, P + L.g2[d], gr2);
-  T2O_FENCE();
   // r2 = W2 relu(f1) + c2 + y
-  dw_accumulate<ET, FT>(lg + G.W2[d], FF, gr2, c.f1r, stage);
-  vec_accumulate<ET>(lg + G.c2[d], gr2);
-  T2O_FENCE();
+  if (rec) {
+    rec_store<ET>(rec, R::GR2, gr2);
+    rec_store<FT>(rec, R::F1R, c.f1r);
+  }
+  vec_accumulate_g<ET>(gs + G.c2[d], gr2);
   f4 gf1[FT];
-  matvec<FT, ET>(P + L.W2T[d], E, gr2, gf1);
+  matvec_t<FT, ET>(P + L.W2[d], FF, gr2, gf1);
 #pragma unroll
   for (int t = 0; t < FT; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) gf1[t][r] = c.f1r[t][r] > 0.f ? gf1[t][r] : 0.f;
-  T2O_FENCE();
-  dw_accumulate<FT, ET>(lg + G.W1[d], E, gf1, c.y, stage);
-  vec_accumulate<FT>(lg + G.c1[d], gf1);
-  T2O_FENCE();
+  if (rec) {
+    rec_store<FT>(rec, R::GF1, gf1);
+    rec_store<ET>(rec, R::Y, c.y);
+  }
+  vec_accumulate_g<FT>(gs + G.c1[d], gf1);
   f4 gy[ET];
-  matvec<ET, FT>(P + L.W1T[d], FF, gf1, gy);
+  matvec_t<ET, FT>(P + L.W1[d], E, gf1, gy);
 #pragma unroll
   for (int t = 0; t < ET; ++t) gy[t] += gr2[t];
   {  // LN1: y = xh1*g1 + n1
     f4 t0[ET];
 #pragma unroll
     for (int t = 0; t < ET; ++t) t0[t] = gy[t] * c.xh1[t];
-    vec_accumulate<ET>(lg + G.g1[d], t0);
-    vec_accumulate<ET>(lg + G.n1[d], gy);
+    vec_accumulate_g<ET>(gs + G.g1[d], t0);
+    vec_accumulate_g<ET>(gs + G.n1[d], gy);
   }
   layernorm_bwd<ET>(gy, c.xh1, c.rs1, P + L.g1[d], gres);
-  T2O_FENCE();
   // r1 = N z + b_U + x
-  dw_accumulate<ET, HET>(lg + G.N[d], H * E, gres, c.z, stage);
-  vec_accumulate<ET>(lg + G.bu[d], gres);
-  T2O_FENCE();
-  matvec<HET, ET>(P + L.NT[d], E, gres, gz);
-  T2O_FENCE();
+  if (rec) {
+    rec_store<ET>(rec, R::GRES, gres);
+    rec_store<HET>(rec, R::Z, c.z);
+  }
+  vec_accumulate_g<ET>(gs + G.bu[d], gres);
+  matvec_t<HET, ET>(P + L.N[d], H * E, gres, gz);
 }
 
 }  // namespace t2o

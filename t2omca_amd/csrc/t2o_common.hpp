@@ -68,6 +68,24 @@ T2O_DEV void matvec(const float* __restrict__ W, int ldw, const f4* x, f4* y) {
   }
 }
 
+// y[0..OT) = Wᵀ · x[0..IT)  for row-major W [16*IT rows][ldw >= 16*OT] — the
+// transposed product read straight from the same (LDS-resident) copy: lane
+// (g, c) of step s needs Wᵀ[16o+c][16i+4g+s] = W[16i+4g+s][16o+c], one scalar
+// read per MFMA step (consecutive c -> consecutive banks).
+template <int OT, int IT>
+T2O_DEV void matvec_t(const float* __restrict__ W, int ldw, const f4* x, f4* y) {
+  const int c = lane_c(), g = lane_g();
+#pragma unroll
+  for (int o = 0; o < OT; ++o) {
+    f4 acc = zero4();
+#pragma unroll
+    for (int i = 0; i < IT; ++i)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc = mfma4(W[(16 * i + 4 * g + s) * ldw + 16 * o + c], x[i][s], acc);
+    y[o] = acc;
+  }
+}
+
 // T-layout slice of a bias / gamma vector: elements 16t+4g .. 16t+4g+3
 T2O_DEV f4 vec_t(const float* __restrict__ v, int t) { return ld4(v + 16 * t + 4 * lane_g()); }
 
@@ -306,6 +324,63 @@ T2O_DEV void vec_accumulate(float* __restrict__ ldsv, const f4* v) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) atomicAdd(ldsv + 16 * t + 4 * g + r, s[t][r]);
   }
+}
+
+
+// Same sum into a global (per-workgroup slab) vector with hardware float
+// atomics (no return value, fire-and-forget at L2).
+template <int NT>
+T2O_DEV void vec_accumulate_g(float* __restrict__ gv, const f4* v) {
+  const int c = lane_c(), g = lane_g();
+  float s[NT][4];
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s[t][r] = rowsum16_fast(v[t][r]);
+  if (c == 15) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) unsafeAtomicAdd(gv + 16 * t + 4 * g + r, s[t][r]);
+  }
+}
+
+// Flush an MFMA-layout register block acc[o][i] (lane (g,c), reg r holds
+// dW[16o+4g+r][16i+c]) into a global row-major matrix with float atomics.
+template <int OT, int IT>
+T2O_DEV void flush_tiles_g(float* __restrict__ W, int ldw, const f4 (&acc)[OT][IT]) {
+  const int c = lane_c(), g = lane_g();
+#pragma unroll
+  for (int o = 0; o < OT; ++o)
+#pragma unroll
+    for (int i = 0; i < IT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) unsafeAtomicAdd(W + (16 * o + 4 * g + r) * ldw + 16 * i + c, acc[o][i][r]);
+}
+
+// ---- weight-gradient tape ---------------------------------------------------
+// The backward kernels do not accumulate the four big per-block matrices
+// (M, N, W1, W2) themselves: per (row, step, block) they stream the operand
+// pairs of dW = Σ dYᵀ X to an HBM tape record, and t2o_dwgemm.hip contracts
+// the tape over all records with MFMA.  Record layout (floats):
+template <int E, int H, int FF>
+struct TapeRec {
+  static constexpr int X = 0;                 // block input x      (E)   M:  X
+  static constexpr int GU = X + E;            // dL/du              (HE)  M:  dY
+  static constexpr int Z = GU + H * E;        // head outputs z     (HE)  N:  X
+  static constexpr int GRES = Z + H * E;      // dL/d(N z + bu)     (E)   N:  dY
+  static constexpr int Y = GRES + E;          // LN1 output y       (E)   W1: X
+  static constexpr int GF1 = Y + E;           // dL/d(W1 y + c1)    (FF)  W1: dY
+  static constexpr int F1R = GF1 + FF;        // relu(W1 y + c1)    (FF)  W2: X
+  static constexpr int GR2 = F1R + FF;        // dL/d(W2 f + c2 + y)(E)   W2: dY
+  static constexpr int SIZE = GR2 + E;
+};
+
+// store a T-layout vector (NT tiles) into this lane's row of a record
+template <int NT>
+T2O_DEV void rec_store(float* rec, int off, const f4* v) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) st4(rec + off + 16 * t + 4 * lane_g(), v[t]);
 }
 
 }  // namespace t2o

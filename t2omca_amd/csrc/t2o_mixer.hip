@@ -10,6 +10,7 @@
 //   qmode 1  chosen-action Q  gather(Q[:, t], actions)  (online mixer)
 //   qmode 2  double-Q         Q_tgt[argmax(Q_on masked by avail)] (target mixer)
 #include "t2o_dispatch.hpp"
+#include "t2o_dwgemm.hpp"
 #include "t2o_layout.hpp"
 #include "t2o_mixer_block.hpp"
 
@@ -245,13 +246,17 @@ int launch_mixer_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
 }
 
 // ---------------------------------------------------------------------------
-// BPTT.  One wave per episode, 2 waves per workgroup (the shared LDS gradient
-// block + per-wave key/staging buffers fill one CU's 160 KiB).  Per step t
-// (backwards): rebuild X0 from the stored inputs and hyper tokens, run the
-// mixing-head backward on the stored final query rows, then per query tile
-// recompute the blocks with cache and back-propagate.  Outputs per step: grad
-// wrt the qvals (-> the agent's chosen-Q grad) and wrt the agent hidden
-// tokens; the hyper-token grad is carried to step t-1.
+// BPTT.  One wave per episode; the workgroup shares one LDS copy of the
+// forward weights (transposed products via matvec_t) beside each wave's key /
+// staging buffers.  Per step t (backwards): rebuild X0 from the stored inputs
+// and hyper tokens, run the mixing-head backward on the stored final query
+// rows, then per query tile recompute the blocks with cache and
+// back-propagate.  Outputs per step: grad wrt the qvals (-> the agent's
+// chosen-Q grad) and wrt the agent hidden tokens; the hyper-token grad is
+// carried to step t-1.  Weight grads: M/N/W1/W2 operand pairs -> tape records
+// (query row x step), contracted by t2o_dwgemm.hpp into slab k; state
+// embedding / hyper_b2 grads in registers (lane = feature), flushed once;
+// vectors by float atomics into the workgroup's slab.
 struct MixerBwdArgs {
   MixerFwdArgs f;     // net[0] = the network (qmode 0: qv_in = forward qv output)
   t2o_layout G;
@@ -264,7 +269,8 @@ struct MixerBwdArgs {
   float* ghw0;        // [B][3][E] (may be null)
   const float* xmid;  // forward block inputs of blocks 1..D-1 [B][T][D-1][A+3][E] (may be null)
   float* slabs;
-  int lds_grad;
+  float* tape;        // [D][B*T*(A+3)][TapeRec::SIZE]
+  int lds_w;          // floats of LDS taken by the weights
   int waves;          // episodes (waves) per workgroup: 4, 2 or 1, whatever fits in LDS
 };
 
@@ -295,22 +301,29 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   const MixerNet& n = fa.net[0];
   const t2o_layout& L = fa.L;
   const t2o_layout& G = args.G;
-  float* lg = smem;
   const int w = wave_id();
-  float* X0 = smem + args.lds_grad + w * Bd::PERW;
+  float* X0 = smem + args.lds_w + w * Bd::PERW;
   float* WORK = X0 + Dm::X0F;
   float* GOUTB = Bd::GOUT ? WORK : WORK;        // head grads (rows of OUT layout)
   float* stage = WORK + Bd::GOUT;               // staging / gX0 region
-  for (int i = threadIdx.x; i < args.lds_grad; i += blockDim.x) lg[i] = 0.f;
+  float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
+  copy_to_lds(smem, n.pack, L.fwd_total);
+  for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) gs[i] = 0.f;
   __syncthreads();
   const int b = blockIdx.x * args.waves + w;
-  const float* __restrict__ P = n.pack;
+  const float* __restrict__ P = smem;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
+  const size_t nrec = (size_t)fa.B * n.T * Dm::Q;
+  using Rec = TapeRec<E, H, FF>;
   if (b < fa.B) {
     for (int i = lane; i < Dm::X0F; i += 64) X0[i] = 0.f;
     float ghw[3] = {0.f, 0.f, 0.f};  // grad wrt this step's hyper outputs, lane = feature
     const int f = lane < E ? lane : 0;
     const bool fv = lane < E;
+    // register-resident grads, lane = feature f: state embedding We[f][0..16), be[f], hyper_b2
+    float gWe[16], gbe = 0.f, gWo = 0.f, gbo = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) gWe[k] = 0.f;
     for (int t = n.T - 1; t >= 0; --t) {
       const size_t bt = (size_t)b * n.T + t;
       build_keys<E, A>(P, L, fa, n, b, t, X0);
@@ -349,10 +362,8 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
       gout[A + 1] = gyv * hidden * sgn_w2 + ghw[1];
       const float x2 = OUT[(A + 2) * E + f];
       gout[A + 2] = gpre2 * P[L.Wo + f] + ghw[2];
-      if (fv) {
-        atomicAdd(lg + G.Wo + f, gpre2 * x2);
-        if (lane == 0) atomicAdd(lg + G.bo, gpre2);
-      }
+      gWo += gpre2 * x2;
+      gbo += gpre2;
       __builtin_amdgcn_wave_barrier();
       float* GOUT = Bd::GOUT ? GOUTB : stage;
       if (fv) {
@@ -408,9 +419,8 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft) x[ft] = xs[d][ft];
           mixer_block_fwd<E, H, KT, FF, Dm::LDX, true>(P, L, d, X0, Dm::LK, x, &cache);
-          T2O_FENCE();
-          mixer_block_bwd<E, H, KT, FF, Dm::LDX>(P, L, G, lg, stage, d, X0, gX0, cache, gx);
-          T2O_FENCE();
+          float* rec = q < Dm::Q ? args.tape + ((size_t)d * nrec + bt * Dm::Q + q) * Rec::SIZE : nullptr;
+          mixer_block_bwd<E, H, KT, FF, Dm::LDX>(P, L, G, gs, rec, stage, d, X0, gX0, cache, gx);
         }
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft) gq0[qt][ft] = q < Dm::Q ? gx[ft] : zero4();
@@ -444,14 +454,15 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) ghw[k] = GX0[(Dm::NS + A + k) * E + f];
         const float* st = fa.states + b * fa.st_sb + t * fa.st_st;
-        float gbe = 0.f;
-        for (int fs = 0; fs < fa.Fs; ++fs) {
-          float acc = 0.f;
-          for (int j = 0; j < Dm::NS; ++j) acc += GX0[j * E + f] * st[j * fa.Fs + fs];
-          atomicAdd(lg + G.We + f * 16 + fs, acc);
+#pragma unroll
+        for (int fs = 0; fs < 16; ++fs) {
+          if (fs < fa.Fs) {
+            float acc = 0.f;
+            for (int j = 0; j < Dm::NS; ++j) acc += GX0[j * E + f] * st[j * fa.Fs + fs];
+            gWe[fs] += acc;
+          }
         }
         for (int j = 0; j < Dm::NS; ++j) gbe += GX0[j * E + f];
-        atomicAdd(lg + G.be + f, gbe);
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -459,19 +470,24 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) args.ghw0[((size_t)b * 3 + k) * E + f] = ghw[k];
     }
+    if (fv) {
+#pragma unroll
+      for (int fs = 0; fs < 16; ++fs)
+        if (fs < fa.Fs) unsafeAtomicAdd(gs + G.We + f * 16 + fs, gWe[fs]);
+      unsafeAtomicAdd(gs + G.be + f, gbe);
+      unsafeAtomicAdd(gs + G.Wo + f, gWo);
+    }
+    if (lane == 0) unsafeAtomicAdd(gs + G.bo, gbo);
   }
-  __syncthreads();
-  float* slab = args.slabs + (size_t)blockIdx.x * G.grad_total;
-  for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) slab[i] = lg[i];
 }
 
 template <int E, int H, int D, int A, int FF>
 int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
   constexpr int PERW = MixBwdDims<E, A>::PERW;
-  args.lds_grad = (int)((args.G.grad_total + 15) / 16 * 16);
+  args.lds_w = (int)((args.f.L.fwd_total + 15) / 16 * 16);
   size_t lds = 0;
   for (args.waves = 4; args.waves >= 1; args.waves >>= 1) {
-    lds = sizeof(float) * ((size_t)args.lds_grad + args.waves * PERW);
+    lds = sizeof(float) * ((size_t)args.lds_w + args.waves * PERW);
     if (lds <= 160 * 1024) break;
   }
   if (args.waves < 1) return T2O_EUNSUPPORTED;
@@ -480,8 +496,11 @@ int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t 
   auto kern = mixer_bwd_kernel<E, H, D, A, FF>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * args.waves), lds, stream, args);
+  int rc = (int)hipGetLastError();
+  if (rc) return rc;
   *nslab = grid;
-  return (int)hipGetLastError();
+  return launch_dw_gemm<E, H, FF>(args.tape, (int64_t)args.f.B * args.f.net[0].T * MixDims<E, A>::Q, D,
+                                  args.slabs, args.G.grad_total, args.G, grid, stream);
 }
 
 }  // namespace
@@ -544,9 +563,9 @@ extern "C" int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, cons
                                     const float* hw0, const float* qv, const float* hw, const float* xout,
                                     const float* xmid, const float* gy, const float* ghw_ext, float* gqv,
                                     float* ghid, float* ghw0, float* gslabs,
-                                    int max_slabs, int* nslab, int B, int T, void* stream) {
+                                    int max_slabs, int* nslab, float* tape, int B, int T, void* stream) {
   if (!L || L->kind != 1 || !pack || !states || !hid || !qv || !hw || !xout || !gy || !gqv || !ghid ||
-      !gslabs || !nslab || B < 1 || T < 1 || L->E > 64)
+      !gslabs || !nslab || !tape || B < 1 || T < 1 || L->E > 64)
     return T2O_EINVAL;
   MixerBwdArgs a{};
   a.f.L = *L;
@@ -567,6 +586,7 @@ extern "C" int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, cons
   a.ghid = ghid;
   a.ghw0 = ghw0;
   a.slabs = gslabs;
+  a.tape = tape;
   int rc = T2O_EUNSUPPORTED;
   T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
                rc = (launch_mixer_bwd<E_, H_, D_, NE_, FF_>(a, max_slabs, nslab, (hipStream_t)stream)));

@@ -110,14 +110,15 @@ T2O_DEV void mixer_block_fwd(const float* __restrict__ P, const t2o_layout& L, i
 // out = grad wrt block input.  gX0 — MFMA accumulator registers, tile [kt][ft]
 // holds gX0[key 16kt+4g+r][feature 16ft+c] — accumulates the grad wrt the key
 // tokens (a contraction over queries = rows, via the staging transposes).
+// Big-matrix operand pairs go to the query row's tape record (null = padding).
 template <int E, int H, int KT, int FF, int LDX>
 T2O_DEV void mixer_block_bwd(const float* __restrict__ P, const t2o_layout& L, const t2o_layout& G,
-                             float* __restrict__ lg, float* __restrict__ stage, int d,
+                             float* __restrict__ gs, float* __restrict__ rec, float* __restrict__ stage, int d,
                              const float* __restrict__ X0, f4 (&gX0)[KT][E / 16],
                              const MixerCache<E, H, KT, FF>& c, f4* gx) {
   constexpr int ET = E / 16, HET = H * ET;
   f4 gz[HET], gres[ET];
-  post_bwd<E, H, FF>(P, L, G, lg, stage, d, c.post, gx, gz, gres);
+  post_bwd<E, H, FF>(P, L, G, gs, rec, d, c.post, gx, gz, gres);
   f4 gu[HET];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
@@ -129,18 +130,19 @@ T2O_DEV void mixer_block_bwd(const float* __restrict__ P, const t2o_layout& L, c
 #pragma unroll
       for (int r = 0; r < 4; ++r) dot += c.p[hh][kt][r] * gp[kt][r];
     dot = allsum4(dot);
-    f4 gs[KT];
+    f4 gsc[KT];
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) gs[kt] = c.p[hh][kt] * (gp[kt] - dot);
-    keys_combine<E, KT, LDX>(X0, gs, &gu[hh * ET]);
+    for (int kt = 0; kt < KT; ++kt) gsc[kt] = c.p[hh][kt] * (gp[kt] - dot);
+    keys_combine<E, KT, LDX>(X0, gsc, &gu[hh * ET]);
     dw_accumulate_regs<KT, ET>(gX0, c.p[hh], &gz[hh * ET], stage);
-    dw_accumulate_regs<KT, ET>(gX0, gs, &c.u[hh * ET], stage);
-    T2O_FENCE();
+    dw_accumulate_regs<KT, ET>(gX0, gsc, &c.u[hh * ET], stage);
   }
-  dw_accumulate<HET, ET>(lg + G.M[d], E, gu, c.post.x, stage);
-  T2O_FENCE();
+  if (rec) {
+    rec_store<HET>(rec, TapeRec<E, H, FF>::GU, gu);
+    rec_store<ET>(rec, TapeRec<E, H, FF>::X, c.post.x);
+  }
   f4 gxp[ET];
-  matvec<ET, HET>(P + L.MT[d], H * E, gu, gxp);
+  matvec_t<ET, HET>(P + L.M[d], E, gu, gxp);
 #pragma unroll
   for (int t = 0; t < ET; ++t) gx[t] = gxp[t] + gres[t];
 }

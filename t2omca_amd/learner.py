@@ -158,15 +158,17 @@ class TDLearner:
         #    data-parallel sum over ranks divides by the GLOBAL Σ mask)
         td = ops.td_loss(o_on["y"], o_tg["y"], reward, term, filled, w, gamma=self.gamma,
                          td_lambda=self.td_lambda, mask_sum=1.0)
-        # 4. mixer BPTT
+        # 4. mixer BPTT (one weight-grad tape buffer serves both backward passes:
+        #    each pass's contraction runs before the next pass starts, same stream)
+        tape = self._slab("tape", max(ops.tape_floats(self.sm, B * T * (A + 3)), ops.tape_floats(self.sa, B * T * A)))
         slabs_m = self._slab("m", int(ops.lib().t2o_mixer_bwd_max_slabs(B)) * self.sm.layout().grad_total)
         gm, gqv, ghid, _ = ops.mixer_unroll_bwd(self.sm, self.pack_m, state, h_on, o_on, td["gq"], slabs=slabs_m,
-                                                timer=self.timer)
+                                                timer=self.timer, tape=tape)
         # 5. agent BPTT (grads of the chosen Q and, unless detached, of the hidden states)
         slabs_a = self._slab("a", int(ops.lib().t2o_agent_bwd_max_slabs(B, A)) * self.sa.layout().grad_total)
         ga, _ = ops.agent_unroll_bwd(self.sa, self.pack_a, obs, h_on, gchosen=gqv, actions=act,
                                      gh=None if self.detach_mixer_hidden else ghid, slabs=slabs_a,
-                                     timer=self.timer, hmid=hmid)
+                                     timer=self.timer, hmid=hmid, tape=tape)
         # 6. grads in reference parameter order
         self.grad.zero_()
         ops.unpack_grads(self.sa, self.params[:self.na], ga, self.grad[:self.na])

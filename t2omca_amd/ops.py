@@ -119,8 +119,20 @@ def agent_unroll_fwd(shape: NetShape, pack_on, obs, h0_on=None, pack_tg=None, h0
     return q_on, h_on
 
 
+def tape_floats(shape: NetShape, records):
+    """Backward tape workspace (floats) for `records` weight-gradient records."""
+    return int(lib().t2o_bwd_tape_floats(ctypes.byref(shape.layout()), int(records)))
+
+
+def _tape(shape, records, tape, device):
+    n = tape_floats(shape, records)
+    if tape is None or tape.numel() < n:
+        tape = torch.empty(n, device=device)
+    return tape
+
+
 def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchosen=None, actions=None,
-                     gh=None, want_gh0=False, slabs=None, timer=None, hmid=None):
+                     gh=None, want_gh0=False, slabs=None, timer=None, hmid=None, tape=None):
     """BPTT of agent_unroll_fwd over the first T = len(grads) steps.
 
     obs [B, >=T, A, nF]; h_seq [B, Ts>=T, A, E] (forward output); gq [B,T,A,NA],
@@ -141,12 +153,13 @@ def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchose
     if slabs is None or slabs.numel() < nmax * L.grad_total:
         slabs = torch.empty(nmax * L.grad_total, device=obs.device)
     gh0 = torch.empty(B, A, shape.E, device=obs.device) if want_gh0 else None
+    tape = _tape(shape, B * T * A, tape, obs.device)
     nslab = ctypes.c_int(0)
     _mark(timer, "begin:agent_bwd")
     check(lib().t2o_agent_unroll_bwd(ctypes.byref(L), ptr(pack), ptr(obs), obs.stride(0), obs.stride(1),
                                      ptr(h0), ptr(h_seq), ptr(hmid), h_seq.shape[1], ptr(gq), ptr(gchosen),
                                      ptr(actions), act_sb, act_st, ptr(gh), ptr(slabs), nmax,
-                                     ctypes.byref(nslab), ptr(gh0), B, T, A, stream_ptr()),
+                                     ctypes.byref(nslab), ptr(tape), ptr(gh0), B, T, A, stream_ptr()),
           "agent_unroll_bwd")
     _mark(timer, "end:agent_bwd")
     gpack = torch.empty(L.grad_total, device=obs.device)
@@ -213,7 +226,7 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
 
 
 def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_ext=None,
-                     want_ghw0=False, slabs=None, timer=None):
+                     want_ghw0=False, slabs=None, timer=None, tape=None):
     """BPTT of mixer_unroll_fwd (one network, `fwd` = its output dict).
     Returns (gpack, gqv [B,T,A], ghid [B,T,A,E], ghw0 or None)."""
     _dev(pack, states, hid, gy, hw0, ghw_ext)
@@ -228,13 +241,14 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
     gqv = torch.empty(B, T, A, device=dev)
     ghid = torch.empty(B, T, A, E, device=dev)
     ghw0 = torch.empty(B, 3, E, device=dev) if want_ghw0 else None
+    tape = _tape(shape, B * T * (A + 3), tape, dev)
     nslab = ctypes.c_int(0)
     _mark(timer, "begin:mixer_bwd")
     check(lib().t2o_mixer_unroll_bwd(
         ctypes.byref(L), ptr(pack), ptr(states), states.stride(0), states.stride(1), ptr(hid),
         hid.stride(0), hid.stride(1), ptr(hw0), ptr(fwd["qv"]), ptr(fwd["hw"]), ptr(fwd["xout"]),
         ptr(fwd.get("xmid")), ptr(gy), ptr(ghw_ext), ptr(gqv), ptr(ghid), ptr(ghw0), ptr(slabs), nmax, ctypes.byref(nslab),
-        B, T, stream_ptr()), "mixer_unroll_bwd")
+        ptr(tape), B, T, stream_ptr()), "mixer_unroll_bwd")
     _mark(timer, "end:mixer_bwd")
     gpack = torch.empty(L.grad_total, device=dev)
     reduce_slabs(slabs, nslab.value, gpack)
