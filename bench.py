@@ -65,6 +65,23 @@ class KernelTimer:
         return out
 
 
+def traffic_for(kernel, B, T, A):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (profiles/hbm_traffic.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes, corrected
+    as MI355X_MICROARCH.md prescribes, by tools/pmc_traffic.py), or None when that
+    summary was taken on another workload."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "hbm_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("workload") != f"b{B}_t{T}_a{A}":
+        return None
+    k = d.get("kernels", {}).get(kernel)
+    return None if k is None else k.get("hbm_bytes")
+
+
 def cpu_baseline(args):
     """The oracle's PyTorch-CPU TD update on a bounded sample of the same workload."""
     from oracle import ref_learner, ref_model
@@ -138,7 +155,11 @@ def main():
     bytes_ = td_update_bytes(B, T, A)
     dom = max((k for k in flops), key=lambda k: kern.get(k, 0.0))
     dom_ms = kern.get(dom, float("nan"))
-    achieved = flops[dom] / (dom_ms * 1e-3) / 1e12
+    hbm_bound = dom.endswith("_dw")  # tape contractions stream their operands once
+    if hbm_bound:
+        achieved, peak, unit = bytes_[dom] / (dom_ms * 1e-3) / 1e9, PEAK_HBM_GBS, "GB/s"
+    else:
+        achieved, peak, unit = flops[dom] / (dom_ms * 1e-3) / 1e12, PEAK_FP32_TFLOPS, "TFLOP/s"
     out = {
         "metric": "agent-transitions/sec for TD update fwd+bwd (whole node)",
         "value": value,
@@ -156,8 +177,8 @@ def main():
                                f"batch {B} episodes/GPU x T={T}",
                    "global_batch": B * world, "seq_len": T, "agents": A, "emb": 32, "heads": 3, "depth": 2,
                    "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": PEAK_FP32_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_TFLOPS, "traffic": None,
+        "roofline": {"bound": "hbm" if hbm_bound else "mfma", "kernel": dom, "achieved": achieved, "peak": peak,
+                     "unit": unit, "frac": achieved / peak, "traffic": traffic_for(dom, B, T, A),
                      "algorithmic_flops_per_launch": flops[dom],
                      "algorithmic_bytes_per_launch": bytes_[dom],
                      "avg_launch_ms": dom_ms},

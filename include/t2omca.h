@@ -110,8 +110,9 @@ int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, const float*
  * layout, overwritten; *nslab = number written, at most max_slabs =
  * t2o_agent_bwd_max_slabs(B, A)); gh0[b][a][E] = dL/dh0 (may be NULL).
  * Workspace: tape, t2o_bwd_tape_floats(L, T*B*A) floats — the per-record
- * operand pairs of the M/N/W1/W2 weight grads, contracted by a second launch
- * (t2o_dwgemm.hpp) on the same stream before this call returns. */
+ * operand pairs of the M/N/W1/W2 weight grads; the slabs are complete only
+ * after t2o_bwd_tape_contract(L, tape, T*B*A, gslabs, *nslab) on the same
+ * stream. */
 int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack,
                          const float* obs, int64_t obs_sb, int64_t obs_st,
                          const float* h0, const float* h_seq, const float* hmid, int h_ts,
@@ -162,6 +163,12 @@ int t2o_mixer_bwd_max_slabs(int B);
 
 /* Floats of backward tape workspace for `records` records (D * records * (4E + 2HE + 2FF)). */
 int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t records);
+
+/* Contract a backward tape (dM, dN, dW1, dW2 = Σ_records dYᵀ X, split-K over
+ * the nslab slabs the backward call returned) into the M/N/W1/W2 regions of
+ * those slabs.  Must follow the t2o_*_unroll_bwd call that wrote the tape. */
+int t2o_bwd_tape_contract(const t2o_layout* L, const float* tape, int64_t records, float* gslabs, int nslab,
+                          void* stream);
 
 /* TD(λ) targets, masked PER-weighted loss, dL/dQtot and priorities
  * (PyMARL2 NQLearner semantics; see t2o_learner.hip).  qtot [B][T] (online

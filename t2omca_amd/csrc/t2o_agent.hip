@@ -9,7 +9,6 @@
 // run in the same launch on the same observations (blockIdx.y).
 #include "t2o_agent_block.hpp"
 #include "t2o_dispatch.hpp"
-#include "t2o_dwgemm.hpp"
 #include "t2o_layout.hpp"
 
 using namespace t2o;
@@ -31,35 +30,44 @@ struct AgentFwdArgs {
   int64_t obs_sb, obs_st;
   int B, T, A, F;
   int wlds;  // weights staged in LDS (set by the launcher)
+  int rpw;   // rows per wave: 16, or 8 when 16-row tiles would leave SIMDs idle
 };
 
-template <int E, int H, int D, int NE, int FF>
-__global__ __launch_bounds__(256) void agent_fwd_kernel(AgentFwdArgs args) {
+// Rows per wave: one 16-row MFMA tile.  (8-row tiles — half the MFMA columns
+// idle, twice the recurrences in flight — measured slower on config 3: the
+// per-step LDS weight reads are per wave, so they double per row.)
+inline int rows_per_wave(int R) { return (void)R, 16; }
+
+constexpr int AG_FWD_WAVES = 4;  // waves per workgroup sharing one LDS copy of the weights
+
+template <int E, int H, int D, int NE, int FF, bool WLDS>
+__global__ __launch_bounds__(64 * AG_FWD_WAVES) void agent_fwd_kernel(AgentFwdArgs args) {
   constexpr int ET = E / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const AgentNet net = args.net[blockIdx.y];
   const t2o_layout& L = args.L;
   // the forward section of the pack lives in LDS for the whole unroll (when it fits)
-  if (args.wlds) {
+  if constexpr (WLDS) {
     copy_to_lds(smem, net.pack, L.fwd_total);
     __syncthreads();
   }
   const int A = args.A, F = args.F;
   const int R = args.B * A;
-  const int rt = blockIdx.x * 4 + wave_id();
-  if (rt * 16 >= R) return;  // wave-uniform: no barriers after this point
+  const int rt = blockIdx.x * AG_FWD_WAVES + wave_id();
+  if (rt * args.rpw >= R) return;  // wave-uniform: no barriers after this point
   const int c = lane_c(), g = lane_g();
-  const int row_raw = rt * 16 + c;
-  const bool valid = row_raw < R;
+  const int row_raw = rt * args.rpw + c;
+  const bool valid = c < args.rpw && row_raw < R;
   const int row = valid ? row_raw : R - 1;
   const int b = row / A, a = row % A;
-  const float* __restrict__ P = args.wlds ? smem : net.pack;
+  const float* P0 = WLDS ? smem : net.pack;  // compile-time: LDS reads stay ds_read
 
   f4 h[ET];
 #pragma unroll
   for (int t = 0; t < ET; ++t) h[t] = net.h0 ? ld4(net.h0 + (size_t)row * E + 16 * t + 4 * g) : zero4();
 
   for (int step = 0; step < args.T; ++step) {
+    const float* __restrict__ P = step_view(P0);
     const float* ob = args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * NE * F;
     f4 o[NE];
 #pragma unroll
@@ -103,15 +111,16 @@ __global__ __launch_bounds__(256) void agent_fwd_kernel(AgentFwdArgs args) {
 template <int E, int H, int D, int NE, int FF>
 int launch_fwd(const AgentFwdArgs& args, int nnet, hipStream_t stream) {
   const int R = args.B * args.A;
-  const int tiles = (R + 15) / 16;
-  dim3 grid((tiles + 3) / 4, nnet);
   AgentFwdArgs a = args;
+  a.rpw = rows_per_wave(R);
+  const int tiles = (R + a.rpw - 1) / a.rpw;
+  dim3 grid((tiles + AG_FWD_WAVES - 1) / AG_FWD_WAVES, nnet);
   size_t lds = sizeof(float) * (size_t)args.L.fwd_total;
   a.wlds = lds <= 160 * 1024;
   if (!a.wlds) lds = 0;
-  auto kern = agent_fwd_kernel<E, H, D, NE, FF>;
+  auto kern = a.wlds ? agent_fwd_kernel<E, H, D, NE, FF, true> : agent_fwd_kernel<E, H, D, NE, FF, false>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(kern, grid, dim3(256), lds, stream, a);
+  hipLaunchKernelGGL(kern, grid, dim3(64 * AG_FWD_WAVES), lds, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -145,9 +154,10 @@ struct AgentBwdArgs {
   float* tape;  // [D][T*B*A][TapeRec::SIZE]
   float* gh0;
   int B, T, A, F;
+  int rpw;  // rows per wave (rows_per_wave)
 };
 
-constexpr int AG_BWD_WAVES = 2;  // 32 sequences per workgroup: B*A/32 workgroups cover every CU
+constexpr int AG_BWD_WAVES = 2;  // (each wave needs a SIMD's full 512-register file)
 
 template <int E, int H, int D, int NE, int FF>
 __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdArgs args) {
@@ -168,14 +178,14 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
   const int R = args.B * A;
   const int rt = blockIdx.x * AG_BWD_WAVES + wave_id();
   const int c = lane_c(), g = lane_g();
-  const int row_raw = rt * 16 + c;
-  const bool valid = row_raw < R;
+  const int row_raw = rt * args.rpw + c;
+  const bool valid = c < args.rpw && row_raw < R;
   const int row = valid ? row_raw : R - 1;
   const int b = row / A, a = row % A;
-  const float* __restrict__ P = smem;
+  const float* P0 = smem;
   const size_t nrec = (size_t)T * R;
 
-  if (rt * 16 < R) {
+  if (rt * args.rpw < R) {
     f4 gWe[ET][1], gWo[1][ET];
 #pragma unroll
     for (int t = 0; t < ET; ++t) gWe[t][0] = gWo[0][t] = zero4();
@@ -183,6 +193,7 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
 #pragma unroll
     for (int t = 0; t < ET; ++t) gh_rec[t] = zero4();
     for (int step = T - 1; step >= 0; --step) {
+      const float* __restrict__ P = step_view(P0);
       f4 h[ET];
       const float* hp = step == 0 ? args.h0 : args.h_seq + (((size_t)b * args.h_ts + step - 1) * A + a) * E;
       if (step == 0 && args.h0) hp = args.h0 + (size_t)row * E;
@@ -282,7 +293,8 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
 template <int E, int H, int D, int NE, int FF>
 int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
   const int R = args.B * args.A;
-  const int tiles = (R + 15) / 16;
+  args.rpw = rows_per_wave(R);
+  const int tiles = (R + args.rpw - 1) / args.rpw;
   const int grid = (tiles + AG_BWD_WAVES - 1) / AG_BWD_WAVES;
   if (grid > max_slabs) return T2O_EINVAL;
   const size_t lds = sizeof(float) * ((size_t)(args.L.fwd_total + 15) / 16 * 16 + AG_BWD_WAVES * StageDims<1>::FLOATS);
@@ -290,11 +302,8 @@ int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream
   if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * AG_BWD_WAVES), lds, stream, args);
-  int rc = (int)hipGetLastError();
-  if (rc) return rc;
   *nslab = grid;
-  return launch_dw_gemm<E, H, FF>(args.tape, (int64_t)args.T * R, D, args.slabs, args.G.grad_total, args.G, grid,
-                                  stream);
+  return (int)hipGetLastError();
 }
 
 }  // namespace
@@ -366,12 +375,8 @@ extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, cons
   return rc;
 }
 
-extern "C" int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t records) {
-  if (!L || records < 0) return -1;
-  return (int64_t)L->D * records * (4 * L->E + 2 * L->H * L->E + 2 * L->FF);
-}
-
 extern "C" int t2o_agent_bwd_max_slabs(int B, int A) {
-  const int tiles = (B * A + 15) / 16;
+  const int rpw = rows_per_wave(B * A);
+  const int tiles = (B * A + rpw - 1) / rpw;
   return (tiles + AG_BWD_WAVES - 1) / AG_BWD_WAVES;
 }

@@ -86,6 +86,16 @@ T2O_DEV void matvec_t(const float* __restrict__ W, int ldw, const f4* x, f4* y) 
   }
 }
 
+// Weights staged in LDS are invariant across a kernel's step loop, so LICM
+// would hoist every weight read out of the loop into registers (hundreds per
+// lane, then spills).  Re-deriving the base pointer through an opaque zero
+// offset at the top of each iteration keeps the reads as ds_reads at their use.
+T2O_DEV const float* step_view(const float* base) {
+  int off = 0;
+  asm volatile("" : "+s"(off));
+  return base + off;
+}
+
 // T-layout slice of a bias / gamma vector: elements 16t+4g .. 16t+4g+3
 T2O_DEV f4 vec_t(const float* __restrict__ v, int t) { return ld4(v + 16 * t + 4 * lane_g()); }
 

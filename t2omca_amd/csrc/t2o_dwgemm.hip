@@ -1,4 +1,4 @@
-// t2o_dwgemm.hpp — contraction of the weight-gradient tape (TapeRec, t2o_common.hpp).
+// t2o_dwgemm.hip — contraction of the weight-gradient tape (TapeRec, t2o_common.hpp).
 //
 // dM = Σ_n gu_n x_nᵀ,  dN = Σ_n gres_n z_nᵀ,  dW1 = Σ_n gf1_n y_nᵀ,  dW2 = Σ_n gr2_n f1r_nᵀ
 // over every record n (row x step of the agent, query row x step of the mixer)
@@ -10,8 +10,11 @@
 // whole range.  MFMA step: lane (g, c) feeds record n0+g — A = dY[n0+g][16o+c],
 // B = X[n0+g][16i+c] — so each 16x16x4 MFMA adds four records.
 // Bound: HBM (each record is read once: 2304 B per block at E=32, H=3, FF=128).
-#pragma once
+// Called by the host right after t2o_agent_unroll_bwd / t2o_mixer_unroll_bwd
+// with the same slabs: it fills their M/N/W1/W2 regions.
 #include "t2o_common.hpp"
+#include "t2o_dispatch.hpp"
+#include "t2o_layout.hpp"
 
 namespace t2o {
 
@@ -51,7 +54,8 @@ T2O_DEV void dw_pair_step(f4 (&acc)[OT][IT], const float* __restrict__ rp, bool 
     for (int i = 0; i < IT; ++i) acc[o][i] = mfma4(a[o], b[i], acc[o][i]);
 }
 
-template <int E, int H, int FF>
+// KIND (0 agent, 1 mixer) only separates the two instances in profiles.
+template <int E, int H, int FF, int KIND>
 __global__ __launch_bounds__(64 * 2 * T2O_MAX_DEPTH) void dw_gemm_kernel(DwGemmArgs a) {
   using R = TapeRec<E, H, FF>;
   constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
@@ -106,7 +110,7 @@ __global__ __launch_bounds__(64 * 2 * T2O_MAX_DEPTH) void dw_gemm_kernel(DwGemmA
 }
 
 template <int E, int H, int FF>
-int launch_dw_gemm(const float* tape, int64_t nrec, int D, float* slabs, int64_t slab_stride, const t2o_layout& G,
+int launch_dw_gemm(int kind, const float* tape, int64_t nrec, int D, float* slabs, int64_t slab_stride, const t2o_layout& G,
                    int nslab, hipStream_t stream) {
   if (D < 1 || D > T2O_MAX_DEPTH || nslab < 1) return T2O_EINVAL;
   DwGemmArgs a{};
@@ -117,9 +121,28 @@ int launch_dw_gemm(const float* tape, int64_t nrec, int D, float* slabs, int64_t
   a.slab_stride = slab_stride;
   a.G = G;
   a.D = D;
-  auto kern = dw_gemm_kernel<E, H, FF>;
+  auto kern = kind == 0 ? dw_gemm_kernel<E, H, FF, 0> : dw_gemm_kernel<E, H, FF, 1>;
   hipLaunchKernelGGL(kern, dim3(nslab), dim3(64 * 2 * D), 0, stream, a);
   return (int)hipGetLastError();
 }
 
 }  // namespace t2o
+
+using namespace t2o;
+
+extern "C" int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t records) {
+  if (!L || records < 0) return -1;
+  return (int64_t)L->D * records * (4 * L->E + 2 * L->H * L->E + 2 * L->FF);
+}
+
+extern "C" int t2o_bwd_tape_contract(const t2o_layout* L, const float* tape, int64_t records, float* gslabs,
+                                     int nslab, void* stream) {
+  if (!L || !tape || !gslabs || records < 0 || nslab < 1) return T2O_EINVAL;
+  t2o_layout G;
+  grad_layout(*L, G);
+  int rc = T2O_EUNSUPPORTED;
+  T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
+               rc = (launch_dw_gemm<E_, H_, FF_>(L->kind, tape, records, L->D, gslabs, G.grad_total, G, nslab,
+                                                 (hipStream_t)stream)));
+  return rc;
+}

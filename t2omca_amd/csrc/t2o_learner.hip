@@ -45,51 +45,83 @@ __device__ float block_sum(float v, float* red) {
   return s;
 }
 
-// mask[b][t] = filled[t] * (t == 0 ? 1 : 1 - term[t-1])   (PyMARL2 nq_learner)
-__device__ float mask_at(const TDArgs& a, int b, int t) {
-  float m = a.filled ? a.filled[b * a.fl_sb + t * a.fl_st] : 1.f;
-  if (t > 0 && a.term) m *= 1.f - a.term[b * a.tm_sb + (t - 1) * a.tm_st];
-  return m;
-}
-
-__global__ __launch_bounds__(1024) void td_loss_kernel(TDArgs a) {
-  __shared__ float red[16];
+// Episodes are independent: a workgroup stages EP episodes' rows in LDS with
+// coalesced loads, one thread per episode runs the (sequential, as in the
+// reference) backward TD(λ) recursion out of LDS, and the block writes gq /
+// targets back coalesced.  Loss and Σ mask are accumulated with float atomics
+// into loss[] (zeroed by the host entry); with mask_sum <= 0 a second pass
+// divides gq and the loss by the local Σ mask.
+//   mask[b][t] = filled[t] * (t == 0 ? 1 : 1 - term[t-1])   (PyMARL2 nq_learner)
+__global__ __launch_bounds__(256) void td_loss_kernel(TDArgs a, int EP) {
+  extern __shared__ float sm[];
+  __shared__ float red[8];
   const int T = a.T;
-  float msum = 0.f;
-  for (int b = threadIdx.x; b < a.B; b += blockDim.x)
-    for (int t = 0; t < T; ++t) msum += mask_at(a, b, t);
-  const float local_msum = block_sum(msum, red);
-  const float denom = a.mask_sum > 0.f ? a.mask_sum : local_msum;
-  float lsum = 0.f;
-  for (int b = threadIdx.x; b < a.B; b += blockDim.x) {
+  const int b0 = blockIdx.x * EP;
+  const int nb = min(EP, a.B - b0);
+  float* R = sm;                 // reward, then dL/dQtot
+  float* TM = R + EP * T;        // terminated
+  float* FL = TM + EP * T;       // filled, then targets
+  float* Q = FL + EP * T;        // qtot
+  float* QT = Q + EP * T;        // qtot_tgt [EP][T+1]
+  for (int i = threadIdx.x; i < nb * T; i += blockDim.x) {
+    const int b = b0 + i / T, t = i % T;
+    R[i] = a.reward[b * a.rw_sb + t * a.rw_st];
+    TM[i] = a.term ? a.term[b * a.tm_sb + t * a.tm_st] : 0.f;
+    FL[i] = a.filled ? a.filled[b * a.fl_sb + t * a.fl_st] : 1.f;
+    Q[i] = a.qtot[(size_t)b0 * T + i];
+  }
+  for (int i = threadIdx.x; i < nb * (T + 1); i += blockDim.x) QT[i] = a.qtot_tgt[(size_t)b0 * (T + 1) + i];
+  __syncthreads();
+  const float denom = a.mask_sum > 0.f ? a.mask_sum : 1.f;
+  float lsum = 0.f, msum = 0.f;
+  if ((int)threadIdx.x < nb) {
+    const int e = threadIdx.x, b = b0 + e;
+    const float* r = R + e * T;
+    const float* tm = TM + e * T;
+    const float* fl = FL + e * T;
+    const float* q = Q + e * T;
+    const float* qt = QT + e * (T + 1);
     // build_td_lambda_targets: ret[T] = Q[T] * (1 - Σ term); backwards recursion
     float tsum = 0.f;
-    if (a.term)
-      for (int t = 0; t < T; ++t) tsum += a.term[b * a.tm_sb + t * a.tm_st];
-    float ret = a.qtot_tgt[(size_t)b * (T + 1) + T] * (1.f - tsum);
+    for (int t = 0; t < T; ++t) tsum += tm[t];
+    float ret = qt[T] * (1.f - tsum);
     const float w = a.weight ? a.weight[b] : 1.f;
     float absum = 0.f, mb = 0.f, lb = 0.f;
     for (int t = T - 1; t >= 0; --t) {
-      const float m = mask_at(a, b, t);
-      const float r = a.reward[b * a.rw_sb + t * a.rw_st];
-      const float tm = a.term ? a.term[b * a.tm_sb + t * a.tm_st] : 0.f;
-      ret = a.lambda_ * a.gamma * ret +
-            m * (r + (1.f - a.lambda_) * a.gamma * a.qtot_tgt[(size_t)b * (T + 1) + t + 1] * (1.f - tm));
-      if (a.targets) a.targets[(size_t)b * T + t] = ret;
-      const float td = a.qtot[(size_t)b * T + t] - ret;
-      a.gq[(size_t)b * T + t] = w * m * td / denom;
+      const float m = fl[t] * (t > 0 ? 1.f - tm[t - 1] : 1.f);
+      ret = a.lambda_ * a.gamma * ret + m * (r[t] + (1.f - a.lambda_) * a.gamma * qt[t + 1] * (1.f - tm[t]));
+      const float td = q[t] - ret;
+      // in-place: row t of R / FL is not read again
+      R[e * T + t] = w * m * td / denom;
+      FL[e * T + t] = ret;
       absum += fabsf(td) * m;
       mb += m;
       lb += 0.5f * td * td * m;
     }
     a.prio[b] = absum / sqrtf(mb);
-    lsum += lb * w;
+    lsum = lb * w;
+    msum = mb;
   }
-  const float tot = block_sum(lsum, red);
+  __syncthreads();
+  for (int i = threadIdx.x; i < nb * T; i += blockDim.x) {
+    a.gq[(size_t)b0 * T + i] = R[i];
+    if (a.targets) a.targets[(size_t)b0 * T + i] = FL[i];
+  }
+  lsum = block_sum(lsum, red);
+  msum = block_sum(msum, red);
   if (threadIdx.x == 0) {
-    a.loss[0] = tot / denom;
-    a.loss[1] = local_msum;
+    unsafeAtomicAdd(a.loss, lsum / denom);
+    unsafeAtomicAdd(a.loss + 1, msum);
   }
+}
+
+// mask_sum <= 0: normalise by the local Σ mask once it is complete.
+__global__ __launch_bounds__(256) void td_normalise_kernel(float* __restrict__ gq, int64_t n, float* loss) {
+  const float inv = 1.0f / loss[1];  // (PyMARL2: / mask.sum())
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    gq[i] *= inv;
+  __syncthreads();
+  if (blockIdx.x == 0 && threadIdx.x == 0) loss[0] *= inv;  // the grid has one block
 }
 
 // ---- Adam -------------------------------------------------------------------
@@ -153,7 +185,17 @@ extern "C" int t2o_td_loss(const float* qtot, const float* qtot_tgt, const float
   if (!qtot || !qtot_tgt || !reward || !gq || !prio || !loss || B < 1 || T < 1) return T2O_EINVAL;
   TDArgs a{qtot, qtot_tgt, reward, term, filled, per_weight, rw_sb, rw_st, tm_sb, tm_st, fl_sb, fl_st,
            gamma, td_lambda, mask_sum, gq, targets, prio, loss, B, T};
-  hipLaunchKernelGGL(td_loss_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a);
+  hipStream_t s = (hipStream_t)stream;
+  const size_t per_ep = sizeof(float) * (5 * (size_t)T + 1);
+  int ep = (int)((96 * 1024) / per_ep);
+  if (ep > 64) ep = 64;
+  if (ep < 1) return T2O_EUNSUPPORTED;
+  if (hipMemsetAsync(loss, 0, 2 * sizeof(float), s) != hipSuccess) return (int)hipGetLastError();
+  (void)hipFuncSetAttribute((const void*)td_loss_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)(ep * per_ep));
+  hipLaunchKernelGGL(td_loss_kernel, dim3((B + ep - 1) / ep), dim3(256), ep * per_ep, s, a, ep);
+  if (mask_sum <= 0.f)
+    hipLaunchKernelGGL(td_normalise_kernel, dim3(1), dim3(256), 0, s, gq, (int64_t)B * T, loss);
   return (int)hipGetLastError();
 }
 

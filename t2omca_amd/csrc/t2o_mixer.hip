@@ -10,7 +10,6 @@
 //   qmode 1  chosen-action Q  gather(Q[:, t], actions)  (online mixer)
 //   qmode 2  double-Q         Q_tgt[argmax(Q_on masked by avail)] (target mixer)
 #include "t2o_dispatch.hpp"
-#include "t2o_dwgemm.hpp"
 #include "t2o_layout.hpp"
 #include "t2o_mixer_block.hpp"
 
@@ -60,6 +59,9 @@ struct MixDims {
   static constexpr int X0F = KT * 16 * LDX;
   static constexpr int OUTF = QT * 16 * E;
   static constexpr int GX0F = KT * 16 * E;
+  // forward: with one query tile the final query rows are complete only after
+  // every key read of the step, so they can live in the key block itself
+  static constexpr int FWD_PERW = X0F + (QT == 1 ? 0 : OUTF);
 };
 
 T2O_DEV float wave_sum(float v) {
@@ -149,8 +151,8 @@ T2O_DEV float mixer_head(const float* __restrict__ P, const t2o_layout& L, const
   return yv + fmaxf(p2, 0.f);
 }
 
-template <int E, int H, int D, int A, int FF>
-__global__ __launch_bounds__(256) void mixer_fwd_kernel(MixerFwdArgs args) {
+template <int E, int H, int D, int A, int FF, bool WLDS>
+__global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
   using Dm = MixDims<E, A>;
   constexpr int ET = E / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -158,16 +160,16 @@ __global__ __launch_bounds__(256) void mixer_fwd_kernel(MixerFwdArgs args) {
   const MixerNet n = args.net[blockIdx.y];
   const t2o_layout& L = args.L;
   // forward weights in LDS for the unroll when they fit beside the per-wave buffers
-  const int lds_w = args.wlds ? (int)((L.fwd_total + 15) / 16 * 16) : 0;
-  if (args.wlds) {
+  const int lds_w = WLDS ? (int)((L.fwd_total + 15) / 16 * 16) : 0;
+  if constexpr (WLDS) {
     copy_to_lds(smem, n.pack, L.fwd_total);
     __syncthreads();
   }
   const int b = blockIdx.x * args.waves + w;
   if (b >= args.B) return;  // wave-uniform; no block barriers after this point
-  const float* __restrict__ P = args.wlds ? smem : n.pack;
-  float* X0 = smem + lds_w + w * (Dm::X0F + Dm::OUTF);
-  float* OUT = X0 + Dm::X0F;
+  const float* P0 = WLDS ? smem : n.pack;  // compile-time: LDS reads stay ds_read
+  float* X0 = smem + lds_w + w * Dm::FWD_PERW;
+  float* OUT = Dm::QT == 1 ? X0 : X0 + Dm::X0F;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
   for (int i = lane; i < Dm::X0F; i += 64) X0[i] = 0.f;
   for (int i = lane; i < 3 * E; i += 64) {
@@ -175,6 +177,7 @@ __global__ __launch_bounds__(256) void mixer_fwd_kernel(MixerFwdArgs args) {
     X0[(Dm::NS + A + k) * Dm::LDX + f] = n.hw0 ? n.hw0[(size_t)b * 3 * E + i] : 0.f;
   }
   for (int t = 0; t < n.T; ++t) {
+    const float* __restrict__ P = step_view(P0);
     build_keys<E, A>(P, L, args, n, b, t, X0);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -208,14 +211,21 @@ __global__ __launch_bounds__(256) void mixer_fwd_kernel(MixerFwdArgs args) {
       for (int ag = 0; ag < A; ++ag)
         if (lane == ag) n.qv[bt * A + ag] = qv[ag];
     }
-    for (int i = lane; i < 3 * E; i += 64) {
-      const int k = i / E, f = i % E;
-      const float v = OUT[(A + k) * E + f];
-      n.hw[bt * 3 * E + i] = v;
-      X0[(Dm::NS + A + k) * Dm::LDX + f] = v;
+    float hv[(3 * E + 63) / 64];
+#pragma unroll
+    for (int k = 0; k < (3 * E + 63) / 64; ++k) {
+      const int i = lane + 64 * k;
+      hv[k] = i < 3 * E ? OUT[(A + i / E) * E + i % E] : 0.f;
+      if (i < 3 * E) n.hw[bt * 3 * E + i] = hv[k];
     }
     if (n.xout) {
       for (int i = lane; i < Dm::Q * E; i += 64) n.xout[bt * Dm::Q * E + i] = OUT[i];
+    }
+    __builtin_amdgcn_wave_barrier();  // OUT (may alias X0) fully read before the hyper rows change
+#pragma unroll
+    for (int k = 0; k < (3 * E + 63) / 64; ++k) {
+      const int i = lane + 64 * k;
+      if (i < 3 * E) X0[(Dm::NS + A + i / E) * Dm::LDX + i % E] = hv[k];
     }
     __builtin_amdgcn_wave_barrier();
   }
@@ -225,10 +235,10 @@ template <int E, int H, int D, int A, int FF>
 int launch_mixer_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
   using Dm = MixDims<E, A>;
   MixerFwdArgs a = args;
-  const size_t wfl = (args.L.fwd_total + 15) / 16 * 16, perw = Dm::X0F + Dm::OUTF;
+  const size_t wfl = (args.L.fwd_total + 15) / 16 * 16, perw = Dm::FWD_PERW;
   size_t lds = 0;
-  // 4 waves with LDS weights, else 2, else 4 waves reading weights from HBM/L2
-  for (a.waves = 4, a.wlds = 1; a.waves >= 2; a.waves >>= 1) {
+  // 8 (2 per SIMD) / 4 / 2 waves with LDS weights, else 4 waves reading weights from L2
+  for (a.waves = 8, a.wlds = 1; a.waves >= 2; a.waves >>= 1) {
     lds = sizeof(float) * (wfl + a.waves * perw);
     if (lds <= 160 * 1024) break;
   }
@@ -238,7 +248,7 @@ int launch_mixer_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
     lds = sizeof(float) * 4 * perw;
     if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
   }
-  auto kern = mixer_fwd_kernel<E, H, D, A, FF>;
+  auto kern = a.wlds ? mixer_fwd_kernel<E, H, D, A, FF, true> : mixer_fwd_kernel<E, H, D, A, FF, false>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid((args.B + a.waves - 1) / a.waves, nnet);
   hipLaunchKernelGGL(kern, grid, dim3(64 * a.waves), lds, stream, a);
@@ -311,7 +321,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) gs[i] = 0.f;
   __syncthreads();
   const int b = blockIdx.x * args.waves + w;
-  const float* __restrict__ P = smem;
+  const float* P0 = smem;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
   const size_t nrec = (size_t)fa.B * n.T * Dm::Q;
   using Rec = TapeRec<E, H, FF>;
@@ -325,6 +335,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) gWe[k] = 0.f;
     for (int t = n.T - 1; t >= 0; --t) {
+      const float* __restrict__ P = step_view(P0);
       const size_t bt = (size_t)b * n.T + t;
       build_keys<E, A>(P, L, fa, n, b, t, X0);
       for (int i = lane; i < 3 * E; i += 64) {
@@ -496,11 +507,8 @@ int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t 
   auto kern = mixer_bwd_kernel<E, H, D, A, FF>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * args.waves), lds, stream, args);
-  int rc = (int)hipGetLastError();
-  if (rc) return rc;
   *nslab = grid;
-  return launch_dw_gemm<E, H, FF>(args.tape, (int64_t)args.f.B * args.f.net[0].T * MixDims<E, A>::Q, D,
-                                  args.slabs, args.G.grad_total, args.G, grid, stream);
+  return (int)hipGetLastError();
 }
 
 }  // namespace

@@ -162,6 +162,10 @@ def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchose
                                      ctypes.byref(nslab), ptr(tape), ptr(gh0), B, T, A, stream_ptr()),
           "agent_unroll_bwd")
     _mark(timer, "end:agent_bwd")
+    _mark(timer, "begin:agent_dw")
+    check(lib().t2o_bwd_tape_contract(ctypes.byref(L), ptr(tape), B * T * A, ptr(slabs), nslab.value, stream_ptr()),
+          "bwd_tape_contract")
+    _mark(timer, "end:agent_dw")
     gpack = torch.empty(L.grad_total, device=obs.device)
     reduce_slabs(slabs, nslab.value, gpack)
     return gpack, gh0
@@ -196,18 +200,18 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
     if avail is not None:
         assert avail.dtype == torch.int32 and avail.stride(3) == 1 and avail.stride(2) == avail.shape[3]
 
-    def outs(T):
+    def outs(T, bwd):
+        # xout / xmid only feed the backward: the target network skips them
         return dict(y=torch.empty(B, T, device=dev), hw=torch.empty(B, T, 3, E, device=dev),
                     qv=torch.empty(B, T, A, device=dev),
-                    xout=torch.empty(B, T, A + 3, E, device=dev) if want_xout else None,
-                    xmid=torch.empty(B, T, shape.D - 1, A + 3, E, device=dev)
-                    if (want_xout and shape.D > 1) else None)
+                    xout=torch.empty(B, T, A + 3, E, device=dev) if bwd else None,
+                    xmid=torch.empty(B, T, shape.D - 1, A + 3, E, device=dev) if (bwd and shape.D > 1) else None)
 
-    o_on = outs(T_on)
+    o_on = outs(T_on, want_xout)
     o_tg = None
     if pack_tg is not None:
         T_tg = T_tg or hid_tg.shape[1]
-        o_tg = outs(T_tg)
+        o_tg = outs(T_tg, False)
     n_actions = q_on.shape[3] if q_on is not None else 0
     act_sb, act_st = _mstrides(actions)
     av_sb, av_st = _mstrides(avail)
@@ -250,6 +254,10 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
         ptr(fwd.get("xmid")), ptr(gy), ptr(ghw_ext), ptr(gqv), ptr(ghid), ptr(ghw0), ptr(slabs), nmax, ctypes.byref(nslab),
         ptr(tape), B, T, stream_ptr()), "mixer_unroll_bwd")
     _mark(timer, "end:mixer_bwd")
+    _mark(timer, "begin:mixer_dw")
+    check(lib().t2o_bwd_tape_contract(ctypes.byref(L), ptr(tape), B * T * (A + 3), ptr(slabs), nslab.value,
+                                      stream_ptr()), "bwd_tape_contract")
+    _mark(timer, "end:mixer_dw")
     gpack = torch.empty(L.grad_total, device=dev)
     reduce_slabs(slabs, nslab.value, gpack)
     return gpack, gqv, ghid, ghw0

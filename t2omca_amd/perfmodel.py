@@ -39,15 +39,35 @@ def mixer_episode_step_flops(E=32, H=3, D=2, A=8, Fs=8, FF=None):
     return D * Q * row_blk + embed + head
 
 
+def dw_record_flops(E=32, H=3, D=2, FF=None):
+    """FLOPs of the tape contraction per record (all D blocks): 2 x |M|+|N|+|W1|+|W2|."""
+    FF = FF or 4 * E
+    return D * 2 * (2 * H * E * E + 2 * FF * E)
+
+
+def dw_record_bytes(E=32, H=3, D=2, FF=None):
+    """Tape bytes per record (all D blocks): written once by the backward, read once here."""
+    FF = FF or 4 * E
+    return D * 4 * (4 * E + 2 * H * E + 2 * FF)
+
+
 def td_update_flops(B, T, A, E=32, H=3, D=2, F=9, Fs=8, NA=5):
-    """Per-kernel algorithmic FLOPs of one TD update (fwd online+target, bwd = 2x fwd)."""
+    """Per-kernel algorithmic FLOPs of one TD update (fwd online+target, bwd = 2x fwd).
+
+    The backward's share of the M/N/W1/W2 weight-gradient contractions is
+    executed by the tape contraction kernels (agent_dw / mixer_dw); the BPTT
+    kernels are charged the rest."""
     fa = agent_row_step_flops(E, H, D, F, A, NA)
     fm = mixer_episode_step_flops(E, H, D, A, Fs)
+    dw_a = B * T * A * dw_record_flops(E, H, D)
+    dw_m = B * T * (A + 3) * dw_record_flops(E, H, D)
     return {
         "agent_fwd": 2 * B * (T + 1) * A * fa,
         "mixer_fwd": (B * T + B * (T + 1)) * fm,
-        "mixer_bwd": 2 * B * T * fm,
-        "agent_bwd": 2 * B * T * A * fa,
+        "mixer_bwd": 2 * B * T * fm - dw_m,
+        "mixer_dw": dw_m,
+        "agent_bwd": 2 * B * T * A * fa - dw_a,
+        "agent_dw": dw_a,
     }
 
 
@@ -56,11 +76,15 @@ def td_update_bytes(B, T, A, E=32, F=9, Fs=8, NA=5):
     obs = B * (T + 1) * A * A * F * 4
     st = B * (T + 1) * A * Fs * 4
     qh = B * (T + 1) * A * (NA + E) * 4
+    tape_a = B * T * A * dw_record_bytes(E)
+    tape_m = B * T * (A + 3) * dw_record_bytes(E)
     return {
         "agent_fwd": obs + 2 * qh,
         "mixer_fwd": st + 2 * qh + 2 * B * (T + 1) * ((A + 3) * E + 3 * E + A + 1) * 4,
-        "mixer_bwd": st + B * T * ((A + 3) * E + 3 * E + 2 * A + A * E + 2) * 4,
-        "agent_bwd": obs + B * T * A * (2 * E + 2) * 4,
+        "mixer_bwd": st + B * T * ((A + 3) * E + 3 * E + 2 * A + A * E + 2) * 4 + tape_m,
+        "mixer_dw": tape_m,
+        "agent_bwd": obs + B * T * A * (2 * E + 2) * 4 + tape_a,
+        "agent_dw": tape_a,
     }
 
 

@@ -1,0 +1,61 @@
+"""GPU: t2o_td_loss against the oracle's PyMARL2 TD(λ) semantics (oracle/ref_learner.py)
+on ragged episodes (filled tails of zeros, early termination), PER weights, both the local
+(mask_sum <= 0) and the externally supplied (data-parallel) normalisation.  fp32; the
+sequential recursion matches the oracle's order, bar: 1e-5 normwise."""
+import pytest
+import torch
+
+from oracle.ref_learner import build_td_lambda_targets
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(B, T, seed):
+    g = torch.Generator().manual_seed(seed)
+    qtot = torch.randn(B, T, generator=g)
+    qtgt = torch.randn(B, T + 1, generator=g)
+    reward = torch.randn(B, T, generator=g)
+    lens = torch.randint(1, T + 1, (B,), generator=g)
+    filled = (torch.arange(T)[None, :] < lens[:, None]).float()
+    term = torch.zeros(B, T)
+    ended = torch.rand(B, generator=g) < 0.5
+    term[torch.arange(B)[ended], (lens - 1)[ended]] = 1.0
+    w = torch.rand(B, generator=g) * 0.5 + 0.5
+    return qtot, qtgt, reward, term, filled, w
+
+
+def _ref(qtot, qtgt, reward, term, filled, w, gamma, lam):
+    mask = filled.clone()
+    mask[:, 1:] = mask[:, 1:] * (1 - term[:, :-1])
+    tg = build_td_lambda_targets(reward, term, mask, qtgt, gamma, lam)
+    td = qtot - tg
+    msum = mask.sum()
+    loss = (w[:, None] * 0.5 * td ** 2 * mask).sum() / msum
+    gq = w[:, None] * mask * td / msum
+    prio = (td.abs() * mask).sum(1) / mask.sum(1).sqrt()
+    return tg, gq, prio, loss, msum
+
+
+def _nw(a, b):
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("B,T", [(1, 1), (7, 5), (300, 60), (1030, 150)])
+def test_td_loss_matches_oracle(B, T):
+    from t2omca_amd import ops
+    qtot, qtgt, reward, term, filled, w = _case(B, T, B * 31 + T)
+    tg, gq, prio, loss, msum = _ref(qtot.double(), qtgt.double(), reward.double(), term.double(),
+                                    filled.double(), w.double(), 0.99, 0.6)
+    c = lambda t: t.cuda().contiguous()  # noqa: E731
+    out = ops.td_loss(c(qtot), c(qtgt), c(reward), c(term), c(filled), c(w), gamma=0.99, td_lambda=0.6,
+                      mask_sum=0.0)
+    assert _nw(out["targets"].cpu().double(), tg) < 1e-5
+    assert _nw(out["gq"].cpu().double(), gq) < 1e-5
+    assert _nw(out["prio"].cpu().double(), prio) < 1e-5
+    assert abs(float(out["loss"][0]) - float(loss)) <= 1e-5 * max(1.0, abs(float(loss)))
+    assert float(out["loss"][1]) == float(msum)
+    # externally supplied normaliser (data parallel): gq and loss scale by 1/mask_sum
+    out2 = ops.td_loss(c(qtot), c(qtgt), c(reward), c(term), c(filled), c(w), gamma=0.99, td_lambda=0.6,
+                       mask_sum=2.0 * float(msum))
+    assert _nw(out2["gq"].cpu().double(), gq / 2) < 1e-5
+    assert float(out2["loss"][1]) == float(msum)

@@ -26,7 +26,9 @@ def per_kernel(d, counter):
                 if row.get("Counter_Name") != counter:
                     continue
                 name = row["Kernel_Name"]
-                short = next((v for k, v in SHORT.items() if re.search(r"\b" + k + r"\b", name)), None)
+                m = re.search(r"dw_gemm_kernel<[^>]*?(\d+)>", name)
+                short = ("agent_dw", "mixer_dw")[int(m.group(1))] if m else \
+                    next((v for k, v in SHORT.items() if re.search(r"\b" + k + r"\b", name)), None)
                 if short is None:
                     continue
                 vals.setdefault(short, []).append(float(row["Counter_Value"]))
