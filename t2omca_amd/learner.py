@@ -112,6 +112,11 @@ class TDLearner:
             self._slabs[key] = t
         return t[:n].view(shape)
 
+    def _side_stream(self):
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.device)
+        return self._side
+
     def _slab(self, key, n):
         t = self._slabs.get(key)
         if t is None or t.numel() < n:
@@ -158,17 +163,26 @@ class TDLearner:
         #    data-parallel sum over ranks divides by the GLOBAL Σ mask)
         td = ops.td_loss(o_on["y"], o_tg["y"], reward, term, filled, w, gamma=self.gamma,
                          td_lambda=self.td_lambda, mask_sum=1.0)
-        # 4. mixer BPTT (one weight-grad tape buffer serves both backward passes:
-        #    each pass's contraction runs before the next pass starts, same stream)
-        tape = self._slab("tape", max(ops.tape_floats(self.sm, B * T * (A + 3)), ops.tape_floats(self.sa, B * T * A)))
+        # 4. mixer BPTT.  Its weight-grad tape contraction (HBM-bound) runs on a
+        #    side stream, overlapping the agent BPTT (latency-bound, half the SIMDs)
+        tape_m = self._slab("tape_m", ops.tape_floats(self.sm, B * T * (A + 3)))
+        tape_a = self._slab("tape_a", ops.tape_floats(self.sa, B * T * A))
         slabs_m = self._slab("m", int(ops.lib().t2o_mixer_bwd_max_slabs(B)) * self.sm.layout().grad_total)
-        gm, gqv, ghid, _ = ops.mixer_unroll_bwd(self.sm, self.pack_m, state, h_on, o_on, td["gq"], slabs=slabs_m,
-                                                timer=self.timer, tape=tape)
+        contract_m, gqv, ghid, _ = ops.mixer_unroll_bwd(self.sm, self.pack_m, state, h_on, o_on, td["gq"],
+                                                        slabs=slabs_m, timer=self.timer, tape=tape_m,
+                                                        defer_contract=True)
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream()
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            gm = contract_m()
         # 5. agent BPTT (grads of the chosen Q and, unless detached, of the hidden states)
         slabs_a = self._slab("a", int(ops.lib().t2o_agent_bwd_max_slabs(B, A)) * self.sa.layout().grad_total)
         ga, _ = ops.agent_unroll_bwd(self.sa, self.pack_a, obs, h_on, gchosen=gqv, actions=act,
                                      gh=None if self.detach_mixer_hidden else ghid, slabs=slabs_a,
-                                     timer=self.timer, hmid=hmid, tape=tape)
+                                     timer=self.timer, hmid=hmid, tape=tape_a)
+        main.wait_stream(side)
+        gm.record_stream(main)
         # 6. grads in reference parameter order
         self.grad.zero_()
         ops.unpack_grads(self.sa, self.params[:self.na], ga, self.grad[:self.na])

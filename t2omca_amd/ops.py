@@ -162,13 +162,7 @@ def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchose
                                      ctypes.byref(nslab), ptr(tape), ptr(gh0), B, T, A, stream_ptr()),
           "agent_unroll_bwd")
     _mark(timer, "end:agent_bwd")
-    _mark(timer, "begin:agent_dw")
-    check(lib().t2o_bwd_tape_contract(ctypes.byref(L), ptr(tape), B * T * A, ptr(slabs), nslab.value, stream_ptr()),
-          "bwd_tape_contract")
-    _mark(timer, "end:agent_dw")
-    gpack = torch.empty(L.grad_total, device=obs.device)
-    reduce_slabs(slabs, nslab.value, gpack)
-    return gpack, gh0
+    return tape_contract(shape, tape, B * T * A, slabs, nslab.value, timer, "agent_dw"), gh0
 
 
 def _mstrides(t):
@@ -229,10 +223,26 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
     return (o_on, o_tg) if pack_tg is not None else o_on
 
 
+def tape_contract(shape: NetShape, tape, records, slabs, nslab, timer=None, tag="dw"):
+    """Fill the M/N/W1/W2 regions of the backward's slabs from its tape, then sum
+    the slabs.  Returns the compact gradient block (on the current stream)."""
+    L = shape.layout()
+    _mark(timer, "begin:" + tag)
+    check(lib().t2o_bwd_tape_contract(ctypes.byref(L), ptr(tape), int(records), ptr(slabs), int(nslab),
+                                      stream_ptr()), "bwd_tape_contract")
+    _mark(timer, "end:" + tag)
+    gpack = torch.empty(L.grad_total, device=slabs.device)
+    reduce_slabs(slabs, nslab, gpack)
+    return gpack
+
+
 def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_ext=None,
-                     want_ghw0=False, slabs=None, timer=None, tape=None):
+                     want_ghw0=False, slabs=None, timer=None, tape=None, defer_contract=False):
     """BPTT of mixer_unroll_fwd (one network, `fwd` = its output dict).
-    Returns (gpack, gqv [B,T,A], ghid [B,T,A,E], ghw0 or None)."""
+    Returns (gpack, gqv [B,T,A], ghid [B,T,A,E], ghw0 or None).  With
+    defer_contract the first item is instead a zero-argument callable that runs
+    the tape contraction + slab sum (on whatever stream is current when called)
+    and returns gpack."""
     _dev(pack, states, hid, gy, hw0, ghw_ext)
     B, T = gy.shape
     A, E = hid.shape[2], shape.E
@@ -254,13 +264,8 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
         ptr(fwd.get("xmid")), ptr(gy), ptr(ghw_ext), ptr(gqv), ptr(ghid), ptr(ghw0), ptr(slabs), nmax, ctypes.byref(nslab),
         ptr(tape), B, T, stream_ptr()), "mixer_unroll_bwd")
     _mark(timer, "end:mixer_bwd")
-    _mark(timer, "begin:mixer_dw")
-    check(lib().t2o_bwd_tape_contract(ctypes.byref(L), ptr(tape), B * T * (A + 3), ptr(slabs), nslab.value,
-                                      stream_ptr()), "bwd_tape_contract")
-    _mark(timer, "end:mixer_dw")
-    gpack = torch.empty(L.grad_total, device=dev)
-    reduce_slabs(slabs, nslab.value, gpack)
-    return gpack, gqv, ghid, ghw0
+    contract = lambda: tape_contract(shape, tape, B * T * (A + 3), slabs, nslab.value, timer, "mixer_dw")  # noqa: E731
+    return (contract if defer_contract else contract()), gqv, ghid, ghw0
 
 
 def td_loss(qtot, qtot_tgt, reward, terminated=None, filled=None, per_weight=None, gamma=0.99,
