@@ -46,13 +46,20 @@ enum {
   T2O_EUNSUPPORTED = -2 /* no kernel instantiated for this (E, H, D, n) */
 };
 
-/* Offsets (in floats) of every tensor of one network's device pack.  The pack
+/* Offsets (in elements) of every tensor of one network's device pack.  The pack
  * holds the folded weights the kernels read (M_h = Wk_hᵀWq_h/√E,
  * N_h = U_h·Wv_h, zero-padded embedding / head matrices) plus transposed
- * copies for the backward.  A gradient slab uses the same layout; its
- * transposed entries are unused.  kind 0 = agent, 1 = mixer. */
+ * copies for the backward.  Order: forward matrices [0, vec_lo), forward
+ * vectors (biases, LayerNorm) [vec_lo, fwd_total), transposed copies
+ * [fwd_total, total).  kind 0 = agent, 1 = mixer.
+ * prec 0 (fp32): the pack is `total` floats.  prec 1 (bf16 MFMA operands): the
+ * fp32 pack is followed, at float offset `total`, by a bf16 image of it (the
+ * kernels read matrices from the image and vectors from the fp32 part); the
+ * buffer is `pack_floats` floats.  Activations, LayerNorm, softmax, recurrent
+ * state and every accumulation stay fp32 in both modes. */
 typedef struct {
   int32_t kind, E, H, D, F, NA, FF, n_ent;
+  int32_t prec, reserved_;
   int64_t WeT, We, be;        /* WeT[16][E], We[E][16], be[E] (F <= 16) */
   int64_t Wo, bo, WoT;        /* agent: q_basic padded Wo[16][E], bo[16], WoT[E][16];
                                  mixer: hyper_b2.weight in Wo row 0, bias in bo[0] */
@@ -62,13 +69,18 @@ typedef struct {
   int64_t W1[T2O_MAX_DEPTH], W1T[T2O_MAX_DEPTH], c1[T2O_MAX_DEPTH]; /* [FF][E],[E][FF],[FF] */
   int64_t W2[T2O_MAX_DEPTH], W2T[T2O_MAX_DEPTH], c2[T2O_MAX_DEPTH]; /* [E][FF],[FF][E],[E] */
   int64_t g2[T2O_MAX_DEPTH], n2[T2O_MAX_DEPTH];
-  int64_t fwd_total;          /* floats [0, fwd_total) = every tensor the forward reads */
-  int64_t total;              /* pack size in floats */
+  int64_t fwd_total;          /* elements [0, fwd_total) = every tensor the forward reads */
+  int64_t total;              /* elements of the pack */
   int64_t grad_total;         /* size of the compact gradient block (no transposes) */
+  int64_t vec_lo;             /* first vector element (see above) */
+  int64_t pack_floats;        /* buffer size of a pack in floats (prec 1: fp32 + bf16 image) */
 } t2o_layout;
 
-/* Fill *L for a network; returns 0 or T2O_EINVAL. */
-int t2o_layout_init(t2o_layout* L, int kind, int E, int H, int D, int F, int NA, int FF, int n_ent);
+/* Fill *L for a network (prec 0 = fp32, 1 = bf16 MFMA operands); returns 0 or T2O_EINVAL. */
+int t2o_layout_init(t2o_layout* L, int kind, int E, int H, int D, int F, int NA, int FF, int n_ent, int prec);
+
+/* sizeof(t2o_layout), for bindings to check their mirror of the struct. */
+int t2o_layout_sizeof(void);
 
 /* Reference parameter order (state_dict order of transf_agent.py /
  * n_transf_mixer.py, SURVEY.md §8 b) flattened into one fp32 buffer:

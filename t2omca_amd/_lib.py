@@ -15,17 +15,19 @@ _I64x = ctypes.c_int64 * MAX_DEPTH
 
 
 class Layout(ctypes.Structure):
-    _fields_ = ([(n, ctypes.c_int32) for n in ("kind", "E", "H", "D", "F", "NA", "FF", "n_ent")] +
+    _fields_ = ([(n, ctypes.c_int32) for n in ("kind", "E", "H", "D", "F", "NA", "FF", "n_ent", "prec",
+                                                "reserved_")] +
                 [(n, ctypes.c_int64) for n in ("WeT", "We", "be", "Wo", "bo", "WoT")] +
                 [(n, _I64x) for n in ("M", "MT", "N", "NT", "bu", "g1", "n1", "W1", "W1T", "c1",
                                       "W2", "W2T", "c2", "g2", "n2")] +
-                [("fwd_total", ctypes.c_int64), ("total", ctypes.c_int64), ("grad_total", ctypes.c_int64)])
+                [(n, ctypes.c_int64) for n in ("fwd_total", "total", "grad_total", "vec_lo", "pack_floats")])
 
 
 EXPORTS = {
     # name: (restype, argtypes)
-    "t2o_layout_init": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_int] * 8),
+    "t2o_layout_init": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_int] * 9),
     "t2o_param_count": (ctypes.c_int64, [ctypes.c_int] * 7),
+    "t2o_layout_sizeof": (ctypes.c_int, []),
     "t2o_pack_params": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p]),
     "t2o_unpack_grads": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_void_p, ctypes.c_void_p,
@@ -102,7 +104,7 @@ def stream_ptr(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
-def make_layout(kind, E, H, D, F, NA, FF, n_ent):
+def make_layout(kind, E, H, D, F, NA, FF, n_ent, prec=0):
     L = Layout()
-    check(lib().t2o_layout_init(ctypes.byref(L), kind, E, H, D, F, NA, FF, n_ent), "t2o_layout_init")
+    check(lib().t2o_layout_init(ctypes.byref(L), kind, E, H, D, F, NA, FF, n_ent, prec), "t2o_layout_init")
     return L

@@ -40,16 +40,19 @@ inline int rows_per_wave(int R) { return (void)R, 16; }
 
 constexpr int AG_FWD_WAVES = 4;  // waves per workgroup sharing one LDS copy of the weights
 
-template <int E, int H, int D, int NE, int FF, bool WLDS>
+template <int E, int H, int D, int NE, int FF, bool WLDS, typename WT>
 __global__ __launch_bounds__(64 * AG_FWD_WAVES) void agent_fwd_kernel(AgentFwdArgs args) {
   constexpr int ET = E / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const AgentNet net = args.net[blockIdx.y];
   const t2o_layout& L = args.L;
   // the forward section of the pack lives in LDS for the whole unroll (when it fits)
+  Wts<WT> P0;
   if constexpr (WLDS) {
-    copy_to_lds(smem, net.pack, L.fwd_total);
+    P0 = stage_weights(smem, net.pack, L, L.fwd_total, WT{});
     __syncthreads();
+  } else {
+    P0 = global_weights(net.pack, L, WT{});
   }
   const int A = args.A, F = args.F;
   const int R = args.B * A;
@@ -60,14 +63,13 @@ __global__ __launch_bounds__(64 * AG_FWD_WAVES) void agent_fwd_kernel(AgentFwdAr
   const bool valid = c < args.rpw && row_raw < R;
   const int row = valid ? row_raw : R - 1;
   const int b = row / A, a = row % A;
-  const float* P0 = WLDS ? smem : net.pack;  // compile-time: LDS reads stay ds_read
 
   f4 h[ET];
 #pragma unroll
   for (int t = 0; t < ET; ++t) h[t] = net.h0 ? ld4(net.h0 + (size_t)row * E + 16 * t + 4 * g) : zero4();
 
   for (int step = 0; step < args.T; ++step) {
-    const float* __restrict__ P = step_view(P0);
+    const Wts<WT> P = step_view(P0);
     const float* ob = args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * NE * F;
     f4 o[NE];
 #pragma unroll
@@ -91,8 +93,8 @@ __global__ __launch_bounds__(64 * AG_FWD_WAVES) void agent_fwd_kernel(AgentFwdAr
     }
     f4 q = zero4();
 #pragma unroll
-    for (int i = 0; i < ET; ++i) q = mma_tile(P + L.Wo, E, 0, i, x[i], q);
-    q += vec_t(P + L.bo, 0);
+    for (int i = 0; i < ET; ++i) q = mma_tile(P.w + L.Wo, E, 0, i, x[i], q);
+    q += vec_t(P.v + L.bo, 0);
 #pragma unroll
     for (int t = 0; t < ET; ++t) h[t] = x[t];
     if (valid) {
@@ -108,17 +110,17 @@ __global__ __launch_bounds__(64 * AG_FWD_WAVES) void agent_fwd_kernel(AgentFwdAr
   }
 }
 
-template <int E, int H, int D, int NE, int FF>
+template <int E, int H, int D, int NE, int FF, typename WT>
 int launch_fwd(const AgentFwdArgs& args, int nnet, hipStream_t stream) {
   const int R = args.B * args.A;
   AgentFwdArgs a = args;
   a.rpw = rows_per_wave(R);
   const int tiles = (R + a.rpw - 1) / a.rpw;
   dim3 grid((tiles + AG_FWD_WAVES - 1) / AG_FWD_WAVES, nnet);
-  size_t lds = sizeof(float) * (size_t)args.L.fwd_total;
+  size_t lds = sizeof(float) * (size_t)lds_weight_floats<WT>(args.L, args.L.fwd_total);
   a.wlds = lds <= 160 * 1024;
   if (!a.wlds) lds = 0;
-  auto kern = a.wlds ? agent_fwd_kernel<E, H, D, NE, FF, true> : agent_fwd_kernel<E, H, D, NE, FF, false>;
+  auto kern = a.wlds ? agent_fwd_kernel<E, H, D, NE, FF, true, WT> : agent_fwd_kernel<E, H, D, NE, FF, false, WT>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, grid, dim3(64 * AG_FWD_WAVES), lds, stream, a);
   return (int)hipGetLastError();
@@ -159,7 +161,7 @@ struct AgentBwdArgs {
 
 constexpr int AG_BWD_WAVES = 2;  // (each wave needs a SIMD's full 512-register file)
 
-template <int E, int H, int D, int NE, int FF>
+template <int E, int H, int D, int NE, int FF, typename WT>
 __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdArgs args) {
   constexpr int ET = E / 16;
   constexpr int STAGE = StageDims<1>::FLOATS;
@@ -167,10 +169,13 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const t2o_layout& L = args.L;
   const t2o_layout& G = args.G;
-  const int lds_w = (int)((L.fwd_total + 15) / 16 * 16);
+  // fp32 reads the forward matrices transposed in place; bf16 stages the
+  // whole pack (its transposed copies included)
+  const int64_t nw = sizeof(WT) == 4 ? L.fwd_total : L.total;
+  const int lds_w = (int)((lds_weight_floats<WT>(L, nw) + 15) / 16 * 16);
   float* stage = smem + lds_w + wave_id() * STAGE;
   float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
-  copy_to_lds(smem, args.pack, L.fwd_total);
+  const Wts<WT> P0 = stage_weights(smem, args.pack, L, nw, WT{});
   for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) gs[i] = 0.f;
   __syncthreads();
 
@@ -182,7 +187,6 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
   const bool valid = c < args.rpw && row_raw < R;
   const int row = valid ? row_raw : R - 1;
   const int b = row / A, a = row % A;
-  const float* P0 = smem;
   const size_t nrec = (size_t)T * R;
 
   if (rt * args.rpw < R) {
@@ -193,7 +197,7 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
 #pragma unroll
     for (int t = 0; t < ET; ++t) gh_rec[t] = zero4();
     for (int step = T - 1; step >= 0; --step) {
-      const float* __restrict__ P = step_view(P0);
+      const Wts<WT> P = step_view(P0);
       f4 h[ET];
       const float* hp = step == 0 ? args.h0 : args.h_seq + (((size_t)b * args.h_ts + step - 1) * A + a) * E;
       if (step == 0 && args.h0) hp = args.h0 + (size_t)row * E;
@@ -267,10 +271,10 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
         for (int t = 0; t < ET; ++t) x[t] = xs[d][t];
         agent_block_fwd<E, H, NE, FF, true>(P, L, d, h, o, x, &cache);
         if (d == D - 1) {  // q = Wo x + bo
-          dw_accumulate_regs<1, ET>(gWo, &gq, x, stage);
+          dw_accumulate_regs<1, ET, sizeof(WT) == 2>(gWo, &gq, x, stage);
           vec_accumulate_g<1>(gs + G.bo, &gq);
           f4 t1[ET];
-          matvec_t<ET, 1>(P + L.Wo, E, &gq, t1);
+          matvec_tr<ET, 1>(P, L.Wo, E, L.WoT, 16, &gq, t1);
 #pragma unroll
           for (int t = 0; t < ET; ++t) gx[t] += t1[t];
         }
@@ -290,15 +294,17 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
   }
 }
 
-template <int E, int H, int D, int NE, int FF>
+template <int E, int H, int D, int NE, int FF, typename WT>
 int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
   const int R = args.B * args.A;
   args.rpw = rows_per_wave(R);
   const int tiles = (R + args.rpw - 1) / args.rpw;
   const int grid = (tiles + AG_BWD_WAVES - 1) / AG_BWD_WAVES;
   if (grid > max_slabs) return T2O_EINVAL;
-  const size_t lds = sizeof(float) * ((size_t)(args.L.fwd_total + 15) / 16 * 16 + AG_BWD_WAVES * StageDims<1>::FLOATS);
-  auto kern = agent_bwd_kernel<E, H, D, NE, FF>;
+  const int64_t nw = sizeof(WT) == 4 ? args.L.fwd_total : args.L.total;
+  const size_t lds =
+      sizeof(float) * ((size_t)(lds_weight_floats<WT>(args.L, nw) + 15) / 16 * 16 + AG_BWD_WAVES * StageDims<1>::FLOATS);
+  auto kern = agent_bwd_kernel<E, H, D, NE, FF, WT>;
   if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * AG_BWD_WAVES), lds, stream, args);
@@ -332,7 +338,9 @@ extern "C" int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, c
   args.A = A;
   args.F = L->F;
   int rc = T2O_EUNSUPPORTED;
-  T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF, rc = (launch_fwd<E_, H_, D_, NE_, FF_>(args, nnet, (hipStream_t)stream)));
+  T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
+               rc = (L->prec ? launch_fwd<E_, H_, D_, NE_, FF_, __bf16>(args, nnet, (hipStream_t)stream)
+                             : launch_fwd<E_, H_, D_, NE_, FF_, float>(args, nnet, (hipStream_t)stream)));
   return rc;
 }
 
@@ -371,7 +379,8 @@ extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, cons
   args.F = L->F;
   int rc = T2O_EUNSUPPORTED;
   T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
-               rc = (launch_bwd<E_, H_, D_, NE_, FF_>(args, max_slabs, nslab, (hipStream_t)stream)));
+               rc = (L->prec ? launch_bwd<E_, H_, D_, NE_, FF_, __bf16>(args, max_slabs, nslab, (hipStream_t)stream)
+                             : launch_bwd<E_, H_, D_, NE_, FF_, float>(args, max_slabs, nslab, (hipStream_t)stream)));
   return rc;
 }
 

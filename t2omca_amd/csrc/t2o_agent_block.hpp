@@ -32,19 +32,19 @@ struct AgentCache {
 
 // Forward of block d.  h: hidden token (layer-0 key 0), o: observations,
 // x: in = block input query, out = block output.
-template <int E, int H, int NE, int FF, bool CACHE>
-T2O_DEV void agent_block_fwd(const float* __restrict__ P, const t2o_layout& L, int d, const f4* h,
+template <int E, int H, int NE, int FF, bool CACHE, typename WT>
+T2O_DEV void agent_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* h,
                              const f4 (&o)[NE], f4* x, AgentCache<E, H, NE, FF>* cache) {
   constexpr int ET = E / 16, HET = H * ET;
-  const float* be = P + L.be;
+  const float* be = P.v + L.be;
   f4 u[HET];
-  matvec<HET, ET>(P + L.M[d], E, x, u);
+  matvec<HET, ET>(P.w + L.M[d], E, x, u);
   f4 z[HET];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
     float p[NE + 1];
     f4 w;
-    matvec<1, ET>(P + L.WeT, E, &u[hh * ET], &w);
+    matvec<1, ET>(P.w + L.WeT, E, &u[hh * ET], &w);
     float cpart = 0.f, s0part = 0.f;
 #pragma unroll
     for (int t = 0; t < ET; ++t) {
@@ -80,7 +80,7 @@ T2O_DEV void agent_block_fwd(const float* __restrict__ P, const t2o_layout& L, i
       Ps += p[j + 1];
     }
     f4 zz[ET];
-    matvec<ET, 1>(P + L.We, 16, &oh, zz);
+    matvec<ET, 1>(P.w + L.We, 16, &oh, zz);
 #pragma unroll
     for (int t = 0; t < ET; ++t) z[hh * ET + t] = zz[t] + p[0] * h[t] + Ps * vec_t(be, t);
     if constexpr (CACHE) {
@@ -102,13 +102,14 @@ T2O_DEV void agent_block_fwd(const float* __restrict__ P, const t2o_layout& L, i
 // path (token 0); gbe the grad wrt the embedding bias; gWe (MFMA register
 // block, [E][16] as ET x 1 tiles) the grad wrt the embedding weight.  M's
 // operand pair goes to the tape record (t2o_common.hpp TapeRec).
-template <int E, int H, int NE, int FF>
-T2O_DEV void agent_block_bwd(const float* __restrict__ P, const t2o_layout& L, const t2o_layout& G,
+template <int E, int H, int NE, int FF, typename WT>
+T2O_DEV void agent_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G,
                              float* __restrict__ gs, float* __restrict__ rec, float* __restrict__ stage, int d,
                              const f4* h, const f4 (&o)[NE], const AgentCache<E, H, NE, FF>& c, f4* gx,
                              f4* gh_in, f4* gbe, f4 (&gWe)[E / 16][1]) {
   constexpr int ET = E / 16, HET = H * ET;
-  const float* be = P + L.be;
+  constexpr bool BF = sizeof(WT) == 2;
+  const float* be = P.v + L.be;
   f4 gz[HET], gres[ET];
   post_bwd<E, H, FF>(P, L, G, gs, rec, d, c.post, gx, gz, gres);
   f4 gu[HET];
@@ -130,8 +131,8 @@ T2O_DEV void agent_block_bwd(const float* __restrict__ P, const t2o_layout& L, c
     const float gp0 = allsum4(gp0p);
     const float gP = allsum4(gPp);
     f4 goh;
-    matvec_t<1, ET>(P + L.We, 16, gzh, &goh);
-    dw_accumulate_regs<ET, 1>(gWe, gzh, &c.oh[hh], stage);
+    matvec_tr<1, ET>(P, L.We, 16, L.WeT, E, gzh, &goh);
+    dw_accumulate_regs<ET, 1, BF>(gWe, gzh, &c.oh[hh], stage);
     // softmax backward over [token 0, entities]
     float gp[NE + 1];
     gp[0] = gp0;
@@ -154,14 +155,14 @@ T2O_DEV void agent_block_bwd(const float* __restrict__ P, const t2o_layout& L, c
     }
     // s_h0 = u_h·h ; s_hj = (WeT u_h)·o_j + u_h·be
     f4 t1[ET];
-    matvec<ET, 1>(P + L.We, 16, &gw, t1);
+    matvec<ET, 1>(P.w + L.We, 16, &gw, t1);
 #pragma unroll
     for (int t = 0; t < ET; ++t) {
       gu[hh * ET + t] = t1[t] + gs0 * h[t] + gc * vec_t(be, t);
       gh_in[t] += gs0 * uh[t];
       gbe[t] += gc * uh[t];
     }
-    dw_accumulate_regs<ET, 1>(gWe, uh, &gw, stage);
+    dw_accumulate_regs<ET, 1, BF>(gWe, uh, &gw, stage);
   }
   // u = M x
   if (rec) {
@@ -169,7 +170,7 @@ T2O_DEV void agent_block_bwd(const float* __restrict__ P, const t2o_layout& L, c
     rec_store<ET>(rec, TapeRec<E, H, FF>::X, c.post.x);
   }
   f4 gxp[ET];
-  matvec_t<ET, HET>(P + L.M[d], E, gu, gxp);
+  matvec_tr<ET, HET>(P, L.M[d], E, L.MT[d], H * E, gu, gxp);
 #pragma unroll
   for (int t = 0; t < ET; ++t) gx[t] = gxp[t] + gres[t];
 }

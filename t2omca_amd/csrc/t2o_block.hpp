@@ -25,29 +25,28 @@ struct PostCache {
 };
 
 // x: in = block input, out = block output.
-template <int E, int H, int FF, bool CACHE>
-T2O_DEV void post_fwd(const float* __restrict__ P, const t2o_layout& L, int d, const f4* z, f4* x,
-                      PostCache<E, H, FF>* c) {
+template <int E, int H, int FF, bool CACHE, typename WT>
+T2O_DEV void post_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* z, f4* x, PostCache<E, H, FF>* c) {
   constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
   f4 r1[ET];
-  matvec<ET, HET>(P + L.N[d], H * E, z, r1);
+  matvec<ET, HET>(P.w + L.N[d], H * E, z, r1);
 #pragma unroll
-  for (int t = 0; t < ET; ++t) r1[t] += vec_t(P + L.bu[d], t) + x[t];
+  for (int t = 0; t < ET; ++t) r1[t] += vec_t(P.v + L.bu[d], t) + x[t];
   f4 y[ET], xh1[ET];
   float rs1;
-  layernorm_fwd<ET>(r1, P + L.g1[d], P + L.n1[d], y, xh1, rs1);
+  layernorm_fwd<ET>(r1, P.v + L.g1[d], P.v + L.n1[d], y, xh1, rs1);
   f4 f1[FT], f1r[FT];
-  matvec<FT, ET>(P + L.W1[d], E, y, f1);
+  matvec<FT, ET>(P.w + L.W1[d], E, y, f1);
 #pragma unroll
   for (int t = 0; t < FT; ++t) {
-    f1[t] += vec_t(P + L.c1[d], t);
+    f1[t] += vec_t(P.v + L.c1[d], t);
 #pragma unroll
     for (int r = 0; r < 4; ++r) f1r[t][r] = fmaxf(f1[t][r], 0.f);
   }
   f4 r2[ET];
-  matvec<ET, FT>(P + L.W2[d], FF, f1r, r2);
+  matvec<ET, FT>(P.w + L.W2[d], FF, f1r, r2);
 #pragma unroll
-  for (int t = 0; t < ET; ++t) r2[t] += vec_t(P + L.c2[d], t) + y[t];
+  for (int t = 0; t < ET; ++t) r2[t] += vec_t(P.v + L.c2[d], t) + y[t];
   if constexpr (CACHE) {
 #pragma unroll
     for (int t = 0; t < ET; ++t) {
@@ -63,7 +62,7 @@ T2O_DEV void post_fwd(const float* __restrict__ P, const t2o_layout& L, int d, c
   }
   f4 xh2[ET];
   float rs2;
-  layernorm_fwd<ET>(r2, P + L.g2[d], P + L.n2[d], x, xh2, rs2);
+  layernorm_fwd<ET>(r2, P.v + L.g2[d], P.v + L.n2[d], x, xh2, rs2);
   if constexpr (CACHE) {
 #pragma unroll
     for (int t = 0; t < ET; ++t) c->xh2[t] = xh2[t];
@@ -76,8 +75,8 @@ T2O_DEV void post_fwd(const float* __restrict__ P, const t2o_layout& L, int d, c
 // the big weight grads (N, W1, W2) go to this row's tape record `rec` (null for
 // padding rows); vector grads go to the workgroup's global slab gs (layout G).
 // Weights are read from P (LDS); transposed products use matvec_t.
-template <int E, int H, int FF>
-T2O_DEV void post_bwd(const float* __restrict__ P, const t2o_layout& L, const t2o_layout& G,
+template <int E, int H, int FF, typename WT>
+T2O_DEV void post_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G,
                       float* __restrict__ gs, float* __restrict__ rec, int d, const PostCache<E, H, FF>& c,
                       const f4* gx, f4* gz, f4* gres) {
   constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
@@ -90,7 +89,7 @@ T2O_DEV void post_bwd(const float* __restrict__ P, const t2o_layout& L, const t2
     vec_accumulate_g<ET>(gs + G.n2[d], gx);
   }
   f4 gr2[ET];
-  layernorm_bwd<ET>(gx, c.xh2, c.rs2, P + L.g2[d], gr2);
+  layernorm_bwd<ET>(gx, c.xh2, c.rs2, P.v + L.g2[d], gr2);
   // r2 = W2 relu(f1) + c2 + y
   if (rec) {
     rec_store<ET>(rec, R::GR2, gr2);
@@ -98,7 +97,7 @@ T2O_DEV void post_bwd(const float* __restrict__ P, const t2o_layout& L, const t2
   }
   vec_accumulate_g<ET>(gs + G.c2[d], gr2);
   f4 gf1[FT];
-  matvec_t<FT, ET>(P + L.W2[d], FF, gr2, gf1);
+  matvec_tr<FT, ET>(P, L.W2[d], FF, L.W2T[d], E, gr2, gf1);
 #pragma unroll
   for (int t = 0; t < FT; ++t)
 #pragma unroll
@@ -109,7 +108,7 @@ T2O_DEV void post_bwd(const float* __restrict__ P, const t2o_layout& L, const t2
   }
   vec_accumulate_g<FT>(gs + G.c1[d], gf1);
   f4 gy[ET];
-  matvec_t<ET, FT>(P + L.W1[d], E, gf1, gy);
+  matvec_tr<ET, FT>(P, L.W1[d], E, L.W1T[d], FF, gf1, gy);
 #pragma unroll
   for (int t = 0; t < ET; ++t) gy[t] += gr2[t];
   {  // LN1: y = xh1*g1 + n1
@@ -119,14 +118,14 @@ T2O_DEV void post_bwd(const float* __restrict__ P, const t2o_layout& L, const t2
     vec_accumulate_g<ET>(gs + G.g1[d], t0);
     vec_accumulate_g<ET>(gs + G.n1[d], gy);
   }
-  layernorm_bwd<ET>(gy, c.xh1, c.rs1, P + L.g1[d], gres);
+  layernorm_bwd<ET>(gy, c.xh1, c.rs1, P.v + L.g1[d], gres);
   // r1 = N z + b_U + x
   if (rec) {
     rec_store<ET>(rec, R::GRES, gres);
     rec_store<HET>(rec, R::Z, c.z);
   }
   vec_accumulate_g<ET>(gs + G.bu[d], gres);
-  matvec_t<HET, ET>(P + L.N[d], H * E, gres, gz);
+  matvec_tr<HET, ET>(P, L.N[d], H * E, L.NT[d], E, gres, gz);
 }
 
 }  // namespace t2o

@@ -86,6 +86,70 @@ T2O_DEV void matvec_t(const float* __restrict__ W, int ldw, const f4* x, f4* y) 
   }
 }
 
+// ---- bf16 MFMA operands (prec 1) ---------------------------------------------
+// v_mfma_f32_16x16x16_bf16 takes, per lane, 4 consecutive K values of A and B:
+// lane (g, c) gives A[c][4g..4g+3] and B[4g..4g+3][c] — exactly one T-layout
+// f4 rounded to bf16 for B and 4 consecutive bf16 of a weight row for A, so a
+// 16x16 tile is ONE MFMA instead of four f32 ones.  16x16x32 takes 8 K values
+// per lane; feeding it (tile i, tile i+1) pairs with the same pairing in A and
+// B contracts two 16-feature tiles per instruction.  Accumulation is fp32.
+typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef short s4v __attribute__((ext_vector_type(4)));
+
+T2O_DEV bf4 to_bf4(f4 x) { return __builtin_convertvector(x, bf4); }
+T2O_DEV bf4 ldb4(const __bf16* p) { return *reinterpret_cast<const bf4*>(p); }
+T2O_DEV f4 mfma_b16(bf4 a, bf4 b, f4 acc) {
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s4v, a), __builtin_bit_cast(s4v, b), acc, 0, 0,
+                                                    0);
+}
+T2O_DEV f4 mfma_b32(bf4 a0, bf4 a1, bf4 b0, bf4 b1, f4 acc) {
+  const bf8 a = __builtin_shufflevector(a0, a1, 0, 1, 2, 3, 4, 5, 6, 7);
+  const bf8 b = __builtin_shufflevector(b0, b1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+}
+
+T2O_DEV f4 mma_tile(const __bf16* __restrict__ W, int ldw, int o, int i, f4 x, f4 acc) {
+  return mfma_b16(ldb4(W + (size_t)(16 * o + lane_c()) * ldw + 16 * i + 4 * lane_g()), to_bf4(x), acc);
+}
+
+// y[0..OT) = W · x[0..IT), bf16 weights and operands, fp32 accumulate
+template <int OT, int IT>
+T2O_DEV void matvec(const __bf16* __restrict__ W, int ldw, const f4* x, f4* y) {
+  const int c = lane_c(), g = lane_g();
+  bf4 xb[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) xb[i] = to_bf4(x[i]);
+#pragma unroll
+  for (int o = 0; o < OT; ++o) {
+    const __bf16* row = W + (size_t)(16 * o + c) * ldw + 4 * g;
+    f4 acc = zero4();
+#pragma unroll
+    for (int i = 0; i + 1 < IT; i += 2) acc = mfma_b32(ldb4(row + 16 * i), ldb4(row + 16 * i + 16), xb[i], xb[i + 1], acc);
+    if constexpr (IT & 1) acc = mfma_b16(ldb4(row + 16 * (IT - 1)), xb[IT - 1], acc);
+    y[o] = acc;
+  }
+}
+
+// The kernels' weight view: matrices (fp32 or bf16) and vectors (always fp32).
+template <typename WT>
+struct Wts {
+  const WT* w;
+  const float* v;
+  T2O_DEV float s(int64_t off) const { return (float)w[off]; }
+};
+
+// y = Wᵀ x: fp32 reads W transposed in place (matvec_t); bf16 uses the pack's
+// transposed copy WT [16*OT rows][ldT] with the plain product.
+template <int OT, int IT>
+T2O_DEV void matvec_tr(const Wts<float>& P, int64_t off, int ld, int64_t offT, int ldT, const f4* x, f4* y);
+template <int OT, int IT>
+T2O_DEV void matvec_tr(const Wts<__bf16>& P, int64_t off, int ld, int64_t offT, int ldT, const f4* x, f4* y) {
+  (void)off;
+  (void)ld;
+  matvec<OT, IT>(P.w + offT, ldT, x, y);
+}
+
 // Weights staged in LDS are invariant across a kernel's step loop, so LICM
 // would hoist every weight read out of the loop into registers (hundreds per
 // lane, then spills).  Re-deriving the base pointer through an opaque zero
@@ -94,6 +158,19 @@ T2O_DEV const float* step_view(const float* base) {
   int off = 0;
   asm volatile("" : "+s"(off));
   return base + off;
+}
+template <typename WT>
+T2O_DEV Wts<WT> step_view(const Wts<WT>& p) {
+  int off = 0;
+  asm volatile("" : "+s"(off));
+  return Wts<WT>{p.w + off, p.v + off};
+}
+
+template <int OT, int IT>
+T2O_DEV void matvec_tr(const Wts<float>& P, int64_t off, int ld, int64_t offT, int ldT, const f4* x, f4* y) {
+  (void)offT;
+  (void)ldT;
+  matvec_t<OT, IT>(P.w + off, ld, x, y);
 }
 
 // T-layout slice of a bias / gamma vector: elements 16t+4g .. 16t+4g+3
@@ -215,6 +292,31 @@ T2O_DEV void copy_to_lds(float* __restrict__ dst, const float* __restrict__ src,
   for (int64_t i = 4 * (int64_t)threadIdx.x; i < n; i += 4 * (int64_t)blockDim.x) st4(dst + i, ld4(src + i));
 }
 
+// ---- a kernel's weight view ---------------------------------------------------
+// fp32: the first n elements of the pack, copied as is.  bf16: the bf16 image of
+// the first n elements (matrices; vector slots ride along unused) followed by
+// the fp32 vector range [vec_lo, fwd_total).  Vectors are addressed with the
+// pack's own offsets through a shifted base.
+T2O_DEV Wts<float> stage_weights(float* smem, const float* pack, const t2o_layout& L, int64_t n, float) {
+  copy_to_lds(smem, pack, n);
+  return Wts<float>{smem, smem};
+}
+T2O_DEV Wts<__bf16> stage_weights(float* smem, const float* pack, const t2o_layout& L, int64_t n, __bf16) {
+  copy_to_lds(smem, pack + L.total, n / 2);
+  float* v = smem + n / 2;
+  copy_to_lds(v, pack + L.vec_lo, L.fwd_total - L.vec_lo);
+  return Wts<__bf16>{reinterpret_cast<const __bf16*>(smem), v - L.vec_lo};
+}
+T2O_DEV Wts<float> global_weights(const float* pack, const t2o_layout&, float) { return Wts<float>{pack, pack}; }
+T2O_DEV Wts<__bf16> global_weights(const float* pack, const t2o_layout& L, __bf16) {
+  return Wts<__bf16>{reinterpret_cast<const __bf16*>(pack + L.total), pack};
+}
+// LDS floats taken by stage_weights
+template <typename WT>
+__host__ __device__ inline int64_t lds_weight_floats(const t2o_layout& L, int64_t n) {
+  return sizeof(WT) == 4 ? n : n / 2 + (L.fwd_total - L.vec_lo);
+}
+
 // ---- weight-gradient accumulation -------------------------------------------
 // dW[16*OT x 16*IT] += Σ_rows dY[row]ᵀ ⊗ X[row] over the wave's 16 rows, added
 // into an LDS accumulator (row-major, leading dim ldw) with ds_add_f32.
@@ -281,13 +383,54 @@ T2O_DEV void dw_accumulate(float* __restrict__ ldsW, int ldw, const f4* dY, cons
 
 // Same contraction, accumulated into MFMA accumulator registers acc[o][i]
 // (a wave-private gradient block that stays in registers across calls).
-template <int OT, int IT>
+// BF: bf16 operands, one 16x16x16 MFMA over the 16 rows per tile pair.
+template <int OT, int IT, bool BF = false>
 T2O_DEV void dw_accumulate_regs(f4 (&acc)[OT][IT], const f4* dY, const f4* X, float* stage) {
   constexpr int NS = OT < IT ? OT : IT;
   constexpr int LD = StageDims<NS>::LD;
   float* st_full = stage;
   float* st_tile = stage + 16 * LD;
   const int c = lane_c(), g = lane_g();
+  if constexpr (BF) {
+    if constexpr (IT <= OT) {
+#pragma unroll
+      for (int i = 0; i < IT; ++i) stage_tile(st_full, LD, 16 * i, X[i]);
+#pragma unroll
+      for (int o = 0; o < OT; ++o) {
+        stage_tile(st_tile, 16, 0, dY[o]);
+        f4 a;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = st_tile[(4 * g + j) * 16 + c];
+        const bf4 ab = to_bf4(a);
+#pragma unroll
+        for (int i = 0; i < IT; ++i) {
+          f4 b;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) b[j] = st_full[(4 * g + j) * LD + 16 * i + c];
+          acc[o][i] = mfma_b16(ab, to_bf4(b), acc[o][i]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int o = 0; o < OT; ++o) stage_tile(st_full, LD, 16 * o, dY[o]);
+#pragma unroll
+      for (int i = 0; i < IT; ++i) {
+        stage_tile(st_tile, 16, 0, X[i]);
+        f4 b;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = st_tile[(4 * g + j) * 16 + c];
+        const bf4 bb = to_bf4(b);
+#pragma unroll
+        for (int o = 0; o < OT; ++o) {
+          f4 a;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) a[j] = st_full[(4 * g + j) * LD + 16 * o + c];
+          acc[o][i] = mfma_b16(to_bf4(a), bb, acc[o][i]);
+        }
+      }
+    }
+    return;
+  }
   if constexpr (IT <= OT) {
 #pragma unroll
     for (int i = 0; i < IT; ++i) stage_tile(st_full, LD, 16 * i, X[i]);

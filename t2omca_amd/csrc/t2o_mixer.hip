@@ -101,8 +101,8 @@ T2O_DEV void load_qv(const MixerFwdArgs& a, const MixerNet& n, int b, int t, flo
 
 // Build the key block X0 rows for step t: state-entity embeddings and agent
 // hidden tokens (the hyper-token rows are carried separately).
-template <int E, int A>
-T2O_DEV void build_keys(const float* __restrict__ P, const t2o_layout& L, const MixerFwdArgs& a,
+template <int E, int A, typename WT>
+T2O_DEV void build_keys(const Wts<WT>& P, const t2o_layout& L, const MixerFwdArgs& a,
                         const MixerNet& n, int b, int t, float* X0) {
   using Dm = MixDims<E, A>;
   constexpr int ET = E / 16;
@@ -118,10 +118,10 @@ T2O_DEV void build_keys(const float* __restrict__ P, const t2o_layout& L, const 
       sv[r] = (j < Dm::NS && f < a.Fs) ? st[j * a.Fs + f] : 0.f;
     }
     f4 emb[ET];
-    matvec<ET, 1>(P + L.We, 16, &sv, emb);
+    matvec<ET, 1>(P.w + L.We, 16, &sv, emb);
     if (j < Dm::NS) {
 #pragma unroll
-      for (int ft = 0; ft < ET; ++ft) st4(X0 + j * Dm::LDX + 16 * ft + 4 * g, emb[ft] + vec_t(P + L.be, ft));
+      for (int ft = 0; ft < ET; ++ft) st4(X0 + j * Dm::LDX + 16 * ft + 4 * g, emb[ft] + vec_t(P.v + L.be, ft));
     }
   }
   const float* hd = n.hid + b * n.hid_sb + t * n.hid_st;
@@ -133,8 +133,8 @@ T2O_DEV void build_keys(const float* __restrict__ P, const t2o_layout& L, const 
 
 // Mixing head (n_transf_mixer.py:75-89) on the final query rows OUT[q][f],
 // lanes = features.  Returns y; writes hyper tokens back into X0.
-template <int E, int A>
-T2O_DEV float mixer_head(const float* __restrict__ P, const t2o_layout& L, const float* OUT,
+template <int E, int A, typename WT>
+T2O_DEV float mixer_head(const Wts<WT>& P, const t2o_layout& L, const float* OUT,
                          const float (&qv)[A], float& pre_h, float& pre2) {
   const int f = threadIdx.x & 63;
   const bool fv = f < E;
@@ -146,12 +146,12 @@ T2O_DEV float mixer_head(const float* __restrict__ P, const t2o_layout& L, const
   const float hidden = elu1(ph);
   const float w2 = fabsf(OUT[(A + 1) * E + fc]);
   const float yv = wave_sum(fv ? hidden * w2 : 0.f);
-  const float p2 = wave_sum(fv ? P[L.Wo + fc] * OUT[(A + 2) * E + fc] : 0.f) + P[L.bo];
+  const float p2 = wave_sum(fv ? P.s(L.Wo + fc) * OUT[(A + 2) * E + fc] : 0.f) + P.v[L.bo];
   pre2 = p2;
   return yv + fmaxf(p2, 0.f);
 }
 
-template <int E, int H, int D, int A, int FF, bool WLDS>
+template <int E, int H, int D, int A, int FF, bool WLDS, typename WT>
 __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
   using Dm = MixDims<E, A>;
   constexpr int ET = E / 16;
@@ -160,14 +160,16 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
   const MixerNet n = args.net[blockIdx.y];
   const t2o_layout& L = args.L;
   // forward weights in LDS for the unroll when they fit beside the per-wave buffers
-  const int lds_w = WLDS ? (int)((L.fwd_total + 15) / 16 * 16) : 0;
+  const int lds_w = WLDS ? (int)((lds_weight_floats<WT>(L, L.fwd_total) + 15) / 16 * 16) : 0;
+  Wts<WT> P0;
   if constexpr (WLDS) {
-    copy_to_lds(smem, n.pack, L.fwd_total);
+    P0 = stage_weights(smem, n.pack, L, L.fwd_total, WT{});
     __syncthreads();
+  } else {
+    P0 = global_weights(n.pack, L, WT{});
   }
   const int b = blockIdx.x * args.waves + w;
   if (b >= args.B) return;  // wave-uniform; no block barriers after this point
-  const float* P0 = WLDS ? smem : n.pack;  // compile-time: LDS reads stay ds_read
   float* X0 = smem + lds_w + w * Dm::FWD_PERW;
   float* OUT = Dm::QT == 1 ? X0 : X0 + Dm::X0F;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
@@ -177,7 +179,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
     X0[(Dm::NS + A + k) * Dm::LDX + f] = n.hw0 ? n.hw0[(size_t)b * 3 * E + i] : 0.f;
   }
   for (int t = 0; t < n.T; ++t) {
-    const float* __restrict__ P = step_view(P0);
+    const Wts<WT> P = step_view(P0);
     build_keys<E, A>(P, L, args, n, b, t, X0);
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -231,11 +233,11 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
   }
 }
 
-template <int E, int H, int D, int A, int FF>
+template <int E, int H, int D, int A, int FF, typename WT>
 int launch_mixer_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
   using Dm = MixDims<E, A>;
   MixerFwdArgs a = args;
-  const size_t wfl = (args.L.fwd_total + 15) / 16 * 16, perw = Dm::FWD_PERW;
+  const size_t wfl = (lds_weight_floats<WT>(args.L, args.L.fwd_total) + 15) / 16 * 16, perw = Dm::FWD_PERW;
   size_t lds = 0;
   // 8 (2 per SIMD) / 4 / 2 waves with LDS weights, else 4 waves reading weights from L2
   for (a.waves = 8, a.wlds = 1; a.waves >= 2; a.waves >>= 1) {
@@ -248,7 +250,7 @@ int launch_mixer_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
     lds = sizeof(float) * 4 * perw;
     if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
   }
-  auto kern = a.wlds ? mixer_fwd_kernel<E, H, D, A, FF, true> : mixer_fwd_kernel<E, H, D, A, FF, false>;
+  auto kern = a.wlds ? mixer_fwd_kernel<E, H, D, A, FF, true, WT> : mixer_fwd_kernel<E, H, D, A, FF, false, WT>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid((args.B + a.waves - 1) / a.waves, nnet);
   hipLaunchKernelGGL(kern, grid, dim3(64 * a.waves), lds, stream, a);
@@ -301,7 +303,7 @@ struct MixBwdDims {
   static constexpr int PERW = Dm::X0F + WORK;
 };
 
-template <int E, int H, int D, int A, int FF>
+template <int E, int H, int D, int A, int FF, typename WT>
 __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   using Dm = MixDims<E, A>;
   using Bd = MixBwdDims<E, A>;
@@ -317,11 +319,10 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   float* GOUTB = Bd::GOUT ? WORK : WORK;        // head grads (rows of OUT layout)
   float* stage = WORK + Bd::GOUT;               // staging / gX0 region
   float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
-  copy_to_lds(smem, n.pack, L.fwd_total);
+  const Wts<WT> P0 = stage_weights(smem, n.pack, L, sizeof(WT) == 4 ? L.fwd_total : L.total, WT{});
   for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) gs[i] = 0.f;
   __syncthreads();
   const int b = blockIdx.x * args.waves + w;
-  const float* P0 = smem;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
   const size_t nrec = (size_t)fa.B * n.T * Dm::Q;
   using Rec = TapeRec<E, H, FF>;
@@ -335,7 +336,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
     for (int k = 0; k < 16; ++k) gWe[k] = 0.f;
     for (int t = n.T - 1; t >= 0; --t) {
-      const float* __restrict__ P = step_view(P0);
+      const Wts<WT> P = step_view(P0);
       const size_t bt = (size_t)b * n.T + t;
       build_keys<E, A>(P, L, fa, n, b, t, X0);
       for (int i = lane; i < 3 * E; i += 64) {
@@ -372,7 +373,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
       gout[A] = gpre + ghw[0];
       gout[A + 1] = gyv * hidden * sgn_w2 + ghw[1];
       const float x2 = OUT[(A + 2) * E + f];
-      gout[A + 2] = gpre2 * P[L.Wo + f] + ghw[2];
+      gout[A + 2] = gpre2 * P.s(L.Wo + f) + ghw[2];
       gWo += gpre2 * x2;
       gbo += gpre2;
       __builtin_amdgcn_wave_barrier();
@@ -492,10 +493,11 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   }
 }
 
-template <int E, int H, int D, int A, int FF>
+template <int E, int H, int D, int A, int FF, typename WT>
 int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
   constexpr int PERW = MixBwdDims<E, A>::PERW;
-  args.lds_w = (int)((args.f.L.fwd_total + 15) / 16 * 16);
+  const t2o_layout& L = args.f.L;
+  args.lds_w = (int)((lds_weight_floats<WT>(L, sizeof(WT) == 4 ? L.fwd_total : L.total) + 15) / 16 * 16);
   size_t lds = 0;
   for (args.waves = 4; args.waves >= 1; args.waves >>= 1) {
     lds = sizeof(float) * ((size_t)args.lds_w + args.waves * PERW);
@@ -504,7 +506,7 @@ int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t 
   if (args.waves < 1) return T2O_EUNSUPPORTED;
   const int grid = (args.f.B + args.waves - 1) / args.waves;
   if (grid > max_slabs) return T2O_EINVAL;
-  auto kern = mixer_bwd_kernel<E, H, D, A, FF>;
+  auto kern = mixer_bwd_kernel<E, H, D, A, FF, WT>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * args.waves), lds, stream, args);
   *nslab = grid;
@@ -560,7 +562,8 @@ extern "C" int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, c
   }
   int rc = T2O_EUNSUPPORTED;
   T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
-               rc = (launch_mixer_fwd<E_, H_, D_, NE_, FF_>(a, nnet, (hipStream_t)stream)));
+               rc = (L->prec ? launch_mixer_fwd<E_, H_, D_, NE_, FF_, __bf16>(a, nnet, (hipStream_t)stream)
+                             : launch_mixer_fwd<E_, H_, D_, NE_, FF_, float>(a, nnet, (hipStream_t)stream)));
   return rc;
 }
 
@@ -597,6 +600,7 @@ extern "C" int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, cons
   a.tape = tape;
   int rc = T2O_EUNSUPPORTED;
   T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
-               rc = (launch_mixer_bwd<E_, H_, D_, NE_, FF_>(a, max_slabs, nslab, (hipStream_t)stream)));
+               rc = (L->prec ? launch_mixer_bwd<E_, H_, D_, NE_, FF_, __bf16>(a, max_slabs, nslab, (hipStream_t)stream)
+                             : launch_mixer_bwd<E_, H_, D_, NE_, FF_, float>(a, max_slabs, nslab, (hipStream_t)stream)));
   return rc;
 }

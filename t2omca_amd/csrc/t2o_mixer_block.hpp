@@ -25,7 +25,7 @@ struct MixerCache {
 };
 
 // Sᵀ-style product: out[kt] (keys 16kt+4g+r, query c) = Σ_f X0[key][f] v[f]
-template <int E, int KT, int LDX>
+template <int E, int KT, int LDX, bool BF>
 T2O_DEV void keys_dot(const float* __restrict__ X0, const f4* v, f4* out) {
   constexpr int ET = E / 16;
   const int c = lane_c(), g = lane_g();
@@ -35,17 +35,21 @@ T2O_DEV void keys_dot(const float* __restrict__ X0, const f4* v, f4* out) {
 #pragma unroll
     for (int ft = 0; ft < ET; ++ft) {
       const f4 a = ld4(X0 + (16 * kt + c) * LDX + 16 * ft + 4 * g);
-      acc = mfma4(a[0], v[ft][0], acc);
-      acc = mfma4(a[1], v[ft][1], acc);
-      acc = mfma4(a[2], v[ft][2], acc);
-      acc = mfma4(a[3], v[ft][3], acc);
+      if constexpr (BF) {
+        acc = mfma_b16(to_bf4(a), to_bf4(v[ft]), acc);
+      } else {
+        acc = mfma4(a[0], v[ft][0], acc);
+        acc = mfma4(a[1], v[ft][1], acc);
+        acc = mfma4(a[2], v[ft][2], acc);
+        acc = mfma4(a[3], v[ft][3], acc);
+      }
     }
     out[kt] = acc;
   }
 }
 
 // Zᵀ-style product: out[ft] (features 16ft+4g+r, query c) = Σ_key X0[key][f] w[key]
-template <int E, int KT, int LDX>
+template <int E, int KT, int LDX, bool BF>
 T2O_DEV void keys_combine(const float* __restrict__ X0, const f4* w, f4* out) {
   constexpr int ET = E / 16;
   const int c = lane_c(), g = lane_g();
@@ -53,26 +57,34 @@ T2O_DEV void keys_combine(const float* __restrict__ X0, const f4* w, f4* out) {
   for (int ft = 0; ft < ET; ++ft) {
     f4 acc = zero4();
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt)
+    for (int kt = 0; kt < KT; ++kt) {
+      if constexpr (BF) {
+        f4 a;
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        acc = mfma4(X0[(16 * kt + 4 * g + s) * LDX + 16 * ft + c], w[kt][s], acc);
+        for (int s = 0; s < 4; ++s) a[s] = X0[(16 * kt + 4 * g + s) * LDX + 16 * ft + c];
+        acc = mfma_b16(to_bf4(a), to_bf4(w[kt]), acc);
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = mfma4(X0[(16 * kt + 4 * g + s) * LDX + 16 * ft + c], w[kt][s], acc);
+      }
+    }
     out[ft] = acc;
   }
 }
 
-template <int E, int H, int KT, int FF, int LDX, bool CACHE>
-T2O_DEV void mixer_block_fwd(const float* __restrict__ P, const t2o_layout& L, int d,
+template <int E, int H, int KT, int FF, int LDX, bool CACHE, typename WT>
+T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
                              const float* __restrict__ X0, int Lk, f4* x, MixerCache<E, H, KT, FF>* cache) {
   constexpr int ET = E / 16, HET = H * ET;
+  constexpr bool BF = sizeof(WT) == 2;
   const int g = lane_g();
   f4 u[HET];
-  matvec<HET, ET>(P + L.M[d], E, x, u);
+  matvec<HET, ET>(P.w + L.M[d], E, x, u);
   f4 z[HET];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
     f4 s[KT];
-    keys_dot<E, KT, LDX>(X0, &u[hh * ET], s);
+    keys_dot<E, KT, LDX, BF>(X0, &u[hh * ET], s);
     float m = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt)
@@ -93,7 +105,7 @@ T2O_DEV void mixer_block_fwd(const float* __restrict__ P, const t2o_layout& L, i
     const float il = 1.0f / allsum4(l);
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) s[kt] *= il;
-    keys_combine<E, KT, LDX>(X0, s, &z[hh * ET]);
+    keys_combine<E, KT, LDX, BF>(X0, s, &z[hh * ET]);
     if constexpr (CACHE) {
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt) cache->p[hh][kt] = s[kt];
@@ -111,19 +123,20 @@ T2O_DEV void mixer_block_fwd(const float* __restrict__ P, const t2o_layout& L, i
 // holds gX0[key 16kt+4g+r][feature 16ft+c] — accumulates the grad wrt the key
 // tokens (a contraction over queries = rows, via the staging transposes).
 // Big-matrix operand pairs go to the query row's tape record (null = padding).
-template <int E, int H, int KT, int FF, int LDX>
-T2O_DEV void mixer_block_bwd(const float* __restrict__ P, const t2o_layout& L, const t2o_layout& G,
+template <int E, int H, int KT, int FF, int LDX, typename WT>
+T2O_DEV void mixer_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G,
                              float* __restrict__ gs, float* __restrict__ rec, float* __restrict__ stage, int d,
                              const float* __restrict__ X0, f4 (&gX0)[KT][E / 16],
                              const MixerCache<E, H, KT, FF>& c, f4* gx) {
   constexpr int ET = E / 16, HET = H * ET;
+  constexpr bool BF = sizeof(WT) == 2;
   f4 gz[HET], gres[ET];
   post_bwd<E, H, FF>(P, L, G, gs, rec, d, c.post, gx, gz, gres);
   f4 gu[HET];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
     f4 gp[KT];
-    keys_dot<E, KT, LDX>(X0, &gz[hh * ET], gp);
+    keys_dot<E, KT, LDX, BF>(X0, &gz[hh * ET], gp);
     float dot = 0.f;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt)
@@ -133,16 +146,16 @@ T2O_DEV void mixer_block_bwd(const float* __restrict__ P, const t2o_layout& L, c
     f4 gsc[KT];
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) gsc[kt] = c.p[hh][kt] * (gp[kt] - dot);
-    keys_combine<E, KT, LDX>(X0, gsc, &gu[hh * ET]);
-    dw_accumulate_regs<KT, ET>(gX0, c.p[hh], &gz[hh * ET], stage);
-    dw_accumulate_regs<KT, ET>(gX0, gsc, &c.u[hh * ET], stage);
+    keys_combine<E, KT, LDX, BF>(X0, gsc, &gu[hh * ET]);
+    dw_accumulate_regs<KT, ET, BF>(gX0, c.p[hh], &gz[hh * ET], stage);
+    dw_accumulate_regs<KT, ET, BF>(gX0, gsc, &c.u[hh * ET], stage);
   }
   if (rec) {
     rec_store<HET>(rec, TapeRec<E, H, FF>::GU, gu);
     rec_store<ET>(rec, TapeRec<E, H, FF>::X, c.post.x);
   }
   f4 gxp[ET];
-  matvec_t<ET, HET>(P + L.M[d], E, gu, gxp);
+  matvec_tr<ET, HET>(P, L.M[d], E, L.MT[d], H * E, gu, gxp);
 #pragma unroll
   for (int t = 0; t < ET; ++t) gx[t] = gxp[t] + gres[t];
 }

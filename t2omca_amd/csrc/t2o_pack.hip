@@ -156,33 +156,46 @@ int launch(const SegTable& t, const float* src, const float* src2, float* dst, v
   return (int)hipGetLastError();
 }
 
+__global__ void to_bf16_kernel(const float* __restrict__ src, __bf16* __restrict__ dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = (__bf16)src[i];
+}
 }  // namespace
 
-extern "C" int t2o_layout_init(t2o_layout* L, int kind, int E, int H, int D, int F, int NA, int FF, int n_ent) {
+extern "C" int t2o_layout_init(t2o_layout* L, int kind, int E, int H, int D, int F, int NA, int FF, int n_ent,
+                               int prec) {
   if (!L || (kind != 0 && kind != 1) || E <= 0 || E % 16 || H < 1 || D < 1 || D > T2O_MAX_DEPTH ||
-      F < 1 || F > 16 || NA < 1 || NA > 16 || FF <= 0 || FF % 16 || n_ent < 1)
+      F < 1 || F > 16 || NA < 1 || NA > 16 || FF <= 0 || FF % 16 || n_ent < 1 || (prec != 0 && prec != 1))
     return T2O_EINVAL;
   t2o_layout z{};
   *L = z;
   L->kind = kind; L->E = E; L->H = H; L->D = D; L->F = F; L->NA = NA; L->FF = FF; L->n_ent = n_ent;
+  L->prec = prec;
   int64_t o = 0;
   const int64_t HE = (int64_t)H * E;
-  // forward section first (one contiguous copy into LDS), backward extras after
+  for (int d = 0; d < T2O_MAX_DEPTH; ++d)
+    L->M[d] = L->MT[d] = L->N[d] = L->NT[d] = L->bu[d] = L->g1[d] = L->n1[d] = L->W1[d] = L->W1T[d] = L->c1[d] =
+        L->W2[d] = L->W2T[d] = L->c2[d] = L->g2[d] = L->n2[d] = -1;
+  // forward matrices, then forward vectors (one contiguous LDS copy; in bf16
+  // mode the vectors stay fp32), then the backward's transposed copies.  Every
+  // size is a multiple of 16 elements, so every section stays 64-B aligned.
   L->WeT = o; o += 16 * (int64_t)E;
   L->We = o; o += (int64_t)E * 16;
-  L->be = o; o += E;
   L->Wo = o; o += 16 * (int64_t)E;
-  L->bo = o; o += 16;
-  for (int d = 0; d < T2O_MAX_DEPTH; ++d) {
-    if (d >= D) { L->M[d] = L->MT[d] = L->N[d] = L->NT[d] = L->bu[d] = L->g1[d] = L->n1[d] = L->W1[d] = L->W1T[d] = L->c1[d] = L->W2[d] = L->W2T[d] = L->c2[d] = L->g2[d] = L->n2[d] = -1; continue; }
+  for (int d = 0; d < D; ++d) {
     L->M[d] = o; o += HE * E;
     L->N[d] = o; o += E * HE;
+    L->W1[d] = o; o += (int64_t)FF * E;
+    L->W2[d] = o; o += (int64_t)E * FF;
+  }
+  L->vec_lo = o;
+  L->be = o; o += E;
+  L->bo = o; o += 16;
+  for (int d = 0; d < D; ++d) {
     L->bu[d] = o; o += E;
     L->g1[d] = o; o += E;
     L->n1[d] = o; o += E;
-    L->W1[d] = o; o += (int64_t)FF * E;
     L->c1[d] = o; o += FF;
-    L->W2[d] = o; o += (int64_t)E * FF;
     L->c2[d] = o; o += E;
     L->g2[d] = o; o += E;
     L->n2[d] = o; o += E;
@@ -196,11 +209,14 @@ extern "C" int t2o_layout_init(t2o_layout* L, int kind, int E, int H, int D, int
     L->W2T[d] = o; o += (int64_t)FF * E;
   }
   L->total = o;
+  L->pack_floats = prec ? o + ((o + 1) / 2 + 3) / 4 * 4 : o;
   t2o_layout G;
   grad_layout(*L, G);
   L->grad_total = G.grad_total;
   return 0;
 }
+
+extern "C" int t2o_layout_sizeof(void) { return (int)sizeof(t2o_layout); }
 
 extern "C" int64_t t2o_param_count(int kind, int E, int H, int D, int F, int NA, int FF) {
   return param_offsets(kind, E, H, D, F, NA, FF).total;
@@ -239,7 +255,16 @@ extern "C" int t2o_pack_params(const t2o_layout* L, const float* params, float* 
     add(t, SEG_COPY, 1, E, L->g2[d], P.g2[d]);
     add(t, SEG_COPY, 1, E, L->n2[d], P.n2[d]);
   }
-  return launch(t, params, nullptr, pack, stream);
+  if (int rc = launch(t, params, nullptr, pack, stream)) return rc;
+  if (L->prec == 1) {  // bf16 image of the whole pack right after it (round to nearest even)
+    const int64_t n = L->total;
+    int blocks = (int)((n + 255) / 256);
+    if (blocks > 1024) blocks = 1024;
+    hipLaunchKernelGGL(to_bf16_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, pack,
+                       reinterpret_cast<__bf16*>(pack + n), n);
+    return (int)hipGetLastError();
+  }
+  return 0;
 }
 
 extern "C" int t2o_unpack_grads(const t2o_layout* L, const float* params, const float* gpack, float* grad,

@@ -22,6 +22,8 @@ priorities are copied out):
   [data parallel: one all_reduce of the flat grad + Σ mask over RCCL]
   clip_grad_norm_ + Adam                           t2o_adam_step
 """
+import dataclasses
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -47,12 +49,20 @@ def _bind_flat(modules, device):
 class TDLearner:
     def __init__(self, agent, mixer, *, lr=1e-3, gamma=0.99, td_lambda=0.6, grad_norm_clip=10.0,
                  target_update_interval=200, optim_betas=(0.9, 0.999), optim_eps=1e-8, weight_decay=0.0,
-                 detach_mixer_hidden=False, process_group=None, priorities_to_cpu=True):
+                 detach_mixer_hidden=False, process_group=None, priorities_to_cpu=True, precision="fp32"):
         dev = next(agent.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("TDLearner needs the modules on a HIP device (no CPU fallback)")
+        if precision not in ("fp32", "bf16"):
+            raise ValueError("precision must be 'fp32' or 'bf16'")
         self.agent, self.mixer = agent, mixer
-        self.sa, self.sm = agent.shape, mixer.shape
+        # bf16: MFMA operands (weights, activations entering a matrix product) in
+        # bf16; accumulation, LayerNorm, softmax, recurrent state, TD targets, grads
+        # and the Adam master weights stay fp32
+        prec = 1 if precision == "bf16" else 0
+        self.precision = precision
+        self.sa = dataclasses.replace(agent.shape, prec=prec)
+        self.sm = dataclasses.replace(mixer.shape, prec=prec)
         self.na, self.nm = self.sa.n_params, self.sm.n_params
         assert self.na == sum(p.numel() for p in agent.parameters())
         assert self.nm == sum(p.numel() for p in mixer.parameters())
@@ -73,8 +83,8 @@ class TDLearner:
         self.step_count = 0
         self.last_target_update_episode = 0
         self.timer = None   # optional callable(tag) recording HIP events around the big kernels
-        self.pack_a = torch.empty(self.sa.layout().total, device=dev)
-        self.pack_m = torch.empty(self.sm.layout().total, device=dev)
+        self.pack_a = torch.empty(self.sa.layout().pack_floats, device=dev)
+        self.pack_m = torch.empty(self.sm.layout().pack_floats, device=dev)
         self.pack_at = torch.empty_like(self.pack_a)
         self.pack_mt = torch.empty_like(self.pack_m)
         self._pack_targets()

@@ -35,6 +35,7 @@ class NetShape:
     NA: int
     FF: int
     n_ent: int
+    prec: int = 0   # 0 fp32, 1 bf16 MFMA operands (fp32 accumulate / LayerNorm / softmax / state)
 
     def layout(self):
         return _layout_cached(self)
@@ -50,7 +51,7 @@ _LAYOUTS = {}
 def _layout_cached(s):
     L = _LAYOUTS.get(s)
     if L is None:
-        L = _lib.make_layout(s.kind, s.E, s.H, s.D, s.F, s.NA, s.FF, s.n_ent)
+        L = _lib.make_layout(s.kind, s.E, s.H, s.D, s.F, s.NA, s.FF, s.n_ent, s.prec)
         _LAYOUTS[s] = L
     return L
 
@@ -61,7 +62,7 @@ def pack_params(shape: NetShape, params: torch.Tensor, out: torch.Tensor = None)
     L = shape.layout()
     assert params.numel() == shape.n_params and params.is_contiguous()
     if out is None:
-        out = torch.empty(L.total, device=params.device, dtype=torch.float32)
+        out = torch.empty(L.pack_floats, device=params.device, dtype=torch.float32)
     check(lib().t2o_pack_params(ctypes.byref(L), ptr(params), ptr(out), stream_ptr()), "pack_params")
     return out
 

@@ -48,9 +48,30 @@ def test_layout_and_param_count(kind, F, NA):
 def test_layout_rejects_bad_shapes():
     from t2omca_amd import _lib
     L = _lib.Layout()
-    assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 30, 3, 2, 9, 5, 128, 8) != 0  # E % 16
-    assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 32, 3, 9, 9, 5, 128, 8) != 0  # depth > 4
-    assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 32, 3, 2, 20, 5, 128, 8) != 0  # F > 16
+    assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 30, 3, 2, 9, 5, 128, 8, 0) != 0  # E % 16
+    assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 32, 3, 9, 9, 5, 128, 8, 0) != 0  # depth > 4
+    assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 32, 3, 2, 20, 5, 128, 8, 0) != 0  # F > 16
+    assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 32, 3, 2, 9, 5, 128, 8, 2) != 0  # precision
+
+
+def test_layout_struct_matches_c():
+    from t2omca_amd import _lib
+    assert ctypes.sizeof(_lib.Layout) == _lib.lib().t2o_layout_sizeof()
+
+
+@pytest.mark.parametrize("kind,F,NA", [(0, 9, 5), (1, 8, 1)])
+def test_bf16_layout(kind, F, NA):
+    """prec 1: same element layout, vectors contiguous in [vec_lo, fwd_total), bf16 image after the fp32 pack."""
+    from t2omca_amd import _lib
+    L32 = _lib.make_layout(kind, 32, 3, 2, F, NA, 128, 8, 0)
+    L16 = _lib.make_layout(kind, 32, 3, 2, F, NA, 128, 8, 1)
+    assert L16.prec == 1 and L16.total == L32.total and L16.fwd_total == L32.fwd_total
+    assert L32.pack_floats == L32.total
+    assert L16.pack_floats >= L16.total + (L16.total + 1) // 2 and L16.pack_floats % 4 == 0
+    vecs = [L16.be, L16.bo] + [getattr(L16, k)[d] for k in ("bu", "g1", "n1", "c1", "c2", "g2", "n2") for d in range(2)]
+    mats = [L16.WeT, L16.We, L16.Wo] + [getattr(L16, k)[d] for k in ("M", "N", "W1", "W2") for d in range(2)]
+    assert min(vecs) == L16.vec_lo and max(vecs) < L16.fwd_total
+    assert max(mats) < L16.vec_lo and L16.vec_lo % 16 == 0
 
 
 def test_product_path_refuses_cpu_tensors():
