@@ -156,7 +156,7 @@ def main():
     value = transitions / elapsed
     kern = {k: sum(v) / len(v) for k, v in timer.durations().items()}
     flops = td_update_flops(B, T, A)
-    bytes_ = td_update_bytes(B, T, A)
+    bytes_ = td_update_bytes(B, T, A, elem=2 if args.dtype == "bf16" else 4)
     # dominant kernel on the critical path (mixer_dw runs on a side stream, hidden
     # behind agent_bwd, so its event interval includes contention, not its cost)
     dom = max((k for k in flops if k != "mixer_dw"), key=lambda k: kern.get(k, 0.0))

@@ -121,16 +121,16 @@ int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, const float*
  * Outputs: gslabs[nslab][grad_total] per-workgroup partial gradients (compact
  * layout, overwritten; *nslab = number written, at most max_slabs =
  * t2o_agent_bwd_max_slabs(B, A)); gh0[b][a][E] = dL/dh0 (may be NULL).
- * Workspace: tape, t2o_bwd_tape_floats(L, T*B*A) floats — the per-record
- * operand pairs of the M/N/W1/W2 weight grads; the slabs are complete only
- * after t2o_bwd_tape_contract(L, tape, T*B*A, gslabs, *nslab) on the same
- * stream. */
+ * Workspace: tape, t2o_bwd_tape_floats(L, tiles) floats with tiles =
+ * T * ceil(B*A/16) — the per-record operand pairs of the M/N/W1/W2 weight
+ * grads; the slabs are complete only after t2o_bwd_tape_contract(L, tape,
+ * tiles, gslabs, *nslab) on the same stream. */
 int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack,
                          const float* obs, int64_t obs_sb, int64_t obs_st,
                          const float* h0, const float* h_seq, const float* hmid, int h_ts,
                          const float* gq, const float* gchosen, const int64_t* actions,
                          int64_t act_sb, int64_t act_st, const float* gh,
-                         float* gslabs, int max_slabs, int* nslab, float* tape, float* gh0,
+                         float* gslabs, int max_slabs, int* nslab, void* tape, float* gh0,
                          int B, int T, int A, void* stream);
 int t2o_agent_bwd_max_slabs(int B, int A);
 
@@ -164,22 +164,23 @@ int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, const float*
  * extra grad on the hyper outputs.  Outputs: gqv[B][T][A] (dL/dqvals),
  * ghid[B][T][A][E] (dL/dhidden states), ghw0[B][3][E] (may be NULL), partial
  * weight-grad slabs as for the agent (max_slabs = t2o_mixer_bwd_max_slabs(B)),
- * tape workspace of t2o_bwd_tape_floats(L, B*T*(A+3)) floats. */
+ * tape workspace of t2o_bwd_tape_floats(L, tiles) floats, tiles = B*T*ceil((A+3)/16). */
 int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, const float* states,
                          int64_t st_sb, int64_t st_st, const float* hid, int64_t hid_sb,
                          int64_t hid_st, const float* hw0, const float* qv, const float* hw,
                          const float* xout, const float* xmid, const float* gy, const float* ghw_ext, float* gqv,
-                         float* ghid, float* ghw0, float* gslabs, int max_slabs, int* nslab, float* tape,
+                         float* ghid, float* ghw0, float* gslabs, int max_slabs, int* nslab, void* tape,
                          int B, int T, void* stream);
 int t2o_mixer_bwd_max_slabs(int B);
 
-/* Floats of backward tape workspace for `records` records (D * records * (4E + 2HE + 2FF)). */
-int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t records);
+/* Floats of backward tape workspace for `tiles` tiles of 16 records:
+ * D * tiles * 16 * (4E + 2HE + 2FF) elements of 4 (fp32) or 2 (bf16) bytes. */
+int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t tiles);
 
 /* Contract a backward tape (dM, dN, dW1, dW2 = Σ_records dYᵀ X, split-K over
  * the nslab slabs the backward call returned) into the M/N/W1/W2 regions of
  * those slabs.  Must follow the t2o_*_unroll_bwd call that wrote the tape. */
-int t2o_bwd_tape_contract(const t2o_layout* L, const float* tape, int64_t records, float* gslabs, int nslab,
+int t2o_bwd_tape_contract(const t2o_layout* L, const void* tape, int64_t tiles, float* gslabs, int nslab,
                           void* stream);
 
 /* TD(λ) targets, masked PER-weighted loss, dL/dQtot and priorities

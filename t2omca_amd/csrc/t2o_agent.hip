@@ -134,7 +134,7 @@ int launch_fwd(const AgentFwdArgs& args, int nnet, hipStream_t stream) {
 // it recomputes the step's forward from the stored h_{t-1} and block inputs
 // (hmid), then back-propagates the incoming grads (dL/dq_t, dL/dh_t from the
 // mixer and from step t+1) and produces dL/dh_{t-1}.  Weight grads:
-//   M, N, W1, W2   operand pairs -> tape record (step*R + row, per block);
+//   M, N, W1, W2   operand pairs -> tape tile (step, 16-row tile) per block;
 //                  t2o_dwgemm.hpp contracts them into slab k afterwards
 //   We, Wo         MFMA register blocks for the whole unroll, flushed once
 //   vectors        DPP row sums + float atomics into the workgroup's slab
@@ -153,7 +153,7 @@ struct AgentBwdArgs {
   int64_t act_sb, act_st;
   const float* gh;
   float* slabs;
-  float* tape;  // [D][T*B*A][TapeRec::SIZE]
+  void* tape;  // [D][T * ceil(B*A/16)][TapeRec::SIZE][16] in the MFMA operand type
   float* gh0;
   int B, T, A, F;
   int rpw;  // rows per wave (rows_per_wave)
@@ -187,7 +187,8 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
   const bool valid = c < args.rpw && row_raw < R;
   const int row = valid ? row_raw : R - 1;
   const int b = row / A, a = row % A;
-  const size_t nrec = (size_t)T * R;
+  const size_t tiles_per_step = (size_t)(R + 15) / 16;
+  const size_t ntiles = (size_t)T * tiles_per_step;
 
   if (rt * args.rpw < R) {
     f4 gWe[ET][1], gWo[1][ET];
@@ -278,7 +279,8 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
 #pragma unroll
           for (int t = 0; t < ET; ++t) gx[t] += t1[t];
         }
-        float* rec = valid ? args.tape + ((size_t)d * nrec + (size_t)step * R + row) * Rec::SIZE : nullptr;
+        // padding rows write their (zero-gradient) records too: a tile is written whole
+        WT* rec = static_cast<WT*>(args.tape) + ((size_t)d * ntiles + (size_t)step * tiles_per_step + rt) * Rec::SIZE * 16;
         agent_block_bwd<E, H, NE, FF>(P, L, G, gs, rec, stage, d, h, o, cache, gx, gh_in, gbe, gWe);
       }
       vec_accumulate_g<ET>(gs + G.be, gbe);
@@ -348,7 +350,7 @@ extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, cons
                                     int64_t obs_st, const float* h0, const float* h_seq, const float* hmid, int h_ts,
                                     const float* gq, const float* gchosen, const int64_t* actions,
                                     int64_t act_sb, int64_t act_st, const float* gh, float* gslabs,
-                                    int max_slabs, int* nslab, float* tape, float* gh0, int B, int T, int A,
+                                    int max_slabs, int* nslab, void* tape, float* gh0, int B, int T, int A,
                                     void* stream) {
   if (!L || L->kind != 0 || !pack || !obs || !h_seq || !gslabs || !nslab || !tape || B < 1 || T < 1 || A < 1 ||
       L->n_ent != A || h_ts < T || (gchosen && !actions))

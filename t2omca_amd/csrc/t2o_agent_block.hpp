@@ -104,7 +104,7 @@ T2O_DEV void agent_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const
 // operand pair goes to the tape record (t2o_common.hpp TapeRec).
 template <int E, int H, int NE, int FF, typename WT>
 T2O_DEV void agent_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G,
-                             float* __restrict__ gs, float* __restrict__ rec, float* __restrict__ stage, int d,
+                             float* __restrict__ gs, WT* __restrict__ rec, float* __restrict__ stage, int d,
                              const f4* h, const f4 (&o)[NE], const AgentCache<E, H, NE, FF>& c, f4* gx,
                              f4* gh_in, f4* gbe, f4 (&gWe)[E / 16][1]) {
   constexpr int ET = E / 16, HET = H * ET;
@@ -166,8 +166,8 @@ T2O_DEV void agent_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_la
   }
   // u = M x
   if (rec) {
-    rec_store<HET>(rec, TapeRec<E, H, FF>::GU, gu);
-    rec_store<ET>(rec, TapeRec<E, H, FF>::X, c.post.x);
+    tile_store<HET>(rec, TapeRec<E, H, FF>::GU, gu);
+    tile_store<ET>(rec, TapeRec<E, H, FF>::X, c.post.x);
   }
   f4 gxp[ET];
   matvec_tr<ET, HET>(P, L.M[d], E, L.MT[d], H * E, gu, gxp);

@@ -72,12 +72,12 @@ T2O_DEV void post_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* z,
 
 // gx: grad wrt block output.  Produces gz (grad wrt z, HET tiles) and gres
 // (grad wrt the block input through the LN1 residual).  The operand pairs of
-// the big weight grads (N, W1, W2) go to this row's tape record `rec` (null for
-// padding rows); vector grads go to the workgroup's global slab gs (layout G).
+// the big weight grads (N, W1, W2) go to the wave's tape tile (TapeRec; null:
+// no tape); vector grads go to the workgroup's global slab gs (layout G).
 // Weights are read from P (LDS); transposed products use matvec_t.
 template <int E, int H, int FF, typename WT>
 T2O_DEV void post_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G,
-                      float* __restrict__ gs, float* __restrict__ rec, int d, const PostCache<E, H, FF>& c,
+                      float* __restrict__ gs, WT* __restrict__ rec, int d, const PostCache<E, H, FF>& c,
                       const f4* gx, f4* gz, f4* gres) {
   constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
   using R = TapeRec<E, H, FF>;
@@ -92,8 +92,8 @@ T2O_DEV void post_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G
   layernorm_bwd<ET>(gx, c.xh2, c.rs2, P.v + L.g2[d], gr2);
   // r2 = W2 relu(f1) + c2 + y
   if (rec) {
-    rec_store<ET>(rec, R::GR2, gr2);
-    rec_store<FT>(rec, R::F1R, c.f1r);
+    tile_store<ET>(rec, R::GR2, gr2);
+    tile_store<FT>(rec, R::F1R, c.f1r);
   }
   vec_accumulate_g<ET>(gs + G.c2[d], gr2);
   f4 gf1[FT];
@@ -103,8 +103,8 @@ T2O_DEV void post_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G
 #pragma unroll
     for (int r = 0; r < 4; ++r) gf1[t][r] = c.f1r[t][r] > 0.f ? gf1[t][r] : 0.f;
   if (rec) {
-    rec_store<FT>(rec, R::GF1, gf1);
-    rec_store<ET>(rec, R::Y, c.y);
+    tile_store<FT>(rec, R::GF1, gf1);
+    tile_store<ET>(rec, R::Y, c.y);
   }
   vec_accumulate_g<FT>(gs + G.c1[d], gf1);
   f4 gy[ET];
@@ -121,8 +121,8 @@ T2O_DEV void post_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G
   layernorm_bwd<ET>(gy, c.xh1, c.rs1, P.v + L.g1[d], gres);
   // r1 = N z + b_U + x
   if (rec) {
-    rec_store<ET>(rec, R::GRES, gres);
-    rec_store<HET>(rec, R::Z, c.z);
+    tile_store<ET>(rec, R::GRES, gres);
+    tile_store<HET>(rec, R::Z, c.z);
   }
   vec_accumulate_g<ET>(gs + G.bu[d], gres);
   matvec_tr<HET, ET>(P, L.N[d], H * E, L.NT[d], E, gres, gz);

@@ -109,8 +109,19 @@ T2O_DEV f4 mfma_b32(bf4 a0, bf4 a1, bf4 b0, bf4 b1, f4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
 }
 
+// Bank-conflict-free bf16 weight rows: a weight row is only 64 B at E=32, so
+// the 16 rows a wave reads at once would pile onto 4 bank groups.  The bf16
+// image stores element (r, col) at r*ld + (col ^ bf_swz(r, ld)) — an XOR of
+// whole 8-element groups, so the 4 (or 8) consecutive K values a lane loads
+// stay contiguous — and the readers apply the same XOR.  Only the row's lane
+// index c matters: bf_swz(16o + c, ld) == bf_swz(c, ld).
+__host__ __device__ inline int bf_swz(int row, int ld) {
+  return ld % 32 == 0 ? 8 * ((row >> 2) & 3) : 8 * ((row >> 3) & 1);
+}
+
 T2O_DEV f4 mma_tile(const __bf16* __restrict__ W, int ldw, int o, int i, f4 x, f4 acc) {
-  return mfma_b16(ldb4(W + (size_t)(16 * o + lane_c()) * ldw + 16 * i + 4 * lane_g()), to_bf4(x), acc);
+  const int c = lane_c();
+  return mfma_b16(ldb4(W + (size_t)(16 * o + c) * ldw + ((16 * i + 4 * lane_g()) ^ bf_swz(c, ldw))), to_bf4(x), acc);
 }
 
 // y[0..OT) = W · x[0..IT), bf16 weights and operands, fp32 accumulate
@@ -120,13 +131,16 @@ T2O_DEV void matvec(const __bf16* __restrict__ W, int ldw, const f4* x, f4* y) {
   bf4 xb[IT];
 #pragma unroll
   for (int i = 0; i < IT; ++i) xb[i] = to_bf4(x[i]);
+  const int xs = bf_swz(c, ldw);
 #pragma unroll
   for (int o = 0; o < OT; ++o) {
-    const __bf16* row = W + (size_t)(16 * o + c) * ldw + 4 * g;
+    const __bf16* row = W + (size_t)(16 * o + c) * ldw;
     f4 acc = zero4();
 #pragma unroll
-    for (int i = 0; i + 1 < IT; i += 2) acc = mfma_b32(ldb4(row + 16 * i), ldb4(row + 16 * i + 16), xb[i], xb[i + 1], acc);
-    if constexpr (IT & 1) acc = mfma_b16(ldb4(row + 16 * (IT - 1)), xb[IT - 1], acc);
+    for (int i = 0; i + 1 < IT; i += 2)
+      acc = mfma_b32(ldb4(row + ((16 * i + 4 * g) ^ xs)), ldb4(row + ((16 * i + 16 + 4 * g) ^ xs)), xb[i], xb[i + 1],
+                     acc);
+    if constexpr (IT & 1) acc = mfma_b16(ldb4(row + ((16 * (IT - 1) + 4 * g) ^ xs)), xb[IT - 1], acc);
     y[o] = acc;
   }
 }
@@ -136,7 +150,7 @@ template <typename WT>
 struct Wts {
   const WT* w;
   const float* v;
-  T2O_DEV float s(int64_t off) const { return (float)w[off]; }
+  T2O_DEV float s(int64_t off) const { return (float)w[off]; }  // row 0 of a matrix (unswizzled row)
 };
 
 // y = Wᵀ x: fp32 reads W transposed in place (matvec_t); bf16 uses the pack's
@@ -514,8 +528,8 @@ T2O_DEV void flush_tiles_g(float* __restrict__ W, int ldw, const f4 (&acc)[OT][I
 // ---- weight-gradient tape ---------------------------------------------------
 // The backward kernels do not accumulate the four big per-block matrices
 // (M, N, W1, W2) themselves: per (row, step, block) they stream the operand
-// pairs of dW = Σ dYᵀ X to an HBM tape record, and t2o_dwgemm.hip contracts
-// the tape over all records with MFMA.  Record layout (floats):
+// pairs of dW = Σ dYᵀ X to an HBM tape, and t2o_dwgemm.hip contracts the tape
+// over all records with MFMA.  Feature offsets of one record:
 template <int E, int H, int FF>
 struct TapeRec {
   static constexpr int X = 0;                 // block input x      (E)   M:  X
@@ -528,12 +542,21 @@ struct TapeRec {
   static constexpr int GR2 = F1R + FF;        // dL/d(W2 f + c2 + y)(E)   W2: dY
   static constexpr int SIZE = GR2 + E;
 };
+// Layout: tiles of 16 records (one wave's rows at one step), feature-major
+// inside a tile: element (record 16·tile + c, feature f) of block d sits at
+// ((d·ntiles + tile)·SIZE + f)·16 + c, in the MFMA operand type (fp32, or bf16
+// in bf16 mode).  A wave's tile is one contiguous 18 KiB (bf16) run written
+// whole; the contraction reads 8 (bf16) / 4 (fp32) consecutive records of one
+// feature per lane, which is exactly an MFMA K-slice.
 
-// store a T-layout vector (NT tiles) into this lane's row of a record
-template <int NT>
-T2O_DEV void rec_store(float* rec, int off, const f4* v) {
+// store a T-layout vector (NT tiles, features off + 16t + 4g + r of record c)
+template <int NT, typename TT>
+T2O_DEV void tile_store(TT* __restrict__ tile, int off, const f4* v) {
+  const int c = lane_c(), g = lane_g();
 #pragma unroll
-  for (int t = 0; t < NT; ++t) st4(rec + off + 16 * t + 4 * lane_g(), v[t]);
+  for (int t = 0; t < NT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) tile[(off + 16 * t + 4 * g + r) * 16 + c] = (TT)v[t][r];
 }
 
 }  // namespace t2o

@@ -281,7 +281,7 @@ struct MixerBwdArgs {
   float* ghw0;        // [B][3][E] (may be null)
   const float* xmid;  // forward block inputs of blocks 1..D-1 [B][T][D-1][A+3][E] (may be null)
   float* slabs;
-  float* tape;        // [D][B*T*(A+3)][TapeRec::SIZE]
+  void* tape;         // [D][B*T*QT][TapeRec::SIZE][16] in the MFMA operand type
   int lds_w;          // floats of LDS taken by the weights
   int waves;          // episodes (waves) per workgroup: 4, 2 or 1, whatever fits in LDS
 };
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   __syncthreads();
   const int b = blockIdx.x * args.waves + w;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
-  const size_t nrec = (size_t)fa.B * n.T * Dm::Q;
+  const size_t ntiles = (size_t)fa.B * n.T * Dm::QT;
   using Rec = TapeRec<E, H, FF>;
   if (b < fa.B) {
     for (int i = lane; i < Dm::X0F; i += 64) X0[i] = 0.f;
@@ -431,7 +431,8 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft) x[ft] = xs[d][ft];
           mixer_block_fwd<E, H, KT, FF, Dm::LDX, true>(P, L, d, X0, Dm::LK, x, &cache);
-          float* rec = q < Dm::Q ? args.tape + ((size_t)d * nrec + bt * Dm::Q + q) * Rec::SIZE : nullptr;
+          // one tile per (episode, step, query tile); padding rows carry zero gradients
+          WT* rec = static_cast<WT*>(args.tape) + ((size_t)d * ntiles + bt * Dm::QT + qt) * Rec::SIZE * 16;
           mixer_block_bwd<E, H, KT, FF, Dm::LDX>(P, L, G, gs, rec, stage, d, X0, gX0, cache, gx);
         }
 #pragma unroll
@@ -574,7 +575,7 @@ extern "C" int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, cons
                                     const float* hw0, const float* qv, const float* hw, const float* xout,
                                     const float* xmid, const float* gy, const float* ghw_ext, float* gqv,
                                     float* ghid, float* ghw0, float* gslabs,
-                                    int max_slabs, int* nslab, float* tape, int B, int T, void* stream) {
+                                    int max_slabs, int* nslab, void* tape, int B, int T, void* stream) {
   if (!L || L->kind != 1 || !pack || !states || !hid || !qv || !hw || !xout || !gy || !gqv || !ghid ||
       !gslabs || !nslab || !tape || B < 1 || T < 1 || L->E > 64)
     return T2O_EINVAL;

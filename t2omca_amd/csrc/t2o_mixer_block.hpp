@@ -125,7 +125,7 @@ T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
 // Big-matrix operand pairs go to the query row's tape record (null = padding).
 template <int E, int H, int KT, int FF, int LDX, typename WT>
 T2O_DEV void mixer_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G,
-                             float* __restrict__ gs, float* __restrict__ rec, float* __restrict__ stage, int d,
+                             float* __restrict__ gs, WT* __restrict__ rec, float* __restrict__ stage, int d,
                              const float* __restrict__ X0, f4 (&gX0)[KT][E / 16],
                              const MixerCache<E, H, KT, FF>& c, f4* gx) {
   constexpr int ET = E / 16, HET = H * ET;
@@ -151,8 +151,8 @@ T2O_DEV void mixer_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_la
     dw_accumulate_regs<KT, ET, BF>(gX0, gsc, &c.u[hh * ET], stage);
   }
   if (rec) {
-    rec_store<HET>(rec, TapeRec<E, H, FF>::GU, gu);
-    rec_store<ET>(rec, TapeRec<E, H, FF>::X, c.post.x);
+    tile_store<HET>(rec, TapeRec<E, H, FF>::GU, gu);
+    tile_store<ET>(rec, TapeRec<E, H, FF>::X, c.post.x);
   }
   f4 gxp[ET];
   matvec_tr<ET, HET>(P, L.M[d], E, L.MT[d], H * E, gu, gxp);

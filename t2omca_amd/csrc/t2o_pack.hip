@@ -156,9 +156,23 @@ int launch(const SegTable& t, const float* src, const float* src2, float* dst, v
   return (int)hipGetLastError();
 }
 
-__global__ void to_bf16_kernel(const float* __restrict__ src, __bf16* __restrict__ dst, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    dst[i] = (__bf16)src[i];
+// bf16 image of the pack's matrices (round to nearest even), rows swizzled as
+// bf_swz prescribes; blockIdx.y = matrix.  Vector slots of the image stay unused.
+struct MatTable {
+  int n;
+  int64_t off[4 + 8 * T2O_MAX_DEPTH];
+  int rows[4 + 8 * T2O_MAX_DEPTH], ld[4 + 8 * T2O_MAX_DEPTH];
+};
+
+__global__ void to_bf16_kernel(MatTable t, const float* __restrict__ src, __bf16* __restrict__ dst) {
+  const int m = blockIdx.y;
+  const int64_t off = t.off[m];
+  const int ld = t.ld[m];
+  const int64_t n = (int64_t)t.rows[m] * ld;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / ld), col = (int)(i % ld);
+    dst[off + (int64_t)r * ld + (col ^ bf_swz(r, ld))] = (__bf16)src[off + i];
+  }
 }
 }  // namespace
 
@@ -256,12 +270,30 @@ extern "C" int t2o_pack_params(const t2o_layout* L, const float* params, float* 
     add(t, SEG_COPY, 1, E, L->n2[d], P.n2[d]);
   }
   if (int rc = launch(t, params, nullptr, pack, stream)) return rc;
-  if (L->prec == 1) {  // bf16 image of the whole pack right after it (round to nearest even)
-    const int64_t n = L->total;
-    int blocks = (int)((n + 255) / 256);
-    if (blocks > 1024) blocks = 1024;
-    hipLaunchKernelGGL(to_bf16_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, pack,
-                       reinterpret_cast<__bf16*>(pack + n), n);
+  if (L->prec == 1) {  // bf16 image of the matrices right after the fp32 pack
+    MatTable m{};
+    auto mat = [&](int64_t off, int rows, int ld) {
+      m.off[m.n] = off;
+      m.rows[m.n] = rows;
+      m.ld[m.n] = ld;
+      ++m.n;
+    };
+    mat(L->WeT, 16, E);
+    mat(L->We, E, 16);
+    mat(L->Wo, 16, E);
+    mat(L->WoT, E, 16);
+    for (int d = 0; d < D; ++d) {
+      mat(L->M[d], HE, E);
+      mat(L->MT[d], E, HE);
+      mat(L->N[d], E, HE);
+      mat(L->NT[d], HE, E);
+      mat(L->W1[d], FF, E);
+      mat(L->W1T[d], E, FF);
+      mat(L->W2[d], E, FF);
+      mat(L->W2T[d], FF, E);
+    }
+    hipLaunchKernelGGL(to_bf16_kernel, dim3(16, m.n), dim3(256), 0, (hipStream_t)stream, m, pack,
+                       reinterpret_cast<__bf16*>(pack + L->total));
     return (int)hipGetLastError();
   }
   return 0;

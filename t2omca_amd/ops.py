@@ -120,13 +120,21 @@ def agent_unroll_fwd(shape: NetShape, pack_on, obs, h0_on=None, pack_tg=None, h0
     return q_on, h_on
 
 
-def tape_floats(shape: NetShape, records):
-    """Backward tape workspace (floats) for `records` weight-gradient records."""
-    return int(lib().t2o_bwd_tape_floats(ctypes.byref(shape.layout()), int(records)))
+def tape_floats(shape: NetShape, tiles):
+    """Backward tape workspace (floats) for `tiles` tiles of 16 weight-gradient records."""
+    return int(lib().t2o_bwd_tape_floats(ctypes.byref(shape.layout()), int(tiles)))
 
 
-def _tape(shape, records, tape, device):
-    n = tape_floats(shape, records)
+def agent_tape_tiles(B, T, A):
+    return T * ((B * A + 15) // 16)
+
+
+def mixer_tape_tiles(B, T, A):
+    return B * T * ((A + 3 + 15) // 16)
+
+
+def _tape(shape, tiles, tape, device):
+    n = tape_floats(shape, tiles)
     if tape is None or tape.numel() < n:
         tape = torch.empty(n, device=device)
     return tape
@@ -154,7 +162,8 @@ def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchose
     if slabs is None or slabs.numel() < nmax * L.grad_total:
         slabs = torch.empty(nmax * L.grad_total, device=obs.device)
     gh0 = torch.empty(B, A, shape.E, device=obs.device) if want_gh0 else None
-    tape = _tape(shape, B * T * A, tape, obs.device)
+    tiles = agent_tape_tiles(B, T, A)
+    tape = _tape(shape, tiles, tape, obs.device)
     nslab = ctypes.c_int(0)
     _mark(timer, "begin:agent_bwd")
     check(lib().t2o_agent_unroll_bwd(ctypes.byref(L), ptr(pack), ptr(obs), obs.stride(0), obs.stride(1),
@@ -163,7 +172,7 @@ def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchose
                                      ctypes.byref(nslab), ptr(tape), ptr(gh0), B, T, A, stream_ptr()),
           "agent_unroll_bwd")
     _mark(timer, "end:agent_bwd")
-    return tape_contract(shape, tape, B * T * A, slabs, nslab.value, timer, "agent_dw"), gh0
+    return tape_contract(shape, tape, tiles, slabs, nslab.value, timer, "agent_dw"), gh0
 
 
 def _mstrides(t):
@@ -224,12 +233,12 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
     return (o_on, o_tg) if pack_tg is not None else o_on
 
 
-def tape_contract(shape: NetShape, tape, records, slabs, nslab, timer=None, tag="dw"):
+def tape_contract(shape: NetShape, tape, tiles, slabs, nslab, timer=None, tag="dw"):
     """Fill the M/N/W1/W2 regions of the backward's slabs from its tape, then sum
     the slabs.  Returns the compact gradient block (on the current stream)."""
     L = shape.layout()
     _mark(timer, "begin:" + tag)
-    check(lib().t2o_bwd_tape_contract(ctypes.byref(L), ptr(tape), int(records), ptr(slabs), int(nslab),
+    check(lib().t2o_bwd_tape_contract(ctypes.byref(L), ptr(tape), int(tiles), ptr(slabs), int(nslab),
                                       stream_ptr()), "bwd_tape_contract")
     _mark(timer, "end:" + tag)
     gpack = torch.empty(L.grad_total, device=slabs.device)
@@ -256,7 +265,8 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
     gqv = torch.empty(B, T, A, device=dev)
     ghid = torch.empty(B, T, A, E, device=dev)
     ghw0 = torch.empty(B, 3, E, device=dev) if want_ghw0 else None
-    tape = _tape(shape, B * T * (A + 3), tape, dev)
+    tiles = mixer_tape_tiles(B, T, A)
+    tape = _tape(shape, tiles, tape, dev)
     nslab = ctypes.c_int(0)
     _mark(timer, "begin:mixer_bwd")
     check(lib().t2o_mixer_unroll_bwd(
@@ -265,7 +275,7 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
         ptr(fwd.get("xmid")), ptr(gy), ptr(ghw_ext), ptr(gqv), ptr(ghid), ptr(ghw0), ptr(slabs), nmax, ctypes.byref(nslab),
         ptr(tape), B, T, stream_ptr()), "mixer_unroll_bwd")
     _mark(timer, "end:mixer_bwd")
-    contract = lambda: tape_contract(shape, tape, B * T * (A + 3), slabs, nslab.value, timer, "mixer_dw")  # noqa: E731
+    contract = lambda: tape_contract(shape, tape, tiles, slabs, nslab.value, timer, "mixer_dw")  # noqa: E731
     return (contract if defer_contract else contract()), gqv, ghid, ghw0
 
 

@@ -45,10 +45,11 @@ def dw_record_flops(E=32, H=3, D=2, FF=None):
     return D * 2 * (2 * H * E * E + 2 * FF * E)
 
 
-def dw_record_bytes(E=32, H=3, D=2, FF=None):
-    """Tape bytes per record (all D blocks): written once by the backward, read once here."""
+def dw_record_bytes(E=32, H=3, D=2, FF=None, elem=4):
+    """Tape bytes per record (all D blocks): written once by the backward, read once
+    by the contraction; elem = 4 (fp32 mode) or 2 (bf16 mode)."""
     FF = FF or 4 * E
-    return D * 4 * (4 * E + 2 * H * E + 2 * FF)
+    return D * elem * (4 * E + 2 * H * E + 2 * FF)
 
 
 def td_update_flops(B, T, A, E=32, H=3, D=2, F=9, Fs=8, NA=5):
@@ -71,13 +72,14 @@ def td_update_flops(B, T, A, E=32, H=3, D=2, F=9, Fs=8, NA=5):
     }
 
 
-def td_update_bytes(B, T, A, E=32, F=9, Fs=8, NA=5):
-    """Compulsory HBM bytes per kernel (fp32 inputs read / outputs written once)."""
+def td_update_bytes(B, T, A, E=32, F=9, Fs=8, NA=5, elem=4):
+    """Compulsory HBM bytes per kernel (fp32 inputs read / outputs written once; the
+    weight-gradient tape in the MFMA operand type, `elem` bytes, valid records only)."""
     obs = B * (T + 1) * A * A * F * 4
     st = B * (T + 1) * A * Fs * 4
     qh = B * (T + 1) * A * (NA + E) * 4
-    tape_a = B * T * A * dw_record_bytes(E)
-    tape_m = B * T * (A + 3) * dw_record_bytes(E)
+    tape_a = B * T * A * dw_record_bytes(E, elem=elem)
+    tape_m = B * T * (A + 3) * dw_record_bytes(E, elem=elem)
     return {
         "agent_fwd": obs + 2 * qh,
         "mixer_fwd": st + 2 * qh + 2 * B * (T + 1) * ((A + 3) * E + 3 * E + A + 1) * 4,

@@ -20,7 +20,7 @@ def short(name):
     if m:
         return ("agent_dw", "mixer_dw")[int(m.group(1))]
     for n in NAMES:
-        if re.search(r"\b" + n + r"\b", name):
+        if n in name:
             return n.replace("_kernel", "")
     return None
 

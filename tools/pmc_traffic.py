@@ -28,7 +28,7 @@ def per_kernel(d, counter):
                 name = row["Kernel_Name"]
                 m = re.search(r"dw_gemm_kernel<[^>]*?(\d+)>", name)
                 short = ("agent_dw", "mixer_dw")[int(m.group(1))] if m else \
-                    next((v for k, v in SHORT.items() if re.search(r"\b" + k + r"\b", name)), None)
+                    next((v for k, v in SHORT.items() if k in name), None)
                 if short is None:
                     continue
                 vals.setdefault(short, []).append(float(row["Counter_Value"]))
