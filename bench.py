@@ -47,7 +47,15 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=16, help="episodes in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--serial", action="store_true",
+                    help="no side-stream overlap: every kernel's HIP-event time is its isolated cost")
+    ap.add_argument("--print-workload-tag", action="store_true",
+                    help="print the tag that keys profiles/hbm_traffic.json for these args and exit")
     return ap.parse_args()
+
+
+def workload_tag(args):
+    return f"b{args.batch}_t{args.T}_a{args.agents}_{args.dtype}"
 
 
 class KernelTimer:
@@ -69,7 +77,7 @@ class KernelTimer:
         return out
 
 
-def traffic_for(kernel, B, T, A):
+def traffic_for(kernel, tag):
     """HBM bytes per launch of `kernel` from the committed PMC summary
     (profiles/hbm_traffic.json: rocprofv3 FETCH_SIZE / WRITE_SIZE passes, corrected
     as MI355X_MICROARCH.md prescribes, by tools/pmc_traffic.py), or None when that
@@ -80,7 +88,7 @@ def traffic_for(kernel, B, T, A):
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    if d.get("workload") != f"b{B}_t{T}_a{A}":
+    if d.get("workload") != tag:
         return None
     k = d.get("kernels", {}).get(kernel)
     return None if k is None else k.get("hbm_bytes")
@@ -112,6 +120,9 @@ def cpu_baseline(args):
 
 def main():
     args = parse()
+    if args.print_workload_tag:
+        print(workload_tag(args))
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -129,7 +140,8 @@ def main():
     margs = make_args(A, device=str(dev))
     agent = TransformerAgent(None, margs).to(dev)
     mixer = TransformerMixer(margs).to(dev)
-    learner = TDLearner(agent, mixer, target_update_interval=10 ** 9, precision=args.dtype)
+    learner = TDLearner(agent, mixer, target_update_interval=10 ** 9, precision=args.dtype,
+                        overlap=not args.serial)
     batch, w = make_batch(B, T, A, seed=1 + rank, device=dev)
     for i in range(args.warmup):
         learner.train(batch, 0, i, per_weight=w)
@@ -185,7 +197,7 @@ def main():
                    "global_batch": B * world, "seq_len": T, "agents": A, "emb": 32, "heads": 3, "depth": 2,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm" if hbm_bound else "mfma", "kernel": dom, "achieved": achieved, "peak": peak,
-                     "unit": unit, "frac": achieved / peak, "traffic": traffic_for(dom, B, T, A),
+                     "unit": unit, "frac": achieved / peak, "traffic": traffic_for(dom, workload_tag(args)),
                      "algorithmic_flops_per_launch": flops[dom],
                      "algorithmic_bytes_per_launch": bytes_[dom],
                      "avg_launch_ms": dom_ms},

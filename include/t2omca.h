@@ -123,8 +123,8 @@ int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, const float*
  * t2o_agent_bwd_max_slabs(B, A)); gh0[b][a][E] = dL/dh0 (may be NULL).
  * Workspace: tape, t2o_bwd_tape_floats(L, tiles) floats with tiles =
  * T * ceil(B*A/16) — the per-record operand pairs of the M/N/W1/W2 weight
- * grads; the slabs are complete only after t2o_bwd_tape_contract(L, tape,
- * tiles, gslabs, *nslab) on the same stream. */
+ * grads; the slabs are complete only after t2o_bwd_tape_contract(L, pack,
+ * tape, tiles, gslabs, *nslab) on the same stream. */
 int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack,
                          const float* obs, int64_t obs_sb, int64_t obs_st,
                          const float* h0, const float* h_seq, const float* hmid, int h_ts,
@@ -174,14 +174,16 @@ int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, const float* st
 int t2o_mixer_bwd_max_slabs(int B);
 
 /* Floats of backward tape workspace for `tiles` tiles of 16 records:
- * D * tiles * 16 * (4E + 2HE + 2FF) elements of 4 (fp32) or 2 (bf16) bytes. */
+ * D * tiles * 16 * (4E + 2HE) elements of 4 (fp32) or 2 (bf16) bytes. */
 int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t tiles);
 
 /* Contract a backward tape (dM, dN, dW1, dW2 = Σ_records dYᵀ X, split-K over
  * the nslab slabs the backward call returned) into the M/N/W1/W2 regions of
- * those slabs.  Must follow the t2o_*_unroll_bwd call that wrote the tape. */
-int t2o_bwd_tape_contract(const t2o_layout* L, const void* tape, int64_t tiles, float* gslabs, int nslab,
-                          void* stream);
+ * those slabs.  pack = the same kernel pack the backward used (W1, W2ᵀ, c1
+ * recompute the FFN operands the tape does not store).  Must follow the
+ * t2o_*_unroll_bwd call that wrote the tape. */
+int t2o_bwd_tape_contract(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
+                          float* gslabs, int nslab, void* stream);
 
 /* TD(λ) targets, masked PER-weighted loss, dL/dQtot and priorities
  * (PyMARL2 NQLearner semantics; see t2o_learner.hip).  qtot [B][T] (online

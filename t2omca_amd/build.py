@@ -2,8 +2,8 @@
 
     python -m t2omca_amd.build        (or __graft_entry__.build())
 
-One hipcc invocation compiles every csrc/*.hip translation unit into a single
-C-ABI shared library (declared in include/t2omca.h).  The .so is git-ignored
+Every csrc/*.hip translation unit is compiled to an object in parallel and
+linked into a single C-ABI shared library (declared in include/t2omca.h).  The .so is git-ignored
 but travels to the GPU box inside the repo snapshot.
 """
 import glob
@@ -31,22 +31,39 @@ def _stale():
     return any(os.path.getmtime(p) > t for p in deps)
 
 
-def build(force=False, verbose=False):
+def build(force=False, verbose=False, jobs=None):
+    """Compile each translation unit to an object in parallel, then link the .so."""
     if not force and not _stale():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
+    objdir = os.path.join(LIBDIR, "obj")
+    os.makedirs(objdir, exist_ok=True)
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"]
+    objs, procs = [], []
+    for src in sources():
+        obj = os.path.join(objdir, os.path.basename(src) + ".o")
+        objs.append(obj)
+        cmd = [hipcc] + flags + ["-c", "-o", obj, src]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((src, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)))
+    failed = False
+    for src, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            failed = True
+            sys.stderr.write(out)
+        elif verbose and out.strip():
+            sys.stderr.write(out)
+    if failed:
+        raise RuntimeError("hipcc failed building libt2omca.so")
     tmp = LIB + ".tmp"
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", "-o", tmp] + sources()
-    if verbose:
-        print(" ".join(cmd))
-    r = subprocess.run(cmd, capture_output=True, text=True)
+    r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs,
+                       capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
-        raise RuntimeError("hipcc failed building libt2omca.so")
-    if verbose and r.stderr.strip():
-        sys.stderr.write(r.stderr)
+        raise RuntimeError("hipcc failed linking libt2omca.so")
     os.replace(tmp, LIB)
     return LIB
 

@@ -91,10 +91,7 @@ T2O_DEV void post_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G
   f4 gr2[ET];
   layernorm_bwd<ET>(gx, c.xh2, c.rs2, P.v + L.g2[d], gr2);
   // r2 = W2 relu(f1) + c2 + y
-  if (rec) {
-    tile_store<ET>(rec, R::GR2, gr2);
-    tile_store<FT>(rec, R::F1R, c.f1r);
-  }
+  if (rec) tile_store<ET>(rec, R::GR2, gr2);
   vec_accumulate_g<ET>(gs + G.c2[d], gr2);
   f4 gf1[FT];
   matvec_tr<FT, ET>(P, L.W2[d], FF, L.W2T[d], E, gr2, gf1);
@@ -102,10 +99,7 @@ T2O_DEV void post_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G
   for (int t = 0; t < FT; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) gf1[t][r] = c.f1r[t][r] > 0.f ? gf1[t][r] : 0.f;
-  if (rec) {
-    tile_store<FT>(rec, R::GF1, gf1);
-    tile_store<ET>(rec, R::Y, c.y);
-  }
+  if (rec) tile_store<ET>(rec, R::Y, c.y);  // f1 and gf1 are recomputed from (y, gr2)
   vec_accumulate_g<FT>(gs + G.c1[d], gf1);
   f4 gy[ET];
   matvec_tr<ET, FT>(P, L.W1[d], E, L.W1T[d], FF, gf1, gy);

@@ -527,27 +527,29 @@ T2O_DEV void flush_tiles_g(float* __restrict__ W, int ldw, const f4 (&acc)[OT][I
 
 // ---- weight-gradient tape ---------------------------------------------------
 // The backward kernels do not accumulate the four big per-block matrices
-// (M, N, W1, W2) themselves: per (row, step, block) they stream the operand
-// pairs of dW = Σ dYᵀ X to an HBM tape, and t2o_dwgemm.hip contracts the tape
-// over all records with MFMA.  Feature offsets of one record:
+// (M, N, W1, W2) themselves: per (row, step, block) they stream a record to an
+// HBM tape, and t2o_dwgemm.hip contracts the tape over all records with MFMA:
+//   dM = Σ gu ⊗ x,  dN = Σ gres ⊗ z,  dW2 = Σ gr2 ⊗ relu(f1),  dW1 = Σ gf1 ⊗ y
+// with f1 = W1 y + c1 and gf1 = [f1 > 0] ⊙ W2ᵀ gr2 RECOMPUTED from (y, gr2) by
+// the contraction (two FF-wide operands are 44 % of a full record; recomputing
+// them is a few MFMAs per 16 records in a kernel that is HBM-bound anyway).
+// Feature offsets of one record:
 template <int E, int H, int FF>
 struct TapeRec {
   static constexpr int X = 0;                 // block input x      (E)   M:  X
   static constexpr int GU = X + E;            // dL/du              (HE)  M:  dY
   static constexpr int Z = GU + H * E;        // head outputs z     (HE)  N:  X
   static constexpr int GRES = Z + H * E;      // dL/d(N z + bu)     (E)   N:  dY
-  static constexpr int Y = GRES + E;          // LN1 output y       (E)   W1: X
-  static constexpr int GF1 = Y + E;           // dL/d(W1 y + c1)    (FF)  W1: dY
-  static constexpr int F1R = GF1 + FF;        // relu(W1 y + c1)    (FF)  W2: X
-  static constexpr int GR2 = F1R + FF;        // dL/d(W2 f + c2 + y)(E)   W2: dY
+  static constexpr int Y = GRES + E;          // LN1 output y       (E)   W1: X, and f1
+  static constexpr int GR2 = Y + E;           // dL/d(W2 f + c2 + y)(E)   W2: dY, and gf1
   static constexpr int SIZE = GR2 + E;
 };
 // Layout: tiles of 16 records (one wave's rows at one step), feature-major
 // inside a tile: element (record 16·tile + c, feature f) of block d sits at
 // ((d·ntiles + tile)·SIZE + f)·16 + c, in the MFMA operand type (fp32, or bf16
-// in bf16 mode).  A wave's tile is one contiguous 18 KiB (bf16) run written
-// whole; the contraction reads 8 (bf16) / 4 (fp32) consecutive records of one
-// feature per lane, which is exactly an MFMA K-slice.
+// in bf16 mode).  A wave's tile is one contiguous 10 KiB (bf16) run written
+// whole; the contraction stages tiles in LDS and reads 4 consecutive records
+// of one feature per lane, which is exactly a 16x16x16 MFMA K-slice.
 
 // store a T-layout vector (NT tiles, features off + 16t + 4g + r of record c)
 template <int NT, typename TT>

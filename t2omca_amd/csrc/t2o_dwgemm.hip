@@ -1,21 +1,32 @@
 // t2o_dwgemm.hip — contraction of the weight-gradient tape (TapeRec, t2o_common.hpp).
 //
-// dM = Σ_n gu_n x_nᵀ,  dN = Σ_n gres_n z_nᵀ,  dW1 = Σ_n gf1_n y_nᵀ,  dW2 = Σ_n gr2_n f1r_nᵀ
-// over every record (row x step of the agent, query row x step of the mixer)
-// of every block.  This is a tall-skinny GEMM with K = records: split-K over
-// workgroups (workgroup k contracts one contiguous range of 16-record tiles and
-// writes the four matrices of every block into gradient slab k, whose
-// small-gradient part the backward kernel has already filled), and inside a
-// workgroup one wave per (block, matrix pair) keeps its 28 output tiles in MFMA
-// accumulators for the whole range.  The tape is feature-major inside a tile
-// (TapeRec), so one lane's K-slice is contiguous:
-//   bf16: lane (g, c) loads 8 records (tile t0 + g/2, records 8(g&1)..+7) of
-//         feature 16o+c as one 16-B load -> v_mfma_f32_16x16x32_bf16, 32 records
-//   fp32: lane (g, c) loads records 4g..4g+3 of one tile (16 B) and feeds them
-//         to four v_mfma_f32_16x16x4_f32, 16 records
-// Bound: HBM (each record is read once: 1152 B (bf16) / 2304 B (fp32) per block).
-// Called by the host right after t2o_agent_unroll_bwd / t2o_mixer_unroll_bwd
-// with the same slabs: it fills their M/N/W1/W2 regions.
+// Per block d, over every record n (row x step of the agent, query row x step
+// of the mixer):
+//   dM  = Σ_n gu_n ⊗ x_n          dN  = Σ_n gres_n ⊗ z_n
+//   dW2 = Σ_n gr2_n ⊗ relu(f1_n)  dW1 = Σ_n gf1_n ⊗ y_n
+// where f1 = W1 y + c1 and gf1 = [f1 > 0] ⊙ (W2ᵀ gr2) are recomputed here from
+// the record's (y, gr2) — the backward kernels do not store them.
+//
+// This is a tall-skinny GEMM with K = records (≈1M per block at config 3) and
+// HBM-bound: every tape byte is read once.  Structure:
+//   * split-K over workgroups: 16-record tiles are grouped TG at a time and the
+//     groups dealt round-robin (group k -> workgroup k mod nslab), so the grid
+//     streams one contiguous window of the tape at a time; workgroup k writes
+//     the four matrices of every block into gradient slab k, whose small-
+//     gradient part the backward kernel has already filled;
+//   * each workgroup stages a group (all D blocks) in LDS with full-line 16-B
+//     loads by all its threads, double-buffered in LDS with a two-deep
+//     register ring (prefetch distance two groups), one barrier per group;
+//   * 4 waves per block read the staged tiles: wave 0 dM, wave 1 dN, waves 2
+//     and 3 one half of the FF features each (recompute f1 / gf1 with MFMA
+//     from LDS copies of W1 / W2ᵀ, then dW1 / dW2).  All accumulators stay in
+//     registers for the whole launch.
+// MFMA shapes: bf16 tape -> v_mfma_f32_16x16x16_bf16 (K = 16 records of a
+// tile: lane (g, c) reads records 4g..4g+3 of one feature, one ds_read_b64;
+// the record-major operand of the recompute comes from ds_read_b64_tr_b16);
+// fp32 tape -> four v_mfma_f32_16x16x4_f32 per 16 records.
+#include <type_traits>
+
 #include "t2o_common.hpp"
 #include "t2o_dispatch.hpp"
 #include "t2o_layout.hpp"
@@ -25,11 +36,10 @@ namespace t2o {
 struct DwGemmArgs {
   const void* tape;    // [D][ntiles][SIZE][16]
   int64_t ntiles;      // 16-record tiles per block
-  int64_t chunk;       // tiles per workgroup (multiple of 2)
   float* slabs;        // [nslab][slab_stride], compact gradient layout G
   int64_t slab_stride;
-  t2o_layout G;
-  int D;
+  const float* pack;   // the network's kernel pack (fp32; bf16 image at pack + L.total)
+  t2o_layout L, G;
 };
 
 template <int OT, int IT>
@@ -43,117 +53,351 @@ T2O_DEV void dw_tiles_store(float* __restrict__ W, int ldw, const f4 (&acc)[OT][
       for (int r = 0; r < 4; ++r) W[(16 * o + 4 * g + r) * ldw + 16 * i + c] = acc[o][i][r];
 }
 
-typedef __bf16 bf8v __attribute__((ext_vector_type(8)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 
-// one operand pair over one K-step: acc[o][i] += Σ_k dY[k][16o+c] X[k][16i+c]
-// fp32: `p` = this lane's tile base + its 4-record offset; K-step = 16 records
-template <int OT, int IT>
-T2O_DEV void dw_pair(f4 (&acc)[OT][IT], const float* __restrict__ p, bool ok, int offA, int offB) {
+template <typename TT> struct DwTraits;
+template <> struct DwTraits<__bf16> { static constexpr int TG = 2; };  // tiles per group
+template <> struct DwTraits<float> { static constexpr int TG = 1; };
+
+// ---- operand reads from a staged tile (feature-major, 16 records per row) ----
+// bf16: records 4g..4g+3 of feature row `f` (K-slice of a 16x16x16 MFMA)
+T2O_DEV bf4 kslice(const __bf16* tile, int f) { return ldb4(tile + f * 16 + 4 * lane_g()); }
+// bf16: features f0 + 4g .. +3 of record c (the record-major operand), by the
+// gfx950 transposed LDS read: lane 4q+p of each 16-lane group addresses row
+// f0 + 4g + q, records 4p..4p+3, and lane c receives record c of the 4 rows.
+T2O_DEV bf4 rslice(const __bf16* tile, int f0) {
   const int c = lane_c();
-  f4 a[OT], b[IT];
-#pragma unroll
-  for (int o = 0; o < OT; ++o) a[o] = ok ? ld4(p + (offA + 16 * o + c) * 16) : zero4();
-#pragma unroll
-  for (int i = 0; i < IT; ++i) b[i] = ok ? ld4(p + (offB + 16 * i + c) * 16) : zero4();
-#pragma unroll
-  for (int o = 0; o < OT; ++o)
-#pragma unroll
-    for (int i = 0; i < IT; ++i)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) acc[o][i] = mfma4(a[o][s], b[i][s], acc[o][i]);
-}
-// bf16: K-step = 32 records (two tiles)
-template <int OT, int IT>
-T2O_DEV void dw_pair(f4 (&acc)[OT][IT], const __bf16* __restrict__ p, bool ok, int offA, int offB) {
-  const int c = lane_c();
-  const bf8v z{};
-  bf8v a[OT], b[IT];
-#pragma unroll
-  for (int o = 0; o < OT; ++o) a[o] = ok ? *reinterpret_cast<const bf8v*>(p + (offA + 16 * o + c) * 16) : z;
-#pragma unroll
-  for (int i = 0; i < IT; ++i) b[i] = ok ? *reinterpret_cast<const bf8v*>(p + (offB + 16 * i + c) * 16) : z;
-#pragma unroll
-  for (int o = 0; o < OT; ++o)
-#pragma unroll
-    for (int i = 0; i < IT; ++i) acc[o][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[o], b[i], acc[o][i], 0, 0, 0);
+  const __bf16* p = tile + (f0 + 4 * lane_g() + (c >> 2)) * 16 + 4 * (c & 3);
+  typedef __attribute__((address_space(3))) s4v lds_s4v;
+  const s4v v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(p));
+  return __builtin_bit_cast(bf4, v);
 }
 
-// KIND (0 agent, 1 mixer) only separates the two instances in profiles.
-template <int E, int H, int FF, int KIND, typename TT>
-__global__ __launch_bounds__(64 * 2 * T2O_MAX_DEPTH) void dw_gemm_kernel(DwGemmArgs a) {
+template <int E, int H, int FF, int D, typename TT>
+struct DwDims {
   using R = TapeRec<E, H, FF>;
-  constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
-  constexpr bool BF = sizeof(TT) == 2;
-  const int w = wave_id();
-  const int d = w >> 1;
-  if (d >= a.D) return;
-  const int g = lane_g();
-  const int64_t t0 = (int64_t)blockIdx.x * a.chunk;
-  const int64_t t1 = t0 + a.chunk < a.ntiles ? t0 + a.chunk : a.ntiles;
-  const TT* __restrict__ base = static_cast<const TT*>(a.tape) + (size_t)d * a.ntiles * R::SIZE * 16;
-  float* slab = a.slabs + (size_t)blockIdx.x * a.slab_stride;
-  // this lane's K-slice inside a step: bf16 -> tile t + g/2, records 8(g&1)..;
-  // fp32 -> tile t, records 4g..4g+3
-  auto lane_ptr = [&](int64_t t, bool& ok) {
-    const int64_t tt = BF ? t + (g >> 1) : t;
-    ok = tt < t1;
-    return base + (size_t)(ok ? tt : t0) * R::SIZE * 16 + (BF ? 8 * (g & 1) : 4 * g);
-  };
-  constexpr int STEP = BF ? 2 : 1;  // tiles per K-step
-  if ((w & 1) == 0) {  // M (gu ⊗ x) and W1 (gf1 ⊗ y)
-    f4 accM[HET][ET], accW1[FT][ET];
+  static constexpr int ET = E / 16, HET = H * ET, FT = FF / 16, FH = FT / 2;
+  static constexpr bool BF = sizeof(TT) == 2;
+  static constexpr int TG = DwTraits<TT>::TG;
+  static constexpr int TILE = R::SIZE * 16;                 // elements per tile
+  static constexpr int CPT = TILE * (int)sizeof(TT) / 16;   // 16-B chunks per tile
+  static constexpr int NT = 256 * D;                        // threads
+  static constexpr int GCH = D * TG * CPT;                  // chunks per group
+  static constexpr int NLD = (GCH + NT - 1) / NT;           // chunks per thread
+  static constexpr int GELEM = D * TG * TILE;               // elements per staged group
+  static_assert(FT % 2 == 0, "FF must split into two halves of 16-feature tiles");
+};
+
+// group j of this workgroup: tape -> registers (tiles past the end read as zeros)
+template <typename Dm, typename TT>
+T2O_DEV void dw_load(const DwGemmArgs& a, int64_t j, u4v (&rg)[Dm::NLD]) {
+  const TT* __restrict__ tape = static_cast<const TT*>(a.tape);
+  const int64_t grp = blockIdx.x + j * gridDim.x;
 #pragma unroll
-    for (int o = 0; o < HET; ++o)
+  for (int i = 0; i < Dm::NLD; ++i) {
+    const int q = threadIdx.x + i * Dm::NT;
+    const int dd = q / (Dm::TG * Dm::CPT), rem = q % (Dm::TG * Dm::CPT);
+    const int tt = rem / Dm::CPT, ch = rem % Dm::CPT;
+    const int64_t tile = grp * Dm::TG + tt;
+    rg[i] = u4v{0u, 0u, 0u, 0u};
+    if (q < Dm::GCH && tile < a.ntiles)
+      rg[i] = *reinterpret_cast<const u4v*>(tape + ((size_t)dd * a.ntiles + tile) * Dm::TILE + ch * (16 / sizeof(TT)));
+  }
+}
+// registers -> LDS group buffer (lane-linear: the buffer is [D][TG][tile])
+template <typename Dm, typename TT>
+T2O_DEV void dw_store(TT* buf, const u4v (&rg)[Dm::NLD]) {
 #pragma unroll
-      for (int i = 0; i < ET; ++i) accM[o][i] = zero4();
-#pragma unroll
-    for (int o = 0; o < FT; ++o)
-#pragma unroll
-      for (int i = 0; i < ET; ++i) accW1[o][i] = zero4();
-#pragma unroll 2
-    for (int64_t t = t0; t < t1; t += STEP) {
-      bool ok;  // false only for the missing second tile of an odd range (bf16)
-      const TT* p = lane_ptr(t, ok);
-      dw_pair<HET, ET>(accM, p, ok, R::GU, R::X);
-      dw_pair<FT, ET>(accW1, p, ok, R::GF1, R::Y);
-    }
-    dw_tiles_store<HET, ET>(slab + a.G.M[d], E, accM);
-    dw_tiles_store<FT, ET>(slab + a.G.W1[d], E, accW1);
-  } else {  // N (gres ⊗ z) and W2 (gr2 ⊗ f1r)
-    f4 accN[ET][HET], accW2[ET][FT];
-#pragma unroll
-    for (int o = 0; o < ET; ++o) {
-#pragma unroll
-      for (int i = 0; i < HET; ++i) accN[o][i] = zero4();
-#pragma unroll
-      for (int i = 0; i < FT; ++i) accW2[o][i] = zero4();
-    }
-#pragma unroll 2
-    for (int64_t t = t0; t < t1; t += STEP) {
-      bool ok;
-      const TT* p = lane_ptr(t, ok);
-      dw_pair<ET, HET>(accN, p, ok, R::GRES, R::Z);
-      dw_pair<ET, FT>(accW2, p, ok, R::GR2, R::F1R);
-    }
-    dw_tiles_store<ET, HET>(slab + a.G.N[d], H * E, accN);
-    dw_tiles_store<ET, FT>(slab + a.G.W2[d], FF, accW2);
+  for (int i = 0; i < Dm::NLD; ++i) {
+    const int q = threadIdx.x + i * Dm::NT;
+    if (q < Dm::GCH) *reinterpret_cast<u4v*>(buf + q * (16 / sizeof(TT))) = rg[i];
   }
 }
 
-template <int E, int H, int FF, typename TT>
-int launch_dw_gemm(int kind, const void* tape, int64_t ntiles, int D, float* slabs, int64_t slab_stride,
+// Role state: the accumulators (and, for the FFN roles, the weight fragments)
+// of one wave.  ROLE 0 dM, 1 dN, 2/3 FFN half 0/1.
+template <int ROLE, int E, int H, int FF, int D, typename TT>
+struct DwRole;
+
+template <int E, int H, int FF, int D, typename TT>
+struct DwRole<0, E, H, FF, D, TT> {
+  using Dm = DwDims<E, H, FF, D, TT>;
+  using R = typename Dm::R;
+  f4 acc[Dm::HET][Dm::ET];  // dM[gu feature][x feature]
+  T2O_DEV void init(const DwGemmArgs&, int, const TT*) {
+#pragma unroll
+    for (int o = 0; o < Dm::HET; ++o)
+#pragma unroll
+      for (int i = 0; i < Dm::ET; ++i) acc[o][i] = zero4();
+  }
+  T2O_DEV void tile(const TT* t) {
+    const int c = lane_c(), g = lane_g();
+    if constexpr (Dm::BF) {
+      bf4 xb[Dm::ET];
+#pragma unroll
+      for (int i = 0; i < Dm::ET; ++i) xb[i] = kslice(t, R::X + 16 * i + c);
+#pragma unroll
+      for (int o = 0; o < Dm::HET; ++o) {
+        const bf4 ab = kslice(t, R::GU + 16 * o + c);
+#pragma unroll
+        for (int i = 0; i < Dm::ET; ++i) acc[o][i] = mfma_b16(ab, xb[i], acc[o][i]);
+      }
+    } else {
+      f4 xv[Dm::ET];
+#pragma unroll
+      for (int i = 0; i < Dm::ET; ++i) xv[i] = ld4(t + (R::X + 16 * i + c) * 16 + 4 * g);
+#pragma unroll
+      for (int o = 0; o < Dm::HET; ++o) {
+        const f4 av = ld4(t + (R::GU + 16 * o + c) * 16 + 4 * g);
+#pragma unroll
+        for (int i = 0; i < Dm::ET; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[o][i] = mfma4(av[r], xv[i][r], acc[o][i]);
+      }
+    }
+  }
+  T2O_DEV void finish(const DwGemmArgs& a, float* slab, int d) {
+    dw_tiles_store<Dm::HET, Dm::ET>(slab + a.G.M[d], E, acc);
+  }
+};
+
+template <int E, int H, int FF, int D, typename TT>
+struct DwRole<1, E, H, FF, D, TT> {
+  using Dm = DwDims<E, H, FF, D, TT>;
+  using R = typename Dm::R;
+  f4 acc[Dm::ET][Dm::HET];  // dN[gres feature][z feature]
+  T2O_DEV void init(const DwGemmArgs&, int, const TT*) {
+#pragma unroll
+    for (int o = 0; o < Dm::ET; ++o)
+#pragma unroll
+      for (int i = 0; i < Dm::HET; ++i) acc[o][i] = zero4();
+  }
+  T2O_DEV void tile(const TT* t) {
+    const int c = lane_c(), g = lane_g();
+    if constexpr (Dm::BF) {
+      bf4 gb[Dm::ET];
+#pragma unroll
+      for (int o = 0; o < Dm::ET; ++o) gb[o] = kslice(t, R::GRES + 16 * o + c);
+#pragma unroll
+      for (int i = 0; i < Dm::HET; ++i) {
+        const bf4 zb = kslice(t, R::Z + 16 * i + c);
+#pragma unroll
+        for (int o = 0; o < Dm::ET; ++o) acc[o][i] = mfma_b16(gb[o], zb, acc[o][i]);
+      }
+    } else {
+      f4 gv[Dm::ET];
+#pragma unroll
+      for (int o = 0; o < Dm::ET; ++o) gv[o] = ld4(t + (R::GRES + 16 * o + c) * 16 + 4 * g);
+#pragma unroll
+      for (int i = 0; i < Dm::HET; ++i) {
+        const f4 zv = ld4(t + (R::Z + 16 * i + c) * 16 + 4 * g);
+#pragma unroll
+        for (int o = 0; o < Dm::ET; ++o)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[o][i] = mfma4(gv[o][r], zv[r], acc[o][i]);
+      }
+    }
+  }
+  T2O_DEV void finish(const DwGemmArgs& a, float* slab, int d) {
+    dw_tiles_store<Dm::ET, Dm::HET>(slab + a.G.N[d], H * E, acc);
+  }
+};
+
+// FFN half HALF: recompute f1 = W1 y + c1 and gf1 = [f1 > 0] ⊙ W2ᵀ gr2 for the
+// half's FH feature tiles as [records x features] MFMA tiles (lane (g, c) =
+// records 4g..4g+3 of feature 16J + c — already the K-slice layout of the
+// contraction), then dW2[e][J] += gr2 ⊗ relu(f1), dW1[J][e] += gf1 ⊗ y.
+template <int HALF, int E, int H, int FF, int D, typename TT>
+struct DwFfn {
+  using Dm = DwDims<E, H, FF, D, TT>;
+  using R = typename Dm::R;
+  static constexpr int ET = Dm::ET, FH = Dm::FH;
+  using Frag = typename std::conditional<Dm::BF, bf4, f4>::type;
+  f4 acc1[FH][ET];  // dW1 rows of this half
+  f4 acc2[ET][FH];  // dW2 columns of this half
+  const TT* wl;    // LDS copy of this block's W1 [FF][E] then W2ᵀ [FF][E] (bf16: the pack's swizzled image)
+  float c1v[FH];
+  T2O_DEV void init(const DwGemmArgs& a, int d, const TT* wlds) {
+    const int c = lane_c();
+#pragma unroll
+    for (int o = 0; o < FH; ++o)
+#pragma unroll
+      for (int i = 0; i < ET; ++i) acc1[o][i] = acc2[i][o] = zero4();
+    wl = wlds + (size_t)d * 2 * FF * E;
+#pragma unroll
+    for (int jt = 0; jt < FH; ++jt) c1v[jt] = a.pack[a.L.c1[d] + 16 * (HALF * FH + jt) + c];
+  }
+  // fragment of W (0: W1, 1: W2ᵀ): row 16J + c, features 16s + 4g .. +3
+  T2O_DEV Frag wfrag(int m, int jt, int s) const {
+    const int row = 16 * (HALF * FH + jt) + lane_c();
+    const TT* base = wl + (size_t)m * FF * E + (size_t)row * E;
+    if constexpr (Dm::BF) return ldb4(base + ((16 * s + 4 * lane_g()) ^ bf_swz(row, E)));
+    else return ld4(base + 16 * s + 4 * lane_g());
+  }
+  T2O_DEV void tile(const TT* t) {
+    const int c = lane_c(), g = lane_g();
+    if constexpr (Dm::BF) {
+      bf4 yr[ET], gr[ET], yk[ET], gk[ET];
+#pragma unroll
+      for (int s = 0; s < ET; ++s) {
+        yr[s] = rslice(t, R::Y + 16 * s);
+        gr[s] = rslice(t, R::GR2 + 16 * s);
+        yk[s] = kslice(t, R::Y + 16 * s + c);
+        gk[s] = kslice(t, R::GR2 + 16 * s + c);
+      }
+#pragma unroll
+      for (int jt = 0; jt < FH; ++jt) {
+        f4 f1 = zero4(), gp = zero4();
+#pragma unroll
+        for (int s = 0; s < ET; ++s) {
+          f1 = mfma_b16(yr[s], wfrag(0, jt, s), f1);
+          gp = mfma_b16(gr[s], wfrag(1, jt, s), gp);
+        }
+        f4 fr, gf;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = f1[r] + c1v[jt];
+          fr[r] = fmaxf(v, 0.f);
+          gf[r] = v > 0.f ? gp[r] : 0.f;
+        }
+        const bf4 frb = to_bf4(fr), gfb = to_bf4(gf);
+#pragma unroll
+        for (int e = 0; e < ET; ++e) {
+          acc2[e][jt] = mfma_b16(gk[e], frb, acc2[e][jt]);
+          acc1[jt][e] = mfma_b16(gfb, yk[e], acc1[jt][e]);
+        }
+      }
+    } else {
+      f4 yk[ET], gk[ET];
+#pragma unroll
+      for (int s = 0; s < ET; ++s) {
+        yk[s] = ld4(t + (R::Y + 16 * s + c) * 16 + 4 * g);
+        gk[s] = ld4(t + (R::GR2 + 16 * s + c) * 16 + 4 * g);
+      }
+#pragma unroll
+      for (int jt = 0; jt < FH; ++jt) {
+        f4 f1 = zero4(), gp = zero4();
+#pragma unroll
+        for (int s = 0; s < ET; ++s) {
+          const f4 w1 = wfrag(0, jt, s), w2 = wfrag(1, jt, s);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            // feature k = 16s + 4g + r of record c (K-step r, k index g)
+            const int fk = 16 * s + 4 * g + r;
+            f1 = mfma4(t[(R::Y + fk) * 16 + c], w1[r], f1);
+            gp = mfma4(t[(R::GR2 + fk) * 16 + c], w2[r], gp);
+          }
+        }
+        f4 fr, gf;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = f1[r] + c1v[jt];
+          fr[r] = fmaxf(v, 0.f);
+          gf[r] = v > 0.f ? gp[r] : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < ET; ++e)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            acc2[e][jt] = mfma4(gk[e][r], fr[r], acc2[e][jt]);
+            acc1[jt][e] = mfma4(gf[r], yk[e][r], acc1[jt][e]);
+          }
+      }
+    }
+  }
+  T2O_DEV void finish(const DwGemmArgs& a, float* slab, int d) {
+    dw_tiles_store<FH, ET>(slab + a.G.W1[d] + (int64_t)16 * HALF * FH * E, E, acc1);
+    dw_tiles_store<ET, FH>(slab + a.G.W2[d] + 16 * HALF * FH, FF, acc2);
+  }
+};
+template <int E, int H, int FF, int D, typename TT>
+struct DwRole<2, E, H, FF, D, TT> : DwFfn<0, E, H, FF, D, TT> {};
+template <int E, int H, int FF, int D, typename TT>
+struct DwRole<3, E, H, FF, D, TT> : DwFfn<1, E, H, FF, D, TT> {};
+
+// One wave's whole launch for its role (every role runs the same pipeline and
+// the same barrier sequence; the roles only differ in what they read).
+// Pipeline: LDS double buffer, register ring of two, prefetch distance 2.
+template <int ROLE, int E, int H, int FF, int D, typename TT>
+T2O_DEV void dw_run(const DwGemmArgs& a, TT* buf0, TT* buf1, const TT* wlds, int d) {
+  using Dm = DwDims<E, H, FF, D, TT>;
+  const int64_t ngroups = (a.ntiles + Dm::TG - 1) / Dm::TG;
+  const int64_t nj = (int64_t)blockIdx.x < ngroups ? (ngroups - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  DwRole<ROLE, E, H, FF, D, TT> st;
+  st.init(a, d, wlds);
+  auto compute = [&](const TT* buf) {
+#pragma unroll
+    for (int tt = 0; tt < Dm::TG; ++tt) {
+      st.tile(buf + (d * Dm::TG + tt) * Dm::TILE);
+      T2O_FENCE();  // keep the next tile's LDS reads from being hoisted over these MFMAs
+    }
+  };
+  u4v r0[Dm::NLD], r1[Dm::NLD];
+  if (nj > 0) dw_load<Dm, TT>(a, 0, r0);
+  if (nj > 1) dw_load<Dm, TT>(a, 1, r1);
+  if (nj > 0) dw_store<Dm, TT>(buf0, r0);
+  if (nj > 1) dw_store<Dm, TT>(buf1, r1);
+  if (nj > 2) dw_load<Dm, TT>(a, 2, r0);
+  if (nj > 3) dw_load<Dm, TT>(a, 3, r1);
+  __syncthreads();
+  for (int64_t j = 0; j < nj; j += 2) {
+    compute(buf0);
+    __syncthreads();
+    if (j + 2 < nj) dw_store<Dm, TT>(buf0, r0);
+    if (j + 4 < nj) dw_load<Dm, TT>(a, j + 4, r0);
+    if (j + 1 >= nj) break;
+    compute(buf1);
+    __syncthreads();
+    if (j + 3 < nj) dw_store<Dm, TT>(buf1, r1);
+    if (j + 5 < nj) dw_load<Dm, TT>(a, j + 5, r1);
+  }
+  st.finish(a, a.slabs + (size_t)blockIdx.x * a.slab_stride, d);
+}
+
+template <int E, int H, int FF, int D, int KIND, typename TT>
+__global__ __launch_bounds__(256 * D) void dw_gemm_kernel(DwGemmArgs a) {
+  using Dm = DwDims<E, H, FF, D, TT>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  TT* const buf0 = reinterpret_cast<TT*>(smem);
+  TT* const buf1 = buf0 + Dm::GELEM;
+  TT* const wlds = buf1 + Dm::GELEM;  // [D][W1, W2ᵀ][FF][E]
+  {  // stage W1 / W2ᵀ of every block (made visible by dw_run's first barrier)
+    const TT* img = Dm::BF ? reinterpret_cast<const TT*>(a.pack + a.L.total) : reinterpret_cast<const TT*>(a.pack);
+    constexpr int PER = 16 / sizeof(TT), MAT = FF * E;
+    for (int q = threadIdx.x; q < D * 2 * MAT / PER; q += Dm::NT) {
+      const int e = q * PER, dd = e / (2 * MAT), m = (e / MAT) & 1, k = e % MAT;
+      const int64_t src = (m ? a.L.W2T[dd] : a.L.W1[dd]) + k;
+      *reinterpret_cast<u4v*>(wlds + e) = *reinterpret_cast<const u4v*>(img + src);
+    }
+  }
+  const int w = wave_id();
+  const int d = w >> 2, role = w & 3;
+  switch (role) {  // wave-uniform; the four paths issue the same barriers
+    case 0: dw_run<0, E, H, FF, D, TT>(a, buf0, buf1, wlds, d); break;
+    case 1: dw_run<1, E, H, FF, D, TT>(a, buf0, buf1, wlds, d); break;
+    case 2: dw_run<2, E, H, FF, D, TT>(a, buf0, buf1, wlds, d); break;
+    default: dw_run<3, E, H, FF, D, TT>(a, buf0, buf1, wlds, d); break;
+  }
+}
+
+template <int E, int H, int FF, int D, typename TT>
+int launch_dw_gemm(int kind, const void* tape, int64_t ntiles, const float* pack, float* slabs, const t2o_layout& L,
                    const t2o_layout& G, int nslab, hipStream_t stream) {
-  if (D < 1 || D > T2O_MAX_DEPTH || nslab < 1) return T2O_EINVAL;
+  if (nslab < 1) return T2O_EINVAL;
   DwGemmArgs a{};
   a.tape = tape;
   a.ntiles = ntiles;
-  a.chunk = ((ntiles + nslab - 1) / nslab + 1) / 2 * 2;
   a.slabs = slabs;
-  a.slab_stride = slab_stride;
+  a.slab_stride = G.grad_total;
+  a.pack = pack;
+  a.L = L;
   a.G = G;
-  a.D = D;
-  auto kern = kind == 0 ? dw_gemm_kernel<E, H, FF, 0, TT> : dw_gemm_kernel<E, H, FF, 1, TT>;
-  hipLaunchKernelGGL(kern, dim3(nslab), dim3(64 * 2 * D), 0, stream, a);
+  const size_t lds = sizeof(TT) * ((size_t)2 * D * DwTraits<TT>::TG * TapeRec<E, H, FF>::SIZE * 16 +
+                                    (size_t)D * 2 * FF * E);
+  auto kern = kind == 0 ? dw_gemm_kernel<E, H, FF, D, 0, TT> : dw_gemm_kernel<E, H, FF, D, 1, TT>;
+  if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, dim3(nslab), dim3(256 * D), lds, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -163,20 +407,20 @@ using namespace t2o;
 
 extern "C" int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t tiles) {
   if (!L || tiles < 0) return -1;
-  const int64_t elems = (int64_t)L->D * tiles * 16 * (4 * L->E + 2 * L->H * L->E + 2 * L->FF);
+  const int64_t elems = (int64_t)L->D * tiles * 16 * (4 * L->E + 2 * L->H * L->E);
   return L->prec ? (elems + 1) / 2 : elems;
 }
 
-extern "C" int t2o_bwd_tape_contract(const t2o_layout* L, const void* tape, int64_t tiles, float* gslabs,
-                                     int nslab, void* stream) {
-  if (!L || !tape || !gslabs || tiles < 0 || nslab < 1) return T2O_EINVAL;
+extern "C" int t2o_bwd_tape_contract(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
+                                     float* gslabs, int nslab, void* stream) {
+  if (!L || !pack || !tape || !gslabs || tiles < 0 || nslab < 1) return T2O_EINVAL;
   t2o_layout G;
   grad_layout(*L, G);
   int rc = T2O_EUNSUPPORTED;
   T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
-               rc = (L->prec ? launch_dw_gemm<E_, H_, FF_, __bf16>(L->kind, tape, tiles, L->D, gslabs, G.grad_total,
-                                                                  G, nslab, (hipStream_t)stream)
-                             : launch_dw_gemm<E_, H_, FF_, float>(L->kind, tape, tiles, L->D, gslabs, G.grad_total,
-                                                                 G, nslab, (hipStream_t)stream)));
+               rc = (L->prec ? launch_dw_gemm<E_, H_, FF_, D_, __bf16>(L->kind, tape, tiles, pack, gslabs, *L, G,
+                                                                       nslab, (hipStream_t)stream)
+                             : launch_dw_gemm<E_, H_, FF_, D_, float>(L->kind, tape, tiles, pack, gslabs, *L, G,
+                                                                      nslab, (hipStream_t)stream)));
   return rc;
 }

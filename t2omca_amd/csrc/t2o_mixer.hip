@@ -281,7 +281,7 @@ struct MixerBwdArgs {
   float* ghw0;        // [B][3][E] (may be null)
   const float* xmid;  // forward block inputs of blocks 1..D-1 [B][T][D-1][A+3][E] (may be null)
   float* slabs;
-  void* tape;         // [D][B*T*QT][TapeRec::SIZE][16] in the MFMA operand type
+  void* tape;         // [D][T][B][QT][TapeRec::SIZE][16] in the MFMA operand type
   int lds_w;          // floats of LDS taken by the weights
   int waves;          // episodes (waves) per workgroup: 4, 2 or 1, whatever fits in LDS
 };
@@ -432,7 +432,9 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
           for (int ft = 0; ft < ET; ++ft) x[ft] = xs[d][ft];
           mixer_block_fwd<E, H, KT, FF, Dm::LDX, true>(P, L, d, X0, Dm::LK, x, &cache);
           // one tile per (episode, step, query tile); padding rows carry zero gradients
-          WT* rec = static_cast<WT*>(args.tape) + ((size_t)d * ntiles + bt * Dm::QT + qt) * Rec::SIZE * 16;
+          // tiles are step-major (t, b, qt): at any step the grid writes one contiguous window
+          WT* rec = static_cast<WT*>(args.tape) +
+                    ((size_t)d * ntiles + ((size_t)t * fa.B + b) * Dm::QT + qt) * Rec::SIZE * 16;
           mixer_block_bwd<E, H, KT, FF, Dm::LDX>(P, L, G, gs, rec, stage, d, X0, gX0, cache, gx);
         }
 #pragma unroll

@@ -336,19 +336,39 @@ extern "C" int t2o_unpack_grads(const t2o_layout* L, const float* params, const 
 }
 
 namespace {
-__global__ void reduce_slabs_kernel(const float* __restrict__ slabs, int nslab, int64_t n, float* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int k = 0; k < nslab; ++k) s += slabs[(int64_t)k * n + i];
-    out[i] = s;
+// out[i] = Σ_k slabs[k][i].  A block covers 64 columns as 16 column quads x 16
+// slab lanes: each thread sums every 16th slab of its quad with 16-byte loads
+// (independent, so many are in flight), then the 16 partials of a quad are
+// combined through LDS in a fixed order (deterministic).
+constexpr int RS_QUADS = 16, RS_LANES = 16;
+__global__ __launch_bounds__(256) void reduce_slabs_kernel(const float* __restrict__ slabs, int nslab, int64_t n,
+                                                           float* __restrict__ out) {
+  __shared__ f4 part[RS_LANES][RS_QUADS];
+  const int qd = threadIdx.x % RS_QUADS, ln = threadIdx.x / RS_QUADS;
+  const int64_t col = ((int64_t)blockIdx.x * RS_QUADS + qd) * 4;
+  f4 s = f4{0.f, 0.f, 0.f, 0.f};
+  if (col + 3 < n && (n & 3) == 0) {
+#pragma unroll 4
+    for (int k = ln; k < nslab; k += RS_LANES) s += *reinterpret_cast<const f4*>(slabs + (int64_t)k * n + col);
+  } else {
+    for (int k = ln; k < nslab; k += RS_LANES)
+      for (int r = 0; r < 4; ++r)
+        if (col + r < n) s[r] += slabs[(int64_t)k * n + col + r];
+  }
+  part[ln][qd] = s;
+  __syncthreads();
+  if (ln == 0) {
+    f4 t = part[0][qd];
+    for (int l = 1; l < RS_LANES; ++l) t += part[l][qd];
+    for (int r = 0; r < 4; ++r)
+      if (col + r < n) out[col + r] = t[r];
   }
 }
 }  // namespace
 
 extern "C" int t2o_reduce_slabs(const float* slabs, int nslab, int64_t n, float* out, void* stream) {
   if (!slabs || !out || nslab < 1 || n < 1) return T2O_EINVAL;
-  int blocks = (int)((n + 255) / 256);
-  if (blocks > 2048) blocks = 2048;
+  const int64_t blocks = (n + 4 * RS_QUADS - 1) / (4 * RS_QUADS);
   hipLaunchKernelGGL(reduce_slabs_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slabs, nslab, n, out);
   return (int)hipGetLastError();
 }

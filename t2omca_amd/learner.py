@@ -49,7 +49,8 @@ def _bind_flat(modules, device):
 class TDLearner:
     def __init__(self, agent, mixer, *, lr=1e-3, gamma=0.99, td_lambda=0.6, grad_norm_clip=10.0,
                  target_update_interval=200, optim_betas=(0.9, 0.999), optim_eps=1e-8, weight_decay=0.0,
-                 detach_mixer_hidden=False, process_group=None, priorities_to_cpu=True, precision="fp32"):
+                 detach_mixer_hidden=False, process_group=None, priorities_to_cpu=True, precision="fp32",
+                 overlap=True):
         dev = next(agent.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("TDLearner needs the modules on a HIP device (no CPU fallback)")
@@ -80,6 +81,7 @@ class TDLearner:
         self.detach_mixer_hidden = detach_mixer_hidden
         self.pg = process_group
         self.priorities_to_cpu = priorities_to_cpu
+        self.overlap = overlap  # mixer tape contraction on a side stream beside the agent BPTT
         self.step_count = 0
         self.last_target_update_episode = 0
         self.timer = None   # optional callable(tag) recording HIP events around the big kernels
@@ -182,7 +184,7 @@ class TDLearner:
                                                         slabs=slabs_m, timer=self.timer, tape=tape_m,
                                                         defer_contract=True)
         main = torch.cuda.current_stream(dev)
-        side = self._side_stream()
+        side = self._side_stream() if self.overlap else main
         side.wait_stream(main)
         with torch.cuda.stream(side):
             gm = contract_m()

@@ -172,7 +172,7 @@ def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchose
                                      ctypes.byref(nslab), ptr(tape), ptr(gh0), B, T, A, stream_ptr()),
           "agent_unroll_bwd")
     _mark(timer, "end:agent_bwd")
-    return tape_contract(shape, tape, tiles, slabs, nslab.value, timer, "agent_dw"), gh0
+    return tape_contract(shape, pack, tape, tiles, slabs, nslab.value, timer, "agent_dw"), gh0
 
 
 def _mstrides(t):
@@ -233,12 +233,13 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
     return (o_on, o_tg) if pack_tg is not None else o_on
 
 
-def tape_contract(shape: NetShape, tape, tiles, slabs, nslab, timer=None, tag="dw"):
-    """Fill the M/N/W1/W2 regions of the backward's slabs from its tape, then sum
-    the slabs.  Returns the compact gradient block (on the current stream)."""
+def tape_contract(shape: NetShape, pack, tape, tiles, slabs, nslab, timer=None, tag="dw"):
+    """Fill the M/N/W1/W2 regions of the backward's slabs from its tape (pack =
+    the pack the backward used), then sum the slabs.  Returns the compact
+    gradient block (on the current stream)."""
     L = shape.layout()
     _mark(timer, "begin:" + tag)
-    check(lib().t2o_bwd_tape_contract(ctypes.byref(L), ptr(tape), int(tiles), ptr(slabs), int(nslab),
+    check(lib().t2o_bwd_tape_contract(ctypes.byref(L), ptr(pack), ptr(tape), int(tiles), ptr(slabs), int(nslab),
                                       stream_ptr()), "bwd_tape_contract")
     _mark(timer, "end:" + tag)
     gpack = torch.empty(L.grad_total, device=slabs.device)
@@ -275,7 +276,7 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
         ptr(fwd.get("xmid")), ptr(gy), ptr(ghw_ext), ptr(gqv), ptr(ghid), ptr(ghw0), ptr(slabs), nmax, ctypes.byref(nslab),
         ptr(tape), B, T, stream_ptr()), "mixer_unroll_bwd")
     _mark(timer, "end:mixer_bwd")
-    contract = lambda: tape_contract(shape, tape, tiles, slabs, nslab.value, timer, "mixer_dw")  # noqa: E731
+    contract = lambda: tape_contract(shape, pack, tape, tiles, slabs, nslab.value, timer, "mixer_dw")  # noqa: E731
     return (contract if defer_contract else contract()), gqv, ghid, ghw0
 
 
