@@ -64,70 +64,133 @@ struct MixDims {
   static constexpr int FWD_PERW = X0F + (QT == 1 ? 0 : OUTF);
 };
 
-T2O_DEV float wave_sum(float v) {
+// Σ over lanes 0..E-1 (lane = feature; other lanes must hold 0), wave-uniform:
+// DPP row sums put each 16-lane row's total in its lane 15, then scalar reads.
+template <int E>
+T2O_DEV float feat_sum(float v) {
+  v = rowsum16_fast(v);
+  float s = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 15));
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) v += __shfl_xor(v, o);
-  return v;
+  for (int r = 1; r < (E + 15) / 16; ++r) s += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16 * r + 15));
+  return s;
 }
 
 T2O_DEV float elu1(float x) { return x > 0.f ? x : expm1f(x); }
 
-// qvals of step t for all A agents (every lane computes the same values)
-template <int A>
-T2O_DEV void load_qv(const MixerFwdArgs& a, const MixerNet& n, int b, int t, float (&qv)[A]) {
-  const int NA = a.n_actions;
-#pragma unroll
-  for (int ag = 0; ag < A; ++ag) {
-    if (n.qmode == 0) {
-      qv[ag] = n.qv_in[((size_t)b * n.T + t) * A + ag];
-    } else {
-      const size_t qrow = (((size_t)b * a.q_ts + t) * A + ag) * NA;
-      int act;
-      if (n.qmode == 1) {
-        act = (int)a.actions[b * a.act_sb + t * a.act_st + ag];
-      } else {
-        float best = -INFINITY;
-        act = 0;
-        const int32_t* av = a.avail ? a.avail + b * a.av_sb + t * a.av_st + ag * NA : nullptr;
-        for (int k = 0; k < NA; ++k) {
-          const float v = (av && av[k] == 0) ? -9999999.0f : a.qarg[qrow + k];
-          if (v > best) { best = v; act = k; }
-        }
-      }
-      qv[ag] = n.qsel[qrow + act];
-    }
-  }
-}
+constexpr int MIX_MAXNA = 8;  // n_actions bound of the register-resident Q rows (launcher checks)
 
-// Build the key block X0 rows for step t: state-entity embeddings and agent
-// hidden tokens (the hyper-token rows are carried separately).
-template <int E, int A, typename WT>
-T2O_DEV void build_keys(const Wts<WT>& P, const t2o_layout& L, const MixerFwdArgs& a,
-                        const MixerNet& n, int b, int t, float* X0) {
+// Inputs of one (episode, step) that do not depend on the recurrence, loaded
+// a step AHEAD into registers so their HBM latency hides behind the current
+// step's compute:
+//   st   state features in the embedding's T-layout (row j = 16s + c,
+//        features 4g + r)
+//   hid  the agents' hidden tokens, f4 i = lane + 64k of the [A][E] block
+//   qs / qa / act   (lane a < A only) what the learner's Q selection needs:
+//        qmode 0 qs[0] = qvals; 1 qs = Q row, act = action;
+//        2 qs = target Q row, qa = online Q row masked by avail
+template <int E, int A>
+struct MixIn {
   using Dm = MixDims<E, A>;
-  constexpr int ET = E / 16;
+  static constexpr int HV = (A * E / 4 + 63) / 64;
+  f4 st[Dm::ST];
+  f4 hid[HV];
+  float qs[MIX_MAXNA], qa[MIX_MAXNA];
+  int act;
+};
+
+template <int E, int A>
+T2O_DEV void mix_load(const MixerFwdArgs& a, const MixerNet& n, int b, int t, MixIn<E, A>& in) {
+  using Dm = MixDims<E, A>;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
   const float* st = a.states + b * a.st_sb + t * a.st_st;
 #pragma unroll
   for (int s = 0; s < Dm::ST; ++s) {
     const int j = 16 * s + c;
-    f4 sv;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int f = 4 * g + r;
-      sv[r] = (j < Dm::NS && f < a.Fs) ? st[j * a.Fs + f] : 0.f;
+      in.st[s][r] = (j < Dm::NS && f < a.Fs) ? st[j * a.Fs + f] : 0.f;
     }
+  }
+  const float* hd = n.hid + b * n.hid_sb + t * n.hid_st;
+#pragma unroll
+  for (int k = 0; k < MixIn<E, A>::HV; ++k) {
+    const int i = lane + 64 * k;
+    in.hid[k] = i < A * E / 4 ? ld4(hd + 4 * i) : zero4();
+  }
+  if (lane < A) {
+    if (n.qmode == 0) {
+      in.qs[0] = n.qv_in[((size_t)b * n.T + t) * A + lane];
+    } else {
+      const int NA = a.n_actions;
+      const size_t qrow = (((size_t)b * a.q_ts + t) * A + lane) * NA;
+#pragma unroll
+      for (int k = 0; k < MIX_MAXNA; ++k) in.qs[k] = k < NA ? n.qsel[qrow + k] : 0.f;
+      if (n.qmode == 1) {
+        in.act = (int)a.actions[b * a.act_sb + t * a.act_st + lane];
+      } else {
+        const int32_t* av = a.avail ? a.avail + b * a.av_sb + t * a.av_st + lane * NA : nullptr;
+#pragma unroll
+        for (int k = 0; k < MIX_MAXNA; ++k) {
+          const float q = k < NA ? a.qarg[qrow + k] : -INFINITY;
+          in.qa[k] = (k < NA && av && av[k] == 0) ? -9999999.0f : q;
+        }
+      }
+    }
+  }
+}
+
+// This lane's agent's mixer input (lane a < A): chosen-action Q (qmode 1) or
+// the target Q at the avail-masked online argmax (qmode 2, first max wins).
+template <int E, int A>
+T2O_DEV float mix_qv(const MixerNet& n, const MixIn<E, A>& in) {
+  if (n.qmode == 0) return in.qs[0];
+  int act = 0;
+  if (n.qmode == 1) {
+    act = in.act;
+  } else {
+    float best = in.qa[0];
+#pragma unroll
+    for (int k = 1; k < MIX_MAXNA; ++k)
+      if (in.qa[k] > best) {
+        best = in.qa[k];
+        act = k;
+      }
+  }
+  float v = in.qs[0];
+#pragma unroll
+  for (int k = 1; k < MIX_MAXNA; ++k) v = act == k ? in.qs[k] : v;
+  return v;
+}
+
+// every lane gets all A agents' values (lane a holds agent a's): scalar broadcast
+template <int A>
+T2O_DEV void bcast_agents(float mine, float (&qv)[A]) {
+#pragma unroll
+  for (int ag = 0; ag < A; ++ag) qv[ag] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(mine), ag));
+}
+
+// Key block X0 rows for one step from the prefetched inputs: state-entity
+// embeddings and agent hidden tokens (the hyper-token rows are carried in X0).
+template <int E, int A, typename WT>
+T2O_DEV void mix_keys(const Wts<WT>& P, const t2o_layout& L, const MixIn<E, A>& in, float* X0) {
+  using Dm = MixDims<E, A>;
+  constexpr int ET = E / 16;
+  const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
+#pragma unroll
+  for (int s = 0; s < Dm::ST; ++s) {
+    const int j = 16 * s + c;
     f4 emb[ET];
-    matvec<ET, 1>(P.w + L.We, 16, &sv, emb);
+    matvec<ET, 1>(P.w + L.We, 16, &in.st[s], emb);
     if (j < Dm::NS) {
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) st4(X0 + j * Dm::LDX + 16 * ft + 4 * g, emb[ft] + vec_t(P.v + L.be, ft));
     }
   }
-  const float* hd = n.hid + b * n.hid_sb + t * n.hid_st;
-  for (int i = lane; i < A * E / 4; i += 64) {
-    const int ag = (4 * i) / E, f = (4 * i) % E;
-    st4(X0 + (Dm::NS + ag) * Dm::LDX + f, ld4(hd + 4 * i));
+#pragma unroll
+  for (int k = 0; k < MixIn<E, A>::HV; ++k) {
+    const int i = lane + 64 * k;
+    if (i < A * E / 4) st4(X0 + (Dm::NS + (4 * i) / E) * Dm::LDX + (4 * i) % E, in.hid[k]);
   }
 }
 
@@ -145,8 +208,8 @@ T2O_DEV float mixer_head(const Wts<WT>& P, const t2o_layout& L, const float* OUT
   pre_h = ph;
   const float hidden = elu1(ph);
   const float w2 = fabsf(OUT[(A + 1) * E + fc]);
-  const float yv = wave_sum(fv ? hidden * w2 : 0.f);
-  const float p2 = wave_sum(fv ? P.s(L.Wo + fc) * OUT[(A + 2) * E + fc] : 0.f) + P.v[L.bo];
+  const float yv = feat_sum<E>(fv ? hidden * w2 : 0.f);
+  const float p2 = feat_sum<E>(fv ? P.s(L.Wo + fc) * OUT[(A + 2) * E + fc] : 0.f) + P.v[L.bo];
   pre2 = p2;
   return yv + fmaxf(p2, 0.f);
 }
@@ -178,10 +241,16 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
     const int k = i / E, f = i % E;
     X0[(Dm::NS + A + k) * Dm::LDX + f] = n.hw0 ? n.hw0[(size_t)b * 3 * E + i] : 0.f;
   }
+  MixIn<E, A> in;
+  mix_load<E, A>(args, n, b, 0, in);
   for (int t = 0; t < n.T; ++t) {
     const Wts<WT> P = step_view(P0);
-    build_keys<E, A>(P, L, args, n, b, t, X0);
+    mix_keys<E, A>(P, L, in, X0);
+    const float myq = mix_qv<E, A>(n, in);
+    if (t + 1 < n.T) mix_load<E, A>(args, n, b, t + 1, in);  // prefetch step t+1 (in is consumed)
     __builtin_amdgcn_wave_barrier();
+    KeyFrags<E, Dm::KT, sizeof(WT) == 2> K;
+    K.template load<Dm::LDX>(X0);
 #pragma unroll
     for (int qt = 0; qt < Dm::QT; ++qt) {
       const int q = 16 * qt + c;
@@ -189,6 +258,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft)
         x[ft] = q < Dm::Q ? ld4(X0 + (Dm::NS + q) * Dm::LDX + 16 * ft + 4 * g) : zero4();
+      __builtin_amdgcn_wave_barrier();  // every X0 read done before OUT (may alias X0) is written
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         if (d > 0 && n.xmid && q < Dm::Q) {
@@ -196,23 +266,19 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft) st4(xm + 16 * ft + 4 * g, x[ft]);
         }
-        mixer_block_fwd<E, H, Dm::KT, FF, Dm::LDX, false>(P, L, d, X0, Dm::LK, x, nullptr);
+        mixer_block_fwd<E, H, Dm::KT, FF, false>(P, L, d, K, Dm::LK, x, nullptr);
       }
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) st4(OUT + q * E + 16 * ft + 4 * g, x[ft]);
     }
     __builtin_amdgcn_wave_barrier();
     float qv[A];
-    load_qv<A>(args, n, b, t, qv);
+    bcast_agents<A>(myq, qv);
     float pre_h, pre2;
     const float y = mixer_head<E, A>(P, L, OUT, qv, pre_h, pre2);
     const size_t bt = (size_t)b * n.T + t;
     if (lane == 0) n.y[bt] = y;
-    if (n.qv && lane < A) {
-#pragma unroll
-      for (int ag = 0; ag < A; ++ag)
-        if (lane == ag) n.qv[bt * A + ag] = qv[ag];
-    }
+    if (n.qv && lane < A) n.qv[bt * A + lane] = myq;
     float hv[(3 * E + 63) / 64];
 #pragma unroll
     for (int k = 0; k < (3 * E + 63) / 64; ++k) {
@@ -287,6 +353,70 @@ struct MixerBwdArgs {
 };
 
 
+// The backward's per-step inputs (all forward outputs or replay data, none
+// recurrent), prefetched one step ahead like MixIn.
+template <int E, int A, int D>
+struct MixBwdIn {
+  using Dm = MixDims<E, A>;
+  static constexpr int ET = E / 16;
+  static constexpr int HW = (3 * E + 63) / 64;
+  static constexpr int XO = (Dm::Q * E + 63) / 64;
+  MixIn<E, A> m;
+  float hwp[HW];  // X0 hyper rows: hyper outputs of step t-1 (hw0 / zeros at t = 0)
+  float xo[XO];   // forward final query rows of step t
+  float ghx[3];   // ghw_ext of step t, lane = feature
+  float gy;       // dL/dy of step t
+  f4 xm[Dm::QT][D > 1 ? D - 1 : 1][ET];  // stored inputs of blocks 1..D-1 (T-layout query rows)
+  f4 stT[Dm::ST];  // lane (g, c) reg r: state feature c of entity 16s + 4g + r; column Fs = 1 (bias)
+};
+
+template <int E, int A, int D>
+T2O_DEV void mixb_load(const MixerBwdArgs& args, const MixerNet& n, int b, int t, MixBwdIn<E, A, D>& in) {
+  using Dm = MixDims<E, A>;
+  using In = MixBwdIn<E, A, D>;
+  const MixerFwdArgs& fa = args.f;
+  const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
+  mix_load<E, A>(fa, n, b, t, in.m);
+  const size_t bt = (size_t)b * n.T + t;
+#pragma unroll
+  for (int k = 0; k < In::HW; ++k) {
+    const int i = lane + 64 * k;
+    float v = 0.f;
+    if (i < 3 * E) v = t > 0 ? args.hw[(bt - 1) * 3 * E + i] : (n.hw0 ? n.hw0[(size_t)b * 3 * E + i] : 0.f);
+    in.hwp[k] = v;
+  }
+#pragma unroll
+  for (int k = 0; k < In::XO; ++k) {
+    const int i = lane + 64 * k;
+    in.xo[k] = i < Dm::Q * E ? args.xout[bt * Dm::Q * E + i] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) in.ghx[k] = (args.ghw_ext && lane < E) ? args.ghw_ext[(bt * 3 + k) * E + lane] : 0.f;
+  in.gy = args.gy[bt];
+  if (D > 1 && args.xmid) {
+#pragma unroll
+    for (int qt = 0; qt < Dm::QT; ++qt) {
+      const int q = 16 * qt + c;
+#pragma unroll
+      for (int d = 1; d < D; ++d)
+#pragma unroll
+        for (int ft = 0; ft < In::ET; ++ft)
+          in.xm[qt][d - 1][ft] =
+              q < Dm::Q ? ld4(args.xmid + ((bt * (D - 1) + d - 1) * Dm::Q + q) * E + 16 * ft + 4 * g) : zero4();
+    }
+  }
+  const float* st = fa.states + b * fa.st_sb + t * fa.st_st;
+#pragma unroll
+  for (int s = 0; s < Dm::ST; ++s)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * s + 4 * g + r;
+      float v = 0.f;
+      if (j < Dm::NS) v = c < fa.Fs ? st[j * fa.Fs + c] : (c == fa.Fs ? 1.f : 0.f);
+      in.stT[s][r] = v;
+    }
+}
+
 template <int E, int A>
 struct MixBwdDims {
   using Dm = MixDims<E, A>;
@@ -331,45 +461,54 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
     float ghw[3] = {0.f, 0.f, 0.f};  // grad wrt this step's hyper outputs, lane = feature
     const int f = lane < E ? lane : 0;
     const bool fv = lane < E;
-    // register-resident grads, lane = feature f: state embedding We[f][0..16), be[f], hyper_b2
-    float gWe[16], gbe = 0.f, gWo = 0.f, gbo = 0.f;
+    // state embedding grads as MFMA tiles: lane (g, c) reg r = dWe[16ft+4g+r][c]
+    // (column Fs = d be); hyper_b2 grads per lane (feature)
+    f4 gWe[ET];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) gWe[k] = 0.f;
+    for (int ft = 0; ft < ET; ++ft) gWe[ft] = zero4();
+    float gWo = 0.f, gbo = 0.f;
+    MixBwdIn<E, A, D> cur, nxt;
+    mixb_load<E, A, D>(args, n, b, n.T - 1, cur);
     for (int t = n.T - 1; t >= 0; --t) {
       const Wts<WT> P = step_view(P0);
       const size_t bt = (size_t)b * n.T + t;
-      build_keys<E, A>(P, L, fa, n, b, t, X0);
-      for (int i = lane; i < 3 * E; i += 64) {
-        const int k = i / E, ff = i % E;
-        const float v = t > 0 ? args.hw[(bt - 1) * 3 * E + i] : (n.hw0 ? n.hw0[(size_t)b * 3 * E + i] : 0.f);
-        X0[(Dm::NS + A + k) * Dm::LDX + ff] = v;
+      mix_keys<E, A>(P, L, cur.m, X0);
+#pragma unroll
+      for (int k = 0; k < MixBwdIn<E, A, D>::HW; ++k) {
+        const int i = lane + 64 * k;
+        if (i < 3 * E) X0[(Dm::NS + A + i / E) * Dm::LDX + i % E] = cur.hwp[k];
       }
       float* OUT = stage;  // forward final query rows
-      for (int i = lane; i < Dm::Q * E; i += 64) OUT[i] = args.xout[bt * Dm::Q * E + i];
+#pragma unroll
+      for (int k = 0; k < MixBwdIn<E, A, D>::XO; ++k) {
+        const int i = lane + 64 * k;
+        if (i < Dm::Q * E) OUT[i] = cur.xo[k];
+      }
+      if (t > 0) mixb_load<E, A, D>(args, n, b, t - 1, nxt);  // prefetch step t-1
       __builtin_amdgcn_wave_barrier();
       // ---- mixing head backward (lanes = features)
       float qv[A];
-      load_qv<A>(fa, n, b, t, qv);
+      bcast_agents<A>(cur.m.qs[0], qv);
       float pre_h, pre2;
       (void)mixer_head<E, A>(P, L, OUT, qv, pre_h, pre2);
-      const float gyv = args.gy[bt];
+      const float gyv = cur.gy;
       const float hidden = elu1(pre_h);
       const float xw2 = OUT[(A + 1) * E + f];
       const float sgn_w2 = (xw2 > 0.f) - (xw2 < 0.f);
       const float gpre = gyv * fabsf(xw2) * (pre_h > 0.f ? 1.f : expf(pre_h));
       const float gpre2 = pre2 > 0.f ? gyv : 0.f;
       float gout[A + 3];
+      float gqm = 0.f;  // lane a < A: dL/dqvals[a]
 #pragma unroll
       for (int ag = 0; ag < A; ++ag) {
         const float xa = OUT[ag * E + f];
         gout[ag] = qv[ag] * gpre * ((xa > 0.f) - (xa < 0.f));
-        const float gq = wave_sum(fv ? gpre * fabsf(xa) : 0.f);
-        if (lane == 0) args.gqv[bt * A + ag] = gq;
+        const float gq = feat_sum<E>(fv ? gpre * fabsf(xa) : 0.f);
+        gqm = lane == ag ? gq : gqm;
       }
-      if (args.ghw_ext) {
+      if (lane < A) args.gqv[bt * A + lane] = gqm;
 #pragma unroll
-        for (int k = 0; k < 3; ++k) ghw[k] += args.ghw_ext[(bt * 3 + k) * E + f];
-      }
+      for (int k = 0; k < 3; ++k) ghw[k] += cur.ghx[k];
       gout[A] = gpre + ghw[0];
       gout[A + 1] = gyv * hidden * sgn_w2 + ghw[1];
       const float x2 = OUT[(A + 2) * E + f];
@@ -385,6 +524,8 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
       for (int i = Dm::Q * E + lane; i < Dm::OUTF; i += 64) GOUT[i] = 0.f;
       __builtin_amdgcn_wave_barrier();
       // ---- blocks backward per query tile; gX0 accumulates in registers
+      KeyFrags<E, KT, sizeof(WT) == 2> K;
+      K.template load<Dm::LDX>(X0);
       f4 gX0[KT][ET];
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
@@ -410,16 +551,14 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
           for (int d = 1; d < D; ++d)
 #pragma unroll
-            for (int ft = 0; ft < ET; ++ft)
-              xs[d][ft] = q < Dm::Q ? ld4(args.xmid + ((bt * (D - 1) + d - 1) * Dm::Q + q) * E + 16 * ft + 4 * g)
-                                    : zero4();
+            for (int ft = 0; ft < ET; ++ft) xs[d][ft] = cur.xm[qt][d - 1][ft];
         } else {
 #pragma unroll
           for (int d = 0; d + 1 < D; ++d) {
             f4 x[ET];
 #pragma unroll
             for (int ft = 0; ft < ET; ++ft) x[ft] = xs[d][ft];
-            mixer_block_fwd<E, H, KT, FF, Dm::LDX, false>(P, L, d, X0, Dm::LK, x, nullptr);
+            mixer_block_fwd<E, H, KT, FF, false>(P, L, d, K, Dm::LK, x, nullptr);
 #pragma unroll
             for (int ft = 0; ft < ET; ++ft) xs[d + 1][ft] = x[ft];
           }
@@ -430,16 +569,32 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
           f4 x[ET];
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft) x[ft] = xs[d][ft];
-          mixer_block_fwd<E, H, KT, FF, Dm::LDX, true>(P, L, d, X0, Dm::LK, x, &cache);
+          mixer_block_fwd<E, H, KT, FF, true>(P, L, d, K, Dm::LK, x, &cache);
           // one tile per (episode, step, query tile); padding rows carry zero gradients
           // tiles are step-major (t, b, qt): at any step the grid writes one contiguous window
           WT* rec = static_cast<WT*>(args.tape) +
                     ((size_t)d * ntiles + ((size_t)t * fa.B + b) * Dm::QT + qt) * Rec::SIZE * 16;
-          mixer_block_bwd<E, H, KT, FF, Dm::LDX>(P, L, G, gs, rec, stage, d, X0, gX0, cache, gx);
+          mixer_block_bwd<E, H, KT, FF>(P, L, G, gs, rec, stage, d, K, gX0, cache, gx);
         }
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft) gq0[qt][ft] = q < Dm::Q ? gx[ft] : zero4();
       }
+      // ---- state embedding grads straight from the key-grad registers:
+      // dWe[f][fs] (+ d be[f] in column Fs) += Σ_{entity j} gX0[j][f] · [s_j, 1][fs]
+#pragma unroll
+      for (int s = 0; s < Dm::ST; ++s)
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft) {
+          f4 am;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) am[r] = 16 * s + 4 * g + r < Dm::NS ? gX0[s][ft][r] : 0.f;
+          if constexpr (sizeof(WT) == 2) {
+            gWe[ft] = mfma_b16(to_bf4(am), to_bf4(cur.stT[s]), gWe[ft]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) gWe[ft] = mfma4(am[r], cur.stT[s][r], gWe[ft]);
+          }
+        }
       __builtin_amdgcn_wave_barrier();
       // ---- gX0 registers -> LDS rows [key][feature], plus the query path
       float* GX0 = stage;
@@ -462,36 +617,26 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
         }
       }
       __builtin_amdgcn_wave_barrier();
-      // ---- key-token grads: agent hidden tokens out, hyper tokens carried,
-      // state embeddings -> We / be
-      for (int i = lane; i < A * E; i += 64) args.ghid[bt * A * E + i] = GX0[(Dm::NS) * E + i];
-      if (fv) {
+      // ---- key-token grads: agent hidden tokens out, hyper tokens carried
+      for (int i = lane; i < A * E / 4; i += 64) st4(args.ghid + bt * A * E + 4 * i, ld4(GX0 + Dm::NS * E + 4 * i));
 #pragma unroll
-        for (int k = 0; k < 3; ++k) ghw[k] = GX0[(Dm::NS + A + k) * E + f];
-        const float* st = fa.states + b * fa.st_sb + t * fa.st_st;
-#pragma unroll
-        for (int fs = 0; fs < 16; ++fs) {
-          if (fs < fa.Fs) {
-            float acc = 0.f;
-            for (int j = 0; j < Dm::NS; ++j) acc += GX0[j * E + f] * st[j * fa.Fs + fs];
-            gWe[fs] += acc;
-          }
-        }
-        for (int j = 0; j < Dm::NS; ++j) gbe += GX0[j * E + f];
-      }
+      for (int k = 0; k < 3; ++k) ghw[k] = fv ? GX0[(Dm::NS + A + k) * E + f] : 0.f;
       __builtin_amdgcn_wave_barrier();
+      cur = nxt;
     }
     if (args.ghw0 && fv) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) args.ghw0[((size_t)b * 3 + k) * E + f] = ghw[k];
     }
-    if (fv) {
 #pragma unroll
-      for (int fs = 0; fs < 16; ++fs)
-        if (fs < fa.Fs) unsafeAtomicAdd(gs + G.We + f * 16 + fs, gWe[fs]);
-      unsafeAtomicAdd(gs + G.be + f, gbe);
-      unsafeAtomicAdd(gs + G.Wo + f, gWo);
-    }
+    for (int ft = 0; ft < ET; ++ft)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int fe = 16 * ft + 4 * g + r;
+        if (c < fa.Fs) unsafeAtomicAdd(gs + G.We + fe * 16 + c, gWe[ft][r]);
+        else if (c == fa.Fs) unsafeAtomicAdd(gs + G.be + fe, gWe[ft][r]);
+      }
+    if (fv) unsafeAtomicAdd(gs + G.Wo + f, gWo);
     if (lane == 0) unsafeAtomicAdd(gs + G.bo, gbo);
   }
 }
@@ -554,6 +699,8 @@ extern "C" int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, c
     return false;
   };
   if (!check_mode(qmode_on, qv_on, q_on)) return T2O_EINVAL;
+  if ((qmode_on != 0 || (pack_tg && qmode_tg != 0)) && (n_actions < 1 || n_actions > MIX_MAXNA))
+    return T2O_EUNSUPPORTED;
   a.net[0] = MixerNet{pack_on, hw0_on, hid_on, hid_sb, hid_st, q_on, qv_on, qmode_on, T_on,
                       y_on, hw_on, qvo_on, xout_on, xmid_on};
   int nnet = 1;

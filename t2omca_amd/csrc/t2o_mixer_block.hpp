@@ -6,12 +6,15 @@
 // are read out (w1, b1, w2, b2 — n_transf_mixer.py:75-85), and keys never
 // change across blocks (transformer.py:140), so only those A+3 query rows are
 // propagated.  A wave owns ONE episode: queries sit on the MFMA N axis (lanes),
-// the key block X0 [keys x E] is wave-private LDS, and per head
+// the key block X0 [keys x E] is built in wave-private LDS once per step and
+// held in registers as MFMA fragments (KeyFrags), and per head
 //   Sᵀ = X0 · u_h        (u_h = M_h x, scores for all keys of all queries)
 //   Zᵀ = X0ᵀ · softmax(S)ᵀ
 // are two MFMA products whose outputs are already in the T-layout the next
 // step consumes (keys on the register axis for S, features for Z).
 #pragma once
+#include <type_traits>
+
 #include "t2o_block.hpp"
 
 namespace t2o {
@@ -24,24 +27,53 @@ struct MixerCache {
   f4 p[H][KT];
 };
 
+// The key block X0 of one (episode, step) as MFMA A-operand fragments, read
+// from the wave's LDS copy once per step and reused by every head of every
+// block (and by the backward's products):
+//   dot[kt][ft]  = X0[key 16kt + c][features 16ft + 4g .. +3]   (Sᵀ = X0 · v)
+//   comb[kt][ft] = X0[keys 16kt + 4g .. +3][feature 16ft + c]    (Zᵀ = X0ᵀ · w)
+// bf16 mode holds them as bf16 (4 VGPRs per 16x16 tile pair), fp32 as f32.
+template <int E, int KT, bool BF>
+struct KeyFrags {
+  static constexpr int ET = E / 16;
+  using Frag = typename std::conditional<BF, bf4, f4>::type;
+  Frag dot[KT][ET], comb[KT][ET];
+  template <int LDX>
+  T2O_DEV void load(const float* __restrict__ X0) {
+    const int c = lane_c(), g = lane_g();
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft) {
+        const f4 a = ld4(X0 + (16 * kt + c) * LDX + 16 * ft + 4 * g);
+        f4 b;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) b[s] = X0[(16 * kt + 4 * g + s) * LDX + 16 * ft + c];
+        if constexpr (BF) {
+          dot[kt][ft] = to_bf4(a);
+          comb[kt][ft] = to_bf4(b);
+        } else {
+          dot[kt][ft] = a;
+          comb[kt][ft] = b;
+        }
+      }
+  }
+};
+
 // Sᵀ-style product: out[kt] (keys 16kt+4g+r, query c) = Σ_f X0[key][f] v[f]
-template <int E, int KT, int LDX, bool BF>
-T2O_DEV void keys_dot(const float* __restrict__ X0, const f4* v, f4* out) {
+template <int E, int KT, bool BF>
+T2O_DEV void keys_dot(const KeyFrags<E, KT, BF>& K, const f4* v, f4* out) {
   constexpr int ET = E / 16;
-  const int c = lane_c(), g = lane_g();
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt) {
     f4 acc = zero4();
 #pragma unroll
     for (int ft = 0; ft < ET; ++ft) {
-      const f4 a = ld4(X0 + (16 * kt + c) * LDX + 16 * ft + 4 * g);
       if constexpr (BF) {
-        acc = mfma_b16(to_bf4(a), to_bf4(v[ft]), acc);
+        acc = mfma_b16(K.dot[kt][ft], to_bf4(v[ft]), acc);
       } else {
-        acc = mfma4(a[0], v[ft][0], acc);
-        acc = mfma4(a[1], v[ft][1], acc);
-        acc = mfma4(a[2], v[ft][2], acc);
-        acc = mfma4(a[3], v[ft][3], acc);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc = mfma4(K.dot[kt][ft][s], v[ft][s], acc);
       }
     }
     out[kt] = acc;
@@ -49,32 +81,29 @@ T2O_DEV void keys_dot(const float* __restrict__ X0, const f4* v, f4* out) {
 }
 
 // Zᵀ-style product: out[ft] (features 16ft+4g+r, query c) = Σ_key X0[key][f] w[key]
-template <int E, int KT, int LDX, bool BF>
-T2O_DEV void keys_combine(const float* __restrict__ X0, const f4* w, f4* out) {
+template <int E, int KT, bool BF>
+T2O_DEV void keys_combine(const KeyFrags<E, KT, BF>& K, const f4* w, f4* out) {
   constexpr int ET = E / 16;
-  const int c = lane_c(), g = lane_g();
 #pragma unroll
   for (int ft = 0; ft < ET; ++ft) {
     f4 acc = zero4();
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) {
       if constexpr (BF) {
-        f4 a;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) a[s] = X0[(16 * kt + 4 * g + s) * LDX + 16 * ft + c];
-        acc = mfma_b16(to_bf4(a), to_bf4(w[kt]), acc);
+        acc = mfma_b16(K.comb[kt][ft], to_bf4(w[kt]), acc);
       } else {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc = mfma4(X0[(16 * kt + 4 * g + s) * LDX + 16 * ft + c], w[kt][s], acc);
+        for (int s = 0; s < 4; ++s) acc = mfma4(K.comb[kt][ft][s], w[kt][s], acc);
       }
     }
     out[ft] = acc;
   }
 }
 
-template <int E, int H, int KT, int FF, int LDX, bool CACHE, typename WT>
+template <int E, int H, int KT, int FF, bool CACHE, typename WT>
 T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
-                             const float* __restrict__ X0, int Lk, f4* x, MixerCache<E, H, KT, FF>* cache) {
+                             const KeyFrags<E, KT, sizeof(WT) == 2>& K, int Lk, f4* x,
+                             MixerCache<E, H, KT, FF>* cache) {
   constexpr int ET = E / 16, HET = H * ET;
   constexpr bool BF = sizeof(WT) == 2;
   const int g = lane_g();
@@ -84,7 +113,7 @@ T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
     f4 s[KT];
-    keys_dot<E, KT, LDX, BF>(X0, &u[hh * ET], s);
+    keys_dot<E, KT, BF>(K, &u[hh * ET], s);
     float m = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt)
@@ -105,7 +134,7 @@ T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
     const float il = 1.0f / allsum4(l);
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) s[kt] *= il;
-    keys_combine<E, KT, LDX, BF>(X0, s, &z[hh * ET]);
+    keys_combine<E, KT, BF>(K, s, &z[hh * ET]);
     if constexpr (CACHE) {
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt) cache->p[hh][kt] = s[kt];
@@ -123,10 +152,10 @@ T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
 // holds gX0[key 16kt+4g+r][feature 16ft+c] — accumulates the grad wrt the key
 // tokens (a contraction over queries = rows, via the staging transposes).
 // Big-matrix operand pairs go to the query row's tape record (null = padding).
-template <int E, int H, int KT, int FF, int LDX, typename WT>
+template <int E, int H, int KT, int FF, typename WT>
 T2O_DEV void mixer_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G,
                              float* __restrict__ gs, WT* __restrict__ rec, float* __restrict__ stage, int d,
-                             const float* __restrict__ X0, f4 (&gX0)[KT][E / 16],
+                             const KeyFrags<E, KT, sizeof(WT) == 2>& K, f4 (&gX0)[KT][E / 16],
                              const MixerCache<E, H, KT, FF>& c, f4* gx) {
   constexpr int ET = E / 16, HET = H * ET;
   constexpr bool BF = sizeof(WT) == 2;
@@ -136,7 +165,7 @@ T2O_DEV void mixer_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_la
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
     f4 gp[KT];
-    keys_dot<E, KT, LDX, BF>(X0, &gz[hh * ET], gp);
+    keys_dot<E, KT, BF>(K, &gz[hh * ET], gp);
     float dot = 0.f;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt)
@@ -146,7 +175,7 @@ T2O_DEV void mixer_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_la
     f4 gsc[KT];
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) gsc[kt] = c.p[hh][kt] * (gp[kt] - dot);
-    keys_combine<E, KT, LDX, BF>(X0, gsc, &gu[hh * ET]);
+    keys_combine<E, KT, BF>(K, gsc, &gu[hh * ET]);
     dw_accumulate_regs<KT, ET, BF>(gX0, c.p[hh], &gz[hh * ET], stage);
     dw_accumulate_regs<KT, ET, BF>(gX0, gsc, &c.u[hh * ET], stage);
   }

@@ -16,7 +16,7 @@ NAMES = ["agent_fwd_kernel", "mixer_fwd_kernel", "mixer_bwd_kernel", "agent_bwd_
 
 
 def short(name):
-    m = re.search(r"dw_gemm_kernel(?:<\d+, *\d+, *\d+, *|ILi\d+ELi\d+ELi\d+ELi)(\d)", name)
+    m = re.search(r"dw_gemm_kernel(?:<\d+, *\d+, *\d+, *\d+, *|ILi\d+ELi\d+ELi\d+ELi\d+ELi)(\d)", name)
     if m:
         return ("agent_dw", "mixer_dw")[int(m.group(1))]
     for n in NAMES:

@@ -26,7 +26,7 @@ def per_kernel(d, counter):
                 if row.get("Counter_Name") != counter:
                     continue
                 name = row["Kernel_Name"]
-                m = re.search(r"dw_gemm_kernel(?:<\d+, *\d+, *\d+, *|ILi\d+ELi\d+ELi\d+ELi)(\d)", name)
+                m = re.search(r"dw_gemm_kernel(?:<\d+, *\d+, *\d+, *\d+, *|ILi\d+ELi\d+ELi\d+ELi\d+ELi)(\d)", name)
                 short = ("agent_dw", "mixer_dw")[int(m.group(1))] if m else \
                     next((v for k, v in SHORT.items() if k in name), None)
                 if short is None:
