@@ -68,10 +68,9 @@ __global__ __launch_bounds__(64 * AG_FWD_WAVES) void agent_fwd_kernel(AgentFwdAr
 #pragma unroll
   for (int t = 0; t < ET; ++t) h[t] = net.h0 ? ld4(net.h0 + (size_t)row * E + 16 * t + 4 * g) : zero4();
 
-  for (int step = 0; step < args.T; ++step) {
-    const Wts<WT> P = step_view(P0);
+  // observations of the next step are loaded while the current one computes
+  auto load_obs = [&](int step, f4 (&o)[NE]) {
     const float* ob = args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * NE * F;
-    f4 o[NE];
 #pragma unroll
     for (int j = 0; j < NE; ++j)
 #pragma unroll
@@ -79,6 +78,15 @@ __global__ __launch_bounds__(64 * AG_FWD_WAVES) void agent_fwd_kernel(AgentFwdAr
         const int f = 4 * g + r;
         o[j][r] = f < F ? ob[j * F + f] : 0.f;
       }
+  };
+  f4 on[NE];
+  load_obs(0, on);
+  for (int step = 0; step < args.T; ++step) {
+    const Wts<WT> P = step_view(P0);
+    f4 o[NE];
+#pragma unroll
+    for (int j = 0; j < NE; ++j) o[j] = on[j];
+    if (step + 1 < args.T) load_obs(step + 1, on);
     f4 x[ET];
 #pragma unroll
     for (int t = 0; t < ET; ++t) x[t] = h[t];

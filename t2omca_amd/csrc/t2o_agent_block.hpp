@@ -66,7 +66,7 @@ T2O_DEV void agent_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const
     float l = 0.f;
 #pragma unroll
     for (int j = 0; j <= NE; ++j) {
-      p[j] = expf(p[j] - m);
+      p[j] = exp_fast(p[j] - m);
       l += p[j];
     }
     const float il = 1.0f / l;

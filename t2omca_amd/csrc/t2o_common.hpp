@@ -44,6 +44,11 @@ T2O_DEV f4 mfma4(float a, float b, f4 acc) {
 }
 
 T2O_DEV f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+
+// e^x for softmax arguments (x <= 0, -inf allowed): one v_exp_f32 (2^y, ~1 ulp)
+// of y = x·log2(e) instead of libm expf's range-reduced ~10-instruction expansion.
+// Relative error ≈ |x|·2^-24 + 1 ulp, far inside the fp32 parity bar.
+T2O_DEV float exp_fast(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
 T2O_DEV void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
 
 // acc += W[16o.. , 16i..] (16x16 tile of row-major W, leading dim ldw) · x_tile

@@ -128,7 +128,7 @@ T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
     for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        s[kt][r] = expf(s[kt][r] - m);
+        s[kt][r] = exp_fast(s[kt][r] - m);
         l += s[kt][r];
       }
     const float il = 1.0f / allsum4(l);
