@@ -73,13 +73,15 @@ _lib = None
 
 
 def lib():
-    """Load libt2omca.so (raises if it has not been built)."""
+    """Load libt2omca.so (raises if it has not been built).  T2O_LIB overrides the
+    path (A/B timing of two builds on one box)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB):
-            raise RuntimeError(f"t2omca_amd: {LIB} not built; run `python -m t2omca_amd.build` "
+        path = os.environ.get("T2O_LIB", LIB)
+        if not os.path.exists(path):
+            raise RuntimeError(f"t2omca_amd: {path} not built; run `python -m t2omca_amd.build` "
                                "(there is no CPU fallback)")
-        h = ctypes.CDLL(LIB)
+        h = ctypes.CDLL(path)
         for name, (res, args) in EXPORTS.items():
             fn = getattr(h, name)
             fn.restype = res

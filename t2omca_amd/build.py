@@ -31,12 +31,14 @@ def _stale():
     return any(os.path.getmtime(p) > t for p in deps)
 
 
-def build(force=False, verbose=False, jobs=None):
-    """Compile each translation unit to an object in parallel, then link the .so."""
-    if not force and not _stale():
+def build(force=False, verbose=False, jobs=None, out=None):
+    """Compile each translation unit to an object in parallel, then link the .so
+    (to `out` instead of the package library when given)."""
+    if out is None and not force and not _stale():
         return LIB
+    target = out or LIB
     os.makedirs(LIBDIR, exist_ok=True)
-    objdir = os.path.join(LIBDIR, "obj")
+    objdir = os.path.join(LIBDIR, "obj" if out is None else "obj_" + os.path.basename(out))
     os.makedirs(objdir, exist_ok=True)
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"]
@@ -58,15 +60,16 @@ def build(force=False, verbose=False, jobs=None):
             sys.stderr.write(out)
     if failed:
         raise RuntimeError("hipcc failed building libt2omca.so")
-    tmp = LIB + ".tmp"
+    tmp = target + ".tmp"
     r = subprocess.run([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs,
                        capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError("hipcc failed linking libt2omca.so")
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, target)
+    return target
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    out = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--out=")), None)
+    print(build(force="--force" in sys.argv, verbose=True, out=out))

@@ -69,7 +69,7 @@ T2O_DEV void agent_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const
       p[j] = exp_fast(p[j] - m);
       l += p[j];
     }
-    const float il = 1.0f / l;
+    const float il = rcp_fast(l);
     f4 oh = zero4();
     float Ps = 0.f;
 #pragma unroll

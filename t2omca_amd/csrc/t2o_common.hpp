@@ -49,6 +49,16 @@ T2O_DEV f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 // of y = x·log2(e) instead of libm expf's range-reduced ~10-instruction expansion.
 // Relative error ≈ |x|·2^-24 + 1 ulp, far inside the fp32 parity bar.
 T2O_DEV float exp_fast(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+// 1/x and 1/sqrt(x) as single v_rcp_f32 / v_rsq_f32 (~1 ulp) instead of the
+// IEEE division / sqrt expansions (softmax normaliser, LayerNorm).
+T2O_DEV float rcp_fast(float x) { return __builtin_amdgcn_rcpf(x); }
+T2O_DEV float rsqrt_fast(float x) { return __builtin_amdgcn_rsqf(x); }
+// p[i] when ok, else 0 — one unconditional load from a clamped index (no branch
+// around the load; the index must be valid when ok, and 0 is always valid).
+T2O_DEV float ld_or0(const float* __restrict__ p, int64_t i, bool ok) {
+  const float v = p[ok ? i : 0];
+  return ok ? v : 0.f;
+}
 T2O_DEV void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
 
 // acc += W[16o.. , 16i..] (16x16 tile of row-major W, leading dim ldw) · x_tile
@@ -274,7 +284,7 @@ T2O_DEV void layernorm_fwd(const f4* r, const float* __restrict__ gamma,
     v += (d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]);
   }
   const float var = allsum4(v) * inv_e;
-  rstd = 1.0f / sqrtf(var + 1e-5f);
+  rstd = rsqrt_fast(var + 1e-5f);
 #pragma unroll
   for (int t = 0; t < ET; ++t) {
     xhat[t] = (r[t] - mean) * rstd;

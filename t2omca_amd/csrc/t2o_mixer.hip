@@ -109,7 +109,7 @@ T2O_DEV void mix_load(const MixerFwdArgs& a, const MixerNet& n, int b, int t, Mi
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int f = 4 * g + r;
-      in.st[s][r] = (j < Dm::NS && f < a.Fs) ? st[j * a.Fs + f] : 0.f;
+      in.st[s][r] = ld_or0(st, j * a.Fs + f, j < Dm::NS && f < a.Fs);
     }
   }
   const float* hd = n.hid + b * n.hid_sb + t * n.hid_st;
@@ -412,7 +412,8 @@ T2O_DEV void mixb_load(const MixerBwdArgs& args, const MixerNet& n, int b, int t
     for (int r = 0; r < 4; ++r) {
       const int j = 16 * s + 4 * g + r;
       float v = 0.f;
-      if (j < Dm::NS) v = c < fa.Fs ? st[j * fa.Fs + c] : (c == fa.Fs ? 1.f : 0.f);
+      v = ld_or0(st, j * fa.Fs + c, j < Dm::NS && c < fa.Fs);
+      if (j < Dm::NS && c == fa.Fs) v = 1.f;
       in.stT[s][r] = v;
     }
 }

@@ -131,7 +131,7 @@ T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
         s[kt][r] = exp_fast(s[kt][r] - m);
         l += s[kt][r];
       }
-    const float il = 1.0f / allsum4(l);
+    const float il = rcp_fast(allsum4(l));
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) s[kt] *= il;
     keys_combine<E, KT, BF>(K, s, &z[hh * ET]);
