@@ -174,7 +174,7 @@ int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, const float* st
 int t2o_mixer_bwd_max_slabs(int B);
 
 /* Floats of backward tape workspace for `tiles` tiles of 16 records:
- * D * tiles * 16 * (4E + 2HE) elements of 4 (fp32) or 2 (bf16) bytes. */
+ * D * tiles * 16 * (6E + 2HE) elements of 4 (fp32) or 2 (bf16) bytes. */
 int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t tiles);
 
 /* Contract a backward tape (dM, dN, dW1, dW2 = Σ_records dYᵀ X, split-K over

@@ -166,8 +166,8 @@ T2O_DEV void agent_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_la
   }
   // u = M x
   if (rec) {
-    tile_store<HET>(rec, TapeRec<E, H, FF>::GU, gu);
-    tile_store<ET>(rec, TapeRec<E, H, FF>::X, c.post.x);
+    rec_store<TapeRec<E, H, FF>::SIZE, HET>(rec, TapeRec<E, H, FF>::GU, gu);
+    rec_store<TapeRec<E, H, FF>::SIZE, ET>(rec, TapeRec<E, H, FF>::X, c.post.x);
   }
   f4 gxp[ET];
   matvec_tr<ET, HET>(P, L.M[d], E, L.MT[d], H * E, gu, gxp);

@@ -71,9 +71,10 @@ T2O_DEV void post_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* z,
 }
 
 // gx: grad wrt block output.  Produces gz (grad wrt z, HET tiles) and gres
-// (grad wrt the block input through the LN1 residual).  The operand pairs of
-// the big weight grads (N, W1, W2) go to the wave's tape tile (TapeRec; null:
-// no tape); vector grads go to the workgroup's global slab gs (layout G).
+// (grad wrt the block input through the LN1 residual).  The operands of the
+// big weight grads (N, W1, W2) and of the bu / c1 / c2 / g1 / n1 grads go to
+// the wave's tape tile (TapeRec; null: no tape); the LN2 vector grads go to
+// the workgroup's global slab gs (layout G).
 // Weights are read from P (LDS); transposed products use matvec_t.
 template <int E, int H, int FF, typename WT>
 T2O_DEV void post_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G,
@@ -91,34 +92,29 @@ T2O_DEV void post_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G
   f4 gr2[ET];
   layernorm_bwd<ET>(gx, c.xh2, c.rs2, P.v + L.g2[d], gr2);
   // r2 = W2 relu(f1) + c2 + y
-  if (rec) tile_store<ET>(rec, R::GR2, gr2);
-  vec_accumulate_g<ET>(gs + G.c2[d], gr2);
+  if (rec) rec_store<R::SIZE, ET>(rec, R::GR2, gr2);
   f4 gf1[FT];
   matvec_tr<FT, ET>(P, L.W2[d], FF, L.W2T[d], E, gr2, gf1);
 #pragma unroll
   for (int t = 0; t < FT; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) gf1[t][r] = c.f1r[t][r] > 0.f ? gf1[t][r] : 0.f;
-  if (rec) tile_store<ET>(rec, R::Y, c.y);  // f1 and gf1 are recomputed from (y, gr2)
-  vec_accumulate_g<FT>(gs + G.c1[d], gf1);
+  if (rec) rec_store<R::SIZE, ET>(rec, R::Y, c.y);  // f1, gf1 (and d c1) are recomputed from (y, gr2)
   f4 gy[ET];
   matvec_tr<ET, FT>(P, L.W1[d], E, L.W1T[d], FF, gf1, gy);
 #pragma unroll
   for (int t = 0; t < ET; ++t) gy[t] += gr2[t];
-  {  // LN1: y = xh1*g1 + n1
-    f4 t0[ET];
-#pragma unroll
-    for (int t = 0; t < ET; ++t) t0[t] = gy[t] * c.xh1[t];
-    vec_accumulate_g<ET>(gs + G.g1[d], t0);
-    vec_accumulate_g<ET>(gs + G.n1[d], gy);
+  // LN1: y = xh1*g1 + n1 (d g1, d n1 from the tape's (x̂1, gy))
+  if (rec) {
+    rec_store<R::SIZE, ET>(rec, R::XH1, c.xh1);
+    rec_store<R::SIZE, ET>(rec, R::GY, gy);
   }
   layernorm_bwd<ET>(gy, c.xh1, c.rs1, P.v + L.g1[d], gres);
   // r1 = N z + b_U + x
   if (rec) {
-    tile_store<ET>(rec, R::GRES, gres);
-    tile_store<HET>(rec, R::Z, c.z);
+    rec_store<R::SIZE, ET>(rec, R::GRES, gres);
+    rec_store<R::SIZE, HET>(rec, R::Z, c.z);
   }
-  vec_accumulate_g<ET>(gs + G.bu[d], gres);
   matvec_tr<HET, ET>(P, L.N[d], H * E, L.NT[d], E, gres, gz);
 }
 

@@ -513,6 +513,9 @@ T2O_DEV void vec_accumulate(float* __restrict__ ldsv, const f4* v) {
 // atomics (no return value, fire-and-forget at L2).
 template <int NT>
 T2O_DEV void vec_accumulate_g(float* __restrict__ gv, const f4* v) {
+#ifdef T2O_ABL_NOVEC  // ablation builds only (tools/build_variant.sh): wrong gradients
+  return;
+#endif
   const int c = lane_c(), g = lane_g();
   float s[NT][4];
 #pragma unroll
@@ -542,38 +545,51 @@ T2O_DEV void flush_tiles_g(float* __restrict__ W, int ldw, const f4 (&acc)[OT][I
 
 // ---- weight-gradient tape ---------------------------------------------------
 // The backward kernels do not accumulate the four big per-block matrices
-// (M, N, W1, W2) themselves: per (row, step, block) they stream a record to an
-// HBM tape, and t2o_dwgemm.hip contracts the tape over all records with MFMA:
-//   dM = Σ gu ⊗ x,  dN = Σ gres ⊗ z,  dW2 = Σ gr2 ⊗ relu(f1),  dW1 = Σ gf1 ⊗ y
+// (M, N, W1, W2), nor the FFN / LN1 / unify vectors, themselves: per (row,
+// step, block) they stream a record to an HBM tape, and t2o_dwgemm.hip
+// contracts the tape over all records with MFMA:
+//   dM = Σ gu ⊗ x,  dN = Σ gres ⊗ z,  dW2 = Σ gr2 ⊗ relu(f1),  dW1 = Σ gf1 ⊗ y,
+//   d bu = Σ gres,  d c2 = Σ gr2,  d c1 = Σ gf1,  d n1 = Σ gy,  d g1 = Σ gy ⊙ x̂1
 // with f1 = W1 y + c1 and gf1 = [f1 > 0] ⊙ W2ᵀ gr2 RECOMPUTED from (y, gr2) by
 // the contraction (two FF-wide operands are 44 % of a full record; recomputing
 // them is a few MFMAs per 16 records in a kernel that is HBM-bound anyway).
-// Feature offsets of one record:
+// Only the LN2 vectors (g2, n2) and the small embedding / head grads are still
+// summed inside the backward kernels.  Feature offsets of one record:
 template <int E, int H, int FF>
 struct TapeRec {
   static constexpr int X = 0;                 // block input x      (E)   M:  X
   static constexpr int GU = X + E;            // dL/du              (HE)  M:  dY
   static constexpr int Z = GU + H * E;        // head outputs z     (HE)  N:  X
-  static constexpr int GRES = Z + H * E;      // dL/d(N z + bu)     (E)   N:  dY
+  static constexpr int GRES = Z + H * E;      // dL/d(N z + bu)     (E)   N:  dY, bu
   static constexpr int Y = GRES + E;          // LN1 output y       (E)   W1: X, and f1
-  static constexpr int GR2 = Y + E;           // dL/d(W2 f + c2 + y)(E)   W2: dY, and gf1
-  static constexpr int SIZE = GR2 + E;
+  static constexpr int GR2 = Y + E;           // dL/d(W2 f + c2 + y)(E)   W2: dY, gf1, c2
+  static constexpr int XH1 = GR2 + E;         // LN1 x̂             (E)   g1
+  static constexpr int GY = XH1 + E;          // dL/dy              (E)   g1, n1
+  static constexpr int SIZE = GY + E;
 };
-// Layout: tiles of 16 records (one wave's rows at one step), feature-major
+// Layout: tiles of 16 records (one wave's rows at one step), RECORD-major
 // inside a tile: element (record 16·tile + c, feature f) of block d sits at
-// ((d·ntiles + tile)·SIZE + f)·16 + c, in the MFMA operand type (fp32, or bf16
-// in bf16 mode).  A wave's tile is one contiguous 10 KiB (bf16) run written
-// whole; the contraction stages tiles in LDS and reads 4 consecutive records
-// of one feature per lane, which is exactly a 16x16x16 MFMA K-slice.
+// ((d·ntiles + tile)·16 + c)·SIZE + f, in the MFMA operand type (fp32, or
+// bf16 in bf16 mode).  A writer lane (g, c) holds features 16t + 4g .. +3 of
+// record c, i.e. 8 (bf16) / 16 (fp32) contiguous bytes: one store per 16
+// features.  The contraction stages whole tiles in LDS and reads the
+// feature-major K-slices of its MFMAs with the gfx950 transposed LDS read.
 
 // store a T-layout vector (NT tiles, features off + 16t + 4g + r of record c)
-template <int NT, typename TT>
-T2O_DEV void tile_store(TT* __restrict__ tile, int off, const f4* v) {
-  const int c = lane_c(), g = lane_g();
+template <int SIZE, int NT, typename TT>
+T2O_DEV void rec_store(TT* __restrict__ tile, int off, const f4* v) {
+#ifdef T2O_ABL_NOTAPE  // ablation builds only: wrong gradients
+  return;
+#endif
+  TT* p = tile + lane_c() * SIZE + off + 4 * lane_g();
 #pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) tile[(off + 16 * t + 4 * g + r) * 16 + c] = (TT)v[t][r];
+  for (int t = 0; t < NT; ++t) {
+    if constexpr (sizeof(TT) == 2) {
+      *reinterpret_cast<bf4*>(p + 16 * t) = to_bf4(v[t]);
+    } else {
+      st4(reinterpret_cast<float*>(p + 16 * t), v[t]);
+    }
+  }
 }
 
 }  // namespace t2o

@@ -4,6 +4,7 @@
 // of the mixer):
 //   dM  = Σ_n gu_n ⊗ x_n          dN  = Σ_n gres_n ⊗ z_n
 //   dW2 = Σ_n gr2_n ⊗ relu(f1_n)  dW1 = Σ_n gf1_n ⊗ y_n
+//   d bu = Σ gres,  d c2 = Σ gr2,  d c1 = Σ gf1,  d n1 = Σ gy,  d g1 = Σ gy ⊙ x̂1
 // where f1 = W1 y + c1 and gf1 = [f1 > 0] ⊙ (W2ᵀ gr2) are recomputed here from
 // the record's (y, gr2) — the backward kernels do not store them.
 //
@@ -12,19 +13,21 @@
 //   * split-K over workgroups: 16-record tiles are grouped TG at a time and the
 //     groups dealt round-robin (group k -> workgroup k mod nslab), so the grid
 //     streams one contiguous window of the tape at a time; workgroup k writes
-//     the four matrices of every block into gradient slab k, whose small-
-//     gradient part the backward kernel has already filled;
+//     its matrices and vectors of every block into gradient slab k, whose
+//     other (small-gradient) part the backward kernel has already filled;
 //   * each workgroup stages a group (all D blocks) in LDS with full-line 16-B
-//     loads by all its threads, double-buffered in LDS with a two-deep
-//     register ring (prefetch distance two groups), one barrier per group;
-//   * 4 waves per block read the staged tiles: wave 0 dM, wave 1 dN, waves 2
-//     and 3 one half of the FF features each (recompute f1 / gf1 with MFMA
-//     from LDS copies of W1 / W2ᵀ, then dW1 / dW2).  All accumulators stay in
-//     registers for the whole launch.
-// MFMA shapes: bf16 tape -> v_mfma_f32_16x16x16_bf16 (K = 16 records of a
-// tile: lane (g, c) reads records 4g..4g+3 of one feature, one ds_read_b64;
-// the record-major operand of the recompute comes from ds_read_b64_tr_b16);
-// fp32 tape -> four v_mfma_f32_16x16x4_f32 per 16 records.
+//     loads by all its threads (records padded in LDS so both read kinds below
+//     are bank-conflict-free), double-buffered in LDS with a two-deep register
+//     ring (prefetch distance two groups), one barrier per group;
+//   * 4 waves per block read the staged tiles: wave 0 dM (+ g1, n1), wave 1
+//     dN (+ bu), waves 2 and 3 one half of the FF features each (recompute
+//     f1 / gf1 with MFMA, then dW1 / dW2 and c1; wave 2 also c2).  All
+//     accumulators stay in registers for the whole launch.
+// MFMA shapes: bf16 tape -> v_mfma_f32_16x16x16_bf16 with K = the 16 records
+// of a tile.  The tape is record-major, so the feature-major K-slices (records
+// 4g..4g+3 of one feature) come from ds_read_b64_tr_b16 and the record-major
+// operand of the recompute (features 4g..4g+3 of record c) from a plain
+// ds_read_b64.  fp32 tape -> four v_mfma_f32_16x16x4_f32 per 16 records.
 #include <type_traits>
 
 #include "t2o_common.hpp"
@@ -34,7 +37,7 @@
 namespace t2o {
 
 struct DwGemmArgs {
-  const void* tape;    // [D][ntiles][SIZE][16]
+  const void* tape;    // [D][ntiles][16][SIZE]
   int64_t ntiles;      // 16-record tiles per block
   float* slabs;        // [nslab][slab_stride], compact gradient layout G
   int64_t slab_stride;
@@ -53,25 +56,22 @@ T2O_DEV void dw_tiles_store(float* __restrict__ W, int ldw, const f4 (&acc)[OT][
       for (int r = 0; r < 4; ++r) W[(16 * o + 4 * g + r) * ldw + 16 * i + c] = acc[o][i][r];
 }
 
+// per-lane partial sums of a vector over this lane's records (lane (g, c) =
+// feature 16t + c): sum the 4 lane groups and write from group 0
+template <int NT>
+T2O_DEV void dw_vec_store(float* __restrict__ v, const float (&acc)[NT]) {
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const float s = allsum4(acc[t]);
+    if (lane_g() == 0) v[16 * t + lane_c()] = s;
+  }
+}
+
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 
 template <typename TT> struct DwTraits;
-template <> struct DwTraits<__bf16> { static constexpr int TG = 2; };  // tiles per group
-template <> struct DwTraits<float> { static constexpr int TG = 1; };
-
-// ---- operand reads from a staged tile (feature-major, 16 records per row) ----
-// bf16: records 4g..4g+3 of feature row `f` (K-slice of a 16x16x16 MFMA)
-T2O_DEV bf4 kslice(const __bf16* tile, int f) { return ldb4(tile + f * 16 + 4 * lane_g()); }
-// bf16: features f0 + 4g .. +3 of record c (the record-major operand), by the
-// gfx950 transposed LDS read: lane 4q+p of each 16-lane group addresses row
-// f0 + 4g + q, records 4p..4p+3, and lane c receives record c of the 4 rows.
-T2O_DEV bf4 rslice(const __bf16* tile, int f0) {
-  const int c = lane_c();
-  const __bf16* p = tile + (f0 + 4 * lane_g() + (c >> 2)) * 16 + 4 * (c & 3);
-  typedef __attribute__((address_space(3))) s4v lds_s4v;
-  const s4v v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(p));
-  return __builtin_bit_cast(bf4, v);
-}
+template <> struct DwTraits<__bf16> { static constexpr int TG = 2, PADC = 2; };  // tiles per group, pad chunks
+template <> struct DwTraits<float> { static constexpr int TG = 1, PADC = 1; };
 
 template <int E, int H, int FF, int D, typename TT>
 struct DwDims {
@@ -79,12 +79,16 @@ struct DwDims {
   static constexpr int ET = E / 16, HET = H * ET, FT = FF / 16, FH = FT / 2;
   static constexpr bool BF = sizeof(TT) == 2;
   static constexpr int TG = DwTraits<TT>::TG;
-  static constexpr int TILE = R::SIZE * 16;                 // elements per tile
-  static constexpr int CPT = TILE * (int)sizeof(TT) / 16;   // 16-B chunks per tile
-  static constexpr int NT = 256 * D;                        // threads
-  static constexpr int GCH = D * TG * CPT;                  // chunks per group
-  static constexpr int NLD = (GCH + NT - 1) / NT;           // chunks per thread
-  static constexpr int GELEM = D * TG * TILE;               // elements per staged group
+  static constexpr int PER = 16 / (int)sizeof(TT);          // elements per 16-B chunk
+  static constexpr int CPR = R::SIZE / PER;                  // chunks per record
+  static constexpr int CPT = 16 * CPR;                       // chunks per tile (HBM)
+  static constexpr int RSTR = (CPR + DwTraits<TT>::PADC) * PER;  // padded LDS record stride (elements)
+  static constexpr int TSTR = 16 * RSTR;                     // LDS tile stride (elements)
+  static constexpr int NT = 256 * D;                         // threads
+  static constexpr int GCH = D * TG * CPT;                   // chunks per group
+  static constexpr int NLD = (GCH + NT - 1) / NT;            // chunks per thread
+  static constexpr int GELEM = D * TG * TSTR;                // LDS elements per staged group
+  static_assert(R::SIZE % PER == 0, "record must be a whole number of 16-B chunks");
   static_assert(FT % 2 == 0, "FF must split into two halves of 16-feature tiles");
 };
 
@@ -101,21 +105,67 @@ T2O_DEV void dw_load(const DwGemmArgs& a, int64_t j, u4v (&rg)[Dm::NLD]) {
     const int64_t tile = grp * Dm::TG + tt;
     rg[i] = u4v{0u, 0u, 0u, 0u};
     if (q < Dm::GCH && tile < a.ntiles)
-      rg[i] = *reinterpret_cast<const u4v*>(tape + ((size_t)dd * a.ntiles + tile) * Dm::TILE + ch * (16 / sizeof(TT)));
+      rg[i] = *reinterpret_cast<const u4v*>(tape + ((size_t)dd * a.ntiles + tile) * Dm::CPT * Dm::PER +
+                                            (size_t)ch * Dm::PER);
   }
 }
-// registers -> LDS group buffer (lane-linear: the buffer is [D][TG][tile])
+// registers -> LDS group buffer [D][TG][16 records, padded stride RSTR]
 template <typename Dm, typename TT>
 T2O_DEV void dw_store(TT* buf, const u4v (&rg)[Dm::NLD]) {
 #pragma unroll
   for (int i = 0; i < Dm::NLD; ++i) {
     const int q = threadIdx.x + i * Dm::NT;
-    if (q < Dm::GCH) *reinterpret_cast<u4v*>(buf + q * (16 / sizeof(TT))) = rg[i];
+    if (q < Dm::GCH) {
+      const int tix = q / Dm::CPT, ch = q % Dm::CPT;  // tix = dd * TG + tt
+      const int rec = ch / Dm::CPR, cr = ch % Dm::CPR;
+      *reinterpret_cast<u4v*>(buf + tix * Dm::TSTR + rec * Dm::RSTR + cr * Dm::PER) = rg[i];
+    }
   }
 }
 
-// Role state: the accumulators (and, for the FFN roles, the weight fragments)
-// of one wave.  ROLE 0 dM, 1 dN, 2/3 FFN half 0/1.
+// ---- operand reads from a staged tile (record-major, stride RSTR) -----------
+// K-slice: records 4g..4g+3 of feature f0 + c.  bf16 by the gfx950 transposed
+// LDS read: lane 4q+p of each 16-lane group addresses record 4g + q, features
+// f0 + 4p .. +3, and lane c receives feature f0 + c of the 4 records.
+template <int RSTR>
+T2O_DEV bf4 kslice(const __bf16* tile, int f0) {
+  const int c = lane_c();
+  const __bf16* p = tile + (4 * lane_g() + (c >> 2)) * RSTR + f0 + 4 * (c & 3);
+  typedef __attribute__((address_space(3))) s4v lds_s4v;
+  const s4v v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(p));
+  return __builtin_bit_cast(bf4, v);
+}
+template <int RSTR>
+T2O_DEV f4 kslice(const float* tile, int f0) {
+  const int c = lane_c(), g = lane_g();
+  f4 v;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = tile[(4 * g + r) * RSTR + f0 + c];
+  return v;
+}
+// record-major operand: features f0 + 4g .. +3 of record c
+template <int RSTR>
+T2O_DEV bf4 rslice(const __bf16* tile, int f0) { return ldb4(tile + lane_c() * RSTR + f0 + 4 * lane_g()); }
+template <int RSTR>
+T2O_DEV f4 rslice(const float* tile, int f0) { return ld4(tile + lane_c() * RSTR + f0 + 4 * lane_g()); }
+
+T2O_DEV float bsum4(bf4 v) { return ((float)v[0] + (float)v[1]) + ((float)v[2] + (float)v[3]); }
+T2O_DEV float bsum4(f4 v) { return (v[0] + v[1]) + (v[2] + v[3]); }
+T2O_DEV float bdot4(bf4 a, bf4 b) {
+  return ((float)a[0] * (float)b[0] + (float)a[1] * (float)b[1]) + ((float)a[2] * (float)b[2] + (float)a[3] * (float)b[3]);
+}
+T2O_DEV float bdot4(f4 a, f4 b) { return (a[0] * b[0] + a[1] * b[1]) + (a[2] * b[2] + a[3] * b[3]); }
+
+// acc += A-slice ⊗ B-slice over the tile's 16 records (K-slices as above)
+T2O_DEV f4 kmma(bf4 a, bf4 b, f4 acc) { return mfma_b16(a, b, acc); }
+T2O_DEV f4 kmma(f4 a, f4 b, f4 acc) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) acc = mfma4(a[r], b[r], acc);
+  return acc;
+}
+
+// Role state: the accumulators of one wave.  ROLE 0 dM (+ g1, n1), 1 dN (+ bu),
+// 2/3 FFN half 0/1 (+ c1 of the half; role 2 also c2).
 template <int ROLE, int E, int H, int FF, int D, typename TT>
 struct DwRole;
 
@@ -123,41 +173,39 @@ template <int E, int H, int FF, int D, typename TT>
 struct DwRole<0, E, H, FF, D, TT> {
   using Dm = DwDims<E, H, FF, D, TT>;
   using R = typename Dm::R;
+  using Frag = typename std::conditional<Dm::BF, bf4, f4>::type;
   f4 acc[Dm::HET][Dm::ET];  // dM[gu feature][x feature]
+  float vn1[Dm::ET], vg1[Dm::ET];
   T2O_DEV void init(const DwGemmArgs&, int, const TT*) {
 #pragma unroll
     for (int o = 0; o < Dm::HET; ++o)
 #pragma unroll
       for (int i = 0; i < Dm::ET; ++i) acc[o][i] = zero4();
+#pragma unroll
+    for (int i = 0; i < Dm::ET; ++i) vn1[i] = vg1[i] = 0.f;
   }
   T2O_DEV void tile(const TT* t) {
-    const int c = lane_c(), g = lane_g();
-    if constexpr (Dm::BF) {
-      bf4 xb[Dm::ET];
+    constexpr int S = Dm::RSTR;
+    Frag xb[Dm::ET];
 #pragma unroll
-      for (int i = 0; i < Dm::ET; ++i) xb[i] = kslice(t, R::X + 16 * i + c);
+    for (int i = 0; i < Dm::ET; ++i) xb[i] = kslice<S>(t, R::X + 16 * i);
 #pragma unroll
-      for (int o = 0; o < Dm::HET; ++o) {
-        const bf4 ab = kslice(t, R::GU + 16 * o + c);
+    for (int o = 0; o < Dm::HET; ++o) {
+      const Frag ab = kslice<S>(t, R::GU + 16 * o);
 #pragma unroll
-        for (int i = 0; i < Dm::ET; ++i) acc[o][i] = mfma_b16(ab, xb[i], acc[o][i]);
-      }
-    } else {
-      f4 xv[Dm::ET];
+      for (int i = 0; i < Dm::ET; ++i) acc[o][i] = kmma(ab, xb[i], acc[o][i]);
+    }
 #pragma unroll
-      for (int i = 0; i < Dm::ET; ++i) xv[i] = ld4(t + (R::X + 16 * i + c) * 16 + 4 * g);
-#pragma unroll
-      for (int o = 0; o < Dm::HET; ++o) {
-        const f4 av = ld4(t + (R::GU + 16 * o + c) * 16 + 4 * g);
-#pragma unroll
-        for (int i = 0; i < Dm::ET; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[o][i] = mfma4(av[r], xv[i][r], acc[o][i]);
-      }
+    for (int i = 0; i < Dm::ET; ++i) {
+      const Frag gy = kslice<S>(t, R::GY + 16 * i), xh = kslice<S>(t, R::XH1 + 16 * i);
+      vn1[i] += bsum4(gy);
+      vg1[i] += bdot4(gy, xh);
     }
   }
   T2O_DEV void finish(const DwGemmArgs& a, float* slab, int d) {
     dw_tiles_store<Dm::HET, Dm::ET>(slab + a.G.M[d], E, acc);
+    dw_vec_store<Dm::ET>(slab + a.G.n1[d], vn1);
+    dw_vec_store<Dm::ET>(slab + a.G.g1[d], vg1);
   }
 };
 
@@ -165,41 +213,35 @@ template <int E, int H, int FF, int D, typename TT>
 struct DwRole<1, E, H, FF, D, TT> {
   using Dm = DwDims<E, H, FF, D, TT>;
   using R = typename Dm::R;
+  using Frag = typename std::conditional<Dm::BF, bf4, f4>::type;
   f4 acc[Dm::ET][Dm::HET];  // dN[gres feature][z feature]
+  float vbu[Dm::ET];
   T2O_DEV void init(const DwGemmArgs&, int, const TT*) {
 #pragma unroll
-    for (int o = 0; o < Dm::ET; ++o)
+    for (int o = 0; o < Dm::ET; ++o) {
+      vbu[o] = 0.f;
 #pragma unroll
       for (int i = 0; i < Dm::HET; ++i) acc[o][i] = zero4();
+    }
   }
   T2O_DEV void tile(const TT* t) {
-    const int c = lane_c(), g = lane_g();
-    if constexpr (Dm::BF) {
-      bf4 gb[Dm::ET];
+    constexpr int S = Dm::RSTR;
+    Frag gb[Dm::ET];
 #pragma unroll
-      for (int o = 0; o < Dm::ET; ++o) gb[o] = kslice(t, R::GRES + 16 * o + c);
+    for (int o = 0; o < Dm::ET; ++o) {
+      gb[o] = kslice<S>(t, R::GRES + 16 * o);
+      vbu[o] += bsum4(gb[o]);
+    }
 #pragma unroll
-      for (int i = 0; i < Dm::HET; ++i) {
-        const bf4 zb = kslice(t, R::Z + 16 * i + c);
+    for (int i = 0; i < Dm::HET; ++i) {
+      const Frag zb = kslice<S>(t, R::Z + 16 * i);
 #pragma unroll
-        for (int o = 0; o < Dm::ET; ++o) acc[o][i] = mfma_b16(gb[o], zb, acc[o][i]);
-      }
-    } else {
-      f4 gv[Dm::ET];
-#pragma unroll
-      for (int o = 0; o < Dm::ET; ++o) gv[o] = ld4(t + (R::GRES + 16 * o + c) * 16 + 4 * g);
-#pragma unroll
-      for (int i = 0; i < Dm::HET; ++i) {
-        const f4 zv = ld4(t + (R::Z + 16 * i + c) * 16 + 4 * g);
-#pragma unroll
-        for (int o = 0; o < Dm::ET; ++o)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[o][i] = mfma4(gv[o][r], zv[r], acc[o][i]);
-      }
+      for (int o = 0; o < Dm::ET; ++o) acc[o][i] = kmma(gb[o], zb, acc[o][i]);
     }
   }
   T2O_DEV void finish(const DwGemmArgs& a, float* slab, int d) {
     dw_tiles_store<Dm::ET, Dm::HET>(slab + a.G.N[d], H * E, acc);
+    dw_vec_store<Dm::ET>(slab + a.G.bu[d], vbu);
   }
 };
 
@@ -207,6 +249,8 @@ struct DwRole<1, E, H, FF, D, TT> {
 // half's FH feature tiles as [records x features] MFMA tiles (lane (g, c) =
 // records 4g..4g+3 of feature 16J + c — already the K-slice layout of the
 // contraction), then dW2[e][J] += gr2 ⊗ relu(f1), dW1[J][e] += gf1 ⊗ y.
+// Weight fragments: bf16 from the workgroup's LDS copy of the pack's
+// (swizzled) bf16 image; fp32 straight from the pack (L2-resident).
 template <int HALF, int E, int H, int FF, int D, typename TT>
 struct DwFfn {
   using Dm = DwDims<E, H, FF, D, TT>;
@@ -215,99 +259,86 @@ struct DwFfn {
   using Frag = typename std::conditional<Dm::BF, bf4, f4>::type;
   f4 acc1[FH][ET];  // dW1 rows of this half
   f4 acc2[ET][FH];  // dW2 columns of this half
-  const TT* wl;    // LDS copy of this block's W1 [FF][E] then W2ᵀ [FF][E] (bf16: the pack's swizzled image)
+  float vc1[FH], vc2[ET];
   float c1v[FH];
+  const TT* wl;     // bf16: LDS W1 [FF][E] then W2ᵀ [FF][E] of this block
+  const float* wsrc;
+  int64_t o1, o2;
   T2O_DEV void init(const DwGemmArgs& a, int d, const TT* wlds) {
     const int c = lane_c();
 #pragma unroll
-    for (int o = 0; o < FH; ++o)
+    for (int o = 0; o < FH; ++o) {
+      vc1[o] = 0.f;
 #pragma unroll
       for (int i = 0; i < ET; ++i) acc1[o][i] = acc2[i][o] = zero4();
+    }
+#pragma unroll
+    for (int i = 0; i < ET; ++i) vc2[i] = 0.f;
     wl = wlds + (size_t)d * 2 * FF * E;
+    wsrc = a.pack;
+    o1 = a.L.W1[d];
+    o2 = a.L.W2T[d];
 #pragma unroll
     for (int jt = 0; jt < FH; ++jt) c1v[jt] = a.pack[a.L.c1[d] + 16 * (HALF * FH + jt) + c];
   }
   // fragment of W (0: W1, 1: W2ᵀ): row 16J + c, features 16s + 4g .. +3
   T2O_DEV Frag wfrag(int m, int jt, int s) const {
     const int row = 16 * (HALF * FH + jt) + lane_c();
-    const TT* base = wl + (size_t)m * FF * E + (size_t)row * E;
-    if constexpr (Dm::BF) return ldb4(base + ((16 * s + 4 * lane_g()) ^ bf_swz(row, E)));
-    else return ld4(base + 16 * s + 4 * lane_g());
+    if constexpr (Dm::BF) {
+      const TT* base = wl + (size_t)m * FF * E + (size_t)row * E;
+      return ldb4(base + ((16 * s + 4 * lane_g()) ^ bf_swz(row, E)));
+    } else {
+      return ld4(wsrc + (m ? o2 : o1) + (int64_t)row * E + 16 * s + 4 * lane_g());
+    }
   }
   T2O_DEV void tile(const TT* t) {
-    const int c = lane_c(), g = lane_g();
-    if constexpr (Dm::BF) {
-      bf4 yr[ET], gr[ET], yk[ET], gk[ET];
+    constexpr int S = Dm::RSTR;
+    Frag yr[ET], gr[ET], yk[ET], gk[ET];
+#pragma unroll
+    for (int s = 0; s < ET; ++s) {
+      yr[s] = rslice<S>(t, R::Y + 16 * s);
+      gr[s] = rslice<S>(t, R::GR2 + 16 * s);
+      yk[s] = kslice<S>(t, R::Y + 16 * s);
+      gk[s] = kslice<S>(t, R::GR2 + 16 * s);
+      if (HALF == 0) vc2[s] += bsum4(gk[s]);
+    }
+#pragma unroll
+    for (int jt = 0; jt < FH; ++jt) {
+      f4 f1 = zero4(), gp = zero4();
 #pragma unroll
       for (int s = 0; s < ET; ++s) {
-        yr[s] = rslice(t, R::Y + 16 * s);
-        gr[s] = rslice(t, R::GR2 + 16 * s);
-        yk[s] = kslice(t, R::Y + 16 * s + c);
-        gk[s] = kslice(t, R::GR2 + 16 * s + c);
+        // [records x features]: A = record-major slice, B = weight rows
+        f1 = kmma(yr[s], wfrag(0, jt, s), f1);
+        gp = kmma(gr[s], wfrag(1, jt, s), gp);
+      }
+      f4 fr, gf;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = f1[r] + c1v[jt];
+        fr[r] = fmaxf(v, 0.f);
+        gf[r] = v > 0.f ? gp[r] : 0.f;
+      }
+      vc1[jt] += (gf[0] + gf[1]) + (gf[2] + gf[3]);
+      Frag frb, gfb;
+      if constexpr (Dm::BF) {
+        frb = to_bf4(fr);
+        gfb = to_bf4(gf);
+      } else {
+        frb = fr;
+        gfb = gf;
       }
 #pragma unroll
-      for (int jt = 0; jt < FH; ++jt) {
-        f4 f1 = zero4(), gp = zero4();
-#pragma unroll
-        for (int s = 0; s < ET; ++s) {
-          f1 = mfma_b16(yr[s], wfrag(0, jt, s), f1);
-          gp = mfma_b16(gr[s], wfrag(1, jt, s), gp);
-        }
-        f4 fr, gf;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = f1[r] + c1v[jt];
-          fr[r] = fmaxf(v, 0.f);
-          gf[r] = v > 0.f ? gp[r] : 0.f;
-        }
-        const bf4 frb = to_bf4(fr), gfb = to_bf4(gf);
-#pragma unroll
-        for (int e = 0; e < ET; ++e) {
-          acc2[e][jt] = mfma_b16(gk[e], frb, acc2[e][jt]);
-          acc1[jt][e] = mfma_b16(gfb, yk[e], acc1[jt][e]);
-        }
-      }
-    } else {
-      f4 yk[ET], gk[ET];
-#pragma unroll
-      for (int s = 0; s < ET; ++s) {
-        yk[s] = ld4(t + (R::Y + 16 * s + c) * 16 + 4 * g);
-        gk[s] = ld4(t + (R::GR2 + 16 * s + c) * 16 + 4 * g);
-      }
-#pragma unroll
-      for (int jt = 0; jt < FH; ++jt) {
-        f4 f1 = zero4(), gp = zero4();
-#pragma unroll
-        for (int s = 0; s < ET; ++s) {
-          const f4 w1 = wfrag(0, jt, s), w2 = wfrag(1, jt, s);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            // feature k = 16s + 4g + r of record c (K-step r, k index g)
-            const int fk = 16 * s + 4 * g + r;
-            f1 = mfma4(t[(R::Y + fk) * 16 + c], w1[r], f1);
-            gp = mfma4(t[(R::GR2 + fk) * 16 + c], w2[r], gp);
-          }
-        }
-        f4 fr, gf;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float v = f1[r] + c1v[jt];
-          fr[r] = fmaxf(v, 0.f);
-          gf[r] = v > 0.f ? gp[r] : 0.f;
-        }
-#pragma unroll
-        for (int e = 0; e < ET; ++e)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            acc2[e][jt] = mfma4(gk[e][r], fr[r], acc2[e][jt]);
-            acc1[jt][e] = mfma4(gf[r], yk[e][r], acc1[jt][e]);
-          }
+      for (int e = 0; e < ET; ++e) {
+        acc2[e][jt] = kmma(gk[e], frb, acc2[e][jt]);  // dW2[e][J] += gr2 ⊗ relu(f1)
+        acc1[jt][e] = kmma(gfb, yk[e], acc1[jt][e]);  // dW1[J][e] += gf1 ⊗ y
       }
     }
   }
   T2O_DEV void finish(const DwGemmArgs& a, float* slab, int d) {
     dw_tiles_store<FH, ET>(slab + a.G.W1[d] + (int64_t)16 * HALF * FH * E, E, acc1);
     dw_tiles_store<ET, FH>(slab + a.G.W2[d] + 16 * HALF * FH, FF, acc2);
+    dw_vec_store<FH>(slab + a.G.c1[d] + 16 * HALF * FH, vc1);
+    if (HALF == 0) dw_vec_store<ET>(slab + a.G.c2[d], vc2);
   }
 };
 template <int E, int H, int FF, int D, typename TT>
@@ -328,7 +359,7 @@ T2O_DEV void dw_run(const DwGemmArgs& a, TT* buf0, TT* buf1, const TT* wlds, int
   auto compute = [&](const TT* buf) {
 #pragma unroll
     for (int tt = 0; tt < Dm::TG; ++tt) {
-      st.tile(buf + (d * Dm::TG + tt) * Dm::TILE);
+      st.tile(buf + (d * Dm::TG + tt) * Dm::TSTR);
       T2O_FENCE();  // keep the next tile's LDS reads from being hoisted over these MFMAs
     }
   };
@@ -360,12 +391,12 @@ __global__ __launch_bounds__(256 * D) void dw_gemm_kernel(DwGemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   TT* const buf0 = reinterpret_cast<TT*>(smem);
   TT* const buf1 = buf0 + Dm::GELEM;
-  TT* const wlds = buf1 + Dm::GELEM;  // [D][W1, W2ᵀ][FF][E]
-  {  // stage W1 / W2ᵀ of every block (made visible by dw_run's first barrier)
-    const TT* img = Dm::BF ? reinterpret_cast<const TT*>(a.pack + a.L.total) : reinterpret_cast<const TT*>(a.pack);
-    constexpr int PER = 16 / sizeof(TT), MAT = FF * E;
-    for (int q = threadIdx.x; q < D * 2 * MAT / PER; q += Dm::NT) {
-      const int e = q * PER, dd = e / (2 * MAT), m = (e / MAT) & 1, k = e % MAT;
+  TT* const wlds = buf1 + Dm::GELEM;  // bf16: [D][W1, W2ᵀ][FF][E] (the pack's swizzled image)
+  if constexpr (Dm::BF) {  // made visible by dw_run's first barrier
+    const TT* img = reinterpret_cast<const TT*>(a.pack + a.L.total);
+    constexpr int MAT = FF * E;
+    for (int q = threadIdx.x; q < D * 2 * MAT / Dm::PER; q += Dm::NT) {
+      const int e = q * Dm::PER, dd = e / (2 * MAT), m = (e / MAT) & 1, k = e % MAT;
       const int64_t src = (m ? a.L.W2T[dd] : a.L.W1[dd]) + k;
       *reinterpret_cast<u4v*>(wlds + e) = *reinterpret_cast<const u4v*>(img + src);
     }
@@ -383,6 +414,7 @@ __global__ __launch_bounds__(256 * D) void dw_gemm_kernel(DwGemmArgs a) {
 template <int E, int H, int FF, int D, typename TT>
 int launch_dw_gemm(int kind, const void* tape, int64_t ntiles, const float* pack, float* slabs, const t2o_layout& L,
                    const t2o_layout& G, int nslab, hipStream_t stream) {
+  using Dm = DwDims<E, H, FF, D, TT>;
   if (nslab < 1) return T2O_EINVAL;
   DwGemmArgs a{};
   a.tape = tape;
@@ -392,8 +424,7 @@ int launch_dw_gemm(int kind, const void* tape, int64_t ntiles, const float* pack
   a.pack = pack;
   a.L = L;
   a.G = G;
-  const size_t lds = sizeof(TT) * ((size_t)2 * D * DwTraits<TT>::TG * TapeRec<E, H, FF>::SIZE * 16 +
-                                    (size_t)D * 2 * FF * E);
+  const size_t lds = sizeof(TT) * ((size_t)2 * Dm::GELEM + (Dm::BF ? (size_t)D * 2 * FF * E : 0));
   auto kern = kind == 0 ? dw_gemm_kernel<E, H, FF, D, 0, TT> : dw_gemm_kernel<E, H, FF, D, 1, TT>;
   if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -407,7 +438,7 @@ using namespace t2o;
 
 extern "C" int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t tiles) {
   if (!L || tiles < 0) return -1;
-  const int64_t elems = (int64_t)L->D * tiles * 16 * (4 * L->E + 2 * L->H * L->E);
+  const int64_t elems = (int64_t)L->D * tiles * 16 * (6 * L->E + 2 * L->H * L->E);
   return L->prec ? (elems + 1) / 2 : elems;
 }
 

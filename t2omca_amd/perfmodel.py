@@ -49,7 +49,7 @@ def dw_record_bytes(E=32, H=3, D=2, FF=None, elem=4):
     """Tape bytes per record (all D blocks): written once by the backward, read once
     by the contraction; elem = 4 (fp32 mode) or 2 (bf16 mode)."""
     FF = FF or 4 * E
-    return D * elem * (4 * E + 2 * H * E + 2 * FF)
+    return D * elem * (6 * E + 2 * H * E)
 
 
 def td_update_flops(B, T, A, E=32, H=3, D=2, F=9, Fs=8, NA=5):
