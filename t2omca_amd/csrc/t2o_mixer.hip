@@ -157,9 +157,14 @@ T2O_DEV float mix_qv(const MixerNet& n, const MixIn<E, A>& in) {
         act = k;
       }
   }
+  // a select chain, kept opaque per step: folded into qs[act] it would turn the
+  // whole prefetch struct into a dynamically indexed scratch array
   float v = in.qs[0];
 #pragma unroll
-  for (int k = 1; k < MIX_MAXNA; ++k) v = act == k ? in.qs[k] : v;
+  for (int k = 1; k < MIX_MAXNA; ++k) {
+    v = act == k ? in.qs[k] : v;
+    asm volatile("" : "+v"(v));
+  }
   return v;
 }
 
