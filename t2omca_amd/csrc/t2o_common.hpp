@@ -421,6 +421,35 @@ T2O_DEV void dw_accumulate_regs(f4 (&acc)[OT][IT], const f4* dY, const f4* X, fl
   float* st_tile = stage + 16 * LD;
   const int c = lane_c(), g = lane_g();
   if constexpr (BF) {
+    // bf16: every operand tile is staged once as [16 rows][16 features] bf16
+    // (one 8-byte write per lane) and read back transposed with one
+    // ds_read_b64_tr_b16 — lane (g, c) gets feature c of rows 4g..4g+3, which
+    // is the 16x16x16 K-slice over rows of both operands.
+    static_assert((OT + IT) * 128 <= StageDims<NS>::FLOATS, "stage too small");
+    __bf16* sb = reinterpret_cast<__bf16*>(stage);
+#pragma unroll
+    for (int o = 0; o < OT; ++o) *reinterpret_cast<bf4*>(sb + o * 256 + c * 16 + 4 * g) = to_bf4(dY[o]);
+#pragma unroll
+    for (int i = 0; i < IT; ++i) *reinterpret_cast<bf4*>(sb + (OT + i) * 256 + c * 16 + 4 * g) = to_bf4(X[i]);
+    asm volatile("" ::: "memory");  // a wave's LDS accesses complete in order; keep the compiler's order too
+    typedef __attribute__((address_space(3))) s4v lds_s4v;
+    auto trk = [&](int j) {
+      const __bf16* p = sb + j * 256 + (4 * g + (c >> 2)) * 16 + 4 * (c & 3);
+      return __builtin_bit_cast(bf4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(p)));
+    };
+    bf4 xb[IT];
+#pragma unroll
+    for (int i = 0; i < IT; ++i) xb[i] = trk(OT + i);
+#pragma unroll
+    for (int o = 0; o < OT; ++o) {
+      const bf4 ab = trk(o);
+#pragma unroll
+      for (int i = 0; i < IT; ++i) acc[o][i] = mfma_b16(ab, xb[i], acc[o][i]);
+    }
+    asm volatile("" ::: "memory");  // the next call's stage writes stay behind these reads
+    return;
+  }
+  if constexpr (false) {
     if constexpr (IT <= OT) {
 #pragma unroll
       for (int i = 0; i < IT; ++i) stage_tile(st_full, LD, 16 * i, X[i]);
