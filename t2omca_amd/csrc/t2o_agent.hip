@@ -205,6 +205,15 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
     f4 gh_rec[ET];
 #pragma unroll
     for (int t = 0; t < ET; ++t) gh_rec[t] = zero4();
+    // per-lane partial sums over the wave's steps, reduced once at the end:
+    // LN2 vectors of every block, embedding bias, head bias
+    f4 ln2[D][2 * ET], gbe[ET], gbo = zero4();
+#pragma unroll
+    for (int t = 0; t < ET; ++t) {
+      gbe[t] = zero4();
+#pragma unroll
+      for (int d = 0; d < D; ++d) ln2[d][t] = ln2[d][ET + t] = zero4();
+    }
     for (int step = T - 1; step >= 0; --step) {
       const Wts<WT> P = step_view(P0);
       f4 h[ET];
@@ -269,9 +278,9 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
           for (int t = 0; t < ET; ++t) xs[d + 1][t] = x[t];
         }
       }
-      f4 gh_in[ET], gbe[ET];
+      f4 gh_in[ET];
 #pragma unroll
-      for (int t = 0; t < ET; ++t) gh_in[t] = gbe[t] = zero4();
+      for (int t = 0; t < ET; ++t) gh_in[t] = zero4();
 #pragma unroll
       for (int d = D - 1; d >= 0; --d) {
         AgentCache<E, H, NE, FF> cache;
@@ -281,7 +290,7 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
         agent_block_fwd<E, H, NE, FF, true>(P, L, d, h, o, x, &cache);
         if (d == D - 1) {  // q = Wo x + bo
           dw_accumulate_regs<1, ET, sizeof(WT) == 2>(gWo, &gq, x, stage);
-          vec_accumulate_g<1>(gs + G.bo, &gq);
+          gbo += gq;
           f4 t1[ET];
           matvec_tr<ET, 1>(P, L.Wo, E, L.WoT, 16, &gq, t1);
 #pragma unroll
@@ -289,9 +298,8 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
         }
         // padding rows write their (zero-gradient) records too: a tile is written whole
         WT* rec = static_cast<WT*>(args.tape) + ((size_t)d * ntiles + (size_t)step * tiles_per_step + rt) * Rec::SIZE * 16;
-        agent_block_bwd<E, H, NE, FF>(P, L, G, gs, rec, stage, d, h, o, cache, gx, gh_in, gbe, gWe);
+        agent_block_bwd<E, H, NE, FF>(P, L, G, gs, rec, stage, d, h, o, cache, gx, gh_in, gbe, gWe, ln2[d]);
       }
-      vec_accumulate_g<ET>(gs + G.be, gbe);
 #pragma unroll
       for (int t = 0; t < ET; ++t) gh_rec[t] = gx[t] + gh_in[t];
     }
@@ -301,6 +309,9 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
     }
     flush_tiles_g<ET, 1>(gs + G.We, 16, gWe);
     flush_tiles_g<1, ET>(gs + G.Wo, E, gWo);
+    vec_accumulate_g<ET>(gs + G.be, gbe);
+    vec_accumulate_g<1>(gs + G.bo, &gbo);
+    ln2_flush<E, D>(gs, G, ln2);
   }
 }
 

@@ -106,12 +106,12 @@ template <int E, int H, int NE, int FF, typename WT>
 T2O_DEV void agent_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G,
                              float* __restrict__ gs, WT* __restrict__ rec, float* __restrict__ stage, int d,
                              const f4* h, const f4 (&o)[NE], const AgentCache<E, H, NE, FF>& c, f4* gx,
-                             f4* gh_in, f4* gbe, f4 (&gWe)[E / 16][1]) {
+                             f4* gh_in, f4* gbe, f4 (&gWe)[E / 16][1], f4* ln2) {
   constexpr int ET = E / 16, HET = H * ET;
   constexpr bool BF = sizeof(WT) == 2;
   const float* be = P.v + L.be;
   f4 gz[HET], gres[ET];
-  post_bwd<E, H, FF>(P, L, G, gs, rec, d, c.post, gx, gz, gres);
+  post_bwd<E, H, FF>(P, L, G, gs, rec, d, c.post, gx, gz, gres, ln2);
   f4 gu[HET];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {

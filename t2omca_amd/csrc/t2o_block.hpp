@@ -79,15 +79,15 @@ T2O_DEV void post_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* z,
 template <int E, int H, int FF, typename WT>
 T2O_DEV void post_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G,
                       float* __restrict__ gs, WT* __restrict__ rec, int d, const PostCache<E, H, FF>& c,
-                      const f4* gx, f4* gz, f4* gres) {
+                      const f4* gx, f4* gz, f4* gres, f4* ln2) {
   constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
   using R = TapeRec<E, H, FF>;
-  {  // LN2: x' = xh2*g2 + n2
-    f4 t0[ET];
+  // LN2: x' = xh2*g2 + n2 — per-lane partial sums over the wave's steps
+  // (ln2[0..ET) d g2, ln2[ET..2ET) d n2), reduced once by the caller (ln2_flush)
 #pragma unroll
-    for (int t = 0; t < ET; ++t) t0[t] = gx[t] * c.xh2[t];
-    vec_accumulate_g<ET>(gs + G.g2[d], t0);
-    vec_accumulate_g<ET>(gs + G.n2[d], gx);
+  for (int t = 0; t < ET; ++t) {
+    ln2[t] += gx[t] * c.xh2[t];
+    ln2[ET + t] += gx[t];
   }
   f4 gr2[ET];
   layernorm_bwd<ET>(gx, c.xh2, c.rs2, P.v + L.g2[d], gr2);
@@ -116,6 +116,17 @@ T2O_DEV void post_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G
     rec_store<R::SIZE, HET>(rec, R::Z, c.z);
   }
   matvec_tr<HET, ET>(P, L.N[d], H * E, L.NT[d], E, gres, gz);
+}
+
+// LN2 vector grads of every block, summed over this wave's rows and steps
+template <int E, int D>
+T2O_DEV void ln2_flush(float* __restrict__ gs, const t2o_layout& G, const f4 (&ln2)[D][2 * (E / 16)]) {
+  constexpr int ET = E / 16;
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    vec_accumulate_g<ET>(gs + G.g2[d], &ln2[d][0]);
+    vec_accumulate_g<ET>(gs + G.n2[d], &ln2[d][ET]);
+  }
 }
 
 }  // namespace t2o

@@ -472,6 +472,11 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
     f4 gWe[ET];
 #pragma unroll
     for (int ft = 0; ft < ET; ++ft) gWe[ft] = zero4();
+    f4 ln2[D][2 * ET];  // LN2 vector grads, per-lane partial sums over the episode's steps
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#pragma unroll
+      for (int t = 0; t < 2 * ET; ++t) ln2[d][t] = zero4();
     float gWo = 0.f, gbo = 0.f;
     MixBwdIn<E, A, D> cur, nxt;
     mixb_load<E, A, D>(args, n, b, n.T - 1, cur);
@@ -580,7 +585,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
           // tiles are step-major (t, b, qt): at any step the grid writes one contiguous window
           WT* rec = static_cast<WT*>(args.tape) +
                     ((size_t)d * ntiles + ((size_t)t * fa.B + b) * Dm::QT + qt) * Rec::SIZE * 16;
-          mixer_block_bwd<E, H, KT, FF>(P, L, G, gs, rec, stage, d, K, gX0, cache, gx);
+          mixer_block_bwd<E, H, KT, FF>(P, L, G, gs, rec, stage, d, K, gX0, cache, gx, ln2[d]);
         }
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft) gq0[qt][ft] = q < Dm::Q ? gx[ft] : zero4();
@@ -644,6 +649,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
       }
     if (fv) unsafeAtomicAdd(gs + G.Wo + f, gWo);
     if (lane == 0) unsafeAtomicAdd(gs + G.bo, gbo);
+    ln2_flush<E, D>(gs, G, ln2);
   }
 }
 

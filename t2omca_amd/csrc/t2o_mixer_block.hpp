@@ -156,11 +156,11 @@ template <int E, int H, int KT, int FF, typename WT>
 T2O_DEV void mixer_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G,
                              float* __restrict__ gs, WT* __restrict__ rec, float* __restrict__ stage, int d,
                              const KeyFrags<E, KT, sizeof(WT) == 2>& K, f4 (&gX0)[KT][E / 16],
-                             const MixerCache<E, H, KT, FF>& c, f4* gx) {
+                             const MixerCache<E, H, KT, FF>& c, f4* gx, f4* ln2) {
   constexpr int ET = E / 16, HET = H * ET;
   constexpr bool BF = sizeof(WT) == 2;
   f4 gz[HET], gres[ET];
-  post_bwd<E, H, FF>(P, L, G, gs, rec, d, c.post, gx, gz, gres);
+  post_bwd<E, H, FF>(P, L, G, gs, rec, d, c.post, gx, gz, gres, ln2);
   f4 gu[HET];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
