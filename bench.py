@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=16, help="episodes in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--mode", choices=("train", "forward"), default="train",
+                    help="train: the TD update (the BASELINE metric); forward: online agent + mixer "
+                         "unroll only (configs[1], inference over a replay batch)")
     ap.add_argument("--serial", action="store_true",
                     help="no side-stream overlap: every kernel's HIP-event time is its isolated cost")
     ap.add_argument("--print-workload-tag", action="store_true",
@@ -143,8 +146,21 @@ def main():
     learner = TDLearner(agent, mixer, target_update_interval=10 ** 9, precision=args.dtype,
                         overlap=not args.serial)
     batch, w = make_batch(B, T, A, seed=1 + rank, device=dev)
+    if args.mode == "forward":
+        from t2omca_amd import ops
+        act = batch["actions"][..., 0]
+        ops.pack_params(learner.sa, learner.params[:learner.na], learner.pack_a)
+        ops.pack_params(learner.sm, learner.params[learner.na:], learner.pack_m)
+
+        def step(i):
+            q, h = ops.agent_unroll_fwd(learner.sa, learner.pack_a, batch["obs"])
+            ops.mixer_unroll_fwd(learner.sm, learner.pack_m, batch["state"], h, qmode_on=1, q_on=q, actions=act,
+                                 T_on=T, want_xout=False)
+    else:
+        def step(i):
+            learner.train(batch, 0, i, per_weight=w)
     for i in range(args.warmup):
-        learner.train(batch, 0, i, per_weight=w)
+        step(i)
     timer = KernelTimer()
     learner.timer = timer
     torch.cuda.synchronize()
@@ -153,7 +169,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        learner.train(batch, 0, i, per_weight=w)
+        step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -164,6 +180,21 @@ def main():
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
+    if args.mode == "forward":
+        value = world * B * (T + 1) * A * args.steps / elapsed
+        out = {"metric": "agent-transitions/sec for agent+mixer forward (inference over a replay batch)",
+               "value": value, "unit": "agent-transitions/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+               "data": "synthetic (SURVEY.md §8 d distributions, resident in HBM)",
+               "config": {"workload": f"configs[1]-style: online agent (t=0..T) + online mixer (t<T) unroll, "
+                                      f"{A} AGVs, batch {B} episodes/GPU x T={T}",
+                          "global_batch": B * world, "seq_len": T, "agents": A}}
+        if rank == 0:
+            print(json.dumps(out), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     transitions = world * B * T * A * args.steps
     value = transitions / elapsed
     kern = {k: sum(v) / len(v) for k, v in timer.durations().items()}

@@ -416,79 +416,45 @@ T2O_DEV void dw_accumulate(float* __restrict__ ldsW, int ldw, const f4* dY, cons
 template <int OT, int IT, bool BF = false>
 T2O_DEV void dw_accumulate_regs(f4 (&acc)[OT][IT], const f4* dY, const f4* X, float* stage) {
   constexpr int NS = OT < IT ? OT : IT;
-  constexpr int LD = StageDims<NS>::LD;
-  float* st_full = stage;
-  float* st_tile = stage + 16 * LD;
   const int c = lane_c(), g = lane_g();
   if constexpr (BF) {
-    // bf16: every operand tile is staged once as [16 rows][16 features] bf16
-    // (one 8-byte write per lane) and read back transposed with one
-    // ds_read_b64_tr_b16 — lane (g, c) gets feature c of rows 4g..4g+3, which
-    // is the 16x16x16 K-slice over rows of both operands.
-    static_assert((OT + IT) * 128 <= StageDims<NS>::FLOATS, "stage too small");
+    // bf16: operand tiles are staged as [16 rows][16 features] bf16 (one
+    // 8-byte write per lane) and read back transposed with one
+    // ds_read_b64_tr_b16 — lane (g, c) gets feature c of rows 4g..4g+3, the
+    // 16x16x16 K-slice over rows.  The X side is staged whole, dY one tile at
+    // a time (so the stage holds IT + 1 tiles).
+    static_assert((IT + 1) * 128 <= StageDims<NS>::FLOATS, "stage too small");
     __bf16* sb = reinterpret_cast<__bf16*>(stage);
-#pragma unroll
-    for (int o = 0; o < OT; ++o) *reinterpret_cast<bf4*>(sb + o * 256 + c * 16 + 4 * g) = to_bf4(dY[o]);
-#pragma unroll
-    for (int i = 0; i < IT; ++i) *reinterpret_cast<bf4*>(sb + (OT + i) * 256 + c * 16 + 4 * g) = to_bf4(X[i]);
-    asm volatile("" ::: "memory");  // a wave's LDS accesses complete in order; keep the compiler's order too
     typedef __attribute__((address_space(3))) s4v lds_s4v;
+    auto stw = [&](int j, f4 v) { *reinterpret_cast<bf4*>(sb + j * 256 + c * 16 + 4 * g) = to_bf4(v); };
     auto trk = [&](int j) {
       const __bf16* p = sb + j * 256 + (4 * g + (c >> 2)) * 16 + 4 * (c & 3);
       return __builtin_bit_cast(bf4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(p)));
     };
+#pragma unroll
+    for (int i = 0; i < IT; ++i) stw(1 + i, X[i]);
     bf4 xb[IT];
 #pragma unroll
-    for (int i = 0; i < IT; ++i) xb[i] = trk(OT + i);
-#pragma unroll
     for (int o = 0; o < OT; ++o) {
-      const bf4 ab = trk(o);
+      stw(0, dY[o]);
+      asm volatile("" ::: "memory");  // a wave's LDS accesses complete in order; keep the compiler's order too
+      if (o == 0) {
+#pragma unroll
+        for (int i = 0; i < IT; ++i) xb[i] = trk(1 + i);
+      }
+      const bf4 ab = trk(0);
+      asm volatile("" ::: "memory");
 #pragma unroll
       for (int i = 0; i < IT; ++i) acc[o][i] = mfma_b16(ab, xb[i], acc[o][i]);
     }
-    asm volatile("" ::: "memory");  // the next call's stage writes stay behind these reads
     return;
   }
-  if constexpr (false) {
-    if constexpr (IT <= OT) {
-#pragma unroll
-      for (int i = 0; i < IT; ++i) stage_tile(st_full, LD, 16 * i, X[i]);
-#pragma unroll
-      for (int o = 0; o < OT; ++o) {
-        stage_tile(st_tile, 16, 0, dY[o]);
-        f4 a;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) a[j] = st_tile[(4 * g + j) * 16 + c];
-        const bf4 ab = to_bf4(a);
-#pragma unroll
-        for (int i = 0; i < IT; ++i) {
-          f4 b;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) b[j] = st_full[(4 * g + j) * LD + 16 * i + c];
-          acc[o][i] = mfma_b16(ab, to_bf4(b), acc[o][i]);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int o = 0; o < OT; ++o) stage_tile(st_full, LD, 16 * o, dY[o]);
-#pragma unroll
-      for (int i = 0; i < IT; ++i) {
-        stage_tile(st_tile, 16, 0, X[i]);
-        f4 b;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) b[j] = st_tile[(4 * g + j) * 16 + c];
-        const bf4 bb = to_bf4(b);
-#pragma unroll
-        for (int o = 0; o < OT; ++o) {
-          f4 a;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) a[j] = st_full[(4 * g + j) * LD + 16 * o + c];
-          acc[o][i] = mfma_b16(to_bf4(a), bb, acc[o][i]);
-        }
-      }
-    }
-    return;
-  }
+  // fp32: the side with fewer tiles is staged whole (row stride ≡ 16 mod 32
+  // floats), the other streamed one 16x16 tile at a time; MFMA step s consumes
+  // rows 4s..4s+3 (k = lane group g)
+  constexpr int LD = StageDims<NS>::LD;
+  float* st_full = stage;
+  float* st_tile = stage + 16 * LD;
   if constexpr (IT <= OT) {
 #pragma unroll
     for (int i = 0; i < IT; ++i) stage_tile(st_full, LD, 16 * i, X[i]);

@@ -1,8 +1,9 @@
 // t2o_dispatch.hpp — runtime (E, H, D, n_ent, FF) -> compile-time kernel instance.
 //
-// Instantiated shapes: the reference defaults used by BASELINE configs 1-3
-// (emb 32, 3 heads, depth 2, ff_hidden_mult 4, 8 or 16 AGVs) plus the small
-// shapes of the golden fixtures.  Anything else returns T2O_EUNSUPPORTED
+// Instantiated shapes: the reference defaults used by BASELINE configs 1-4
+// (emb 32, 3 heads, depth 2, ff_hidden_mult 4, 8, 16 or 64 AGVs) plus the
+// small shapes of the golden fixtures.  (64 AGVs runs the generic code with
+// register spills: correct, not tuned — DESIGN.md §9.)  Anything else returns T2O_EUNSUPPORTED
 // (the Python side raises; there is no fallback path).
 #pragma once
 
@@ -20,4 +21,5 @@
     else T2O_CASE(32, 3, 2, 3, 128, STMT)                                  \
     else T2O_CASE(32, 3, 2, 8, 128, STMT)                                  \
     else T2O_CASE(32, 3, 2, 16, 128, STMT)                                 \
+    else T2O_CASE(32, 3, 2, 64, 128, STMT)                                 \
   } while (0)

@@ -439,7 +439,7 @@ struct MixBwdDims {
   static constexpr int PERW = Dm::X0F + WORK;
 };
 
-template <int E, int H, int D, int A, int FF, typename WT>
+template <int E, int H, int D, int A, int FF, bool WLDS, typename WT>
 __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   using Dm = MixDims<E, A>;
   using Bd = MixBwdDims<E, A>;
@@ -455,7 +455,10 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   float* GOUTB = Bd::GOUT ? WORK : WORK;        // head grads (rows of OUT layout)
   float* stage = WORK + Bd::GOUT;               // staging / gX0 region
   float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
-  const Wts<WT> P0 = stage_weights(smem, n.pack, L, sizeof(WT) == 4 ? L.fwd_total : L.total, WT{});
+  // the pack (its transposed copies included in bf16 mode) in LDS when it fits
+  // beside the per-wave buffers, else read through L2 (large mixers)
+  const Wts<WT> P0 = WLDS ? stage_weights(smem, n.pack, L, sizeof(WT) == 4 ? L.fwd_total : L.total, WT{})
+                          : global_weights(n.pack, L, WT{});
   for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) gs[i] = 0.f;
   __syncthreads();
   const int b = blockIdx.x * args.waves + w;
@@ -659,14 +662,23 @@ int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t 
   const t2o_layout& L = args.f.L;
   args.lds_w = (int)((lds_weight_floats<WT>(L, sizeof(WT) == 4 ? L.fwd_total : L.total) + 15) / 16 * 16);
   size_t lds = 0;
+  bool wlds = true;
   for (args.waves = 4; args.waves >= 1; args.waves >>= 1) {
     lds = sizeof(float) * ((size_t)args.lds_w + args.waves * PERW);
     if (lds <= 160 * 1024) break;
   }
-  if (args.waves < 1) return T2O_EUNSUPPORTED;
+  if (args.waves < 1) {  // weights from L2, 4 or fewer waves of per-episode buffers
+    wlds = false;
+    args.lds_w = 0;
+    for (args.waves = 4; args.waves >= 1; args.waves >>= 1) {
+      lds = sizeof(float) * (size_t)args.waves * PERW;
+      if (lds <= 160 * 1024) break;
+    }
+    if (args.waves < 1) return T2O_EUNSUPPORTED;
+  }
   const int grid = (args.f.B + args.waves - 1) / args.waves;
   if (grid > max_slabs) return T2O_EINVAL;
-  auto kern = mixer_bwd_kernel<E, H, D, A, FF, WT>;
+  auto kern = wlds ? mixer_bwd_kernel<E, H, D, A, FF, true, WT> : mixer_bwd_kernel<E, H, D, A, FF, false, WT>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * args.waves), lds, stream, args);
   *nslab = grid;

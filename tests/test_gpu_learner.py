@@ -31,7 +31,7 @@ def _setup(A, seed=0):
     return agent, mixer, pa, pm
 
 
-@pytest.mark.parametrize("A,B,T,lam", [(8, 6, 5, 0.6), (3, 5, 4, 0.0)])
+@pytest.mark.parametrize("A,B,T,lam", [(8, 6, 5, 0.6), (3, 5, 4, 0.0), (16, 3, 4, 0.6), (64, 2, 3, 0.6)])
 def test_td_update_matches_oracle(A, B, T, lam):
     require_gpu()
     from t2omca_amd.learner import TDLearner
