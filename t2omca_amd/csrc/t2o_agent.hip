@@ -7,7 +7,10 @@
 // carries their hidden state in registers across all timesteps (no inter-
 // workgroup synchronisation at all).  A second network (the target agent) can
 // run in the same launch on the same observations (blockIdx.y).
+#include <type_traits>
+
 #include "t2o_agent_block.hpp"
+#include "t2o_agent_block_ch.hpp"
 #include "t2o_dispatch.hpp"
 #include "t2o_layout.hpp"
 
@@ -68,25 +71,35 @@ __global__ __launch_bounds__(64 * AG_FWD_WAVES) void agent_fwd_kernel(AgentFwdAr
 #pragma unroll
   for (int t = 0; t < ET; ++t) h[t] = net.h0 ? ld4(net.h0 + (size_t)row * E + 16 * t + 4 * g) : zero4();
 
-  // observations of the next step are loaded while the current one computes
-  auto load_obs = [&](int step, f4 (&o)[NE]) {
-    const float* ob = args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * NE * F;
+  // few entities: the observations live in registers, the next step's loaded
+  // while the current one computes; many entities: streamed per block in
+  // chunks (t2o_agent_block_ch.hpp)
+  constexpr bool CHUNK = NE > AG_CHUNK_MIN;
+  constexpr int NO = CHUNK ? 1 : NE;
+  auto row_obs = [&](int step) {
+    return args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * NE * F;
+  };
+  auto load_obs = [&](int step, f4 (&o)[NO]) {
+    const float* ob = row_obs(step);
 #pragma unroll
-    for (int j = 0; j < NE; ++j)
+    for (int j = 0; j < NO; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int f = 4 * g + r;
         o[j][r] = f < F ? ob[j * F + f] : 0.f;
       }
   };
-  f4 on[NE];
-  load_obs(0, on);
+  f4 on[NO];
+  if constexpr (!CHUNK) load_obs(0, on);
   for (int step = 0; step < args.T; ++step) {
     const Wts<WT> P = step_view(P0);
-    f4 o[NE];
+    f4 o[NO];
+    if constexpr (!CHUNK) {
 #pragma unroll
-    for (int j = 0; j < NE; ++j) o[j] = on[j];
-    if (step + 1 < args.T) load_obs(step + 1, on);
+      for (int j = 0; j < NE; ++j) o[j] = on[j];
+      if (step + 1 < args.T) load_obs(step + 1, on);
+    }
+    const ObsRow orow{row_obs(step), F};
     f4 x[ET];
 #pragma unroll
     for (int t = 0; t < ET; ++t) x[t] = h[t];
@@ -97,7 +110,12 @@ __global__ __launch_bounds__(64 * AG_FWD_WAVES) void agent_fwd_kernel(AgentFwdAr
 #pragma unroll
         for (int t = 0; t < ET; ++t) st4(hm + 16 * t + 4 * g, x[t]);
       }
-      agent_block_fwd<E, H, NE, FF, false>(P, L, d, h, o, x, nullptr);
+      if constexpr (CHUNK) {
+        agent_block_fwd_ch<E, H, NE, FF, false>(P, L, d, h, orow, x, nullptr);
+      } else {
+        (void)orow;
+        agent_block_fwd<E, H, NE, FF, false>(P, L, d, h, o, x, nullptr);
+      }
     }
     f4 q = zero4();
 #pragma unroll
@@ -222,14 +240,19 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
 #pragma unroll
       for (int t = 0; t < ET; ++t) h[t] = hp ? ld4(hp + 16 * t + 4 * g) : zero4();
       const float* ob = args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * NE * F;
-      f4 o[NE];
+      constexpr bool CHUNK = NE > AG_CHUNK_MIN;  // many entities: streamed per block (t2o_agent_block_ch.hpp)
+      constexpr int NO = CHUNK ? 1 : NE;
+      const ObsRow orow{ob, F};
+      f4 o[NO];
+      if constexpr (!CHUNK) {
 #pragma unroll
-      for (int j = 0; j < NE; ++j)
+        for (int j = 0; j < NE; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int f = 4 * g + r;
-          o[j][r] = f < F ? ob[j * F + f] : 0.f;
-        }
+          for (int r = 0; r < 4; ++r) {
+            const int f = 4 * g + r;
+            o[j][r] = f < F ? ob[j * F + f] : 0.f;
+          }
+      }
       // external grads of this step
       const size_t sidx = ((size_t)b * T + step) * A + a;
       f4 gq = zero4();
@@ -273,7 +296,8 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
           f4 x[ET];
 #pragma unroll
           for (int t = 0; t < ET; ++t) x[t] = xs[d][t];
-          agent_block_fwd<E, H, NE, FF, false>(P, L, d, h, o, x, nullptr);
+          if constexpr (CHUNK) agent_block_fwd_ch<E, H, NE, FF, false>(P, L, d, h, orow, x, nullptr);
+          else agent_block_fwd<E, H, NE, FF, false>(P, L, d, h, o, x, nullptr);
 #pragma unroll
           for (int t = 0; t < ET; ++t) xs[d + 1][t] = x[t];
         }
@@ -283,11 +307,12 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
       for (int t = 0; t < ET; ++t) gh_in[t] = zero4();
 #pragma unroll
       for (int d = D - 1; d >= 0; --d) {
-        AgentCache<E, H, NE, FF> cache;
+        typename std::conditional<CHUNK, AgentCacheCh<E, H, NE, FF>, AgentCache<E, H, NE, FF>>::type cache;
         f4 x[ET];
 #pragma unroll
         for (int t = 0; t < ET; ++t) x[t] = xs[d][t];
-        agent_block_fwd<E, H, NE, FF, true>(P, L, d, h, o, x, &cache);
+        if constexpr (CHUNK) agent_block_fwd_ch<E, H, NE, FF, true>(P, L, d, h, orow, x, &cache);
+        else agent_block_fwd<E, H, NE, FF, true>(P, L, d, h, o, x, &cache);
         if (d == D - 1) {  // q = Wo x + bo
           dw_accumulate_regs<1, ET, sizeof(WT) == 2>(gWo, &gq, x, stage);
           gbo += gq;
@@ -298,7 +323,10 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
         }
         // padding rows write their (zero-gradient) records too: a tile is written whole
         WT* rec = static_cast<WT*>(args.tape) + ((size_t)d * ntiles + (size_t)step * tiles_per_step + rt) * Rec::SIZE * 16;
-        agent_block_bwd<E, H, NE, FF>(P, L, G, gs, rec, stage, d, h, o, cache, gx, gh_in, gbe, gWe, ln2[d]);
+        if constexpr (CHUNK)
+          agent_block_bwd_ch<E, H, NE, FF>(P, L, G, gs, rec, stage, d, h, orow, cache, gx, gh_in, gbe, gWe, ln2[d]);
+        else
+          agent_block_bwd<E, H, NE, FF>(P, L, G, gs, rec, stage, d, h, o, cache, gx, gh_in, gbe, gWe, ln2[d]);
       }
 #pragma unroll
       for (int t = 0; t < ET; ++t) gh_rec[t] = gx[t] + gh_in[t];
