@@ -47,9 +47,12 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=16, help="episodes in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--mode", choices=("train", "forward"), default="train",
+    ap.add_argument("--mode", choices=("train", "forward", "rollout"), default="train",
                     help="train: the TD update (the BASELINE metric); forward: online agent + mixer "
-                         "unroll only (configs[1], inference over a replay batch)")
+                         "unroll only (configs[1], inference over a replay batch); rollout: closed-loop "
+                         "env step + agent step + ε-greedy over --envs envs per GPU (configs[4])")
+    ap.add_argument("--envs", type=int, default=8192, help="rollout mode: envs per GPU")
+    ap.add_argument("--mecs", type=int, default=2, help="rollout mode: MEC servers")
     ap.add_argument("--serial", action="store_true",
                     help="no side-stream overlap: every kernel's HIP-event time is its isolated cost")
     ap.add_argument("--print-workload-tag", action="store_true",
@@ -121,6 +124,49 @@ def cpu_baseline(args):
                       f"min of {len(times)} updates after 1 warm-up, torch CPU fp32, {threads} threads"}
 
 
+def rollout_bench(args, world, rank, dev):
+    """configs[4]: every rank steps its own shard of envs (no collective)."""
+    from t2omca_amd.env import VecEnv
+    from t2omca_amd.modules import TransformerAgent
+    from t2omca_amd.runner import RolloutRunner
+    from t2omca_amd.synthetic import make_args
+    A, T, n = args.agents, args.T, args.envs
+    torch.manual_seed(0)
+    agent = TransformerAgent(None, make_args(A, device=str(dev))).to(dev)
+    env = VecEnv(n, mec_num=args.mecs, agv_num=A, episode_limit=T, seed=1 + rank, device=dev)
+    runner = RolloutRunner(agent, env, seed=rank)
+    for _ in range(args.warmup):
+        runner.run(new_buffers=False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        runner.run(new_buffers=False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    env_steps = world * n * T * args.steps
+    out = {"metric": "agent-transitions/sec for closed-loop rollout (env step + agent step + eps-greedy)",
+           "value": env_steps * A / elapsed, "unit": "agent-transitions/s", "env_steps_per_s": env_steps / elapsed,
+           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "fp32 agent, fp64 env", "data": "simulated (VecEnv, env_spec stand-ins)",
+           "config": {"workload": f"configs[4]: {n} envs/GPU x {A} AGVs x {args.mecs} MEC, episode {T} steps, "
+                                  "one rollout per step", "global_envs": n * world, "agents": A}}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if args.print_workload_tag:
@@ -139,6 +185,8 @@ def main():
     from t2omca_amd.synthetic import make_args, make_batch
 
     A, T, B = args.agents, args.T, args.batch
+    if args.mode == "rollout":
+        return rollout_bench(args, world, rank, dev)
     torch.manual_seed(0)
     margs = make_args(A, device=str(dev))
     agent = TransformerAgent(None, margs).to(dev)

@@ -248,6 +248,17 @@ int t2o_env_run(int mode, const double* spec, void* const* state, void* const* o
                 const int64_t* actions, int64_t act_se, int NE, int A, int M, int C, int QMAX, int T,
                 uint64_t seed, void* stream);
 
+/* ε-greedy action selection (the reference's controller is
+ * absent, contract parallel_runner.py:121 with PyMARL's EpsilonGreedyActionSelector).
+ * q f32 [rows][NA], avail i32 [rows][NA] (rows = envs x agents, dense) ->
+ * actions i64 [rows]: argmax of q over available actions (first maximum), or
+ * with probability epsilon a uniformly drawn available action.  Draws:
+ * u1 = U(seed, row, 2*counter), u2 = U(seed, row, 2*counter+1) of the
+ * env_spec.uniforms stream; random action = floor(u2 * n_avail)-th available.
+ * NA <= 32. */
+int t2o_select_actions(const float* q, const int32_t* avail, int64_t* actions, int64_t rows, int NA,
+                       double epsilon, uint64_t seed, int64_t counter, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -67,6 +67,8 @@ EXPORTS = {
     "t2o_probe_lane_ops": (ctypes.c_int, [ctypes.c_void_p] * 3),
     "t2o_env_run": (ctypes.c_int, [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_int64] +
                     [ctypes.c_int] * 6 + [ctypes.c_uint64, ctypes.c_void_p]),
+    "t2o_select_actions": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_int, ctypes.c_double,
+                                                                 ctypes.c_uint64, ctypes.c_int64, ctypes.c_void_p]),
 }
 
 _lib = None

@@ -80,8 +80,9 @@ class VecEnv:
             arr[i] = None if t is None else t.data_ptr()
         return arr
 
-    def _run(self, mode, actions=None, n_envs=None):
-        out = self._ptrs([self.obs, self.obs64, self.state, self.avail, self.reward, self.terminated,
+    def _run(self, mode, actions=None, n_envs=None, dest=None):
+        d = self._dest(dest)
+        out = self._ptrs([d["obs"], self.obs64, d["state"], d["avail"], self.reward, self.terminated,
                           self.info, self.ack])
         act_p, act_se = None, 0
         if actions is not None:
@@ -92,6 +93,18 @@ class VecEnv:
                                stream_ptr(self.device))
         check(rc, "env_run")
 
+    def _dest(self, dest):
+        """Output buffers of one launch: the env's own, or caller-provided dense
+        [n_envs, ...] slices (e.g. one timestep of a time-major replay batch)."""
+        d = {"obs": self.obs, "state": self.state, "avail": self.avail}
+        if dest:
+            for k, t in dest.items():
+                ref = d[k]
+                if t.shape != ref.shape or t.dtype != ref.dtype or t.device != self.device or not t.is_contiguous():
+                    raise ValueError(f"dest[{k!r}] must be a dense {tuple(ref.shape)} {ref.dtype} device tensor")
+                d[k] = t
+        return d
+
     # -- worker protocol, batched ------------------------------------------------------
     def get_env_info(self, all_envs=False):
         """get_env_info (:421-439) on env 0, as the runner does once at start-up (:34);
@@ -101,19 +114,23 @@ class VecEnv:
                     n_agents=self.A, episode_limit=self.T, n_entities=self.A, obs_entity_feats=9,
                     state_entity_feats=8)
 
-    def reset(self):
-        self._run(1)
-        return self.state, self.avail, self.obs
+    def reset(self, dest=None):
+        """dest: optional dict of output buffers {"obs", "state", "avail"} (dense)."""
+        self._run(1, dest=dest)
+        d = self._dest(dest)
+        return d["state"], d["avail"], d["obs"]
 
-    def step(self, actions):
-        """actions: int64 [n_envs, A] on the device (rows may be strided views)."""
+    def step(self, actions, dest=None):
+        """actions: int64 [n_envs, A] on the device (rows may be strided views);
+        dest: optional dict of output buffers {"obs", "state", "avail"} (dense)."""
         if actions.dtype != torch.int64 or actions.device != self.device or actions.dim() != 2:
             raise TypeError("actions must be an int64 [n_envs, A] device tensor")
         if actions.shape != (self.n_envs, self.A) or actions.stride(1) != 1:
             raise ValueError(f"actions must be [{self.n_envs}, {self.A}] with unit agent stride")
-        self._run(2, actions=actions)
+        self._run(2, actions=actions, dest=dest)
+        d = self._dest(dest)
         info = {k: self.info[:, i] for i, k in enumerate(INFO_KEYS)}
-        return self.reward, self.terminated.bool(), info, self.state, self.avail, self.obs
+        return self.reward, self.terminated.bool(), info, d["state"], d["avail"], d["obs"]
 
     # -- state views (tests / diagnostics) ----------------------------------------------
     @property

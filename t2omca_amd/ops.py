@@ -312,3 +312,21 @@ def adam_step(params, grads, exp_avg, exp_avg_sq, step, *, lr=1e-3, betas=(0.9, 
                               float(weight_decay), float(max_grad_norm), int(step), ptr(grad_div),
                               ptr(grad_norm_out),
                               stream_ptr()), "adam_step")
+
+
+def select_actions(q, avail, epsilon=0.0, seed=0, counter=0, out=None):
+    """ε-greedy actions (include/t2omca.h t2o_select_actions): q f32 [..., NA] and
+    avail i32 [..., NA], dense; returns int64 [...] (or writes `out`)."""
+    _dev(q)
+    if avail.dtype != torch.int32 or not avail.is_cuda:
+        raise TypeError("avail must be an int32 HIP-device tensor")
+    NA = q.shape[-1]
+    assert q.is_contiguous() and avail.is_contiguous() and avail.shape == q.shape
+    rows = q.numel() // NA
+    if out is None:
+        out = torch.empty(q.shape[:-1], dtype=torch.int64, device=q.device)
+    assert out.is_contiguous() and out.numel() == rows and out.dtype == torch.int64
+    check(lib().t2o_select_actions(ptr(q), ptr(avail), ptr(out), rows, NA, float(epsilon),
+                                   ctypes.c_uint64(int(seed) & ((1 << 64) - 1)), int(counter), stream_ptr()),
+          "select_actions")
+    return out
