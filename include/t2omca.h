@@ -259,6 +259,24 @@ int t2o_env_run(int mode, const double* spec, void* const* state, void* const* o
 int t2o_select_actions(const float* q, const int32_t* avail, int64_t* actions, int64_t rows, int NA,
                        double epsilon, uint64_t seed, int64_t counter, void* stream);
 
+/* Prioritized episode replay (the reference's buffer is
+ * absent, contract per_run.py:143-146,216-238, PyMARL2 proportional PER).
+ * p f32 [n] = stored priority**alpha of the n valid episodes.  Sample batch
+ * indices by stratified proportional search (mass_k = (u_k + k) * Σp / batch,
+ * u_k = U(seed, k, counter)) with IS weights (p_i/Σp*n)^-beta normalised by
+ * the weight of min p; workspace: t2o_per_workspace_doubles(n) doubles. */
+int64_t t2o_per_workspace_doubles(int64_t capacity);
+int t2o_per_sample(const float* p, int64_t n, int64_t batch, double beta, uint64_t seed, int64_t counter,
+                   double* workspace, int64_t* idx_out, float* w_out, void* stream);
+/* p[idx[k]] = (prio[k] + eps)**alpha; *max_prio = max(*max_prio, prio[k] + eps). */
+int t2o_per_update(float* p, const int64_t* idx, const float* prio, int64_t n, float alpha, float eps,
+                   float* max_prio, void* stream);
+/* dst + k*dst_stride <- src + idx[k]*src_stride, row_bytes each (rows <= 65535;
+ * copied in the widest of 16/8/4/1-byte units the alignment allows): the
+ * episode gather of a sampled batch. */
+int t2o_gather_rows(const void* src, int64_t src_stride, const int64_t* idx, int64_t rows, void* dst,
+                    int64_t dst_stride, int64_t row_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
