@@ -64,6 +64,18 @@ def workload_tag(args):
     return f"b{args.batch}_t{args.T}_a{args.agents}_{args.dtype}"
 
 
+def train_config_name(A, B, T):
+    """Which BASELINE config a TD-update run is (the learner's shapes depend on the
+    AGV count only: entities = agents, state = 8 features per AGV)."""
+    if (A, B, T) == (8, 1024, 60):
+        return "configs[2]"
+    if A == 64:
+        return "configs[3]-shape (64 AGVs, per-GPU shard)"
+    if B == 32:
+        return "configs[0]-shape (batch 32)"
+    return "configs[2]-style"
+
+
 class KernelTimer:
     """HIP events around each phase of TDLearner.train (same stream as the launches)."""
 
@@ -271,7 +283,7 @@ def main():
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (SURVEY.md §8 d distributions, seeded per rank, resident in HBM)",
-        "config": {"workload": "configs[2]: full TD update fwd+bwd+Adam, 8 AGVs x 4 MEC, "
+        "config": {"workload": f"{train_config_name(A, B, T)}: full TD update fwd+bwd+Adam, {A} AGVs, "
                                f"batch {B} episodes/GPU x T={T}",
                    "global_batch": B * world, "seq_len": T, "agents": A, "emb": 32, "heads": 3, "depth": 2,
                    "parallelism": f"dp{world}"},
