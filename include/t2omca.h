@@ -210,7 +210,8 @@ int t2o_adam_workspace_floats(void);
 
 /* Diagnostic: runs the cross-lane primitives the kernels rely on (4-lane
  * all-reduces via ds_bpermute and via gfx950 permlane swaps, 16-lane DPP row
- * sums) on in[64]; writes 6 x 64 results (tests/test_gpu_primitives.py). */
+ * sums, the batched all-reduce) on in[64]; writes 20 x 64 results
+ * (tests/test_gpu_primitives.py). */
 int t2o_probe_lane_ops(const float* in, float* out, void* stream);
 
 /* Sum nslab partial gradient slabs [nslab][n] into out[n] (out = sum, overwritten). */

@@ -43,8 +43,15 @@ inline int rows_per_wave(int R) { return (void)R, 16; }
 
 constexpr int AG_FWD_WAVES = 4;  // waves per workgroup sharing one LDS copy of the weights
 
+// Up to 8 entities the forward fits 256 VGPRs: capping it there (2 waves per
+// SIMD's worth of registers) keeps the MFMA results in VGPRs instead of
+// accumulation registers the compiler would otherwise copy them out of.
+template <int NE>
+constexpr int agent_fwd_waves_per_eu() { return NE <= 8 ? 2 : 1; }
+
 template <int E, int H, int D, int NE, int FF, bool WLDS, typename WT>
-__global__ __launch_bounds__(64 * AG_FWD_WAVES) void agent_fwd_kernel(AgentFwdArgs args) {
+__global__ __launch_bounds__(64 * AG_FWD_WAVES) __attribute__((amdgpu_waves_per_eu(agent_fwd_waves_per_eu<NE>())))
+void agent_fwd_kernel(AgentFwdArgs args) {
   constexpr int ET = E / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const AgentNet net = args.net[blockIdx.y];

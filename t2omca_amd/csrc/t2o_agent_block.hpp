@@ -53,13 +53,17 @@ T2O_DEV void agent_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const
       cpart += (ut[0] * bt[0] + ut[1] * bt[1]) + (ut[2] * bt[2] + ut[3] * bt[3]);
       s0part += (ut[0] * h[t][0] + ut[1] * h[t][1]) + (ut[2] * h[t][2] + ut[3] * h[t][3]);
     }
-    const float cval = allsum4(cpart);
-    p[0] = allsum4(s0part);
+    // [c, s_0, w·o_1 .. w·o_NE] reduced over the lane groups in one batch
+    float red[NE + 2];
+    red[0] = cpart;
+    red[1] = s0part;
 #pragma unroll
-    for (int j = 0; j < NE; ++j) {
-      const float sp = (w[0] * o[j][0] + w[1] * o[j][1]) + (w[2] * o[j][2] + w[3] * o[j][3]);
-      p[j + 1] = allsum4(sp) + cval;
-    }
+    for (int j = 0; j < NE; ++j) red[j + 2] = (w[0] * o[j][0] + w[1] * o[j][1]) + (w[2] * o[j][2] + w[3] * o[j][3]);
+    allsum4_n(red);
+    const float cval = red[0];
+    p[0] = red[1];
+#pragma unroll
+    for (int j = 0; j < NE; ++j) p[j + 1] = red[j + 2] + cval;
     float m = p[0];
 #pragma unroll
     for (int j = 1; j <= NE; ++j) m = fmaxf(m, p[j]);
@@ -128,19 +132,22 @@ T2O_DEV void agent_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_la
       gh_in[t] += p0 * gzh[t];
       gbe[t] += c.Ps[hh] * gzh[t];
     }
-    const float gp0 = allsum4(gp0p);
-    const float gP = allsum4(gPp);
     f4 goh;
     matvec_tr<1, ET>(P, L.We, 16, L.WeT, E, gzh, &goh);
     dw_accumulate_regs<ET, 1, BF>(gWe, gzh, &c.oh[hh], stage);
-    // softmax backward over [token 0, entities]
-    float gp[NE + 1];
-    gp[0] = gp0;
+    // softmax backward over [token 0, entities]; [gP, gp_0, goh·o_j] reduced in one batch
+    float red[NE + 2];
+    red[0] = gPp;
+    red[1] = gp0p;
 #pragma unroll
-    for (int j = 0; j < NE; ++j) {
-      const float sp = (goh[0] * o[j][0] + goh[1] * o[j][1]) + (goh[2] * o[j][2] + goh[3] * o[j][3]);
-      gp[j + 1] = allsum4(sp) + gP;
-    }
+    for (int j = 0; j < NE; ++j)
+      red[j + 2] = (goh[0] * o[j][0] + goh[1] * o[j][1]) + (goh[2] * o[j][2] + goh[3] * o[j][3]);
+    allsum4_n(red);
+    const float gP = red[0];
+    float gp[NE + 1];
+    gp[0] = red[1];
+#pragma unroll
+    for (int j = 0; j < NE; ++j) gp[j + 1] = red[j + 2] + gP;
     float dot = 0.f;
 #pragma unroll
     for (int j = 0; j <= NE; ++j) dot += c.p[hh][j] * gp[j];

@@ -254,6 +254,47 @@ T2O_DEV float allmax4_fast(float v) { return xor32_max(xor16_max(v)); }
 T2O_DEV float allsum4(float v) { return allsum4_fast(v); }
 T2O_DEV float allmax4(float v) { return allmax4_fast(v); }
 
+// allsum4 of N independent values at once, in place, bit-identical to N
+// allsum4 calls ((v_g0 + v_g1) + (v_g2 + v_g3) in every lane of the row).
+// Values are reduced in fours: permlane16_swap(a, b) leaves (a, b) pair sums in
+// alternating rows, permlane32_swap of two such registers leaves the four row
+// totals one per row group ([A, B, C, D]), and three swaps broadcast them back
+// — 12 VALU per 4 values instead of 24 (no copies needed in the reduction half
+// since the operands are distinct).
+T2O_DEV uint32_t f2u(float v) { return __float_as_uint(v); }
+T2O_DEV float u2f(uint32_t v) { return __uint_as_float(v); }
+T2O_DEV float pair_sum16(float a, float b) {  // [a01, b01, a23, b23]
+  const auto r = __builtin_amdgcn_permlane16_swap(f2u(a), f2u(b), false, false);
+  return u2f(r[0]) + u2f(r[1]);
+}
+template <int N>
+T2O_DEV void allsum4_n(float (&v)[N]) {
+  int i = 0;
+#pragma unroll
+  for (; i + 4 <= N; i += 4) {
+    const float ab = pair_sum16(v[i], v[i + 1]), cd = pair_sum16(v[i + 2], v[i + 3]);
+    const auto q = __builtin_amdgcn_permlane32_swap(f2u(ab), f2u(cd), false, false);
+    const float w = u2f(q[0]) + u2f(q[1]);  // [A, B, C, D]
+    const auto x = __builtin_amdgcn_permlane16_swap(f2u(w), f2u(w), false, false);  // [A,A,C,C], [B,B,D,D]
+    const auto y = __builtin_amdgcn_permlane32_swap(x[0], x[0], false, false);      // [A..], [C..]
+    const auto z = __builtin_amdgcn_permlane32_swap(x[1], x[1], false, false);      // [B..], [D..]
+    v[i] = u2f(y[0]);
+    v[i + 1] = u2f(z[0]);
+    v[i + 2] = u2f(y[1]);
+    v[i + 3] = u2f(z[1]);
+  }
+  if constexpr (N % 4 >= 2) {
+    const float ab = pair_sum16(v[i], v[i + 1]);
+    const auto q = __builtin_amdgcn_permlane32_swap(f2u(ab), f2u(ab), false, false);
+    const float u = u2f(q[0]) + u2f(q[1]);  // [A, B, A, B]
+    const auto x = __builtin_amdgcn_permlane16_swap(f2u(u), f2u(u), false, false);
+    v[i] = u2f(x[0]);
+    v[i + 1] = u2f(x[1]);
+    i += 2;
+  }
+  if constexpr (N % 2) v[i] = allsum4(v[i]);
+}
+
 // Sum over the 16 lanes of a row with DPP (VALU only); the total lands in the
 // row's last lane (c == 15) — other lanes hold partial sums.
 template <int CTRL, int BANK>
@@ -306,8 +347,10 @@ T2O_DEV void layernorm_bwd(const f4* gout, const f4* xhat, float rstd,
     const f4 p = gx[t] * xhat[t];
     s2 += (p[0] + p[1]) + (p[2] + p[3]);
   }
-  const float m1 = allsum4(s1) * inv_e;
-  const float m2 = allsum4(s2) * inv_e;
+  float s[2] = {s1, s2};
+  allsum4_n(s);
+  const float m1 = s[0] * inv_e;
+  const float m2 = s[1] * inv_e;
 #pragma unroll
   for (int t = 0; t < ET; ++t) gin[t] = (gx[t] - m1 - xhat[t] * m2) * rstd;
 }

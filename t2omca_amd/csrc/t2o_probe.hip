@@ -1,5 +1,6 @@
 // t2o_probe.hip — on-device checks of the cross-lane primitives the kernels use
-// (semantics of DPP row reductions and gfx950 permlane swaps are verified by
+// (semantics of DPP row reductions, gfx950 permlane swaps and the batched
+// all-reduce are verified by
 // tests/test_gpu_primitives.py against host-computed expectations).
 #include "t2o_common.hpp"
 
@@ -15,6 +16,15 @@ __global__ void probe_kernel(const float* __restrict__ in, float* __restrict__ o
   out[3 * 64 + l] = rowsum16_fast(v);
   out[4 * 64 + l] = allmax4_shfl(v);
   out[5 * 64 + l] = allmax4_fast(v);
+  // batched all-reduce (7 = one group of four, a pair, a single) vs one at a time
+  float b[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) b[k] = in[(l + 9 * k) % 64] * (float)(k + 1);
+#pragma unroll
+  for (int k = 0; k < 7; ++k) out[(13 + k) * 64 + l] = allsum4(b[k]);
+  allsum4_n(b);
+#pragma unroll
+  for (int k = 0; k < 7; ++k) out[(6 + k) * 64 + l] = b[k];
 }
 }  // namespace
 
