@@ -7,6 +7,7 @@
 // carries their hidden state in registers across all timesteps (no inter-
 // workgroup synchronisation at all).  A second network (the target agent) can
 // run in the same launch on the same observations (blockIdx.y).
+#include <cstdlib>
 #include <type_traits>
 
 #include "t2o_agent_block.hpp"
@@ -350,6 +351,272 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
   }
 }
 
+// ---------------------------------------------------------------------------
+// BPTT with the blocks on separate waves (depth 2, block inputs stored by the
+// forward).  The single-wave kernel above issues, per step, the forward
+// recompute and the backward of both blocks back to back on one SIMD, and with
+// one 16-row tile per wave (8,192 rows = 512 waves) it leaves half the SIMDs
+// idle.  Here each tile gets two waves: wave "d" owns block d (its forward
+// recompute, cache and backward) and the two interleave so that one's recompute
+// overlaps the other's backward (phases separated by workgroup barriers):
+//   block-1 wave:  fwd(T-1) | bwd(T-1) | fwd(T-2) | bwd(T-2) | ...
+//   block-0 wave:     -     | fwd(T-1) | bwd(T-1) | fwd(T-2) | ...
+// Per step the dependent work is bwd1 -> bwd0 -> bwd1 ..., exchanged through
+// LDS (per lane: grad wrt the block-1 input and the block-1 key/value grad of h,
+// 1 -> 0; the recurrent grad wrt h_{t-1}, 0 -> 1), one workgroup barrier per
+// phase.  The backward of a block is the same code as in the single-wave
+// kernel, so records, slabs and the head grads are identical in meaning.
+// T2O_AGENT_BWD=single selects the single-wave kernel (A/B timing, parity cross-check)
+inline bool agent_bwd_single_wave() {
+  static const bool single = [] {
+    const char* e = getenv("T2O_AGENT_BWD");
+    return e && e[0] == 's';
+  }();
+  return single;
+}
+
+constexpr int AGP_TILES = AG_BWD_WAVES;
+
+#ifdef T2O_PHASE_PROF
+// diagnostic builds only (tools/build_variant.sh <name> -DT2O_PHASE_PROF): per-phase
+// cycle counts of one workgroup, read back with t2o_prof_read
+__device__ long long t2o_prof_buf[64 * 2 * 4 * 4];
+#endif  // tiles per workgroup (same slab count as the single-wave kernel)
+
+template <int E>
+constexpr int agp_xch_floats() { return 3 * (E / 16) * 64 * 4; }
+
+// Layout whose block-0 slots hold block d's offsets: the block code is then
+// called with the constant d = 0, and every offset it reads is a scalar.
+T2O_DEV t2o_layout block_view(const t2o_layout& L, int d) {
+  t2o_layout V = L;
+  V.M[0] = L.M[d];
+  V.MT[0] = L.MT[d];
+  V.N[0] = L.N[d];
+  V.NT[0] = L.NT[d];
+  V.bu[0] = L.bu[d];
+  V.g1[0] = L.g1[d];
+  V.n1[0] = L.n1[d];
+  V.W1[0] = L.W1[d];
+  V.W1T[0] = L.W1T[d];
+  V.c1[0] = L.c1[d];
+  V.W2[0] = L.W2[d];
+  V.W2T[0] = L.W2T[d];
+  V.c2[0] = L.c2[d];
+  V.g2[0] = L.g2[d];
+  V.n2[0] = L.n2[d];
+  return V;
+}
+
+template <int E, int H, int D, int NE, int FF, typename WT>
+__global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(AgentBwdArgs args) {
+  static_assert(D == 2, "one wave per block of a depth-2 stack");
+  constexpr int ET = E / 16;
+  constexpr int STAGE = StageDims<1>::FLOATS;
+  constexpr bool BF = sizeof(WT) == 2;
+  constexpr bool CHUNK = NE > AG_CHUNK_MIN;
+  constexpr int NO = CHUNK ? 1 : NE;
+  using Rec = TapeRec<E, H, FF>;
+  using Cache = typename std::conditional<CHUNK, AgentCacheCh<E, H, NE, FF>, AgentCache<E, H, NE, FF>>::type;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const t2o_layout& L = args.L;
+  const t2o_layout& G = args.G;
+  const int64_t nw = sizeof(WT) == 4 ? L.fwd_total : L.total;
+  const int lds_w = (int)((lds_weight_floats<WT>(L, nw) + 15) / 16 * 16);
+  // wave-uniform by construction; readfirstlane tells the compiler, so the block's
+  // layout offsets (L.M[d] ...) are scalar loads, not per-lane global loads
+  const int w = __builtin_amdgcn_readfirstlane(wave_id());
+  const int d = w & 1;   // the block this wave owns
+  const int tl = w >> 1; // tile within the workgroup
+  const t2o_layout Lb = block_view(L, d), Gb = block_view(G, d);
+  float* stage = smem + lds_w + w * STAGE;
+  f4* xch = reinterpret_cast<f4*>(smem + lds_w + 2 * AGP_TILES * STAGE + tl * agp_xch_floats<E>());
+  const int lane = threadIdx.x & 63;
+  float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
+  const Wts<WT> P0 = stage_weights(smem, args.pack, L, nw, WT{});
+  for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) gs[i] = 0.f;
+  __syncthreads();
+
+  const int A = args.A, F = args.F, T = args.T;
+  const int R = args.B * A;
+  const int rt = blockIdx.x * AGP_TILES + tl;
+  const int c = lane_c(), g = lane_g();
+  const bool tile_ok = rt * 16 < R;
+  const int row_raw = rt * 16 + c;
+  const bool valid = row_raw < R;
+  const int row = valid ? row_raw : R - 1;
+  const int b = row / A, a = row % A;
+  const size_t tiles_per_step = (size_t)(R + 15) / 16;
+  const size_t ntiles = (size_t)T * tiles_per_step;
+  // exchange slots: 0 grad wrt block-1 input, 1 block-1 K/V grad of h, 2 grad wrt h_{t-1}
+  auto xput = [&](int k, const f4* v) {
+#pragma unroll
+    for (int t = 0; t < ET; ++t) xch[(k * ET + t) * 64 + lane] = v[t];
+  };
+  auto xget = [&](int k, f4* v) {
+#pragma unroll
+    for (int t = 0; t < ET; ++t) v[t] = xch[(k * ET + t) * 64 + lane];
+  };
+
+  f4 gWe[ET][1], gWo[1][ET], gbe[ET], ln2[2 * ET], gbo = zero4();
+#pragma unroll
+  for (int t = 0; t < ET; ++t) {
+    gWe[t][0] = gWo[0][t] = gbe[t] = zero4();
+    ln2[t] = ln2[ET + t] = zero4();
+  }
+  // Both roles run the same loop body "recompute step; barrier; backward step;
+  // barrier"; the block-0 wave starts one barrier late, so its recompute of a
+  // step overlaps the block-1 backward of the same step and its backward the
+  // block-1 recompute of the next (earlier) one.  The cache lives within one
+  // iteration.  (Loading the next step's inputs a phase ahead measured no
+  // faster: the loads' latency is not on the barrier-paced critical path.)
+  auto load_fwd_inputs = [&](int step, f4* hh, f4 (&oo)[NO], f4* xx) {
+    const float* hp = step == 0 ? (args.h0 ? args.h0 + (size_t)row * E : nullptr)
+                                : args.h_seq + (((size_t)b * args.h_ts + step - 1) * A + a) * E;
+#pragma unroll
+    for (int t = 0; t < ET; ++t) hh[t] = hp ? ld4(hp + 16 * t + 4 * g) : zero4();
+    if constexpr (!CHUNK) {
+      const float* obp = args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * NE * F;
+#pragma unroll
+      for (int j = 0; j < NE; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int f = 4 * g + r;
+          oo[j][r] = f < F ? obp[j * F + f] : 0.f;
+        }
+    }
+    if (d == 0) {
+#pragma unroll
+      for (int t = 0; t < ET; ++t) xx[t] = hh[t];
+    } else {
+      const float* hm = args.hmid + (((size_t)b * args.h_ts + step) * (D - 1) * A + a) * E;
+#pragma unroll
+      for (int t = 0; t < ET; ++t) xx[t] = ld4(hm + 16 * t + 4 * g);
+    }
+  };
+  if (d == 0) __syncthreads();
+  for (int step = T - 1; step >= 0; --step) {
+    Cache cache;
+    f4 h[ET], o[NO], xo[ET];
+    load_fwd_inputs(step, h, o, xo);
+    const float* ob = args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * NE * F;
+    // this step's grads arriving at the stack output (block-1 wave): dL/dh_t from
+    // the mixer and dL/dq_t (the recurrent part of dL/dh_t comes from block 0)
+    f4 ghx[ET], gq = zero4();
+    if (d == 1) {
+      const size_t sidx = ((size_t)b * T + step) * A + a;
+#pragma unroll
+      for (int t = 0; t < ET; ++t) ghx[t] = args.gh ? ld4(args.gh + sidx * E + 16 * t + 4 * g) : zero4();
+      if (args.gq) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * g + r < L.NA) gq[r] = args.gq[sidx * L.NA + 4 * g + r];
+      }
+      if (args.gchosen) {
+        const int64_t act = args.actions[b * args.act_sb + step * args.act_st + a];
+        const float gc = args.gchosen[sidx];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * g + r == act) gq[r] += gc;
+      }
+    }
+#pragma unroll
+    for (int ph = 0; ph < 2; ++ph) {
+      T2O_MARK(0);
+      const Wts<WT> P = step_view(P0);
+      if (ph == 0) {
+#ifdef T2O_PHASE_PROF
+        __builtin_amdgcn_s_waitcnt(0);
+#endif
+        T2O_MARK(1);
+        if constexpr (CHUNK) agent_block_fwd_ch<E, H, NE, FF, true>(P, Lb, 0, h, ObsRow{ob, F}, xo, &cache);
+        else agent_block_fwd<E, H, NE, FF, true>(P, Lb, 0, h, o, xo, &cache);
+      } else {
+        f4 gx[ET], ghi[ET];
+        if (d == 1) {
+          if (step < T - 1) xget(2, gx);
+          else {
+#pragma unroll
+            for (int t = 0; t < ET; ++t) gx[t] = zero4();
+          }
+#pragma unroll
+          for (int t = 0; t < ET; ++t) gx[t] += ghx[t];
+          if (!valid) {
+            gq = zero4();
+#pragma unroll
+            for (int t = 0; t < ET; ++t) gx[t] = zero4();
+          }
+          // q = Wo x + bo on the stack output
+          dw_accumulate_regs<1, ET, BF>(gWo, &gq, xo, stage);
+          gbo += gq;
+          f4 t1[ET];
+          matvec_tr<ET, 1>(P, L.Wo, E, L.WoT, 16, &gq, t1);
+#pragma unroll
+          for (int t = 0; t < ET; ++t) {
+            gx[t] += t1[t];
+            ghi[t] = zero4();
+          }
+        } else {
+          xget(0, gx);
+          xget(1, ghi);
+        }
+#ifdef T2O_PHASE_PROF
+        __builtin_amdgcn_s_waitcnt(0);
+#endif
+        T2O_MARK(1);
+        WT* rec = tile_ok ? static_cast<WT*>(args.tape) +
+                                ((size_t)d * ntiles + (size_t)step * tiles_per_step + rt) * Rec::SIZE * 16
+                          : nullptr;
+        if constexpr (CHUNK)
+          agent_block_bwd_ch<E, H, NE, FF>(P, Lb, Gb, gs, rec, stage, 0, h, ObsRow{ob, F}, cache, gx, ghi, gbe, gWe,
+                                           ln2);
+        else
+          agent_block_bwd<E, H, NE, FF>(P, Lb, Gb, gs, rec, stage, 0, h, o, cache, gx, ghi, gbe, gWe, ln2);
+        if (d == 1) {
+          xput(0, gx);
+          xput(1, ghi);
+        } else {
+          f4 grec[ET];
+#pragma unroll
+          for (int t = 0; t < ET; ++t) grec[t] = gx[t] + ghi[t];
+          xput(2, grec);
+          if (step == 0 && args.gh0 && valid) {
+#pragma unroll
+            for (int t = 0; t < ET; ++t) st4(args.gh0 + (size_t)row * E + 16 * t + 4 * g, grec[t]);
+          }
+        }
+      }
+      T2O_MARK(3);
+      __syncthreads();
+      T2O_MARK(4);
+#ifdef T2O_PHASE_PROF
+      if (blockIdx.x == 7 && lane == 0 && T - 1 - step < 64) {
+        long long* pb = t2o_prof_buf + (((T - 1 - step) * 2 + ph) * 4 + w) * 4;
+        for (int m = 0; m < 4; ++m) pb[m] = t2o_mark_buf[w][m + 1] - t2o_mark_buf[w][m];
+      }
+#endif
+    }
+  }
+  if (d == 1) __syncthreads();
+  if (tile_ok) {
+    flush_tiles_g<ET, 1>(gs + G.We, 16, gWe);
+    vec_accumulate_g<ET>(gs + G.be, gbe);
+    vec_accumulate_g<ET>(gs + Gb.g2[0], &ln2[0]);
+    vec_accumulate_g<ET>(gs + Gb.n2[0], &ln2[ET]);
+    if (d == 1) {
+      flush_tiles_g<1, ET>(gs + G.Wo, E, gWo);
+      vec_accumulate_g<1>(gs + G.bo, &gbo);
+    }
+  }
+}
+
+template <int E, int H, int D, int NE, int FF, typename WT>
+size_t bwd_pipe_lds_bytes(const t2o_layout& L) {
+  const int64_t nw = sizeof(WT) == 4 ? L.fwd_total : L.total;
+  return sizeof(float) * ((size_t)(lds_weight_floats<WT>(L, nw) + 15) / 16 * 16 +
+                          2 * AGP_TILES * StageDims<1>::FLOATS + AGP_TILES * agp_xch_floats<E>());
+}
+
 template <int E, int H, int D, int NE, int FF, typename WT>
 int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
   const int R = args.B * args.A;
@@ -357,6 +624,16 @@ int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream
   const int tiles = (R + args.rpw - 1) / args.rpw;
   const int grid = (tiles + AG_BWD_WAVES - 1) / AG_BWD_WAVES;
   if (grid > max_slabs) return T2O_EINVAL;
+  if constexpr (D == 2) {
+    const size_t lds = bwd_pipe_lds_bytes<E, H, D, NE, FF, WT>(args.L);
+    if (args.hmid && lds <= 160 * 1024 && !agent_bwd_single_wave()) {
+      auto kern = agent_bwd_pipe_kernel<E, H, D, NE, FF, WT>;
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * 2 * AGP_TILES), lds, stream, args);
+      *nslab = grid;
+      return (int)hipGetLastError();
+    }
+  }
   const int64_t nw = sizeof(WT) == 4 ? args.L.fwd_total : args.L.total;
   const size_t lds =
       sizeof(float) * ((size_t)(lds_weight_floats<WT>(args.L, nw) + 15) / 16 * 16 + AG_BWD_WAVES * StageDims<1>::FLOATS);
@@ -439,6 +716,12 @@ extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, cons
                              : launch_bwd<E_, H_, D_, NE_, FF_, float>(args, max_slabs, nslab, (hipStream_t)stream)));
   return rc;
 }
+
+#ifdef T2O_PHASE_PROF
+extern "C" int t2o_prof_read(long long* host_out) {
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(t2o_prof_buf), sizeof(t2o_prof_buf));
+}
+#endif
 
 extern "C" int t2o_agent_bwd_max_slabs(int B, int A) {
   const int rpw = rows_per_wave(B * A);

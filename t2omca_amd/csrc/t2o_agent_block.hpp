@@ -98,6 +98,7 @@ T2O_DEV void agent_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const
 #pragma unroll
     for (int t = 0; t < HET; ++t) cache->u[t] = u[t];
   }
+  T2O_MARK(2);
   post_fwd<E, H, FF, CACHE>(P, L, d, z, x, CACHE ? &cache->post : nullptr);
 }
 
@@ -116,6 +117,7 @@ T2O_DEV void agent_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_la
   const float* be = P.v + L.be;
   f4 gz[HET], gres[ET];
   post_bwd<E, H, FF>(P, L, G, gs, rec, d, c.post, gx, gz, gres, ln2);
+  T2O_MARK(2);
   f4 gu[HET];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {

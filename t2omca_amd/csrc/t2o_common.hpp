@@ -39,6 +39,19 @@ T2O_DEV f4 zero4() { return f4{0.f, 0.f, 0.f, 0.f}; }
 // otherwise keeps every layer's weight fragments live at once and spills.
 #define T2O_FENCE() __builtin_amdgcn_sched_barrier(0)
 
+// Diagnostic builds only (-DT2O_PHASE_PROF): cycle stamps of one workgroup's waves
+#ifdef T2O_PHASE_PROF
+__device__ long long t2o_mark_buf[8][8];
+#define T2O_MARK(n)                                                                         \
+  do {                                                                                     \
+    if (blockIdx.x == 7 && (threadIdx.x & 63) == 0) t2o_mark_buf[threadIdx.x >> 6][n] = clock64(); \
+  } while (0)
+#else
+#define T2O_MARK(n) \
+  do {            \
+  } while (0)
+#endif
+
 T2O_DEV f4 mfma4(float a, float b, f4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
 }

@@ -118,23 +118,36 @@ T2O_DEV void mix_load(const MixerFwdArgs& a, const MixerNet& n, int b, int t, Mi
     const int i = lane + 64 * k;
     in.hid[k] = i < A * E / 4 ? ld4(hd + 4 * i) : zero4();
   }
-  if (lane < A) {
-    if (n.qmode == 0) {
-      in.qs[0] = n.qv_in[((size_t)b * n.T + t) * A + lane];
+  // per-agent inputs, lane a < A holds agent a's; branch-free: lanes >= A and
+  // action slots >= NA load an in-bounds duplicate and discard it (selects, not
+  // exec-masked loads — this runs every step on the recurrence's critical path)
+  const int la = lane < A ? lane : A - 1;
+  if (n.qmode == 0) {
+    in.qs[0] = n.qv_in[((size_t)b * n.T + t) * A + la];
+  } else {
+    const int NA = a.n_actions;
+    const size_t qrow = (((size_t)b * a.q_ts + t) * A + la) * NA;
+#pragma unroll
+    for (int k = 0; k < MIX_MAXNA; ++k) {
+      const float v = n.qsel[qrow + (k < NA ? k : NA - 1)];
+      in.qs[k] = k < NA ? v : 0.f;
+    }
+    if (n.qmode == 1) {
+      in.act = (int)a.actions[b * a.act_sb + t * a.act_st + la];
+    } else if (a.avail) {
+      const int32_t* av = a.avail + b * a.av_sb + t * a.av_st + la * NA;
+#pragma unroll
+      for (int k = 0; k < MIX_MAXNA; ++k) {
+        const int kk = k < NA ? k : NA - 1;
+        const float q = a.qarg[qrow + kk];
+        const int ok = av[kk];
+        in.qa[k] = k < NA ? (ok == 0 ? -9999999.0f : q) : -INFINITY;
+      }
     } else {
-      const int NA = a.n_actions;
-      const size_t qrow = (((size_t)b * a.q_ts + t) * A + lane) * NA;
 #pragma unroll
-      for (int k = 0; k < MIX_MAXNA; ++k) in.qs[k] = k < NA ? n.qsel[qrow + k] : 0.f;
-      if (n.qmode == 1) {
-        in.act = (int)a.actions[b * a.act_sb + t * a.act_st + lane];
-      } else {
-        const int32_t* av = a.avail ? a.avail + b * a.av_sb + t * a.av_st + lane * NA : nullptr;
-#pragma unroll
-        for (int k = 0; k < MIX_MAXNA; ++k) {
-          const float q = k < NA ? a.qarg[qrow + k] : -INFINITY;
-          in.qa[k] = (k < NA && av && av[k] == 0) ? -9999999.0f : q;
-        }
+      for (int k = 0; k < MIX_MAXNA; ++k) {
+        const float q = a.qarg[qrow + (k < NA ? k : NA - 1)];
+        in.qa[k] = k < NA ? q : -INFINITY;
       }
     }
   }

@@ -19,6 +19,8 @@ def short(name):
     m = re.search(r"dw_gemm_kernel(?:<\d+, *\d+, *\d+, *\d+, *|ILi\d+ELi\d+ELi\d+ELi\d+ELi)(\d)", name)
     if m:
         return ("agent_dw", "mixer_dw")[int(m.group(1))]
+    if "agent_bwd_pipe_kernel" in name:
+        return "agent_bwd"
     for n in NAMES:
         if n in name:
             return n.replace("_kernel", "")
