@@ -16,164 +16,203 @@ using namespace t2o;
 
 namespace {
 
-enum SegKind : int {
-  SEG_COPY = 0,     // dst[i] = src[i]
-  SEG_PAD2D,        // dst[r][c] (R x C) = r<sr && c<sc ? src[r*sc + c] : 0
-  SEG_TPAD2D,       // dst[r][c] (R x C) = c<sr && r<sc ? src[c*sc + r] : 0   (transpose of src[sr][sc])
-  SEG_FOLD_M,       // dst[hE+i][k]   = s Σ_m Wk[hE+m][i] Wq[hE+m][k]
-  SEG_FOLD_MT,      // dst[k][hE+i]   = same value
-  SEG_FOLD_N,       // dst[o][hE+k]   = Σ_m U[o][hE+m] Wv[hE+m][k]
-  SEG_FOLD_NT,      // dst[hE+k][o]
-  SEG_ADD,          // dst[i] += src[i]
-  SEG_ADD_PAD2D,    // dst[r][c] (r<R, c<C, ld C) += src[r*sc + c]   (src rows padded: ld sc)
-  SEG_UNFOLD_WQ,    // dst(Wq)[hE+m][k] += s Σ_i Wk[hE+m][i] gM[hE+i][k]
-  SEG_UNFOLD_WK,    // dst(Wk)[hE+m][i] += s Σ_k Wq[hE+m][k] gM[hE+i][k]
-  SEG_UNFOLD_WV,    // dst(Wv)[hE+m][k] += Σ_o U[o][hE+m] gN[o][hE+k]
-  SEG_UNFOLD_U,     // dst(U)[o][hE+m]  += Σ_k gN[o][hE+k] Wv[hE+m][k]
+// One launch per call: a table of tasks, each a range of workgroups.
+//   elementwise tasks (copies, pads, transposes, grad adds): 1024 elements per
+//     workgroup, optionally also writing the bf16 image of a matrix entry;
+//   fold / unfold tasks: one workgroup per (block, head) E x E product, its
+//     operands staged in LDS (each output is an E-long dot product from LDS).
+enum TaskKind : int {
+  T_COPY = 0,     // dst[i] = src[a + i]
+  T_PAD2D,        // dst[r][c] (R x C) = r<sr && c<sc ? src[a + r*sc + c] : 0
+  T_TPAD2D,       // dst[r][c] (R x C) = c<sr && r<sc ? src[a + c*sc + r] : 0   (transpose of src[sr][sc])
+  T_ADD,          // dst[i] += src2[a + i]
+  T_ADD_PAD2D,    // dst[r][c] (R x C, ld C) += src2[a + r*sc + c]
+  T_FOLD_M,       // head h: M[hE+i][k] = MT[k][hE+i] = s Σ_m Wk[hE+m][i] Wq[hE+m][k]
+  T_FOLD_N,       // head h: N[o][hE+k] = NT[hE+k][o] = Σ_m U[o][hE+m] Wv[hE+m][k]
+  T_UNFOLD_QK,    // head h: gWq[hE+m][k] += s Σ_i Wk[hE+m][i] gM[hE+i][k]; gWk[hE+m][i] += s Σ_k Wq[hE+m][k] gM[hE+i][k]
+  T_UNFOLD_VU,    // head h: gWv[hE+m][k] += Σ_o U[o][hE+m] gN[o][hE+k];  gU[o][hE+m] += Σ_k gN[o][hE+k] Wv[hE+m][k]
 };
 
-struct Seg {
+struct Task {
   int kind;
-  int R, C;        // destination rows / cols (n = R*C)
-  int sr, sc;      // source dims (pad/transposes)
-  int64_t dst, a, b;  // float offsets: dst in dst buffer; a/b in source buffers
+  int R, C;          // elementwise: destination rows / cols
+  int sr, sc;        // source dims (pads / transposes)
+  int h, bf;         // head (fold tasks); bf: also write the bf16 image (ld = C)
+  int64_t dst, dst2; // destination offsets (fold: M and MT, or N and NT; unfold: the two grads)
+  int64_t a, b, c;   // source offsets
 };
 
-// One launch per table keeps the kernel-argument block well under 4 KiB.
-constexpr int MAX_SEGS = 24;
-struct SegTable {
-  int n;
-  int E, H;
+constexpr int MAX_TASKS = 40;
+constexpr int EW_PER_BLOCK = 1024;
+struct TaskTable {
+  int n, E, H;
   float scale;
-  Seg s[MAX_SEGS];
-  int64_t start[MAX_SEGS + 1];
+  Task t[MAX_TASKS];
+  int blk[MAX_TASKS + 1];  // first workgroup of each task
 };
 
-__global__ void seg_kernel(SegTable tab, const float* __restrict__ src, const float* __restrict__ src2,
-                           float* __restrict__ dst) {
-  const int64_t total = tab.start[tab.n];
-  for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-       idx += (int64_t)gridDim.x * blockDim.x) {
-    int k = 0;
-    while (idx >= tab.start[k + 1]) ++k;
-    const Seg sg = tab.s[k];
-    const int64_t li = idx - tab.start[k];
-    const int r = (int)(li / sg.C), cc = (int)(li % sg.C);
-    const int E = tab.E;
-    float v;
-    switch (sg.kind) {
-      case SEG_COPY: dst[sg.dst + li] = src[sg.a + li]; break;
-      case SEG_PAD2D:
-        dst[sg.dst + li] = (r < sg.sr && cc < sg.sc) ? src[sg.a + (int64_t)r * sg.sc + cc] : 0.f;
-        break;
-      case SEG_TPAD2D:
-        dst[sg.dst + li] = (cc < sg.sr && r < sg.sc) ? src[sg.a + (int64_t)cc * sg.sc + r] : 0.f;
-        break;
-      case SEG_FOLD_M:
-      case SEG_FOLD_MT: {
-        // value M[row][col] with row = hE+i, col = k
-        const int row = sg.kind == SEG_FOLD_M ? r : cc;
-        const int col = sg.kind == SEG_FOLD_M ? cc : r;
-        const int h = row / E, i = row % E;
-        const float* Wk = src + sg.a + (int64_t)h * E * E;
-        const float* Wq = src + sg.b + (int64_t)h * E * E;
-        float acc = 0.f;
-        for (int m = 0; m < E; ++m) acc = fmaf(Wk[m * E + i], Wq[m * E + col], acc);
-        dst[sg.dst + li] = acc * tab.scale;
-        break;
+T2O_DEV void put(float* dst, __bf16* dstb, int64_t off, int r, int col, int ld, float v, bool bf) {
+  dst[off + (int64_t)r * ld + col] = v;
+  if (bf) dstb[off + (int64_t)r * ld + (col ^ bf_swz(r, ld))] = (__bf16)v;
+}
+
+// an E x E operand (row stride ld) into LDS
+T2O_DEV void stage(float* s, const float* g, int E, int ld) {
+  for (int i = threadIdx.x; i < E * E; i += blockDim.x) s[i] = g[(int64_t)(i / E) * ld + i % E];
+}
+
+__global__ __launch_bounds__(256) void pack_kernel(TaskTable tab, const float* __restrict__ src,
+                                                   const float* __restrict__ src2, float* __restrict__ dst,
+                                                   __bf16* __restrict__ dstb) {
+  extern __shared__ float sm[];
+  int k = 0;
+  while ((int)blockIdx.x >= tab.blk[k + 1]) ++k;
+  const Task tk = tab.t[k];
+  const int lb = (int)blockIdx.x - tab.blk[k];
+  const int E = tab.E, HE = tab.H * E, h = tk.h;
+  const bool bf = tk.bf != 0;
+  switch (tk.kind) {
+    case T_COPY:
+    case T_PAD2D:
+    case T_TPAD2D:
+    case T_ADD:
+    case T_ADD_PAD2D: {
+      const int64_t n = (int64_t)tk.R * tk.C;
+      for (int64_t li = (int64_t)lb * EW_PER_BLOCK + threadIdx.x; li < n && li < (int64_t)(lb + 1) * EW_PER_BLOCK;
+           li += blockDim.x) {
+        const int r = (int)(li / tk.C), cc = (int)(li % tk.C);
+        float v;
+        if (tk.kind == T_COPY) v = src[tk.a + li];
+        else if (tk.kind == T_PAD2D) v = (r < tk.sr && cc < tk.sc) ? src[tk.a + (int64_t)r * tk.sc + cc] : 0.f;
+        else if (tk.kind == T_TPAD2D) v = (cc < tk.sr && r < tk.sc) ? src[tk.a + (int64_t)cc * tk.sc + r] : 0.f;
+        else if (tk.kind == T_ADD) v = dst[tk.dst + li] + src2[tk.a + li];
+        else v = dst[tk.dst + li] + src2[tk.a + (int64_t)r * tk.sc + cc];
+        put(dst, dstb, tk.dst, r, cc, tk.C, v, bf);
       }
-      case SEG_FOLD_N:
-      case SEG_FOLD_NT: {
-        const int o = sg.kind == SEG_FOLD_N ? r : cc;
-        const int hk = sg.kind == SEG_FOLD_N ? cc : r;
-        const int h = hk / E, kk = hk % E;
-        const int HE = tab.H * E;
-        const float* U = src + sg.a;
-        const float* Wv = src + sg.b + (int64_t)h * E * E;
-        float acc = 0.f;
-        for (int m = 0; m < E; ++m) acc = fmaf(U[(int64_t)o * HE + h * E + m], Wv[m * E + kk], acc);
-        dst[sg.dst + li] = acc;
-        break;
-      }
-      case SEG_ADD: dst[sg.dst + li] += src2[sg.a + li]; break;
-      case SEG_ADD_PAD2D: dst[sg.dst + li] += src2[sg.a + (int64_t)r * sg.sc + cc]; break;
-      case SEG_UNFOLD_WQ: {  // dst index (hE+m, k); src = params, src2 = gpack
-        const int h = r / E, m = r % E;
-        const float* Wk = src + sg.a + (int64_t)h * E * E;
-        const float* gM = src2 + sg.b + (int64_t)h * E * E;
-        float acc = 0.f;
-        for (int i = 0; i < E; ++i) acc = fmaf(Wk[m * E + i], gM[i * E + cc], acc);
-        dst[sg.dst + li] += acc * tab.scale;
-        break;
-      }
-      case SEG_UNFOLD_WK: {  // dst index (hE+m, i)
-        const int h = r / E, m = r % E;
-        const float* Wq = src + sg.a + (int64_t)h * E * E;
-        const float* gM = src2 + sg.b + (int64_t)h * E * E;
-        float acc = 0.f;
-        for (int kk = 0; kk < E; ++kk) acc = fmaf(Wq[m * E + kk], gM[cc * E + kk], acc);
-        dst[sg.dst + li] += acc * tab.scale;
-        break;
-      }
-      case SEG_UNFOLD_WV: {  // dst index (hE+m, k)
-        const int h = r / E, m = r % E;
-        const int HE = tab.H * E;
-        const float* U = src + sg.a;
-        const float* gN = src2 + sg.b;
-        float acc = 0.f;
-        for (int o = 0; o < E; ++o) acc = fmaf(U[(int64_t)o * HE + h * E + m], gN[(int64_t)o * HE + h * E + cc], acc);
-        dst[sg.dst + li] += acc;
-        break;
-      }
-      case SEG_UNFOLD_U: {  // dst index (o, hE+m)
-        const int h = cc / E, m = cc % E;
-        const int HE = tab.H * E;
-        const float* Wv = src + sg.a + (int64_t)h * E * E;
-        const float* gN = src2 + sg.b;
-        float acc = 0.f;
-        for (int kk = 0; kk < E; ++kk) acc = fmaf(gN[(int64_t)r * HE + h * E + kk], Wv[m * E + kk], acc);
-        dst[sg.dst + li] += acc;
-        break;
-      }
-      default: (void)v; break;
+      break;
     }
+    case T_FOLD_M: {  // a = Wk, b = Wq (params, [HE][E] row-major)
+      float* wk = sm;
+      float* wq = sm + E * E;
+      stage(wk, src + tk.a + (int64_t)h * E * E, E, E);
+      stage(wq, src + tk.b + (int64_t)h * E * E, E, E);
+      __syncthreads();
+      for (int o = threadIdx.x; o < E * E; o += blockDim.x) {
+        const int i = o / E, kk = o % E;
+        float acc = 0.f;
+        for (int m = 0; m < E; ++m) acc = fmaf(wk[m * E + i], wq[m * E + kk], acc);
+        acc *= tab.scale;
+        put(dst, dstb, tk.dst, h * E + i, kk, E, acc, bf);   // M  [HE][E]
+        put(dst, dstb, tk.dst2, kk, h * E + i, HE, acc, bf); // MT [E][HE]
+      }
+      break;
+    }
+    case T_FOLD_N: {  // a = U ([E][HE]), b = Wv ([HE][E])
+      float* u = sm;
+      float* wv = sm + E * E;
+      stage(u, src + tk.a + (int64_t)h * E, E, HE);
+      stage(wv, src + tk.b + (int64_t)h * E * E, E, E);
+      __syncthreads();
+      for (int o = threadIdx.x; o < E * E; o += blockDim.x) {
+        const int oo = o / E, kk = o % E;
+        float acc = 0.f;
+        for (int m = 0; m < E; ++m) acc = fmaf(u[oo * E + m], wv[m * E + kk], acc);
+        put(dst, dstb, tk.dst, oo, h * E + kk, HE, acc, bf);   // N  [E][HE]
+        put(dst, dstb, tk.dst2, h * E + kk, oo, E, acc, bf);   // NT [HE][E]
+      }
+      break;
+    }
+    case T_UNFOLD_QK: {  // a = Wq, b = Wk (params), c = gM (gpack [HE][E]); dst = gWq, dst2 = gWk
+      float* wq = sm;
+      float* wk = sm + E * E;
+      float* gm = sm + 2 * E * E;
+      stage(wq, src + tk.a + (int64_t)h * E * E, E, E);
+      stage(wk, src + tk.b + (int64_t)h * E * E, E, E);
+      stage(gm, src2 + tk.c + (int64_t)h * E * E, E, E);
+      __syncthreads();
+      for (int o = threadIdx.x; o < E * E; o += blockDim.x) {
+        const int m = o / E, kk = o % E;
+        float aq = 0.f, ak = 0.f;
+        for (int i = 0; i < E; ++i) {
+          aq = fmaf(wk[m * E + i], gm[i * E + kk], aq);  // gWq[m][kk]
+          ak = fmaf(wq[m * E + i], gm[kk * E + i], ak);  // gWk[m][kk] (kk plays i)
+        }
+        dst[tk.dst + (int64_t)(h * E + m) * E + kk] += aq * tab.scale;
+        dst[tk.dst2 + (int64_t)(h * E + m) * E + kk] += ak * tab.scale;
+      }
+      break;
+    }
+    case T_UNFOLD_VU: {  // a = U, b = Wv (params), c = gN (gpack [E][HE]); dst = gWv, dst2 = gU
+      float* u = sm;
+      float* wv = sm + E * E;
+      float* gn = sm + 2 * E * E;
+      stage(u, src + tk.a + (int64_t)h * E, E, HE);
+      stage(wv, src + tk.b + (int64_t)h * E * E, E, E);
+      stage(gn, src2 + tk.c + (int64_t)h * E, E, HE);
+      __syncthreads();
+      for (int o = threadIdx.x; o < E * E; o += blockDim.x) {
+        const int m = o / E, kk = o % E;
+        float av = 0.f, au = 0.f;
+        for (int j = 0; j < E; ++j) {
+          av = fmaf(u[j * E + m], gn[j * E + kk], av);   // gWv[m][kk] = Σ_o U[o][m] gN[o][kk]
+          au = fmaf(gn[m * E + j], wv[kk * E + j], au);  // gU[m][kk] = Σ_k gN[m][k] Wv[kk][k]  (m = o, kk = m')
+        }
+        dst[tk.dst + (int64_t)(h * E + m) * E + kk] += av;
+        dst[tk.dst2 + (int64_t)m * HE + h * E + kk] += au;
+      }
+      break;
+    }
+    default: break;
   }
 }
 
-void add(SegTable& t, int kind, int R, int C, int64_t dst, int64_t a, int64_t b = 0, int sr = 0, int sc = 0) {
-  Seg& s = t.s[t.n];
-  s.kind = kind; s.R = R; s.C = C; s.sr = sr; s.sc = sc; s.dst = dst; s.a = a; s.b = b;
-  t.start[t.n + 1] = t.start[t.n] + (int64_t)R * C;
-  t.n++;
-}
-
-int launch(const SegTable& t, const float* src, const float* src2, float* dst, void* stream) {
-  const int64_t total = t.start[t.n];
-  if (total == 0) return 0;
-  int blocks = (int)((total + 255) / 256);
-  if (blocks > 1024) blocks = 1024;
-  hipLaunchKernelGGL(seg_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, t, src, src2, dst);
-  return (int)hipGetLastError();
-}
-
-// bf16 image of the pack's matrices (round to nearest even), rows swizzled as
-// bf_swz prescribes; blockIdx.y = matrix.  Vector slots of the image stay unused.
-struct MatTable {
-  int n;
-  int64_t off[4 + 8 * T2O_MAX_DEPTH];
-  int rows[4 + 8 * T2O_MAX_DEPTH], ld[4 + 8 * T2O_MAX_DEPTH];
+// Collects tasks and launches them (several launches only when a table fills:
+// the kernel-argument block stays under 4 KiB).
+struct Builder {
+  TaskTable tab{};
+  int nb = 0, rc = 0;
+  const float* src;
+  const float* src2;
+  float* dst;
+  __bf16* dstb;
+  void* stream;
+  Builder(int E, int H, const float* s, const float* s2, float* d, __bf16* db, void* st)
+      : src(s), src2(s2), dst(d), dstb(db), stream(st) {
+    tab.E = E;
+    tab.H = H;
+    tab.scale = 1.0f / sqrtf((float)E);
+  }
+  Task& next(int blocks) {
+    if (tab.n == MAX_TASKS) flush();
+    Task& t = tab.t[tab.n];
+    t = Task{};
+    tab.blk[tab.n] = nb;
+    nb += blocks;
+    tab.blk[++tab.n] = nb;
+    return t;
+  }
+  void ew(int kind, int R, int C, int64_t dst_off, int64_t a, int sr = 0, int sc = 0, int bf = 0) {
+    Task& t = next((int)(((int64_t)R * C + EW_PER_BLOCK - 1) / EW_PER_BLOCK));
+    t.kind = kind; t.R = R; t.C = C; t.sr = sr; t.sc = sc; t.bf = bf; t.dst = dst_off; t.a = a;
+  }
+  void head(int kind, int h, int64_t dst_off, int64_t dst2_off, int64_t a, int64_t b, int64_t c = 0, int bf = 0) {
+    Task& t = next(1);
+    t.kind = kind; t.h = h; t.bf = bf; t.dst = dst_off; t.dst2 = dst2_off; t.a = a; t.b = b; t.c = c;
+  }
+  void flush() {
+    if (nb > 0 && rc == 0) {
+      const size_t lds = sizeof(float) * 3 * (size_t)tab.E * tab.E;
+      hipLaunchKernelGGL(pack_kernel, dim3(nb), dim3(256), lds, (hipStream_t)stream, tab, src, src2, dst, dstb);
+      rc = (int)hipGetLastError();
+    }
+    tab.n = 0;
+    nb = 0;
+  }
+  int finish() {
+    flush();
+    return rc;
+  }
 };
-
-__global__ void to_bf16_kernel(MatTable t, const float* __restrict__ src, __bf16* __restrict__ dst) {
-  const int m = blockIdx.y;
-  const int64_t off = t.off[m];
-  const int ld = t.ld[m];
-  const int64_t n = (int64_t)t.rows[m] * ld;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int r = (int)(i / ld), col = (int)(i % ld);
-    dst[off + (int64_t)r * ld + (col ^ bf_swz(r, ld))] = (__bf16)src[off + i];
-  }
-}
 }  // namespace
 
 extern "C" int t2o_layout_init(t2o_layout* L, int kind, int E, int H, int D, int F, int NA, int FF, int n_ent,
@@ -239,100 +278,70 @@ extern "C" int64_t t2o_param_count(int kind, int E, int H, int D, int F, int NA,
 extern "C" int t2o_pack_params(const t2o_layout* L, const float* params, float* pack, void* stream) {
   if (!L || !params || !pack) return T2O_EINVAL;
   const int E = L->E, H = L->H, D = L->D, F = L->F, FF = L->FF;
-  const int HE = H * E;
+  if (E > 64) return T2O_EUNSUPPORTED;
   const ParamOffsets P = param_offsets(L->kind, E, H, D, F, L->NA, FF);
-  SegTable t{};
-  t.E = E; t.H = H; t.scale = 1.0f / sqrtf((float)E);
-  add(t, SEG_TPAD2D, 16, E, L->WeT, P.We, 0, E, F);   // WeT[f][e] = We[e][f]
-  add(t, SEG_PAD2D, E, 16, L->We, P.We, 0, E, F);
-  add(t, SEG_COPY, 1, E, L->be, P.be);
+  // bf16 mode: every matrix also goes to the swizzled bf16 image after the fp32 pack
+  const int bf = L->prec == 1;
+  __bf16* img = bf ? reinterpret_cast<__bf16*>(pack + L->total) : nullptr;
+  Builder b(E, H, params, nullptr, pack, img, stream);
+  b.ew(T_TPAD2D, 16, E, L->WeT, P.We, E, F, bf);   // WeT[f][e] = We[e][f]
+  b.ew(T_PAD2D, E, 16, L->We, P.We, E, F, bf);
+  b.ew(T_COPY, 1, E, L->be, P.be);
   const int no = L->kind == 0 ? L->NA : 1;
-  add(t, SEG_PAD2D, 16, E, L->Wo, P.Wo, 0, no, E);
-  add(t, SEG_PAD2D, 1, 16, L->bo, P.bo, 0, 1, no);
-  add(t, SEG_TPAD2D, E, 16, L->WoT, P.Wo, 0, no, E);
+  b.ew(T_PAD2D, 16, E, L->Wo, P.Wo, no, E, bf);
+  b.ew(T_PAD2D, 1, 16, L->bo, P.bo, 1, no);
+  b.ew(T_TPAD2D, E, 16, L->WoT, P.Wo, no, E, bf);
   for (int d = 0; d < D; ++d) {
-    if (int rc = launch(t, params, nullptr, pack, stream)) return rc;
-    t.n = 0;
-    add(t, SEG_FOLD_M, HE, E, L->M[d], P.Wk[d], P.Wq[d]);
-    add(t, SEG_FOLD_MT, E, HE, L->MT[d], P.Wk[d], P.Wq[d]);
-    add(t, SEG_FOLD_N, E, HE, L->N[d], P.U[d], P.Wv[d]);
-    add(t, SEG_FOLD_NT, HE, E, L->NT[d], P.U[d], P.Wv[d]);
-    add(t, SEG_COPY, 1, E, L->bu[d], P.bu[d]);
-    add(t, SEG_COPY, 1, E, L->g1[d], P.g1[d]);
-    add(t, SEG_COPY, 1, E, L->n1[d], P.n1[d]);
-    add(t, SEG_COPY, FF, E, L->W1[d], P.W1[d]);
-    add(t, SEG_TPAD2D, E, FF, L->W1T[d], P.W1[d], 0, FF, E);
-    add(t, SEG_COPY, 1, FF, L->c1[d], P.c1[d]);
-    add(t, SEG_COPY, E, FF, L->W2[d], P.W2[d]);
-    add(t, SEG_TPAD2D, FF, E, L->W2T[d], P.W2[d], 0, E, FF);
-    add(t, SEG_COPY, 1, E, L->c2[d], P.c2[d]);
-    add(t, SEG_COPY, 1, E, L->g2[d], P.g2[d]);
-    add(t, SEG_COPY, 1, E, L->n2[d], P.n2[d]);
-  }
-  if (int rc = launch(t, params, nullptr, pack, stream)) return rc;
-  if (L->prec == 1) {  // bf16 image of the matrices right after the fp32 pack
-    MatTable m{};
-    auto mat = [&](int64_t off, int rows, int ld) {
-      m.off[m.n] = off;
-      m.rows[m.n] = rows;
-      m.ld[m.n] = ld;
-      ++m.n;
-    };
-    mat(L->WeT, 16, E);
-    mat(L->We, E, 16);
-    mat(L->Wo, 16, E);
-    mat(L->WoT, E, 16);
-    for (int d = 0; d < D; ++d) {
-      mat(L->M[d], HE, E);
-      mat(L->MT[d], E, HE);
-      mat(L->N[d], E, HE);
-      mat(L->NT[d], HE, E);
-      mat(L->W1[d], FF, E);
-      mat(L->W1T[d], E, FF);
-      mat(L->W2[d], E, FF);
-      mat(L->W2T[d], FF, E);
+    for (int h = 0; h < H; ++h) {
+      b.head(T_FOLD_M, h, L->M[d], L->MT[d], P.Wk[d], P.Wq[d], 0, bf);
+      b.head(T_FOLD_N, h, L->N[d], L->NT[d], P.U[d], P.Wv[d], 0, bf);
     }
-    hipLaunchKernelGGL(to_bf16_kernel, dim3(16, m.n), dim3(256), 0, (hipStream_t)stream, m, pack,
-                       reinterpret_cast<__bf16*>(pack + L->total));
-    return (int)hipGetLastError();
+    b.ew(T_COPY, 1, E, L->bu[d], P.bu[d]);
+    b.ew(T_COPY, 1, E, L->g1[d], P.g1[d]);
+    b.ew(T_COPY, 1, E, L->n1[d], P.n1[d]);
+    b.ew(T_COPY, FF, E, L->W1[d], P.W1[d], 0, 0, bf);
+    b.ew(T_TPAD2D, E, FF, L->W1T[d], P.W1[d], FF, E, bf);
+    b.ew(T_COPY, 1, FF, L->c1[d], P.c1[d]);
+    b.ew(T_COPY, E, FF, L->W2[d], P.W2[d], 0, 0, bf);
+    b.ew(T_TPAD2D, FF, E, L->W2T[d], P.W2[d], E, FF, bf);
+    b.ew(T_COPY, 1, E, L->c2[d], P.c2[d]);
+    b.ew(T_COPY, 1, E, L->g2[d], P.g2[d]);
+    b.ew(T_COPY, 1, E, L->n2[d], P.n2[d]);
   }
-  return 0;
+  return b.finish();
 }
 
 extern "C" int t2o_unpack_grads(const t2o_layout* L, const float* params, const float* gpack, float* grad,
                                 void* stream) {
   if (!L || !params || !gpack || !grad) return T2O_EINVAL;
   const int E = L->E, H = L->H, D = L->D, F = L->F, FF = L->FF;
-  const int HE = H * E;
+  if (E > 64) return T2O_EUNSUPPORTED;
   const ParamOffsets P = param_offsets(L->kind, E, H, D, F, L->NA, FF);
   t2o_layout G;
   grad_layout(*L, G);
-  SegTable t{};
-  t.E = E; t.H = H; t.scale = 1.0f / sqrtf((float)E);
+  Builder b(E, H, params, gpack, grad, nullptr, stream);
   // gWe[e][f] += gpack.We[e][f] (ld 16)
-  add(t, SEG_ADD_PAD2D, E, F, P.We, G.We, 0, 0, 16);
-  add(t, SEG_ADD, 1, E, P.be, G.be);
+  b.ew(T_ADD_PAD2D, E, F, P.We, G.We, 0, 16);
+  b.ew(T_ADD, 1, E, P.be, G.be);
   const int no = L->kind == 0 ? L->NA : 1;
-  add(t, SEG_ADD_PAD2D, no, E, P.Wo, G.Wo, 0, 0, E);
-  add(t, SEG_ADD, 1, no, P.bo, G.bo);
+  b.ew(T_ADD_PAD2D, no, E, P.Wo, G.Wo, 0, E);
+  b.ew(T_ADD, 1, no, P.bo, G.bo);
   for (int d = 0; d < D; ++d) {
-    if (int rc = launch(t, params, gpack, grad, stream)) return rc;
-    t.n = 0;
-    add(t, SEG_UNFOLD_WQ, HE, E, P.Wq[d], P.Wk[d], G.M[d]);
-    add(t, SEG_UNFOLD_WK, HE, E, P.Wk[d], P.Wq[d], G.M[d]);
-    add(t, SEG_UNFOLD_WV, HE, E, P.Wv[d], P.U[d], G.N[d]);
-    add(t, SEG_UNFOLD_U, E, HE, P.U[d], P.Wv[d], G.N[d]);
-    add(t, SEG_ADD, 1, E, P.bu[d], G.bu[d]);
-    add(t, SEG_ADD, 1, E, P.g1[d], G.g1[d]);
-    add(t, SEG_ADD, 1, E, P.n1[d], G.n1[d]);
-    add(t, SEG_ADD, FF, E, P.W1[d], G.W1[d]);
-    add(t, SEG_ADD, 1, FF, P.c1[d], G.c1[d]);
-    add(t, SEG_ADD, E, FF, P.W2[d], G.W2[d]);
-    add(t, SEG_ADD, 1, E, P.c2[d], G.c2[d]);
-    add(t, SEG_ADD, 1, E, P.g2[d], G.g2[d]);
-    add(t, SEG_ADD, 1, E, P.n2[d], G.n2[d]);
+    for (int h = 0; h < H; ++h) {
+      b.head(T_UNFOLD_QK, h, P.Wq[d], P.Wk[d], P.Wq[d], P.Wk[d], G.M[d]);
+      b.head(T_UNFOLD_VU, h, P.Wv[d], P.U[d], P.U[d], P.Wv[d], G.N[d]);
+    }
+    b.ew(T_ADD, 1, E, P.bu[d], G.bu[d]);
+    b.ew(T_ADD, 1, E, P.g1[d], G.g1[d]);
+    b.ew(T_ADD, 1, E, P.n1[d], G.n1[d]);
+    b.ew(T_ADD, FF, E, P.W1[d], G.W1[d]);
+    b.ew(T_ADD, 1, FF, P.c1[d], G.c1[d]);
+    b.ew(T_ADD, E, FF, P.W2[d], G.W2[d]);
+    b.ew(T_ADD, 1, E, P.c2[d], G.c2[d]);
+    b.ew(T_ADD, 1, E, P.g2[d], G.g2[d]);
+    b.ew(T_ADD, 1, E, P.n2[d], G.n2[d]);
   }
-  return launch(t, params, gpack, grad, stream);
+  return b.finish();
 }
 
 namespace {

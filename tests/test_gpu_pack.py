@@ -75,3 +75,44 @@ def test_pack_and_unpack(kind):
         n = v.numel()
         assert normwise(grad[off:off + n].view_as(v), exp[k]) < 1e-5, k
         off += n
+
+
+def _bf_swz(r, ld):
+    """include/t2omca.h bf16 image swizzle (t2o_common.hpp bf_swz)."""
+    return 8 * ((r >> 2) & 3) if ld % 32 == 0 else 8 * ((r >> 3) & 1)
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_pack_bf16_image(kind):
+    """prec 1: every matrix of the pack also sits, rounded to bf16 (RNE) and
+    row-swizzled, in the image after the fp32 pack; the fp32 pack is unchanged."""
+    require_gpu()
+    from t2omca_amd import ops
+    E, H, D, A = 32, 3, 2, 8
+    cfg = dict(n_agents=A, n_entities=A, obs_entity_feats=9, emb=E, heads=H, depth=D,
+               ff_hidden_mult=4, n_actions=5, state_entity_feats=8, mixer_emb=E, mixer_heads=H,
+               mixer_depth=D)
+    p = ref_model.init_params("agent" if kind == 0 else "mixer", cfg, 12)
+    F = 9 if kind == 0 else 8
+    NA = 5 if kind == 0 else 1
+    s32 = ops.NetShape(kind, E, H, D, F, NA, 4 * E, A)
+    s16 = ops.NetShape(kind, E, H, D, F, NA, 4 * E, A, prec=1)
+    L = s16.layout()
+    flat = flat_from_dict(p).cuda()
+    p32 = ops.pack_params(s32, flat).cpu()
+    p16 = ops.pack_params(s16, flat).cpu()
+    assert torch.equal(p16[:L.total], p32)
+    img = p16[L.total:].view(torch.int32).numpy().view(np.uint16)
+    img = torch.from_numpy(img.astype(np.int32))
+    HE, FF = H * E, 4 * E
+    mats = [(L.WeT, 16, E), (L.We, E, 16), (L.Wo, 16, E), (L.WoT, E, 16)]
+    for d in range(D):
+        mats += [(L.M[d], HE, E), (L.MT[d], E, HE), (L.N[d], E, HE), (L.NT[d], HE, E),
+                 (L.W1[d], FF, E), (L.W1T[d], E, FF), (L.W2[d], E, FF), (L.W2T[d], FF, E)]
+    for off, rows, ld in mats:
+        ref = p32[off:off + rows * ld].view(rows, ld).to(torch.bfloat16).view(torch.int16).int() & 0xFFFF
+        got = torch.empty_like(ref)
+        for r in range(rows):
+            idx = torch.arange(ld) ^ _bf_swz(r, ld)
+            got[r] = img[off + r * ld + idx]
+        assert torch.equal(got, ref), (off, rows, ld)
