@@ -53,6 +53,10 @@ def parse():
                          "env step + agent step + ε-greedy over --envs envs per GPU (configs[4])")
     ap.add_argument("--envs", type=int, default=8192, help="rollout mode: envs per GPU")
     ap.add_argument("--mecs", type=int, default=2, help="rollout mode: MEC servers")
+    ap.add_argument("--priorities", choices=("device", "cpu"), default="device",
+                    help="where each update's |TD errors| go: device (consumed by the device-resident "
+                         "PrioritizedReplayBuffer, t2omca_amd/replay.py) or cpu (the reference driver's "
+                         "host-side buffer contract: one device->host copy and sync per update)")
     ap.add_argument("--serial", action="store_true",
                     help="no side-stream overlap: every kernel's HIP-event time is its isolated cost")
     ap.add_argument("--print-workload-tag", action="store_true",
@@ -204,7 +208,7 @@ def main():
     agent = TransformerAgent(None, margs).to(dev)
     mixer = TransformerMixer(margs).to(dev)
     learner = TDLearner(agent, mixer, target_update_interval=10 ** 9, precision=args.dtype,
-                        overlap=not args.serial)
+                        overlap=not args.serial, priorities_to_cpu=args.priorities == "cpu")
     batch, w = make_batch(B, T, A, seed=1 + rank, device=dev)
     if args.mode == "forward":
         from t2omca_amd import ops
@@ -286,7 +290,7 @@ def main():
         "config": {"workload": f"{train_config_name(A, B, T)}: full TD update fwd+bwd+Adam, {A} AGVs, "
                                f"batch {B} episodes/GPU x T={T}",
                    "global_batch": B * world, "seq_len": T, "agents": A, "emb": 32, "heads": 3, "depth": 2,
-                   "parallelism": f"dp{world}"},
+                   "parallelism": f"dp{world}", "priorities": args.priorities},
         "roofline": {"bound": "hbm" if hbm_bound else "mfma", "kernel": dom, "achieved": achieved, "peak": peak,
                      "unit": unit, "frac": achieved / peak, "traffic": traffic_for(dom, workload_tag(args)),
                      "algorithmic_flops_per_launch": flops[dom],
