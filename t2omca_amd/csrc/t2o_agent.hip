@@ -375,13 +375,7 @@ inline bool agent_bwd_single_wave() {
   return single;
 }
 
-constexpr int AGP_TILES = AG_BWD_WAVES;
-
-#ifdef T2O_PHASE_PROF
-// diagnostic builds only (tools/build_variant.sh <name> -DT2O_PHASE_PROF): per-phase
-// cycle counts of one workgroup, read back with t2o_prof_read
-__device__ long long t2o_prof_buf[64 * 2 * 4 * 4];
-#endif  // tiles per workgroup (same slab count as the single-wave kernel)
+constexpr int AGP_TILES = AG_BWD_WAVES;  // tiles per workgroup (same slab count as the single-wave kernel)
 
 template <int E>
 constexpr int agp_xch_floats() { return 3 * (E / 16) * 64 * 4; }
@@ -496,6 +490,9 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
   };
   if (d == 0) __syncthreads();
   for (int step = T - 1; step >= 0; --step) {
+#ifdef T2O_TIMELINE
+    T2O_STAMP(2 * (T - 1 - step), 0);
+#endif
     Cache cache;
     f4 h[ET], o[NO], xo[ET];
     load_fwd_inputs(step, h, o, xo);
@@ -523,6 +520,9 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
 #pragma unroll
     for (int ph = 0; ph < 2; ++ph) {
       T2O_MARK(0);
+#ifdef T2O_TIMELINE
+      if (ph == 0) T2O_STAMP(2 * (T - 1 - step), 1);
+#endif
       const Wts<WT> P = step_view(P0);
       if (ph == 0) {
 #ifdef T2O_PHASE_PROF
@@ -587,13 +587,15 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
         }
       }
       T2O_MARK(3);
+#ifdef T2O_TIMELINE
+      T2O_STAMP(2 * (T - 1 - step) + ph, 2 * (1 - ph));
+#endif
       __syncthreads();
       T2O_MARK(4);
-#ifdef T2O_PHASE_PROF
-      if (blockIdx.x == 7 && lane == 0 && T - 1 - step < 64) {
-        long long* pb = t2o_prof_buf + (((T - 1 - step) * 2 + ph) * 4 + w) * 4;
-        for (int m = 0; m < 4; ++m) pb[m] = t2o_mark_buf[w][m + 1] - t2o_mark_buf[w][m];
-      }
+#ifdef T2O_TIMELINE
+      T2O_STAMP(2 * (T - 1 - step) + ph, 3 - 2 * ph);
+#else
+      T2O_PROF_SAVE((T - 1 - step) * 2 + ph, 4);
 #endif
     }
   }
@@ -717,11 +719,8 @@ extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, cons
   return rc;
 }
 
-#ifdef T2O_PHASE_PROF
-extern "C" int t2o_prof_read(long long* host_out) {
-  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(t2o_prof_buf), sizeof(t2o_prof_buf));
-}
-#endif
+// diagnostic builds only (-DT2O_PHASE_PROF, tools/phase_prof.py)
+T2O_PROF_READER(t2o_prof_read_agent)
 
 extern "C" int t2o_agent_bwd_max_slabs(int B, int A) {
   const int rpw = rows_per_wave(B * A);

@@ -42,13 +42,40 @@ T2O_DEV f4 zero4() { return f4{0.f, 0.f, 0.f, 0.f}; }
 // Diagnostic builds only (-DT2O_PHASE_PROF): cycle stamps of one workgroup's waves
 #ifdef T2O_PHASE_PROF
 __device__ long long t2o_mark_buf[8][8];
+__device__ long long t2o_prof_buf[128 * 8 * 4];  // [slot][wave][delta]
 #define T2O_MARK(n)                                                                         \
   do {                                                                                     \
     if (blockIdx.x == 7 && (threadIdx.x & 63) == 0) t2o_mark_buf[threadIdx.x >> 6][n] = clock64(); \
   } while (0)
+// deltas between marks 0..NM of this wave into slot `slot` (WG 7, first 8 waves)
+#define T2O_PROF_SAVE(slot, NM)                                                                   \
+  do {                                                                                           \
+    const int w_ = threadIdx.x >> 6;                                                             \
+    if (blockIdx.x == 7 && (threadIdx.x & 63) == 0 && (slot) < 128 && w_ < 8)                     \
+      for (int m_ = 0; m_ < (NM) && m_ < 4; ++m_)                                               \
+        t2o_prof_buf[((slot) * 8 + w_) * 4 + m_] = t2o_mark_buf[w_][m_ + 1] - t2o_mark_buf[w_][m_]; \
+  } while (0)
+// absolute stamp into slot/idx (timeline builds: -DT2O_PHASE_PROF -DT2O_TIMELINE)
+#define T2O_STAMP(slot, idx)                                                                     \
+  do {                                                                                           \
+    const int w_ = threadIdx.x >> 6;                                                             \
+    if (blockIdx.x == 7 && (threadIdx.x & 63) == 0 && (slot) < 128 && w_ < 8)                     \
+      t2o_prof_buf[((slot) * 8 + w_) * 4 + (idx)] = clock64();                                   \
+  } while (0)
+#define T2O_PROF_READER(fn)                                                          \
+  extern "C" int fn(long long* host_out) {                                          \
+    return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(t2o_prof_buf), sizeof(t2o_prof_buf)); \
+  }
 #else
 #define T2O_MARK(n) \
   do {            \
+  } while (0)
+#define T2O_PROF_SAVE(slot, NM) \
+  do {                        \
+  } while (0)
+#define T2O_PROF_READER(fn)
+#define T2O_STAMP(slot, idx) \
+  do {                     \
   } while (0)
 #endif
 

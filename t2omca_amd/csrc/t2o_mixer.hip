@@ -262,6 +262,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
   MixIn<E, A> in;
   mix_load<E, A>(args, n, b, 0, in);
   for (int t = 0; t < n.T; ++t) {
+    T2O_MARK(0);
     const Wts<WT> P = step_view(P0);
     mix_keys<E, A>(P, L, in, X0);
     const float myq = mix_qv<E, A>(n, in);
@@ -269,6 +270,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
     __builtin_amdgcn_wave_barrier();
     KeyFrags<E, Dm::KT, sizeof(WT) == 2> K;
     K.template load<Dm::LDX>(X0);
+    T2O_MARK(1);
 #pragma unroll
     for (int qt = 0; qt < Dm::QT; ++qt) {
       const int q = 16 * qt + c;
@@ -285,6 +287,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
           for (int ft = 0; ft < ET; ++ft) st4(xm + 16 * ft + 4 * g, x[ft]);
         }
         mixer_block_fwd<E, H, Dm::KT, FF, false>(P, L, d, K, Dm::LK, x, nullptr);
+        if (qt == 0) T2O_MARK(2 + d);
       }
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) st4(OUT + q * E + 16 * ft + 4 * g, x[ft]);
@@ -314,6 +317,8 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
       if (i < 3 * E) X0[(Dm::NS + A + i / E) * Dm::LDX + i % E] = hv[k];
     }
     __builtin_amdgcn_wave_barrier();
+    T2O_MARK(2 + D);
+    if (blockIdx.y == 0) T2O_PROF_SAVE(t, 2 + D);
   }
 }
 
@@ -699,6 +704,9 @@ int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t 
 }
 
 }  // namespace
+
+// diagnostic builds only (-DT2O_PHASE_PROF, tools/phase_prof.py)
+T2O_PROF_READER(t2o_prof_read_mixer)
 
 extern "C" int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, const float* pack_tg,
                                     const float* states, int64_t st_sb, int64_t st_st,

@@ -1,6 +1,8 @@
-"""Diagnostic: per-phase cycle counts of the pipelined agent BPTT (variant build
-with -DT2O_PHASE_PROF, loaded through T2O_LIB).  Runs one TD update and prints
-median work / barrier-wait cycles per (phase, role)."""
+"""Diagnostic: in-kernel cycle stamps (variant build with -DT2O_PHASE_PROF, loaded
+through T2O_LIB).  Runs TD updates and prints median cycles per segment for one
+workgroup (WG 7) of the agent BPTT (per phase) and the mixer forward (per step).
+s_memtime ticks are shader cycles (MI355X_MICROARCH.md); the stamps themselves
+cost a few percent."""
 import ctypes
 import os
 import statistics as st
@@ -18,20 +20,31 @@ from t2omca_amd.synthetic import make_args, make_batch  # noqa: E402
 A, B, T = 8, 1024, 60
 torch.manual_seed(0)
 margs = make_args(A, device="cuda")
-learner = TDLearner(TransformerAgent(None, margs).cuda(), TransformerMixer(margs).cuda(), overlap=False)
+learner = TDLearner(TransformerAgent(None, margs).cuda(), TransformerMixer(margs).cuda(), overlap=False,
+                    precision="bf16")
 batch, w = make_batch(B, T, A, seed=1, device="cuda")
 for _ in range(2):
     learner.train(batch, 0, 0, per_weight=w)
 torch.cuda.synchronize()
-buf = np.zeros(64 * 2 * 4 * 4, dtype=np.int64)
-f = lib().t2o_prof_read
-f.argtypes = [ctypes.c_void_p]
-assert f(buf.ctypes.data) == 0
-buf = buf.reshape(64, 2, 4, 4)[1:T]  # skip the first iteration (prologue) and the tail
-for ph in range(2):
+
+
+def read(fn):
+    buf = np.zeros(128 * 8 * 4, dtype=np.int64)
+    f = getattr(lib(), fn)
+    f.argtypes = [ctypes.c_void_p]
+    assert f(buf.ctypes.data) == 0
+    return buf.reshape(128, 8, 4)
+
+
+ag = read("t2o_prof_read_agent")[2:2 * T - 2].reshape(T - 2, 2, 8, 4)
+print("agent BPTT (two waves per tile), median cycles per phase segment:")
+for ph, kind in enumerate(("fwd: inputs | attention | post | barrier", "bwd: inputs | post | attention | barrier")):
     for wv in range(4):
-        d = wv & 1
-        kind = "bwd" if ph == 1 else "fwd"
-        m = [st.median(buf[:, ph, wv, i]) for i in range(4)]
-        print(f"phase {ph} wave {wv} block {d} {kind}: inputs {m[0]:7.0f}  part1 {m[1]:7.0f}  "
-              f"part2 {m[2]:7.0f}  barrier {m[3]:7.0f}  (fwd: attention | post; bwd: post | attention; block-0 waves run one phase late)")
+        m = [st.median(ag[:, ph, wv, i]) for i in range(4)]
+        print(f"  {kind.split(':')[0]} wave {wv} (block {wv & 1}): " + "  ".join(f"{x:7.0f}" for x in m) +
+              f"   [{kind.split(': ')[1]}]")
+mx = read("t2o_prof_read_mixer")[1:T - 1]
+print("mixer forward (online net), median cycles per step segment: keys | block 0 | block 1 | head+rest")
+for wv in range(8):
+    m = [st.median(mx[:, wv, i]) for i in range(4)]
+    print(f"  wave {wv}: " + "  ".join(f"{x:7.0f}" for x in m) + f"   total {sum(m):7.0f}")
