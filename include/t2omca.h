@@ -249,6 +249,32 @@ int t2o_env_run(int mode, const double* spec, void* const* state, void* const* o
                 const int64_t* actions, int64_t act_se, int NE, int A, int M, int C, int QMAX, int T,
                 uint64_t seed, void* stream);
 
+/* t2o_env_run with n_out = 8 (as above) or 11 output pointers; the extra three
+ * carry the compact observation wire format (replaces storing
+ * get_obs's dense [A][9A] output, environment_multi_mec.py:148-186):
+ *   out[8]  wire i32[NE][A][4], written with every obs the worker returns
+ *           (modes 1, 2): per entity j, w0 = job size, w1 = data_delay,
+ *           w2 = offload delay x 100 (exact integer: the fp64 value is
+ *           rint(x*100)/100), w3 = thr | qlen << 16 | (ack+1) << 24 | mec << 26;
+ *           all zero fields when the queue is empty (get_agent_inf :123-146);
+ *   out[9]  snap_n i64[NE], out[10] snap f64[NE][2][9A]: the normaliser's
+ *           count, mean and S right before the worker's get_obs in mode 1 (the
+ *           state the episode's first returned obs is normalised from).
+ * out[9] / out[10] are both set or both NULL.  Needs latency_max <= 65535. */
+int t2o_env_run_ex(int mode, const double* spec, void* const* state, void* const* out, int n_out,
+                   const int64_t* actions, int64_t act_se, int NE, int A, int M, int C, int QMAX, int T,
+                   uint64_t seed, void* stream);
+
+/* Dense normalised observations from the wire format: for each episode b,
+ * starting from (snap_n[b], snap[b]), replays get_obs's sequential normaliser
+ * (normalization.py:12-35, agent by agent, t = 0..T1-1) on the observation
+ * get_obs_agent (:148-182) builds from wire[b][t] — bit-identical to the env's
+ * own obs output.  wire: int32 element strides w_sb / w_st (multiples of 4,
+ * 16-B aligned), rows [A][4] dense; obs: f32 element strides o_sb / o_st, each
+ * step a dense [A][9A]; obs64 (optional) dense f64 [B][T1][A][9A].  A <= 64. */
+int t2o_obs_expand(const int32_t* wire, int64_t w_sb, int64_t w_st, const int64_t* snap_n, const double* snap,
+                   float* obs, int64_t o_sb, int64_t o_st, double* obs64, int B, int T1, int A, void* stream);
+
 /* ε-greedy action selection (the reference's controller is
  * absent, contract parallel_runner.py:121 with PyMARL's EpsilonGreedyActionSelector).
  * q f32 [rows][NA], avail i32 [rows][NA] (rows = envs x agents, dense) ->

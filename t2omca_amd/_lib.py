@@ -67,6 +67,12 @@ EXPORTS = {
     "t2o_probe_lane_ops": (ctypes.c_int, [ctypes.c_void_p] * 3),
     "t2o_env_run": (ctypes.c_int, [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_int64] +
                     [ctypes.c_int] * 6 + [ctypes.c_uint64, ctypes.c_void_p]),
+    "t2o_env_run_ex": (ctypes.c_int, [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_void_p,
+                                                                                ctypes.c_int64] +
+                       [ctypes.c_int] * 6 + [ctypes.c_uint64, ctypes.c_void_p]),
+    "t2o_obs_expand": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                      ctypes.c_void_p] + [ctypes.c_int] * 3 + [ctypes.c_void_p]),
     "t2o_per_workspace_doubles": (ctypes.c_int64, [ctypes.c_int64]),
     "t2o_per_sample": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_double,
                                       ctypes.c_uint64, ctypes.c_int64] + [ctypes.c_void_p] * 4),

@@ -61,6 +61,11 @@ struct EnvOut {
   double* info;         // [NE][6]: delay_reward, overtime, utilization, conflict_ratio,
                         //          task_completion_rate, task_completion_delay (NaN if not terminal)
   int32_t* ack;         // [NE][A]
+  // compact observation wire format, written beside (or instead
+  // of) the dense obs by every get_obs whose result the worker returns:
+  int32_t* wire;        // [NE][A][4] (may be null), see WIRE_* below
+  int64_t* snap_n;      // [NE]  normaliser count before the worker's get_obs in reset
+  double* snap;         // [NE][2][9A] normaliser mean, S at the same point
 };
 
 struct EnvArgs {
@@ -170,6 +175,27 @@ struct EnvLds {
   double rd[MAXA];
   int tn[MAXA], ts[MAXA];
 };
+
+// ---- compact observation wire format ---------------------
+// Everything get_obs_agent (:148-182) reads about entity j, as 4 int32:
+//   w0 size, w1 data_delay (get_agent_inf's round() to int), w2 the offload
+//   delay in hundredths (the fp64 value is rint(x*100)/100, so rint(v*100) is
+//   an exact integer k and k/100.0 reproduces v bit for bit),
+//   w3 thr (bits 0-15) | queue length (16-23) | ack+1 (24-25) | mec_index (26-31).
+// All fields are 0 when the queue is empty (get_agent_inf returns zeros).
+// Together with the normaliser (n, mean, S) at the start of the episode, the
+// wire records of t = 0..T reproduce every returned obs exactly (t2o_obs_expand).
+__device__ void write_wire(const EnvArgs& a, int e, const EnvLds& L) {
+  const int lane = threadIdx.x & 63;
+  if (!a.o.wire || lane >= a.A) return;
+  const double* inf = L.inf[lane];
+  int4 w;
+  w.x = (int)inf[0];
+  w.y = (int)inf[1];
+  w.z = (int)rint(inf[2] * 100.0);
+  w.w = ((int)inf[3] & 0xFFFF) | ((int)inf[4] << 16) | ((L.ack[lane] + 1) << 24) | (L.mec[lane] << 26);
+  reinterpret_cast<int4*>(a.o.wire)[(size_t)e * a.A + lane] = w;
+}
 
 // get_obs (:184-186) = A sequential normaliser updates; writes outputs if out != 0.
 // The update count n is kept in a register by every lane (the caller loads and
@@ -318,6 +344,15 @@ __global__ __launch_bounds__(64) void env_kernel(EnvArgs a) {
     fill_lds(a, e, L);
     get_obs(a, e, L, false, n);  // reset()'s own get_obs
     write_state_avail(a, e, L);
+    if (a.o.snap) {  // the normaliser the episode's first returned obs starts from
+      const int n9 = 9 * A;
+      for (int p = lane; p < n9; p += 64) {
+        a.o.snap[(size_t)e * 2 * n9 + p] = a.s.nrm_mean[(size_t)e * n9 + p];
+        a.o.snap[(size_t)e * 2 * n9 + n9 + p] = a.s.nrm_S[(size_t)e * n9 + p];
+      }
+      if (lane == 0) a.o.snap_n[e] = n;
+    }
+    write_wire(a, e, L);
     get_obs(a, e, L, true, n);   // the worker's get_obs
     if (lane == 0) a.s.nrm_n[e] = n;
     return;
@@ -453,15 +488,98 @@ __global__ __launch_bounds__(64) void env_kernel(EnvArgs a) {
   int64_t n = a.s.nrm_n[e];
   fill_lds(a, e, L);
   write_state_avail(a, e, L);
+  write_wire(a, e, L);
   get_obs(a, e, L, true, n);
   if (lane == 0) a.s.nrm_n[e] = n;
 }
 
+// ---- t2o_obs_expand: wire records -> dense normalised obs --------------------
+// One thread per (episode, feature p = 9j + f): the normaliser is elementwise,
+// so feature p's running (mean, S) is a private chain over (t, agent i) in the
+// reference's order (get_obs updates agent by agent, normalization.py:12-35),
+// with the same IEEE operations as get_obs above.  The wire rows of one step
+// (A x 16 B per episode) are staged in LDS and read as broadcasts.
+constexpr int XP_THREADS = 576;  // 9 x 64 features at A = 64
+
+struct ExpandArgs {
+  const int32_t* wire;
+  int64_t w_sb, w_st;  // int32-element strides of episode / step
+  const int64_t* snap_n;
+  const double* snap;  // [B][2][9A]
+  float* obs;
+  int64_t o_sb, o_st;  // float-element strides of episode / step
+  double* obs64;       // dense [B][T1][A][9A] or null
+  int B, T1, A, epb;
+};
+
+__global__ __launch_bounds__(XP_THREADS) void obs_expand_kernel(ExpandArgs a) {
+  __shared__ int4 rows[64];  // [episode-in-block * A + agent]: epb * A <= 64
+  const int A = a.A, n9 = 9 * A;
+  const int le = threadIdx.x / n9, p = threadIdx.x % n9;
+  const int b = blockIdx.x * a.epb + le;
+  const bool live = le < a.epb && b < a.B;
+  const int j = p / 9, f = p % 9;
+  double mean = 0.0, S = 0.0;
+  int64_t n = 0;
+  if (live) {
+    n = a.snap_n[b];
+    mean = a.snap[(size_t)b * 2 * n9 + p];
+    S = a.snap[(size_t)b * 2 * n9 + n9 + p];
+  }
+  const int nrows = a.epb * A;
+  for (int t = 0; t < a.T1; ++t) {
+    __syncthreads();
+    for (int r = threadIdx.x; r < nrows; r += blockDim.x) {
+      const int bb = blockIdx.x * a.epb + r / A;
+      if (bb < a.B)
+        rows[r] = *reinterpret_cast<const int4*>(a.wire + (size_t)bb * a.w_sb + (size_t)t * a.w_st + 4 * (r % A));
+    }
+    __syncthreads();
+    if (!live) continue;
+    const int4 wj = rows[le * A + j];
+    const int mec_j = (wj.w >> 26) & 63;
+    double xj;  // entity j's field f as seen from an agent of the same MEC (f < 8)
+    switch (f) {
+      case 0: case 1: case 2: xj = (f == ((wj.w >> 24) & 3)) ? 1.0 : 0.0; break;
+      case 3: xj = (double)wj.x; break;
+      case 4: xj = (double)wj.y; break;
+      case 5: xj = (double)wj.z / 100.0; break;
+      case 6: xj = (double)(wj.w & 0xFFFF); break;
+      default: xj = (double)((wj.w >> 16) & 0xFF); break;
+    }
+    float* orow = a.obs ? a.obs + (size_t)b * a.o_sb + (size_t)t * a.o_st : nullptr;
+    double* orow64 = a.obs64 ? a.obs64 + (((size_t)b * a.T1 + t) * A) * n9 : nullptr;
+    for (int i = 0; i < A; ++i) {
+      ++n;
+      const int mec_i = (rows[le * A + i].w >> 26) & 63;
+      double x = 0.0;
+      if (mec_i == mec_j) x = f < 8 ? xj : (i == j ? 1.0 : 0.0);
+      double m, d;
+      if (n == 1) {
+        m = x;
+        d = x;
+      } else {
+        const double old = mean;
+        m = old + (x - old) / (double)n;
+        S = S + (x - old) * (x - m);
+        d = sqrt(S / (double)n);
+      }
+      mean = m;
+      const double v = (x - m) / (d + 1e-8);
+      if (orow) orow[(size_t)i * n9 + p] = (float)v;
+      if (orow64) orow64[(size_t)i * n9 + p] = v;
+    }
+  }
+}
+
 }  // namespace
 
-extern "C" int t2o_env_run(int mode, const double* spec, void* const* state, void* const* out,
-                           const int64_t* actions, int64_t act_se, int NE, int A, int M, int C, int QMAX, int T,
-                           uint64_t seed, void* stream) {
+extern "C" int t2o_env_run_ex(int mode, const double* spec, void* const* state, void* const* out, int n_out,
+                              const int64_t* actions, int64_t act_se, int NE, int A, int M, int C, int QMAX, int T,
+                              uint64_t seed, void* stream) {
+  if ((out && n_out != 8 && n_out != 11) || (n_out == 11 && out && (out[9] == nullptr) != (out[10] == nullptr)) ||
+      (spec && (int)spec[9] > 0xFFFF) || QMAX > 255)
+    return T2O_EINVAL;
   if (NE < 1 || A < 1 || A > MAXA || M < 1 || M > 16 || C < 1 || C > 16 || QMAX < 1 || !spec || !state ||
       (mode == 2 && (!actions || !out)) || (mode == 1 && !out) || mode < 0 || mode > 3)
     return T2O_EINVAL;
@@ -475,7 +593,12 @@ extern "C" int t2o_env_run(int mode, const double* spec, void* const* state, voi
                  (double*)state[16]};
   if (out)
     a.o = EnvOut{(float*)out[0], (double*)out[1], (float*)out[2], (int32_t*)out[3], (double*)out[4],
-                 (uint8_t*)out[5], (double*)out[6], (int32_t*)out[7]};
+                 (uint8_t*)out[5], (double*)out[6], (int32_t*)out[7], nullptr, nullptr, nullptr};
+  if (out && n_out == 11) {
+    a.o.wire = (int32_t*)out[8];
+    a.o.snap_n = (int64_t*)out[9];
+    a.o.snap = (double*)out[10];
+  }
   a.actions = actions;
   a.act_se = act_se;
   a.NE = NE;
@@ -487,5 +610,28 @@ extern "C" int t2o_env_run(int mode, const double* spec, void* const* state, voi
   a.seed = seed;
   a.mode = mode;
   hipLaunchKernelGGL(env_kernel, dim3(NE), dim3(64), 0, (hipStream_t)stream, a);
+  return (int)hipGetLastError();
+}
+
+extern "C" int t2o_env_run(int mode, const double* spec, void* const* state, void* const* out,
+                           const int64_t* actions, int64_t act_se, int NE, int A, int M, int C, int QMAX, int T,
+                           uint64_t seed, void* stream) {
+  if (!spec) return T2O_EINVAL;
+  return t2o_env_run_ex(mode, spec, state, out, 8, actions, act_se, NE, A, M, C, QMAX, T, seed, stream);
+}
+
+extern "C" int t2o_obs_expand(const int32_t* wire, int64_t w_sb, int64_t w_st, const int64_t* snap_n,
+                              const double* snap, float* obs, int64_t o_sb, int64_t o_st, double* obs64, int B,
+                              int T1, int A, void* stream) {
+  if (!wire || !snap_n || !snap || (!obs && !obs64) || B < 1 || T1 < 1 || A < 1 || A > MAXA ||
+      (w_sb | w_st) % 4 != 0 || (obs && o_st < (int64_t)A * 9 * A) || (obs && B > 1 && o_sb < (int64_t)A * 9 * A))
+    return T2O_EINVAL;
+  if (((uintptr_t)wire & 15) != 0) return T2O_EINVAL;
+  ExpandArgs a{wire, w_sb, w_st, snap_n, snap, obs, o_sb, o_st, obs64, B, T1, A, 0};
+  const int n9 = 9 * A;
+  a.epb = XP_THREADS / n9 < 1 ? 1 : XP_THREADS / n9;
+  const int threads = (a.epb * n9 + 63) / 64 * 64;
+  const int blocks = (B + a.epb - 1) / a.epb;
+  hipLaunchKernelGGL(obs_expand_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }

@@ -10,6 +10,11 @@ methods are the batched form of parallel_runner.py's env-worker protocol
     reset()            -> state, avail, obs                       (:257-263)
     step(actions)      -> reward, terminated, info, state, avail, obs (:239-256)
 
+With ``wire=True`` every returned obs is also (or, with dest["obs"] = None,
+only) written in the compact wire format of SURVEY.md §8 f3: ``wire``
+[n_envs, A, 4] int32 per step plus the normaliser snapshot ``snap_n`` /
+``snap`` taken at reset; ``ops.obs_expand`` rebuilds the dense obs exactly.
+
 Shapes: obs [n_envs, A, 9A] f32, state [n_envs, 8A] f32, avail
 [n_envs, A, nA] i32, reward [n_envs] f64, terminated [n_envs] bool, info a dict
 of [n_envs] f64 tensors (task_completion_* are NaN except on the terminal step).
@@ -39,7 +44,7 @@ def spec_vector(edge_only=False):
 
 class VecEnv:
     def __init__(self, n_envs, mec_num=2, agv_num=16, num_channels=4, episode_limit=150, seed=0,
-                 edge_only=False, device="cuda", keep_obs64=False):
+                 edge_only=False, device="cuda", keep_obs64=False, wire=False):
         device = torch.device(device)
         if device.type != "cuda":
             raise RuntimeError("VecEnv runs on the HIP device only (the numpy restatement in oracle/ is test-only)")
@@ -71,6 +76,11 @@ class VecEnv:
         self.terminated = torch.empty(NE, dtype=torch.uint8, device=device)
         self.info = torch.empty(NE, 6, **f64)
         self.ack = torch.empty(NE, A, **i32)
+        # compact obs wire format: per-step entity records and the
+        # normaliser snapshot each episode starts from (t2o_env_run_ex, t2o_obs_expand)
+        self.wire = torch.empty(NE, A, 4, **i32) if wire else None
+        self.snap_n = torch.empty(NE, dtype=torch.int64, device=device) if wire else None
+        self.snap = torch.empty(NE, 2, 9 * A, **f64) if wire else None
         self._run(0)  # construction
 
     # -- raw launches --------------------------------------------------------------
@@ -82,24 +92,31 @@ class VecEnv:
 
     def _run(self, mode, actions=None, n_envs=None, dest=None):
         d = self._dest(dest)
-        out = self._ptrs([d["obs"], self.obs64, d["state"], d["avail"], self.reward, self.terminated,
-                          self.info, self.ack])
+        outs = [d["obs"], self.obs64, d["state"], d["avail"], self.reward, self.terminated, self.info, self.ack]
+        if self.wire is not None:
+            outs += [d["wire"], self.snap_n, self.snap]
         act_p, act_se = None, 0
         if actions is not None:
             act_p, act_se = ctypes.c_void_p(actions.data_ptr()), actions.stride(0)
-        rc = lib().t2o_env_run(mode, ctypes.c_void_p(self._spec.data_ptr()), self._ptrs(self._state), out,
-                               act_p, act_se, n_envs or self.n_envs, self.A, self.M, self.C, self.qmax,
-                               self.T, ctypes.c_uint64(self.seed & ((1 << 64) - 1)),
-                               stream_ptr(self.device))
+        rc = lib().t2o_env_run_ex(mode, ctypes.c_void_p(self._spec.data_ptr()), self._ptrs(self._state),
+                                  self._ptrs(outs), len(outs), act_p, act_se, n_envs or self.n_envs, self.A, self.M,
+                                  self.C, self.qmax, self.T, ctypes.c_uint64(self.seed & ((1 << 64) - 1)),
+                                  stream_ptr(self.device))
         check(rc, "env_run")
 
     def _dest(self, dest):
         """Output buffers of one launch: the env's own, or caller-provided dense
-        [n_envs, ...] slices (e.g. one timestep of a time-major replay batch)."""
-        d = {"obs": self.obs, "state": self.state, "avail": self.avail}
+        [n_envs, ...] slices (e.g. one timestep of a time-major replay batch).
+        dest["obs"] = None skips the dense obs (wire-format rollouts)."""
+        d = {"obs": self.obs, "state": self.state, "avail": self.avail, "wire": self.wire}
         if dest:
             for k, t in dest.items():
                 ref = d[k]
+                if t is None and k == "obs" and self.wire is not None:
+                    d[k] = None
+                    continue
+                if ref is None:
+                    raise ValueError(f"dest[{k!r}]: this VecEnv was built without that output")
                 if t.shape != ref.shape or t.dtype != ref.dtype or t.device != self.device or not t.is_contiguous():
                     raise ValueError(f"dest[{k!r}] must be a dense {tuple(ref.shape)} {ref.dtype} device tensor")
                 d[k] = t
@@ -115,7 +132,9 @@ class VecEnv:
                     state_entity_feats=8)
 
     def reset(self, dest=None):
-        """dest: optional dict of output buffers {"obs", "state", "avail"} (dense)."""
+        """dest: optional dict of output buffers {"obs", "state", "avail", "wire"}
+        (dense).  With wire=True the normaliser snapshot of the new episode is in
+        self.snap_n / self.snap after the call."""
         self._run(1, dest=dest)
         d = self._dest(dest)
         return d["state"], d["avail"], d["obs"]

@@ -23,6 +23,7 @@ priorities are copied out):
   clip_grad_norm_ + Adam                           t2o_adam_step
 """
 import dataclasses
+import os
 
 import numpy as np
 import torch
@@ -136,9 +137,71 @@ class TDLearner:
             self._slabs[key] = t
         return t
 
+    # -- checkpoints (per_run.py:159-189 load, :265-279 save) -----------------
+    def cuda(self):
+        """per_run.py:156 calls learner.cuda(); the learner already lives on its HIP device."""
+        return self
+
+    def _optimiser_view(self):
+        """A torch.optim.Adam over the modules' parameters (mac then mixer, the
+        order of a PyMARL2 NQLearner's optimiser) carrying this learner's moments,
+        so opt.th is a standard Adam state_dict."""
+        params = list(self.agent.parameters()) + list(self.mixer.parameters())
+        opt = torch.optim.Adam(params, lr=self.lr, betas=self.betas, eps=self.eps, weight_decay=self.wd)
+        off = 0
+        for p in params:
+            k = p.numel()
+            if self.step_count:
+                opt.state[p] = {"step": torch.tensor(float(self.step_count)),
+                                "exp_avg": self.exp_avg[off:off + k].view_as(p),
+                                "exp_avg_sq": self.exp_avg_sq[off:off + k].view_as(p)}
+            off += k
+        return opt
+
+    def save_models(self, path):
+        """PyMARL layout: {path}/agent.th, mixer.th (reference state_dict keys) and
+        opt.th (torch Adam state_dict)."""
+        torch.save(self.agent.state_dict(), os.path.join(path, "agent.th"))
+        torch.save(self.mixer.state_dict(), os.path.join(path, "mixer.th"))
+        torch.save(self._optimiser_view().state_dict(), os.path.join(path, "opt.th"))
+
+    def load_models(self, path):
+        """Inverse of save_models; also takes checkpoints written by the reference
+        framework.  As PyMARL2's NQLearner does, the target agent is reloaded from
+        agent.th and the target mixer is left as it is; opt.th is optional."""
+        def load(name):
+            return torch.load(os.path.join(path, name), map_location=self.device, weights_only=True)
+        with torch.no_grad():
+            self.agent.load_state_dict(load("agent.th"))  # copies into the flat-buffer views
+            self.mixer.load_state_dict(load("mixer.th"))
+            self.target_params[:self.na].copy_(self.params[:self.na])
+        self._pack_targets()
+        if not os.path.exists(os.path.join(path, "opt.th")):
+            return
+        opt = self._optimiser_view()
+        opt.load_state_dict(load("opt.th"))
+        off, steps = 0, set()
+        for p in list(self.agent.parameters()) + list(self.mixer.parameters()):
+            k = p.numel()
+            st = opt.state.get(p)
+            if st:
+                self.exp_avg[off:off + k].copy_(st["exp_avg"].reshape(-1))
+                self.exp_avg_sq[off:off + k].copy_(st["exp_avg_sq"].reshape(-1))
+                steps.add(int(float(st["step"])))
+            off += k
+        if len(steps) > 1:
+            raise ValueError(f"opt.th: parameters carry different Adam step counts {sorted(steps)}")
+        self.step_count = steps.pop() if steps else 0
+
     # -- the TD update -------------------------------------------------------
     def train(self, batch, t_env=0, episode_num=0, per_weight=None):
-        obs = batch["obs"]
+        if "obs" in _keys(batch):
+            obs = batch["obs"]
+        else:  # compact wire-format batch (SURVEY.md §8 f3): dense obs rebuilt on the device
+            wire = batch["obs_wire"]
+            b, T1, A = wire.shape[:3]
+            obs = ops.obs_expand(wire, batch["obs_nrm_n"], batch["obs_nrm"],
+                                 out=self._buf("obs", (b, T1, A, 9 * A)))
         state = batch["state"]
         actions = batch["actions"]
         avail = batch["avail_actions"]

@@ -330,3 +330,29 @@ def select_actions(q, avail, epsilon=0.0, seed=0, counter=0, out=None):
                                    ctypes.c_uint64(int(seed) & ((1 << 64) - 1)), int(counter), stream_ptr()),
           "select_actions")
     return out
+
+
+def obs_expand(wire, snap_n, snap, out=None, out64=None):
+    """Dense normalised obs from the compact wire format (SURVEY.md §8 f3,
+    include/t2omca.h t2o_obs_expand).  wire int32 [B, T1, A, 4] (episode / step
+    strides free, agent rows dense), snap_n int64 [B], snap f64 [B, 2, 9A];
+    returns f32 [B, T1, A, 9A] (or writes `out`, any episode / step strides with
+    dense steps); out64 optionally receives the fp64 values (dense)."""
+    for t in (wire, snap_n, snap, out, out64):
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("obs_expand needs HIP-device tensors (no CPU fallback)")
+    if wire.dtype != torch.int32 or snap_n.dtype != torch.int64 or snap.dtype != torch.float64:
+        raise TypeError("obs_expand: wire int32, snap_n int64, snap float64")
+    B, T1, A, four = wire.shape
+    assert four == 4 and wire.stride(3) == 1 and wire.stride(2) == 4
+    assert snap_n.shape == (B,) and snap.shape == (B, 2, 9 * A) and snap.is_contiguous() and snap_n.is_contiguous()
+    if out is None:
+        out = torch.empty(B, T1, A, 9 * A, device=wire.device)
+    assert out.dtype == torch.float32 and out.shape == (B, T1, A, 9 * A)
+    assert out.stride(3) == 1 and out.stride(2) == 9 * A
+    if out64 is not None:
+        assert out64.dtype == torch.float64 and out64.shape == out.shape and out64.is_contiguous()
+    check(lib().t2o_obs_expand(ptr(wire), wire.stride(0), wire.stride(1), ptr(snap_n), ptr(snap), ptr(out),
+                               out.stride(0), out.stride(1), ptr(out64), B, T1, A, stream_ptr(wire.device)),
+          "obs_expand")
+    return out

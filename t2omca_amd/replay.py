@@ -25,6 +25,9 @@ from ._lib import check, lib, ptr, stream_ptr
 
 
 class PrioritizedReplayBuffer:
+    # per-episode fields (no time axis): the wire-format obs normaliser snapshot
+    EPISODE_KEYS = ("obs_nrm_n", "obs_nrm")
+
     def __init__(self, example_batch, buffer_size, max_seq_length, alpha, beta, t_max, *, device="cuda", seed=0):
         """example_batch: a dict of [n, max_seq_length, ...] tensors (e.g. one
         RolloutRunner batch) giving the scheme (keys, per-step shapes, dtypes)."""
@@ -35,7 +38,7 @@ class PrioritizedReplayBuffer:
         self.seed = int(seed)
         self.data = {}
         for k, v in example_batch.items():
-            if v.shape[1] != self.max_seq_length:
+            if k not in self.EPISODE_KEYS and v.shape[1] != self.max_seq_length:
                 raise ValueError(f"{k}: time extent {v.shape[1]} != max_seq_length {self.max_seq_length}")
             self.data[k] = torch.zeros((self.buffer_size,) + tuple(v.shape[1:]), dtype=v.dtype, device=self.device)
         self.p = torch.zeros(self.buffer_size, dtype=torch.float32, device=self.device)  # priority ** alpha

@@ -25,6 +25,13 @@ the env kernel; the batch dict holds the [n, T+1, ...] views the learner takes
 
 ε schedule: PyMARL's DecayThenFlatSchedule (linear), evaluated per rollout at
 t_env as the reference's selector does; test_mode selects greedily.
+
+compact_obs=True (the env must be a VecEnv(wire=True)): the
+batch carries the observation wire format instead of the dense obs —
+``obs_wire`` [n, T+1, A, 4] int32 plus the per-episode normaliser snapshot
+``obs_nrm_n`` [n] / ``obs_nrm`` [n, 2, 9A] — and each step's dense obs goes only
+to a one-step scratch buffer the agent reads.  ``ops.obs_expand`` (called by
+TDLearner.train when the batch has no ``obs``) rebuilds the dense obs exactly.
 """
 import torch
 
@@ -44,7 +51,10 @@ class LinearSchedule:
 
 class RolloutRunner:
     def __init__(self, agent, env, *, epsilon_start=1.0, epsilon_finish=0.05, epsilon_anneal_time=50000,
-                 seed=0):
+                 seed=0, compact_obs=False):
+        if compact_obs and getattr(env, "wire", None) is None:
+            raise ValueError("compact_obs needs a VecEnv built with wire=True")
+        self.compact_obs = bool(compact_obs)
         if env.A != agent.shape.n_ent or env.n_actions != agent.shape.NA:
             raise ValueError("agent and env disagree on agents / actions")
         self.agent, self.env = agent, env
@@ -59,8 +69,13 @@ class RolloutRunner:
     # -- replay batch ---------------------------------------------------------
     def _alloc(self):
         n, T1, A, NA, dev = self.n, self.T + 1, self.A, self.NA, self.device
+        if self.compact_obs:
+            obs = dict(obs_wire=torch.empty(T1, n, A, 4, dtype=torch.int32, device=dev))
+            self._obs_step = torch.empty(n, A, 9 * A, device=dev)
+        else:
+            obs = dict(obs=torch.empty(T1, n, A, 9 * A, device=dev))
         return dict(
-            obs=torch.empty(T1, n, A, 9 * A, device=dev),
+            **obs,
             state=torch.empty(T1, n, 8 * A, device=dev),
             avail_actions=torch.empty(T1, n, A, NA, dtype=torch.int32, device=dev),
             actions=torch.zeros(T1, n, A, 1, dtype=torch.int64, device=dev),
@@ -78,24 +93,32 @@ class RolloutRunner:
         env, shape = self.env, self.agent.shape
         pack = ops.pack_params(shape, torch.cat([p.detach().reshape(-1) for p in self.agent.parameters()]))
         eps = 0.0 if test_mode else self.schedule.eval(self.t_env)
-        env.reset(dest={"obs": tm["obs"][0], "state": tm["state"][0], "avail": tm["avail_actions"][0]})
+        env.reset(dest=self._dest(tm, 0))
         ret = torch.zeros(self.n, dtype=torch.float64, device=self.device)
         h = None
         for t in range(self.T + 1):
-            q, h_seq = ops.agent_unroll_fwd(shape, pack, tm["obs"][t].unsqueeze(1), h0_on=h)
+            obs_t = self._obs_step if self.compact_obs else tm["obs"][t]
+            q, h_seq = ops.agent_unroll_fwd(shape, pack, obs_t.unsqueeze(1), h0_on=h)
             h = h_seq.view(self.n * self.A, shape.E)
             counter = (self.episode * (self.T + 1) + t)
             ops.select_actions(q[:, 0], tm["avail_actions"][t], eps, self.seed, counter,
                                out=tm["actions"][t, :, :, 0])
             if t == self.T:
                 break
-            reward, _, _, _, _, _ = env.step(tm["actions"][t, :, :, 0],
-                                            dest={"obs": tm["obs"][t + 1], "state": tm["state"][t + 1],
-                                                  "avail": tm["avail_actions"][t + 1]})
+            reward, _, _, _, _, _ = env.step(tm["actions"][t, :, :, 0], dest=self._dest(tm, t + 1))
             tm["reward"][t, :, 0].copy_(reward)
             ret += reward
         if not test_mode:
             self.t_env += self.n * self.T
         self.episode += 1
         batch = {k: v.transpose(0, 1) for k, v in tm.items()}
+        if self.compact_obs:  # per-episode: the normaliser each episode's obs start from
+            batch["obs_nrm_n"] = env.snap_n.clone()
+            batch["obs_nrm"] = env.snap.clone()
         return batch, ret
+
+    def _dest(self, tm, t):
+        if self.compact_obs:
+            return {"obs": self._obs_step, "wire": tm["obs_wire"][t], "state": tm["state"][t],
+                    "avail": tm["avail_actions"][t]}
+        return {"obs": tm["obs"][t], "state": tm["state"][t], "avail": tm["avail_actions"][t]}

@@ -1,0 +1,121 @@
+"""GPU: the compact observation wire format.
+
+* the env kernel's wire rows and normaliser snapshots equal the numpy
+  restatement's (oracle/ref_wire.py, itself pinned to the reference env's obs in
+  tests/test_wire_oracle.py) on the reference-produced golden trajectories;
+* t2o_obs_expand rebuilds the env's own dense obs bit for bit (f32 and f64) on
+  larger random rollouts, including A = 64 / M = 16 and several episodes per env
+  (the normaliser carries over between episodes);
+* a wire-format rollout batch trains to the same TD update as the dense one.
+Bar: bit-exact (gradients: 1e-5 normwise, float-atomic summation order)."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ref_wire
+from oracle.ref_env import RefEnv
+from tests.gpu_util import require_gpu
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "env_*.npz"))))
+def test_env_wire_matches_oracle_on_reference_trajectories(path):
+    require_gpu()
+    from t2omca_amd.env import VecEnv
+    z = np.load(path)
+    M, A, T, eps, seed = (int(z[k]) for k in ("M", "A", "T", "episodes", "seed"))
+    NE = len({k.split("/")[0] for k in z.files if k.startswith("env")})
+    env = VecEnv(NE, mec_num=M, agv_num=A, episode_limit=T, seed=seed, wire=True)
+    env.get_env_info(all_envs=True)
+    refs = []
+    for e in range(NE):
+        r = RefEnv(M, A, T, seed, e)
+        r.get_env_info()
+        refs.append(ref_wire.record_episodes(r, z[f"env{e}/actions"], eps))
+    k = 0
+    for ep in range(eps):
+        env.reset()
+        for e in range(NE):
+            n, mean, S = refs[e][ep][0]
+            assert int(env.snap_n[e]) == n
+            assert np.array_equal(env.snap[e, 0].cpu().numpy(), mean)
+            assert np.array_equal(env.snap[e, 1].cpu().numpy(), S)
+        for t in range(T + 1):
+            if t:
+                env.step(torch.from_numpy(np.stack([z[f"env{e}/actions"][k] for e in range(NE)]).astype(np.int64))
+                         .cuda())
+                k += 1
+            got = env.wire.cpu().numpy()
+            for e in range(NE):
+                assert np.array_equal(got[e], refs[e][ep][1][t]), (path, ep, t, e)
+
+
+@pytest.mark.parametrize("NE,M,A,T,eps", [(96, 2, 8, 12, 2), (40, 4, 16, 9, 2), (12, 16, 64, 5, 2), (5, 3, 3, 7, 3)])
+def test_obs_expand_reproduces_env_obs(NE, M, A, T, eps):
+    require_gpu()
+    from t2omca_amd import ops
+    from t2omca_amd.env import VecEnv
+    env = VecEnv(NE, mec_num=M, agv_num=A, episode_limit=T, seed=7, keep_obs64=True, wire=True)
+    env.get_env_info()
+    rng = np.random.default_rng(1)
+    for _ in range(eps):
+        wire = torch.empty(T + 1, NE, A, 4, dtype=torch.int32, device="cuda")
+        dense = torch.empty(T + 1, NE, A, 9 * A, device="cuda")
+        dense64 = torch.empty(T + 1, NE, A, 9 * A, dtype=torch.float64, device="cuda")
+        env.reset(dest={"wire": wire[0], "obs": dense[0]})
+        dense64[0].copy_(env.obs64)
+        snap_n, snap = env.snap_n.clone(), env.snap.clone()
+        for t in range(T):
+            acts = torch.from_numpy(rng.integers(0, env.n_actions, (NE, A))).cuda()
+            env.step(acts, dest={"wire": wire[t + 1], "obs": dense[t + 1]})
+            dense64[t + 1].copy_(env.obs64)
+        # time-major views: episode stride A*4 / A*9A, step stride NE*...
+        out64 = torch.empty(NE, T + 1, A, 9 * A, dtype=torch.float64, device="cuda")
+        got = ops.obs_expand(wire.transpose(0, 1), snap_n, snap, out64=out64)
+        torch.cuda.synchronize()
+        assert torch.equal(got, dense.transpose(0, 1))
+        assert torch.equal(out64, dense64.transpose(0, 1))
+        # strided output straight into a time-major buffer
+        tm = torch.full((T + 1, NE, A, 9 * A), float("nan"), device="cuda")
+        ops.obs_expand(wire.transpose(0, 1), snap_n, snap, out=tm.transpose(0, 1))
+        assert torch.equal(tm, dense)
+
+
+def test_wire_rollout_trains_like_dense():
+    """RolloutRunner(compact_obs=True) -> replay -> TDLearner equals the dense path."""
+    require_gpu()
+    from t2omca_amd.env import VecEnv
+    from t2omca_amd.learner import TDLearner
+    from t2omca_amd.modules import TransformerAgent, TransformerMixer
+    from t2omca_amd.replay import PrioritizedReplayBuffer
+    from t2omca_amd.runner import RolloutRunner
+    from t2omca_amd.synthetic import make_args
+    A, M, T, n = 8, 2, 6, 16
+    results = []
+    for compact in (False, True):
+        torch.manual_seed(0)
+        args = make_args(A)
+        agent, mixer = TransformerAgent(None, args).cuda(), TransformerMixer(args).cuda()
+        env = VecEnv(n, mec_num=M, agv_num=A, episode_limit=T, seed=3, wire=compact)
+        env.get_env_info()
+        runner = RolloutRunner(agent, env, seed=5, compact_obs=compact)
+        batch, _ = runner.run()
+        if compact:
+            assert "obs" not in batch and batch["obs_wire"].shape == (n, T + 1, A, 4)
+        buf = PrioritizedReplayBuffer(batch, 32, T + 1, 0.6, 0.4, 1000)
+        buf.insert_episode_batch(batch)
+        sample, idx, w = buf.sample(8, 0)
+        learner = TDLearner(agent, mixer)
+        info = learner.train(sample, 0, 0, per_weight=w)
+        torch.cuda.synchronize()
+        results.append((learner.grad.clone(), info["td_errors_abs"].clone(), idx.clone()))
+    assert torch.equal(results[0][2], results[1][2])
+    assert torch.equal(results[0][1], results[1][1])  # forward + TD: bit-identical
+    # the BPTT sums a few small grads with float atomics (order-dependent rounding)
+    g0, g1 = results[0][0], results[1][0]
+    assert float((g0 - g1).abs().max() / g0.abs().max()) < 1e-5
