@@ -494,12 +494,15 @@ __global__ __launch_bounds__(64) void env_kernel(EnvArgs a) {
 }
 
 // ---- t2o_obs_expand: wire records -> dense normalised obs --------------------
-// One thread per (episode, feature p = 9j + f): the normaliser is elementwise,
-// so feature p's running (mean, S) is a private chain over (t, agent i) in the
-// reference's order (get_obs updates agent by agent, normalization.py:12-35),
-// with the same IEEE operations as get_obs above.  The wire rows of one step
-// (A x 16 B per episode) are staged in LDS and read as broadcasts.
-constexpr int XP_THREADS = 576;  // 9 x 64 features at A = 64
+// One thread per (episode b, feature p = 9j + f), flattened over b·9A so every
+// CU gets waves whatever A is: the normaliser is elementwise, so feature p's
+// running (mean, S) is a private chain over (t, agent i) in the reference's order
+// (get_obs updates agent by agent, normalization.py:12-35), with the same IEEE
+// operations as get_obs above.  Each one-wave workgroup stages the wire rows of
+// the (at most A·(64/9A + 2) <= 128) episode rows its lanes touch at step t in
+// LDS and reads them as broadcasts.  The chain is fp64 division/sqrt bound.
+constexpr int XP_THREADS = 64;
+constexpr int XP_ROWS = 128;
 
 struct ExpandArgs {
   const int32_t* wire;
@@ -509,16 +512,23 @@ struct ExpandArgs {
   float* obs;
   int64_t o_sb, o_st;  // float-element strides of episode / step
   double* obs64;       // dense [B][T1][A][9A] or null
-  int B, T1, A, epb;
+  int B, T1, A;
 };
 
 __global__ __launch_bounds__(XP_THREADS) void obs_expand_kernel(ExpandArgs a) {
-  __shared__ int4 rows[64];  // [episode-in-block * A + agent]: epb * A <= 64
+  __shared__ int4 rows[XP_ROWS];  // [(episode - b0) * A + agent]
   const int A = a.A, n9 = 9 * A;
-  const int le = threadIdx.x / n9, p = threadIdx.x % n9;
-  const int b = blockIdx.x * a.epb + le;
-  const bool live = le < a.epb && b < a.B;
+  const int64_t total = (int64_t)a.B * n9;
+  const int64_t g0 = (int64_t)blockIdx.x * XP_THREADS;
+  const int64_t gid = g0 + threadIdx.x;
+  const bool live = gid < total;
+  const int b0 = (int)(g0 / n9);
+  const int b1 = (int)(((g0 + XP_THREADS < total ? g0 + XP_THREADS : total) - 1) / n9);
+  const int nrows = (b1 - b0 + 1) * A;
+  const int b = live ? (int)(gid / n9) : b0;
+  const int p = (int)(gid - (int64_t)b * n9);
   const int j = p / 9, f = p % 9;
+  const int rb = (b - b0) * A;
   double mean = 0.0, S = 0.0;
   int64_t n = 0;
   if (live) {
@@ -526,17 +536,14 @@ __global__ __launch_bounds__(XP_THREADS) void obs_expand_kernel(ExpandArgs a) {
     mean = a.snap[(size_t)b * 2 * n9 + p];
     S = a.snap[(size_t)b * 2 * n9 + n9 + p];
   }
-  const int nrows = a.epb * A;
   for (int t = 0; t < a.T1; ++t) {
     __syncthreads();
-    for (int r = threadIdx.x; r < nrows; r += blockDim.x) {
-      const int bb = blockIdx.x * a.epb + r / A;
-      if (bb < a.B)
-        rows[r] = *reinterpret_cast<const int4*>(a.wire + (size_t)bb * a.w_sb + (size_t)t * a.w_st + 4 * (r % A));
-    }
+    for (int r = threadIdx.x; r < nrows; r += XP_THREADS)
+      rows[r] = *reinterpret_cast<const int4*>(a.wire + (size_t)(b0 + r / A) * a.w_sb + (size_t)t * a.w_st +
+                                               4 * (r % A));
     __syncthreads();
     if (!live) continue;
-    const int4 wj = rows[le * A + j];
+    const int4 wj = rows[rb + j];
     const int mec_j = (wj.w >> 26) & 63;
     double xj;  // entity j's field f as seen from an agent of the same MEC (f < 8)
     switch (f) {
@@ -551,27 +558,25 @@ __global__ __launch_bounds__(XP_THREADS) void obs_expand_kernel(ExpandArgs a) {
     double* orow64 = a.obs64 ? a.obs64 + (((size_t)b * a.T1 + t) * A) * n9 : nullptr;
     for (int i = 0; i < A; ++i) {
       ++n;
-      const int mec_i = (rows[le * A + i].w >> 26) & 63;
+      const int mec_i = (rows[rb + i].w >> 26) & 63;
       double x = 0.0;
       if (mec_i == mec_j) x = f < 8 ? xj : (i == j ? 1.0 : 0.0);
-      double m, d;
+      double m, v;
       if (n == 1) {
         m = x;
-        d = x;
+        v = (x - m) / (x + 1e-8);
       } else {
         const double old = mean;
         m = old + (x - old) / (double)n;
         S = S + (x - old) * (x - m);
-        d = sqrt(S / (double)n);
+        v = (x - m) / (sqrt(S / (double)n) + 1e-8);
       }
       mean = m;
-      const double v = (x - m) / (d + 1e-8);
       if (orow) orow[(size_t)i * n9 + p] = (float)v;
       if (orow64) orow64[(size_t)i * n9 + p] = v;
     }
   }
 }
-
 }  // namespace
 
 extern "C" int t2o_env_run_ex(int mode, const double* spec, void* const* state, void* const* out, int n_out,
@@ -627,11 +632,8 @@ extern "C" int t2o_obs_expand(const int32_t* wire, int64_t w_sb, int64_t w_st, c
       (w_sb | w_st) % 4 != 0 || (obs && o_st < (int64_t)A * 9 * A) || (obs && B > 1 && o_sb < (int64_t)A * 9 * A))
     return T2O_EINVAL;
   if (((uintptr_t)wire & 15) != 0) return T2O_EINVAL;
-  ExpandArgs a{wire, w_sb, w_st, snap_n, snap, obs, o_sb, o_st, obs64, B, T1, A, 0};
-  const int n9 = 9 * A;
-  a.epb = XP_THREADS / n9 < 1 ? 1 : XP_THREADS / n9;
-  const int threads = (a.epb * n9 + 63) / 64 * 64;
-  const int blocks = (B + a.epb - 1) / a.epb;
-  hipLaunchKernelGGL(obs_expand_kernel, dim3(blocks), dim3(threads), 0, (hipStream_t)stream, a);
+  ExpandArgs a{wire, w_sb, w_st, snap_n, snap, obs, o_sb, o_st, obs64, B, T1, A};
+  const int64_t blocks = ((int64_t)B * 9 * A + XP_THREADS - 1) / XP_THREADS;
+  hipLaunchKernelGGL(obs_expand_kernel, dim3((unsigned)blocks), dim3(XP_THREADS), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
