@@ -380,28 +380,6 @@ constexpr int AGP_TILES = AG_BWD_WAVES;  // tiles per workgroup (same slab count
 template <int E>
 constexpr int agp_xch_floats() { return 3 * (E / 16) * 64 * 4; }
 
-// Layout whose block-0 slots hold block d's offsets: the block code is then
-// called with the constant d = 0, and every offset it reads is a scalar.
-T2O_DEV t2o_layout block_view(const t2o_layout& L, int d) {
-  t2o_layout V = L;
-  V.M[0] = L.M[d];
-  V.MT[0] = L.MT[d];
-  V.N[0] = L.N[d];
-  V.NT[0] = L.NT[d];
-  V.bu[0] = L.bu[d];
-  V.g1[0] = L.g1[d];
-  V.n1[0] = L.n1[d];
-  V.W1[0] = L.W1[d];
-  V.W1T[0] = L.W1T[d];
-  V.c1[0] = L.c1[d];
-  V.W2[0] = L.W2[d];
-  V.W2T[0] = L.W2T[d];
-  V.c2[0] = L.c2[d];
-  V.g2[0] = L.g2[d];
-  V.n2[0] = L.n2[d];
-  return V;
-}
-
 template <int E, int H, int D, int NE, int FF, typename WT>
 __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(AgentBwdArgs args) {
   static_assert(D == 2, "one wave per block of a depth-2 stack");

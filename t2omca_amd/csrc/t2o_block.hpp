@@ -118,6 +118,113 @@ T2O_DEV void post_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G
   matvec_tr<HET, ET>(P, L.N[d], H * E, L.NT[d], E, gres, gz);
 }
 
+// Lean variant for the two-wave pipelined kernels, whose cache must live in
+// half a register file: the tape operands already known in the forward (x, z,
+// y) are written to the record by the recompute itself, and the FFN's ReLU is
+// kept as a bit mask (its only use in the backward).  Same records, same math.
+template <int E, int H, int FF>
+struct PostCacheLean {
+  static constexpr int ET = E / 16, FT = FF / 16;
+  static_assert(FT * 4 <= 32, "ReLU mask is one 32-bit register");
+  f4 xh1[ET];
+  float rs1;
+  uint32_t relu;  // bit 4t + r: f1[t][r] > 0
+  f4 xh2[ET];
+  float rs2;
+};
+
+template <int E, int H, int FF, typename WT>
+T2O_DEV void post_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d, const f4* z, f4* x,
+                           PostCacheLean<E, H, FF>* c, WT* __restrict__ rec) {
+  constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
+  using R = TapeRec<E, H, FF>;
+  if (rec) {
+    rec_store<R::SIZE, ET>(rec, R::X, x);
+    rec_store<R::SIZE, HET>(rec, R::Z, z);
+  }
+  f4 r1[ET];
+  matvec<ET, HET>(P.w + L.N[d], H * E, z, r1);
+#pragma unroll
+  for (int t = 0; t < ET; ++t) r1[t] += vec_t(P.v + L.bu[d], t) + x[t];
+  f4 y[ET];
+  layernorm_fwd<ET>(r1, P.v + L.g1[d], P.v + L.n1[d], y, c->xh1, c->rs1);
+  if (rec) rec_store<R::SIZE, ET>(rec, R::Y, y);
+  f4 f1[FT], f1r[FT];
+  matvec<FT, ET>(P.w + L.W1[d], E, y, f1);
+  uint32_t m = 0;
+#pragma unroll
+  for (int t = 0; t < FT; ++t) {
+    f1[t] += vec_t(P.v + L.c1[d], t);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      f1r[t][r] = fmaxf(f1[t][r], 0.f);
+      m |= (f1r[t][r] > 0.f ? 1u : 0u) << (4 * t + r);
+    }
+  }
+  c->relu = m;
+  f4 r2[ET];
+  matvec<ET, FT>(P.w + L.W2[d], FF, f1r, r2);
+#pragma unroll
+  for (int t = 0; t < ET; ++t) r2[t] += vec_t(P.v + L.c2[d], t) + y[t];
+  layernorm_fwd<ET>(r2, P.v + L.g2[d], P.v + L.n2[d], x, c->xh2, c->rs2);
+}
+
+// post_bwd for the lean cache (the X, Z, Y record fields were written forward)
+template <int E, int H, int FF, typename WT>
+T2O_DEV void post_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restrict__ gs, WT* __restrict__ rec,
+                           int d, const PostCacheLean<E, H, FF>& c, const f4* gx, f4* gz, f4* gres, f4* ln2) {
+  constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
+  using R = TapeRec<E, H, FF>;
+#pragma unroll
+  for (int t = 0; t < ET; ++t) {
+    ln2[t] += gx[t] * c.xh2[t];
+    ln2[ET + t] += gx[t];
+  }
+  f4 gr2[ET];
+  layernorm_bwd<ET>(gx, c.xh2, c.rs2, P.v + L.g2[d], gr2);
+  if (rec) rec_store<R::SIZE, ET>(rec, R::GR2, gr2);
+  f4 gf1[FT];
+  matvec_tr<FT, ET>(P, L.W2[d], FF, L.W2T[d], E, gr2, gf1);
+#pragma unroll
+  for (int t = 0; t < FT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gf1[t][r] = (c.relu >> (4 * t + r)) & 1u ? gf1[t][r] : 0.f;
+  f4 gy[ET];
+  matvec_tr<ET, FT>(P, L.W1[d], E, L.W1T[d], FF, gf1, gy);
+#pragma unroll
+  for (int t = 0; t < ET; ++t) gy[t] += gr2[t];
+  if (rec) {
+    rec_store<R::SIZE, ET>(rec, R::XH1, c.xh1);
+    rec_store<R::SIZE, ET>(rec, R::GY, gy);
+  }
+  layernorm_bwd<ET>(gy, c.xh1, c.rs1, P.v + L.g1[d], gres);
+  if (rec) rec_store<R::SIZE, ET>(rec, R::GRES, gres);
+  matvec_tr<HET, ET>(P, L.N[d], H * E, L.NT[d], E, gres, gz);
+  (void)gs;
+}
+
+// Layout whose block-0 slots hold block d's offsets: the block code is then
+// called with the constant d = 0, and every offset it reads is a scalar.
+T2O_DEV t2o_layout block_view(const t2o_layout& L, int d) {
+  t2o_layout V = L;
+  V.M[0] = L.M[d];
+  V.MT[0] = L.MT[d];
+  V.N[0] = L.N[d];
+  V.NT[0] = L.NT[d];
+  V.bu[0] = L.bu[d];
+  V.g1[0] = L.g1[d];
+  V.n1[0] = L.n1[d];
+  V.W1[0] = L.W1[d];
+  V.W1T[0] = L.W1T[d];
+  V.c1[0] = L.c1[d];
+  V.W2[0] = L.W2[d];
+  V.W2T[0] = L.W2T[d];
+  V.c2[0] = L.c2[d];
+  V.g2[0] = L.g2[d];
+  V.n2[0] = L.n2[d];
+  return V;
+}
+
 // LN2 vector grads of every block, summed over this wave's rows and steps
 template <int E, int D>
 T2O_DEV void ln2_flush(float* __restrict__ gs, const t2o_layout& G, const f4 (&ln2)[D][2 * (E / 16)]) {

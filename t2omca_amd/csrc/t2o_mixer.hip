@@ -190,8 +190,8 @@ T2O_DEV void bcast_agents(float mine, float (&qv)[A]) {
 
 // Key block X0 rows for one step from the prefetched inputs: state-entity
 // embeddings and agent hidden tokens (the hyper-token rows are carried in X0).
-template <int E, int A, typename WT>
-T2O_DEV void mix_keys(const Wts<WT>& P, const t2o_layout& L, const MixIn<E, A>& in, float* X0) {
+template <int E, int A, typename WT, typename In>
+T2O_DEV void mix_keys(const Wts<WT>& P, const t2o_layout& L, const In& in, float* X0) {
   using Dm = MixDims<E, A>;
   constexpr int ET = E / 16;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
@@ -674,11 +674,397 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   }
 }
 
+// ---- two waves per episode (depth 2, one query tile) ------------------------
+// As the agent's pipelined BPTT (t2o_agent.hip, agent_bwd_pipe_kernel): each
+// wave of a pair owns one transformer block of one episode, and the two
+// interleave so that one's recompute overlaps the other's backward (phases
+// separated by workgroup barriers):
+//   block-1 wave: keys+fwd1(T-1) | head+bwd1(T-1) | keys+fwd1(T-2) | head+bwd1(T-2) | ...
+//   block-0 wave:        -       |   fwd0(T-1)    |  bwd0+X0(T-1)  |   fwd0(T-2)    | ...
+// The dependent chain per step is head -> bwd1 -> bwd0 -> hyper-token grads ->
+// head of the step before; the recomputes (key block, block forwards with
+// cache) come off it.  Pair LDS: the key block X0 (written by the block-1
+// wave's recompute, read by both recomputes, untouched in backward phases) and
+// one region R owned by whichever wave is in its backward phase: head rows and
+// dW staging, then the hand-over 1 -> 0 [block-1 key grads (rows < LK) | grad
+// wrt the block-1 input (query rows, in R's padding rows)], then the step's
+// total key grads written by the block-0 wave, whose hyper rows the block-1
+// wave reads at its next backward.  Per-step math, records and slab sums are
+// those of mixer_bwd_kernel.
+template <int E, int A>
+struct MixPipeDims {
+  using Dm = MixDims<E, A>;
+  using Bd = MixBwdDims<E, A>;
+  static constexpr int XCH = Dm::LK * E;  // offset of the query-row grads in R
+  static constexpr int REGION = Bd::W0 > Dm::GX0F ? Bd::W0 : Dm::GX0F;
+  static constexpr int PAIRF = Dm::X0F + REGION;
+  static constexpr bool OK = Dm::QT == 1 && XCH + Dm::Q * E <= REGION;
+};
+
+// T2O_MIXER_BWD=single selects the one-wave kernel (A/B timing, parity cross-check)
+inline bool mixer_bwd_single_wave() {
+  static const bool single = [] {
+    const char* e = getenv("T2O_MIXER_BWD");
+    return e && e[0] == 's';
+  }();
+  return single;
+}
+
+// The block-1 wave's per-step inputs (none recurrent), prefetched a phase
+// ahead: the backward's Q selection is qmode 0, so only qvals ride along.
+template <int E, int A>
+struct MixPIn {
+  using Dm = MixDims<E, A>;
+  static constexpr int ET = E / 16;
+  static constexpr int HV = MixIn<E, A>::HV, HW = MixBwdIn<E, A, 2>::HW, XO = MixBwdIn<E, A, 2>::XO;
+  f4 st[Dm::ST];
+  f4 hid[HV];
+  float qv;
+  float hwp[HW];
+  float xo[XO];
+  float ghx[3];
+  float gy;
+  f4 xm[ET];  // stored block-1 input (T-layout query rows)
+};
+
+template <int E, int A>
+T2O_DEV void mixp_load(const MixerBwdArgs& args, int b, int t, MixPIn<E, A>& in) {
+  using Dm = MixDims<E, A>;
+  using In = MixPIn<E, A>;
+  const MixerFwdArgs& fa = args.f;
+  const MixerNet& n = fa.net[0];
+  const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
+  const float* st = fa.states + b * fa.st_sb + t * fa.st_st;
+#pragma unroll
+  for (int s = 0; s < Dm::ST; ++s) {
+    const int j = 16 * s + c;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int f = 4 * g + r;
+      in.st[s][r] = ld_or0(st, j * fa.Fs + f, j < Dm::NS && f < fa.Fs);
+    }
+  }
+  const float* hd = n.hid + b * n.hid_sb + t * n.hid_st;
+#pragma unroll
+  for (int k = 0; k < In::HV; ++k) {
+    const int i = lane + 64 * k;
+    in.hid[k] = i < A * E / 4 ? ld4(hd + 4 * i) : zero4();
+  }
+  const size_t bt = (size_t)b * n.T + t;
+  in.qv = n.qv_in[bt * A + (lane < A ? lane : A - 1)];
+#pragma unroll
+  for (int k = 0; k < In::HW; ++k) {
+    const int i = lane + 64 * k;
+    float v = 0.f;
+    if (i < 3 * E) v = t > 0 ? args.hw[(bt - 1) * 3 * E + i] : (n.hw0 ? n.hw0[(size_t)b * 3 * E + i] : 0.f);
+    in.hwp[k] = v;
+  }
+#pragma unroll
+  for (int k = 0; k < In::XO; ++k) {
+    const int i = lane + 64 * k;
+    in.xo[k] = i < Dm::Q * E ? args.xout[bt * Dm::Q * E + i] : 0.f;
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) in.ghx[k] = (args.ghw_ext && lane < E) ? args.ghw_ext[(bt * 3 + k) * E + lane] : 0.f;
+  in.gy = args.gy[bt];
+#pragma unroll
+  for (int ft = 0; ft < In::ET; ++ft)
+    in.xm[ft] = c < Dm::Q ? ld4(args.xmid + (bt * Dm::Q + c) * E + 16 * ft + 4 * g) : zero4();
+}
+
+template <int E, int A>
+T2O_DEV void mixp_load_stT(const MixerFwdArgs& fa, int b, int t, f4 (&stT)[MixDims<E, A>::ST]) {
+  using Dm = MixDims<E, A>;
+  const int c = lane_c(), g = lane_g();
+  const float* st = fa.states + b * fa.st_sb + t * fa.st_st;
+#pragma unroll
+  for (int s = 0; s < Dm::ST; ++s)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * s + 4 * g + r;
+      float v = ld_or0(st, j * fa.Fs + c, j < Dm::NS && c < fa.Fs);
+      if (j < Dm::NS && c == fa.Fs) v = 1.f;
+      stT[s][r] = v;
+    }
+}
+
+// block-1 wave: key block + block-1 recompute, then head + block-1 backward
+template <int E, int H, int A, int FF, typename WT>
+T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_layout& L, const t2o_layout& Lb,
+                         const t2o_layout& Gb, float* __restrict__ gs, float* X0, float* R, int b) {
+  using Dm = MixDims<E, A>;
+  using Pd = MixPipeDims<E, A>;
+  using In = MixPIn<E, A>;
+  using Rec = TapeRec<E, H, FF>;
+  constexpr int ET = E / 16, KT = Dm::KT;
+  constexpr bool BF = sizeof(WT) == 2;
+  const MixerFwdArgs& fa = args.f;
+  const MixerNet& n = fa.net[0];
+  const int T = n.T;
+  const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
+  const int f = lane < E ? lane : 0;
+  const bool fv = lane < E;
+  const size_t ntiles = (size_t)fa.B * T;
+  constexpr size_t RECD = 1;  // tape block
+  f4 ln2[2 * ET];
+#pragma unroll
+  for (int i = 0; i < 2 * ET; ++i) ln2[i] = zero4();
+  float gWo = 0.f, gbo = 0.f;
+  In cur;
+  for (int t = T - 1; t >= 0; --t) {
+    const size_t bt = (size_t)b * T + t;
+    WT* rec = static_cast<WT*>(args.tape) + (RECD * ntiles + (size_t)t * fa.B + b) * Rec::SIZE * 16;
+    MixerCacheLean<E, H, KT, FF> cache;
+    KeyFrags<E, KT, BF> K;
+    {  // ---- recompute: key block of step t, block-1 forward with cache
+      // (this phase has slack under the block-0 backward: the step's inputs load here)
+      mixp_load<E, A>(args, b, t, cur);
+      const Wts<WT> P = step_view(P0);
+      mix_keys<E, A>(P, L, cur, X0);
+#pragma unroll
+      for (int k = 0; k < In::HW; ++k) {
+        const int i = lane + 64 * k;
+        if (i < 3 * E) X0[(Dm::NS + A + i / E) * Dm::LDX + i % E] = cur.hwp[k];
+      }
+      __builtin_amdgcn_wave_barrier();
+      K.template load<Dm::LDX>(X0);
+      f4 x[ET];
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft) x[ft] = cur.xm[ft];
+      mixer_block_fwd_lean<E, H, KT, FF>(P, Lb, 0, K, Dm::LK, x, cache, rec);
+    }
+    __syncthreads();
+    {  // ---- backward: mixing head, block 1
+      const Wts<WT> P = step_view(P0);
+      float ghw[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) ghw[k] = (t < T - 1 && fv) ? R[(Dm::NS + A + k) * E + f] : 0.f;
+      __builtin_amdgcn_wave_barrier();
+      float* OUT = R;  // forward final query rows, then their grads in place
+#pragma unroll
+      for (int k = 0; k < In::XO; ++k) {
+        const int i = lane + 64 * k;
+        if (i < Dm::Q * E) OUT[i] = cur.xo[k];
+      }
+      __builtin_amdgcn_wave_barrier();
+      float qv[A];
+      bcast_agents<A>(cur.qv, qv);
+      float pre_h, pre2;
+      (void)mixer_head<E, A>(P, L, OUT, qv, pre_h, pre2);
+      const float gyv = cur.gy;
+      const float hidden = elu1(pre_h);
+      const float xw2 = OUT[(A + 1) * E + f];
+      const float sgn_w2 = (xw2 > 0.f) - (xw2 < 0.f);
+      const float gpre = gyv * fabsf(xw2) * (pre_h > 0.f ? 1.f : expf(pre_h));
+      const float gpre2 = pre2 > 0.f ? gyv : 0.f;
+      float gout[A + 3];
+      float gqm = 0.f;
+#pragma unroll
+      for (int ag = 0; ag < A; ++ag) {
+        const float xa = OUT[ag * E + f];
+        gout[ag] = qv[ag] * gpre * ((xa > 0.f) - (xa < 0.f));
+        const float gq = feat_sum<E>(fv ? gpre * fabsf(xa) : 0.f);
+        gqm = lane == ag ? gq : gqm;
+      }
+      if (lane < A) args.gqv[bt * A + lane] = gqm;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) ghw[k] += cur.ghx[k];
+      gout[A] = gpre + ghw[0];
+      gout[A + 1] = gyv * hidden * sgn_w2 + ghw[1];
+      const float x2 = OUT[(A + 2) * E + f];
+      gout[A + 2] = gpre2 * P.s(L.Wo + f) + ghw[2];
+      gWo += gpre2 * x2;
+      gbo += gpre2;
+      __builtin_amdgcn_wave_barrier();
+      if (fv) {
+#pragma unroll
+        for (int q = 0; q < A + 3; ++q) OUT[q * E + f] = gout[q];
+      }
+      __builtin_amdgcn_wave_barrier();
+      f4 gx[ET];
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft) gx[ft] = c < Dm::Q ? ld4(OUT + c * E + 16 * ft + 4 * g) : zero4();
+      __builtin_amdgcn_wave_barrier();
+      f4 gX0[KT][ET];
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft) gX0[kt][ft] = zero4();
+      mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, gX0, cache, gx, ln2);
+      __builtin_amdgcn_wave_barrier();
+      // hand-over to the block-0 wave
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * kt + 4 * g + r;
+            if (row < Dm::LK) R[row * E + 16 * ft + c] = gX0[kt][ft][r];
+          }
+      if (c < Dm::Q) {
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft) st4(R + Pd::XCH + c * E + 16 * ft + 4 * g, gx[ft]);
+      }
+    }
+    __syncthreads();
+  }
+  __syncthreads();  // the block-0 wave's last backward phase
+  vec_accumulate_g<ET>(gs + Gb.g2[0], &ln2[0]);
+  vec_accumulate_g<ET>(gs + Gb.n2[0], &ln2[ET]);
+  if (fv) unsafeAtomicAdd(gs + Gb.Wo + f, gWo);
+  if (lane == 0) unsafeAtomicAdd(gs + Gb.bo, gbo);
+}
+
+// block-0 wave: block-0 recompute, then block-0 backward and the step's key grads
+template <int E, int H, int A, int FF, typename WT>
+T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_layout& Lb, const t2o_layout& Gb,
+                         float* __restrict__ gs, const float* X0, float* R, int b) {
+  using Dm = MixDims<E, A>;
+  using Pd = MixPipeDims<E, A>;
+  using Rec = TapeRec<E, H, FF>;
+  constexpr int ET = E / 16, KT = Dm::KT;
+  constexpr bool BF = sizeof(WT) == 2;
+  const MixerFwdArgs& fa = args.f;
+  const int T = fa.net[0].T;
+  const size_t ntiles = (size_t)fa.B * T;
+  constexpr size_t RECD = 0;  // tape block
+  const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
+  const int f = lane < E ? lane : 0;
+  const bool fv = lane < E;
+  f4 ln2[2 * ET], gWe[ET];
+#pragma unroll
+  for (int i = 0; i < ET; ++i) ln2[i] = ln2[ET + i] = gWe[i] = zero4();
+  f4 stT[Dm::ST];
+  __syncthreads();  // one phase behind the block-1 wave
+  for (int t = T - 1; t >= 0; --t) {
+    const size_t bt = (size_t)b * T + t;
+    WT* rec = static_cast<WT*>(args.tape) + (RECD * ntiles + (size_t)t * fa.B + b) * Rec::SIZE * 16;
+    MixerCacheLean<E, H, KT, FF> cache;
+    KeyFrags<E, KT, BF> K;
+    {  // ---- recompute: block-0 forward with cache (queries = X0's last A+3 rows)
+      mixp_load_stT<E, A>(fa, b, t, stT);  // for this step's state-embedding grads
+      const Wts<WT> P = step_view(P0);
+      K.template load<Dm::LDX>(X0);
+      f4 x[ET];
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft) x[ft] = c < Dm::Q ? ld4(X0 + (Dm::NS + c) * Dm::LDX + 16 * ft + 4 * g) : zero4();
+      mixer_block_fwd_lean<E, H, KT, FF>(P, Lb, 0, K, Dm::LK, x, cache, rec);
+    }
+    __syncthreads();
+    {  // ---- backward: block 0, then the step's key-token grads
+      const Wts<WT> P = step_view(P0);
+      f4 gX0[KT][ET], gx[ET];
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * kt + 4 * g + r;
+            gX0[kt][ft][r] = row < Dm::LK ? R[row * E + 16 * ft + c] : 0.f;
+          }
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft) gx[ft] = c < Dm::Q ? ld4(R + Pd::XCH + c * E + 16 * ft + 4 * g) : zero4();
+      __builtin_amdgcn_wave_barrier();
+      mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, gX0, cache, gx, ln2);
+      // state embedding grads from the key-grad registers (as mixer_bwd_kernel)
+#pragma unroll
+      for (int s = 0; s < Dm::ST; ++s)
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft) {
+          f4 am;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) am[r] = 16 * s + 4 * g + r < Dm::NS ? gX0[s][ft][r] : 0.f;
+          if constexpr (BF) {
+            gWe[ft] = mfma_b16(to_bf4(am), to_bf4(stT[s]), gWe[ft]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) gWe[ft] = mfma4(am[r], stT[s][r], gWe[ft]);
+          }
+        }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) R[(16 * kt + 4 * g + r) * E + 16 * ft + c] = gX0[kt][ft][r];
+      __builtin_amdgcn_wave_barrier();
+      if (c < Dm::Q) {  // the query path: block-0 input rows are X0's last A+3 rows
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft) {
+          float* dst = R + (Dm::NS + c) * E + 16 * ft + 4 * g;
+          st4(dst, ld4(dst) + gx[ft]);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      for (int i = lane; i < A * E / 4; i += 64) st4(args.ghid + bt * A * E + 4 * i, ld4(R + Dm::NS * E + 4 * i));
+      if (t == 0 && args.ghw0 && fv) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) args.ghw0[((size_t)b * 3 + k) * E + f] = R[(Dm::NS + A + k) * E + f];
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int ft = 0; ft < ET; ++ft)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int fe = 16 * ft + 4 * g + r;
+      if (c < fa.Fs) unsafeAtomicAdd(gs + Gb.We + fe * 16 + c, gWe[ft][r]);
+      else if (c == fa.Fs) unsafeAtomicAdd(gs + Gb.be + fe, gWe[ft][r]);
+    }
+  vec_accumulate_g<ET>(gs + Gb.g2[0], &ln2[0]);
+  vec_accumulate_g<ET>(gs + Gb.n2[0], &ln2[ET]);
+  (void)fv;
+}
+
+template <int E, int H, int D, int A, int FF, typename WT>
+__global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) {
+  static_assert(D == 2 && MixPipeDims<E, A>::OK, "one wave per block of a depth-2 stack, one query tile");
+  using Dm = MixDims<E, A>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const t2o_layout& L = args.f.L;
+  const t2o_layout& G = args.G;
+  const int w = __builtin_amdgcn_readfirstlane(wave_id());
+  const int d = w & 1;   // the block this wave owns
+  const int pr = w >> 1; // the episode within the workgroup
+  float* X0 = smem + args.lds_w + pr * MixPipeDims<E, A>::PAIRF;
+  float* R = X0 + Dm::X0F;
+  float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
+  const Wts<WT> P0 = stage_weights(smem, args.f.net[0].pack, L, sizeof(WT) == 4 ? L.fwd_total : L.total, WT{});
+  for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) gs[i] = 0.f;
+  if (d == 1)
+    for (int i = threadIdx.x & 63; i < Dm::X0F; i += 64) X0[i] = 0.f;
+  __syncthreads();
+  const int b = blockIdx.x * args.waves + pr;  // the launcher makes every pair valid
+  const t2o_layout Lb = block_view(L, d), Gb = block_view(G, d);
+  if (d == 1) mixp_block1<E, H, A, FF, WT>(args, P0, L, Lb, Gb, gs, X0, R, b);
+  else mixp_block0<E, H, A, FF, WT>(args, P0, Lb, Gb, gs, X0, R, b);
+}
+
 template <int E, int H, int D, int A, int FF, typename WT>
 int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
   constexpr int PERW = MixBwdDims<E, A>::PERW;
   const t2o_layout& L = args.f.L;
   args.lds_w = (int)((lds_weight_floats<WT>(L, sizeof(WT) == 4 ? L.fwd_total : L.total) + 15) / 16 * 16);
+  if constexpr (D == 2 && MixPipeDims<E, A>::OK) {
+    if (args.xmid && !mixer_bwd_single_wave()) {
+      for (int pairs = 4; pairs >= 1; pairs >>= 1) {
+        const size_t lds = sizeof(float) * ((size_t)args.lds_w + (size_t)pairs * MixPipeDims<E, A>::PAIRF);
+        if (lds > 160 * 1024 || args.f.B % pairs) continue;
+        args.waves = pairs;
+        const int grid = args.f.B / pairs;
+        if (grid > max_slabs) return T2O_EINVAL;
+        auto kern = mixer_bwd_pipe_kernel<E, H, D, A, FF, WT>;
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(128 * pairs), lds, stream, args);
+        *nslab = grid;
+        return (int)hipGetLastError();
+      }
+    }
+  }
   size_t lds = 0;
   bool wlds = true;
   for (args.waves = 4; args.waves >= 1; args.waves >>= 1) {

@@ -189,4 +189,89 @@ T2O_DEV void mixer_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_la
   for (int t = 0; t < ET; ++t) gx[t] = gxp[t] + gres[t];
 }
 
+// Lean cache (PostCacheLean) versions for the two-wave pipelined backward:
+// the forward recompute writes the record's X, Z, Y fields itself.
+template <int E, int H, int KT, int FF>
+struct MixerCacheLean {
+  static constexpr int ET = E / 16, HET = H * ET;
+  PostCacheLean<E, H, FF> post;
+  f4 u[HET];
+  f4 p[H][KT];
+};
+
+template <int E, int H, int KT, int FF, typename WT>
+T2O_DEV void mixer_block_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d,
+                                  const KeyFrags<E, KT, sizeof(WT) == 2>& K, int Lk, f4* x,
+                                  MixerCacheLean<E, H, KT, FF>& cache, WT* __restrict__ rec) {
+  constexpr int ET = E / 16, HET = H * ET;
+  constexpr bool BF = sizeof(WT) == 2;
+  const int g = lane_g();
+  matvec<HET, ET>(P.w + L.M[d], E, x, cache.u);
+  f4 z[HET];
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh) {
+    f4 s[KT];
+    keys_dot<E, KT, BF>(K, &cache.u[hh * ET], s);
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (16 * kt + 4 * g + r >= Lk) s[kt][r] = -INFINITY;
+        m = fmaxf(m, s[kt][r]);
+      }
+    m = allmax4(m);
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s[kt][r] = exp_fast(s[kt][r] - m);
+        l += s[kt][r];
+      }
+    const float il = rcp_fast(allsum4(l));
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      s[kt] *= il;
+      cache.p[hh][kt] = s[kt];
+    }
+    keys_combine<E, KT, BF>(K, s, &z[hh * ET]);
+  }
+  post_fwd_lean<E, H, FF>(P, L, d, z, x, &cache.post, rec);
+}
+
+template <int E, int H, int KT, int FF, typename WT>
+T2O_DEV void mixer_block_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restrict__ gs,
+                                  WT* __restrict__ rec, float* __restrict__ stage, int d,
+                                  const KeyFrags<E, KT, sizeof(WT) == 2>& K, f4 (&gX0)[KT][E / 16],
+                                  const MixerCacheLean<E, H, KT, FF>& c, f4* gx, f4* ln2) {
+  constexpr int ET = E / 16, HET = H * ET;
+  constexpr bool BF = sizeof(WT) == 2;
+  f4 gz[HET], gres[ET];
+  post_bwd_lean<E, H, FF>(P, L, gs, rec, d, c.post, gx, gz, gres, ln2);
+  f4 gu[HET];
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh) {
+    f4 gp[KT];
+    keys_dot<E, KT, BF>(K, &gz[hh * ET], gp);
+    float dot = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dot += c.p[hh][kt][r] * gp[kt][r];
+    dot = allsum4(dot);
+    f4 gsc[KT];
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) gsc[kt] = c.p[hh][kt] * (gp[kt] - dot);
+    keys_combine<E, KT, BF>(K, gsc, &gu[hh * ET]);
+    dw_accumulate_regs<KT, ET, BF>(gX0, c.p[hh], &gz[hh * ET], stage);
+    dw_accumulate_regs<KT, ET, BF>(gX0, gsc, &c.u[hh * ET], stage);
+  }
+  if (rec) rec_store<TapeRec<E, H, FF>::SIZE, HET>(rec, TapeRec<E, H, FF>::GU, gu);
+  f4 gxp[ET];
+  matvec_tr<ET, HET>(P, L.M[d], E, L.MT[d], H * E, gu, gxp);
+#pragma unroll
+  for (int t = 0; t < ET; ++t) gx[t] = gxp[t] + gres[t];
+}
+
 }  // namespace t2o

@@ -248,20 +248,20 @@ class TDLearner:
                                                         defer_contract=True)
         main = torch.cuda.current_stream(dev)
         side = self._side_stream() if self.overlap else main
+        self.grad.zero_()
         side.wait_stream(main)
         with torch.cuda.stream(side):
             gm = contract_m()
+            # mixer grads in reference parameter order, still off the critical path
+            ops.unpack_grads(self.sm, self.params[self.na:], gm, self.grad[self.na:self.na + self.nm])
         # 5. agent BPTT (grads of the chosen Q and, unless detached, of the hidden states)
         slabs_a = self._slab("a", int(ops.lib().t2o_agent_bwd_max_slabs(B, A)) * self.sa.layout().grad_total)
         ga, _ = ops.agent_unroll_bwd(self.sa, self.pack_a, obs, h_on, gchosen=gqv, actions=act,
                                      gh=None if self.detach_mixer_hidden else ghid, slabs=slabs_a,
                                      timer=self.timer, hmid=hmid, tape=tape_a)
-        main.wait_stream(side)
-        gm.record_stream(main)
-        # 6. grads in reference parameter order
-        self.grad.zero_()
+        # 6. agent grads in reference parameter order
         ops.unpack_grads(self.sa, self.params[:self.na], ga, self.grad[:self.na])
-        ops.unpack_grads(self.sm, self.params[self.na:], gm, self.grad[self.na:self.na + self.nm])
+        main.wait_stream(side)
         self.grad[-1:].copy_(td["loss"][1:2])
         allreduce_grad_and_mask(self.grad, self.pg)
         # 7. clip + Adam

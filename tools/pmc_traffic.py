@@ -14,7 +14,7 @@ import re
 import sys
 
 SHORT = {"agent_fwd_kernel": "agent_fwd", "mixer_fwd_kernel": "mixer_fwd", "mixer_bwd_kernel": "mixer_bwd",
-         "agent_bwd_kernel": "agent_bwd", "agent_bwd_pipe_kernel": "agent_bwd", "td_loss_kernel": "td_loss", "adam_kernel": "adam",
+         "agent_bwd_kernel": "agent_bwd", "agent_bwd_pipe_kernel": "agent_bwd", "mixer_bwd_pipe_kernel": "mixer_bwd", "td_loss_kernel": "td_loss", "adam_kernel": "adam",
          "env_kernel": "env_step", "reduce_slabs_kernel": "reduce_slabs", "seg_kernel": "pack"}
 
 
