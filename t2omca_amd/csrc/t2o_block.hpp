@@ -135,20 +135,18 @@ struct PostCacheLean {
 
 template <int E, int H, int FF, typename WT>
 T2O_DEV void post_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d, const f4* z, f4* x,
-                           PostCacheLean<E, H, FF>* c, WT* __restrict__ rec) {
+                           PostCacheLean<E, H, FF>* c, const MaskedRec<WT>& rec) {
   constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
   using R = TapeRec<E, H, FF>;
-  if (rec) {
-    rec_store<R::SIZE, ET>(rec, R::X, x);
-    rec_store<R::SIZE, HET>(rec, R::Z, z);
-  }
+  rec.template store<ET>(R::X, x);
+  rec.template store<HET>(R::Z, z);
   f4 r1[ET];
   matvec<ET, HET>(P.w + L.N[d], H * E, z, r1);
 #pragma unroll
   for (int t = 0; t < ET; ++t) r1[t] += vec_t(P.v + L.bu[d], t) + x[t];
   f4 y[ET];
   layernorm_fwd<ET>(r1, P.v + L.g1[d], P.v + L.n1[d], y, c->xh1, c->rs1);
-  if (rec) rec_store<R::SIZE, ET>(rec, R::Y, y);
+  rec.template store<ET>(R::Y, y);
   f4 f1[FT], f1r[FT];
   matvec<FT, ET>(P.w + L.W1[d], E, y, f1);
   uint32_t m = 0;
@@ -171,7 +169,7 @@ T2O_DEV void post_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d, const f
 
 // post_bwd for the lean cache (the X, Z, Y record fields were written forward)
 template <int E, int H, int FF, typename WT>
-T2O_DEV void post_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restrict__ gs, WT* __restrict__ rec,
+T2O_DEV void post_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restrict__ gs, const MaskedRec<WT>& rec,
                            int d, const PostCacheLean<E, H, FF>& c, const f4* gx, f4* gz, f4* gres, f4* ln2) {
   constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
   using R = TapeRec<E, H, FF>;
@@ -182,7 +180,7 @@ T2O_DEV void post_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restr
   }
   f4 gr2[ET];
   layernorm_bwd<ET>(gx, c.xh2, c.rs2, P.v + L.g2[d], gr2);
-  if (rec) rec_store<R::SIZE, ET>(rec, R::GR2, gr2);
+  rec.template store<ET>(R::GR2, gr2);
   f4 gf1[FT];
   matvec_tr<FT, ET>(P, L.W2[d], FF, L.W2T[d], E, gr2, gf1);
 #pragma unroll
@@ -193,12 +191,10 @@ T2O_DEV void post_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restr
   matvec_tr<ET, FT>(P, L.W1[d], E, L.W1T[d], FF, gf1, gy);
 #pragma unroll
   for (int t = 0; t < ET; ++t) gy[t] += gr2[t];
-  if (rec) {
-    rec_store<R::SIZE, ET>(rec, R::XH1, c.xh1);
-    rec_store<R::SIZE, ET>(rec, R::GY, gy);
-  }
+  rec.template store<ET>(R::XH1, c.xh1);
+  rec.template store<ET>(R::GY, gy);
   layernorm_bwd<ET>(gy, c.xh1, c.rs1, P.v + L.g1[d], gres);
-  if (rec) rec_store<R::SIZE, ET>(rec, R::GRES, gres);
+  rec.template store<ET>(R::GRES, gres);
   matvec_tr<HET, ET>(P, L.N[d], H * E, L.NT[d], E, gres, gz);
   (void)gs;
 }

@@ -670,4 +670,40 @@ T2O_DEV void rec_store(TT* __restrict__ tile, int off, const f4* v) {
   }
 }
 
+// A tape tile written through a buffer resource: lanes whose record lies at or
+// past `rows` get an out-of-range offset and the buffer unit drops their
+// stores, so a tile of fewer than 16 records needs no per-lane branch (exec-mask
+// control flow around every store costs registers in the two-wave kernels).
+// The tile base must be wave-uniform.
+template <typename TT>
+struct MaskedRec {
+  __amdgpu_buffer_rsrc_t rsrc;
+  int voff;  // bytes: this lane's record, features 4g.. ; or out of range
+  T2O_DEV MaskedRec(TT* tile, int rows, int size) {
+    const uint64_t a = reinterpret_cast<uint64_t>(tile);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    TT* base = reinterpret_cast<TT*>(((uint64_t)hi << 32) | lo);
+    rsrc = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, rows * size * (int)sizeof(TT), 0x00020000);
+    voff = lane_c() < rows ? (lane_c() * size + 4 * lane_g()) * (int)sizeof(TT) : 0x40000000;
+  }
+  // a T-layout vector (NT tiles): features off + 16t + 4g + r of this lane's record
+  template <int NT>
+  T2O_DEV void store(int off, const f4* v) const {
+#ifdef T2O_ABL_NOTAPE  // ablation builds only: wrong gradients
+    return;
+#endif
+    typedef int v2i __attribute__((ext_vector_type(2)));
+    typedef int v4i __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const int o = voff + (off + 16 * t) * (int)sizeof(TT);
+      if constexpr (sizeof(TT) == 2) {
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i, to_bf4(v[t])), rsrc, o, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v[t]), rsrc, o, 0, 0);
+      }
+    }
+  }
+};
+
 }  // namespace t2o

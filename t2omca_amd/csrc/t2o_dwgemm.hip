@@ -73,7 +73,7 @@ template <typename TT> struct DwTraits;
 template <> struct DwTraits<__bf16> { static constexpr int TG = 2, PADC = 2; };  // tiles per group, pad chunks
 template <> struct DwTraits<float> { static constexpr int TG = 1, PADC = 1; };
 
-template <int E, int H, int FF, int D, typename TT>
+template <int E, int H, int FF, int D, typename TT, int RT = 16>
 struct DwDims {
   using R = TapeRec<E, H, FF>;
   static constexpr int ET = E / 16, HET = H * ET, FT = FF / 16, FH = FT / 2;
@@ -81,7 +81,7 @@ struct DwDims {
   static constexpr int TG = DwTraits<TT>::TG;
   static constexpr int PER = 16 / (int)sizeof(TT);          // elements per 16-B chunk
   static constexpr int CPR = R::SIZE / PER;                  // chunks per record
-  static constexpr int CPT = 16 * CPR;                       // chunks per tile (HBM)
+  static constexpr int CPT = RT * CPR;                       // chunks per tile (HBM: RT records)
   static constexpr int RSTR = (CPR + DwTraits<TT>::PADC) * PER;  // padded LDS record stride (elements)
   static constexpr int TSTR = 16 * RSTR;                     // LDS tile stride (elements)
   static constexpr int NT = 256 * D;                         // threads
@@ -349,9 +349,9 @@ struct DwRole<3, E, H, FF, D, TT> : DwFfn<1, E, H, FF, D, TT> {};
 // One wave's whole launch for its role (every role runs the same pipeline and
 // the same barrier sequence; the roles only differ in what they read).
 // Pipeline: LDS double buffer, register ring of two, prefetch distance 2.
-template <int ROLE, int E, int H, int FF, int D, typename TT>
+template <int ROLE, int E, int H, int FF, int D, typename TT, int RT>
 T2O_DEV void dw_run(const DwGemmArgs& a, TT* buf0, TT* buf1, const TT* wlds, int d) {
-  using Dm = DwDims<E, H, FF, D, TT>;
+  using Dm = DwDims<E, H, FF, D, TT, RT>;
   const int64_t ngroups = (a.ntiles + Dm::TG - 1) / Dm::TG;
   const int64_t nj = (int64_t)blockIdx.x < ngroups ? (ngroups - 1 - blockIdx.x) / gridDim.x + 1 : 0;
   DwRole<ROLE, E, H, FF, D, TT> st;
@@ -385,9 +385,9 @@ T2O_DEV void dw_run(const DwGemmArgs& a, TT* buf0, TT* buf1, const TT* wlds, int
   st.finish(a, a.slabs + (size_t)blockIdx.x * a.slab_stride, d);
 }
 
-template <int E, int H, int FF, int D, int KIND, typename TT>
+template <int E, int H, int FF, int D, int KIND, typename TT, int RT>
 __global__ __launch_bounds__(256 * D) void dw_gemm_kernel(DwGemmArgs a) {
-  using Dm = DwDims<E, H, FF, D, TT>;
+  using Dm = DwDims<E, H, FF, D, TT, RT>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   TT* const buf0 = reinterpret_cast<TT*>(smem);
   TT* const buf1 = buf0 + Dm::GELEM;
@@ -401,17 +401,24 @@ __global__ __launch_bounds__(256 * D) void dw_gemm_kernel(DwGemmArgs a) {
       *reinterpret_cast<u4v*>(wlds + e) = *reinterpret_cast<const u4v*>(img + src);
     }
   }
+  if constexpr (RT < 16) {  // compact tiles: LDS records RT..15 stay zero (they add nothing)
+    for (int q = threadIdx.x; q < 2 * D * Dm::TG * (16 - RT) * Dm::CPR; q += Dm::NT) {
+      const int cr = q % Dm::CPR, rr = q / Dm::CPR;
+      const int rec = RT + rr % (16 - RT), tix = rr / (16 - RT);  // tix over both buffers
+      *reinterpret_cast<u4v*>(buf0 + tix * Dm::TSTR + rec * Dm::RSTR + cr * Dm::PER) = u4v{0u, 0u, 0u, 0u};
+    }
+  }
   const int w = wave_id();
   const int d = w >> 2, role = w & 3;
   switch (role) {  // wave-uniform; the four paths issue the same barriers
-    case 0: dw_run<0, E, H, FF, D, TT>(a, buf0, buf1, wlds, d); break;
-    case 1: dw_run<1, E, H, FF, D, TT>(a, buf0, buf1, wlds, d); break;
-    case 2: dw_run<2, E, H, FF, D, TT>(a, buf0, buf1, wlds, d); break;
-    default: dw_run<3, E, H, FF, D, TT>(a, buf0, buf1, wlds, d); break;
+    case 0: dw_run<0, E, H, FF, D, TT, RT>(a, buf0, buf1, wlds, d); break;
+    case 1: dw_run<1, E, H, FF, D, TT, RT>(a, buf0, buf1, wlds, d); break;
+    case 2: dw_run<2, E, H, FF, D, TT, RT>(a, buf0, buf1, wlds, d); break;
+    default: dw_run<3, E, H, FF, D, TT, RT>(a, buf0, buf1, wlds, d); break;
   }
 }
 
-template <int E, int H, int FF, int D, typename TT>
+template <int E, int H, int FF, int D, int NE, typename TT>
 int launch_dw_gemm(int kind, const void* tape, int64_t ntiles, const float* pack, float* slabs, const t2o_layout& L,
                    const t2o_layout& G, int nslab, hipStream_t stream) {
   using Dm = DwDims<E, H, FF, D, TT>;
@@ -425,7 +432,8 @@ int launch_dw_gemm(int kind, const void* tape, int64_t ntiles, const float* pack
   a.L = L;
   a.G = G;
   const size_t lds = sizeof(TT) * ((size_t)2 * Dm::GELEM + (Dm::BF ? (size_t)D * 2 * FF * E : 0));
-  auto kern = kind == 0 ? dw_gemm_kernel<E, H, FF, D, 0, TT> : dw_gemm_kernel<E, H, FF, D, 1, TT>;
+  constexpr int RTM = mixer_tape_records(NE);  // the mixer's query rows per tape tile
+  auto kern = kind == 0 ? dw_gemm_kernel<E, H, FF, D, 0, TT, 16> : dw_gemm_kernel<E, H, FF, D, 1, TT, RTM>;
   if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(nslab), dim3(256 * D), lds, stream, a);
@@ -438,7 +446,7 @@ using namespace t2o;
 
 extern "C" int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t tiles) {
   if (!L || tiles < 0) return -1;
-  const int64_t elems = (int64_t)L->D * tiles * 16 * (6 * L->E + 2 * L->H * L->E);
+  const int64_t elems = (int64_t)L->D * tiles * tape_tile_records(*L) * (6 * L->E + 2 * L->H * L->E);
   return L->prec ? (elems + 1) / 2 : elems;
 }
 
@@ -449,9 +457,9 @@ extern "C" int t2o_bwd_tape_contract(const t2o_layout* L, const float* pack, con
   grad_layout(*L, G);
   int rc = T2O_EUNSUPPORTED;
   T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
-               rc = (L->prec ? launch_dw_gemm<E_, H_, FF_, D_, __bf16>(L->kind, tape, tiles, pack, gslabs, *L, G,
+               rc = (L->prec ? launch_dw_gemm<E_, H_, FF_, D_, NE_, __bf16>(L->kind, tape, tiles, pack, gslabs, *L, G,
                                                                        nslab, (hipStream_t)stream)
-                             : launch_dw_gemm<E_, H_, FF_, D_, float>(L->kind, tape, tiles, pack, gslabs, *L, G,
+                             : launch_dw_gemm<E_, H_, FF_, D_, NE_, float>(L->kind, tape, tiles, pack, gslabs, *L, G,
                                                                       nslab, (hipStream_t)stream)));
   return rc;
 }

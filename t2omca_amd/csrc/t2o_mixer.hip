@@ -604,8 +604,11 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
           mixer_block_fwd<E, H, KT, FF, true>(P, L, d, K, Dm::LK, x, &cache);
           // one tile per (episode, step, query tile); padding rows carry zero gradients
           // tiles are step-major (t, b, qt): at any step the grid writes one contiguous window
-          WT* rec = static_cast<WT*>(args.tape) +
-                    ((size_t)d * ntiles + ((size_t)t * fa.B + b) * Dm::QT + qt) * Rec::SIZE * 16;
+          // (a one-tile mixer's tiles hold just its Q rows: mixer_tape_records)
+          constexpr int RT = mixer_tape_records(A);
+          WT* rec = c < RT ? static_cast<WT*>(args.tape) +
+                                 ((size_t)d * ntiles + ((size_t)t * fa.B + b) * Dm::QT + qt) * Rec::SIZE * RT
+                           : nullptr;
           mixer_block_bwd<E, H, KT, FF>(P, L, G, gs, rec, stage, d, K, gX0, cache, gx, ln2[d]);
         }
 #pragma unroll
@@ -813,7 +816,9 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
   In cur;
   for (int t = T - 1; t >= 0; --t) {
     const size_t bt = (size_t)b * T + t;
-    WT* rec = static_cast<WT*>(args.tape) + (RECD * ntiles + (size_t)t * fa.B + b) * Rec::SIZE * 16;
+    // tape tiles of exactly the Q query rows (mixer_tape_records)
+    const MaskedRec<WT> rec(static_cast<WT*>(args.tape) + (RECD * ntiles + (size_t)t * fa.B + b) * Rec::SIZE * Dm::Q,
+                            Dm::Q, Rec::SIZE);
     MixerCacheLean<E, H, KT, FF> cache;
     KeyFrags<E, KT, BF> K;
     {  // ---- recompute: key block of step t, block-1 forward with cache
@@ -939,7 +944,9 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
   __syncthreads();  // one phase behind the block-1 wave
   for (int t = T - 1; t >= 0; --t) {
     const size_t bt = (size_t)b * T + t;
-    WT* rec = static_cast<WT*>(args.tape) + (RECD * ntiles + (size_t)t * fa.B + b) * Rec::SIZE * 16;
+    // tape tiles of exactly the Q query rows (mixer_tape_records)
+    const MaskedRec<WT> rec(static_cast<WT*>(args.tape) + (RECD * ntiles + (size_t)t * fa.B + b) * Rec::SIZE * Dm::Q,
+                            Dm::Q, Rec::SIZE);
     MixerCacheLean<E, H, KT, FF> cache;
     KeyFrags<E, KT, BF> K;
     {  // ---- recompute: block-0 forward with cache (queries = X0's last A+3 rows)
@@ -1023,6 +1030,7 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
 template <int E, int H, int D, int A, int FF, typename WT>
 __global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) {
   static_assert(D == 2 && MixPipeDims<E, A>::OK, "one wave per block of a depth-2 stack, one query tile");
+  static_assert(mixer_tape_records(A) == MixDims<E, A>::Q, "tape tiles hold exactly the query rows");
   using Dm = MixDims<E, A>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const t2o_layout& L = args.f.L;

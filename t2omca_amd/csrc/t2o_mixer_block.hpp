@@ -202,7 +202,7 @@ struct MixerCacheLean {
 template <int E, int H, int KT, int FF, typename WT>
 T2O_DEV void mixer_block_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d,
                                   const KeyFrags<E, KT, sizeof(WT) == 2>& K, int Lk, f4* x,
-                                  MixerCacheLean<E, H, KT, FF>& cache, WT* __restrict__ rec) {
+                                  MixerCacheLean<E, H, KT, FF>& cache, const MaskedRec<WT>& rec) {
   constexpr int ET = E / 16, HET = H * ET;
   constexpr bool BF = sizeof(WT) == 2;
   const int g = lane_g();
@@ -242,7 +242,7 @@ T2O_DEV void mixer_block_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d,
 
 template <int E, int H, int KT, int FF, typename WT>
 T2O_DEV void mixer_block_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restrict__ gs,
-                                  WT* __restrict__ rec, float* __restrict__ stage, int d,
+                                  const MaskedRec<WT>& rec, float* __restrict__ stage, int d,
                                   const KeyFrags<E, KT, sizeof(WT) == 2>& K, f4 (&gX0)[KT][E / 16],
                                   const MixerCacheLean<E, H, KT, FF>& c, f4* gx, f4* ln2) {
   constexpr int ET = E / 16, HET = H * ET;
@@ -267,7 +267,7 @@ T2O_DEV void mixer_block_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* 
     dw_accumulate_regs<KT, ET, BF>(gX0, c.p[hh], &gz[hh * ET], stage);
     dw_accumulate_regs<KT, ET, BF>(gX0, gsc, &c.u[hh * ET], stage);
   }
-  if (rec) rec_store<TapeRec<E, H, FF>::SIZE, HET>(rec, TapeRec<E, H, FF>::GU, gu);
+  rec.template store<HET>(TapeRec<E, H, FF>::GU, gu);
   f4 gxp[ET];
   matvec_tr<ET, HET>(P, L.M[d], E, L.MT[d], H * E, gu, gxp);
 #pragma unroll

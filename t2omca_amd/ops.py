@@ -121,7 +121,8 @@ def agent_unroll_fwd(shape: NetShape, pack_on, obs, h0_on=None, pack_tg=None, h0
 
 
 def tape_floats(shape: NetShape, tiles):
-    """Backward tape workspace (floats) for `tiles` tiles of 16 weight-gradient records."""
+    """Backward tape workspace (floats) for `tiles` tiles of weight-gradient records
+    (16 per tile; a one-tile mixer stores just its A+3 query rows)."""
     return int(lib().t2o_bwd_tape_floats(ctypes.byref(shape.layout()), int(tiles)))
 
 

@@ -1,8 +1,11 @@
 """GPU cross-check: the two-wave pipelined mixer BPTT (mixer_bwd_pipe_kernel) against the
 one-wave kernel (T2O_MIXER_BWD=single, run in a child process since the switch is read
 once per process).  Both compute the same per-step math in the same operand precision,
-so outputs agree to fp32 summation-order rounding; the pipeline's pair count follows B
-(4, 2 or 1 episodes per workgroup), so the batches below cover each."""
+so fp32 outputs agree to summation-order rounding.  In bf16 mode a one-ulp fp32
+difference (the two kernels sum the key grads of the two blocks in a different order)
+can flip the bf16 rounding of an MFMA operand (2^-8 relative), hence the looser bf16
+bar.  The pipeline's pair count follows B (4, 2 or 1 episodes per workgroup), so the
+batches below cover each."""
 import os
 import subprocess
 import sys
@@ -16,7 +19,7 @@ from tests.gpu_util import flat_from_dict, normwise, require_gpu
 pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CASES = [(8, 8, 6, 0), (8, 6, 5, 1), (8, 7, 4, 0), (3, 4, 9, 1)]  # (A, B, T, prec)
-TOL = 2e-6
+TOL = {0: 2e-6, 1: 1e-4}  # by precision (0 fp32, 1 bf16 operands)
 
 
 def mixer_grads(A, B, T, prec):
@@ -59,4 +62,4 @@ def test_mixer_bwd_pipe_matches_single_wave(tmp_path):
         got = mixer_grads(*case)
         for name, a, b in zip(("params", "qvals", "hidden", "hw0"), got, ref):
             assert torch.isfinite(a).all(), (case, name)
-            assert normwise(a, b) < TOL, (case, name, normwise(a, b))
+            assert normwise(a, b) < TOL[case[3]], (case, name, normwise(a, b))
