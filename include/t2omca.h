@@ -197,6 +197,21 @@ int t2o_td_loss(const float* qtot, const float* qtot_tgt, const float* reward, i
                 float gamma, float td_lambda, float mask_sum, float* gq, float* targets,
                 float* prio, float* loss, int B, int T, void* stream);
 
+/* Element types of the mask inputs of t2o_td_loss_ex. */
+#define T2O_DT_F32 0
+#define T2O_DT_U8 1   /* uint8 / bool: EpisodeBatch "terminated" */
+#define T2O_DT_I32 2
+#define T2O_DT_I64 3  /* int64: EpisodeBatch "filled" */
+
+/* t2o_td_loss with term / filled read in their own storage types (the
+ * reference EpisodeBatch keeps terminated as uint8 and filled as int64,
+ * per_run.py's scheme), so the learner passes the replay views as they are. */
+int t2o_td_loss_ex(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
+                   int64_t rw_st, const void* term, int term_dtype, int64_t tm_sb, int64_t tm_st,
+                   const void* filled, int filled_dtype, int64_t fl_sb, int64_t fl_st,
+                   const float* per_weight, float gamma, float td_lambda, float mask_sum, float* gq,
+                   float* targets, float* prio, float* loss, int B, int T, void* stream);
+
 /* clip_grad_norm_(max_grad_norm) + Adam (torch.optim.Adam semantics, L2
  * weight decay) over n floats.  workspace: t2o_adam_workspace_floats() floats
  * (needed when max_grad_norm > 0).  grad_div [1] (may be NULL): device scalar

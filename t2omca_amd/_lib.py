@@ -61,6 +61,11 @@ EXPORTS = {
                     [ctypes.c_int64] * 2 + [ctypes.c_void_p] + [ctypes.c_int64] * 2 +
                     [ctypes.c_void_p] + [ctypes.c_float] * 3 + [ctypes.c_void_p] * 4 +
                     [ctypes.c_int] * 2 + [ctypes.c_void_p]),
+    "t2o_td_loss_ex": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_int64] * 2 +
+                       [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_int64] * 2 +
+                       [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_int64] * 2 +
+                       [ctypes.c_void_p] + [ctypes.c_float] * 3 + [ctypes.c_void_p] * 4 +
+                       [ctypes.c_int] * 2 + [ctypes.c_void_p]),
     "t2o_adam_step": (ctypes.c_int, [ctypes.c_void_p] * 5 + [ctypes.c_int64] + [ctypes.c_double] * 3 +
                       [ctypes.c_float] * 3 + [ctypes.c_int64] + [ctypes.c_void_p] * 3),
     "t2o_adam_workspace_floats": (ctypes.c_int, []),

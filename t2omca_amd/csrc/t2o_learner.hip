@@ -21,8 +21,8 @@ struct TDArgs {
   const float* qtot;      // [B][T]
   const float* qtot_tgt;  // [B][T+1]
   const float* reward;    // [B][T] strides rw_sb, rw_st
-  const float* term;      // [B][T] strides tm_sb, tm_st (float 0/1)
-  const float* filled;    // [B][T] strides fl_sb, fl_st (float 0/1)
+  const void* term;       // [B][T] strides tm_sb, tm_st (0/1, element type tm_dt)
+  const void* filled;     // [B][T] strides fl_sb, fl_st (0/1, element type fl_dt)
   const float* weight;    // [B] or null
   int64_t rw_sb, rw_st, tm_sb, tm_st, fl_sb, fl_st;
   float gamma, lambda_;
@@ -32,7 +32,18 @@ struct TDArgs {
   float* prio;            // [B]
   float* loss;            // [2]: loss, Σ mask
   int B, T;
+  int tm_dt, fl_dt;       // T2O_DT_* (t2omca.h): the EpisodeBatch's own dtypes, read in place
 };
+
+// one 0/1 mask element of the given storage type as float
+__device__ float mask_at(const void* p, int64_t i, int dt) {
+  switch (dt) {
+    case T2O_DT_U8: return (float)static_cast<const uint8_t*>(p)[i];
+    case T2O_DT_I32: return (float)static_cast<const int32_t*>(p)[i];
+    case T2O_DT_I64: return (float)static_cast<const int64_t*>(p)[i];
+    default: return static_cast<const float*>(p)[i];
+  }
+}
 
 __device__ float block_sum(float v, float* red) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -66,8 +77,8 @@ __global__ __launch_bounds__(256) void td_loss_kernel(TDArgs a, int EP) {
   for (int i = threadIdx.x; i < nb * T; i += blockDim.x) {
     const int b = b0 + i / T, t = i % T;
     R[i] = a.reward[b * a.rw_sb + t * a.rw_st];
-    TM[i] = a.term ? a.term[b * a.tm_sb + t * a.tm_st] : 0.f;
-    FL[i] = a.filled ? a.filled[b * a.fl_sb + t * a.fl_st] : 1.f;
+    TM[i] = a.term ? mask_at(a.term, b * a.tm_sb + t * a.tm_st, a.tm_dt) : 0.f;
+    FL[i] = a.filled ? mask_at(a.filled, b * a.fl_sb + t * a.fl_st, a.fl_dt) : 1.f;
     Q[i] = a.qtot[(size_t)b0 * T + i];
   }
   for (int i = threadIdx.x; i < nb * (T + 1); i += blockDim.x) QT[i] = a.qtot_tgt[(size_t)b0 * (T + 1) + i];
@@ -177,14 +188,16 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
 
 }  // namespace
 
-extern "C" int t2o_td_loss(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
-                           int64_t rw_st, const float* term, int64_t tm_sb, int64_t tm_st, const float* filled,
-                           int64_t fl_sb, int64_t fl_st, const float* per_weight, float gamma, float td_lambda,
-                           float mask_sum, float* gq, float* targets, float* prio, float* loss, int B, int T,
-                           void* stream) {
+extern "C" int t2o_td_loss_ex(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
+                              int64_t rw_st, const void* term, int term_dtype, int64_t tm_sb, int64_t tm_st,
+                              const void* filled, int filled_dtype, int64_t fl_sb, int64_t fl_st,
+                              const float* per_weight, float gamma, float td_lambda, float mask_sum, float* gq,
+                              float* targets, float* prio, float* loss, int B, int T, void* stream) {
   if (!qtot || !qtot_tgt || !reward || !gq || !prio || !loss || B < 1 || T < 1) return T2O_EINVAL;
+  auto dt_ok = [](int dt) { return dt == T2O_DT_F32 || dt == T2O_DT_U8 || dt == T2O_DT_I32 || dt == T2O_DT_I64; };
+  if (!dt_ok(term_dtype) || !dt_ok(filled_dtype)) return T2O_EINVAL;
   TDArgs a{qtot, qtot_tgt, reward, term, filled, per_weight, rw_sb, rw_st, tm_sb, tm_st, fl_sb, fl_st,
-           gamma, td_lambda, mask_sum, gq, targets, prio, loss, B, T};
+           gamma, td_lambda, mask_sum, gq, targets, prio, loss, B, T, term_dtype, filled_dtype};
   hipStream_t s = (hipStream_t)stream;
   const size_t per_ep = sizeof(float) * (5 * (size_t)T + 1);
   int ep = (int)((96 * 1024) / per_ep);
@@ -197,6 +210,15 @@ extern "C" int t2o_td_loss(const float* qtot, const float* qtot_tgt, const float
   if (mask_sum <= 0.f)
     hipLaunchKernelGGL(td_normalise_kernel, dim3(1), dim3(256), 0, s, gq, (int64_t)B * T, loss);
   return (int)hipGetLastError();
+}
+
+extern "C" int t2o_td_loss(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
+                           int64_t rw_st, const float* term, int64_t tm_sb, int64_t tm_st, const float* filled,
+                           int64_t fl_sb, int64_t fl_st, const float* per_weight, float gamma, float td_lambda,
+                           float mask_sum, float* gq, float* targets, float* prio, float* loss, int B, int T,
+                           void* stream) {
+  return t2o_td_loss_ex(qtot, qtot_tgt, reward, rw_sb, rw_st, term, T2O_DT_F32, tm_sb, tm_st, filled, T2O_DT_F32,
+                        fl_sb, fl_st, per_weight, gamma, td_lambda, mask_sum, gq, targets, prio, loss, B, T, stream);
 }
 
 extern "C" int t2o_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,

@@ -216,13 +216,21 @@ class TDLearner:
         if act.stride(2) != 1:
             act = act.contiguous()
         reward = batch["reward"][:, :, 0]
-        term = batch["terminated"][:, :, 0].float()
-        filled = batch["filled"][:, :, 0].float() if "filled" in _keys(batch) else None
+        term = batch["terminated"][:, :, 0]  # uint8 / int64 as the EpisodeBatch keeps them: read in place
+        filled = batch["filled"][:, :, 0] if "filled" in _keys(batch) else None
         w = None
         if per_weight is not None:
             w = torch.as_tensor(np.asarray(per_weight) if not torch.is_tensor(per_weight) else per_weight,
                                 dtype=torch.float32).to(dev).reshape(B).contiguous()
 
+        # the gradient buffer is cleared on the side stream, off the critical path
+        # (after the previous update's Adam, which read it)
+        main = torch.cuda.current_stream(dev)
+        side = self._side_stream() if self.overlap else main
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self.grad.zero_()
+            grad_zeroed = side.record_event()
         ops.pack_params(self.sa, self.params[:self.na], self.pack_a)
         ops.pack_params(self.sm, self.params[self.na:], self.pack_m)
         # 1. agents: online + target over t = 0..T
@@ -246,11 +254,9 @@ class TDLearner:
         contract_m, gqv, ghid, _ = ops.mixer_unroll_bwd(self.sm, self.pack_m, state, h_on, o_on, td["gq"],
                                                         slabs=slabs_m, timer=self.timer, tape=tape_m,
                                                         defer_contract=True)
-        main = torch.cuda.current_stream(dev)
-        side = self._side_stream() if self.overlap else main
-        self.grad.zero_()
         side.wait_stream(main)
         with torch.cuda.stream(side):
+            self.grad[-1:].copy_(td["loss"][1:2])
             gm = contract_m()
             # mixer grads in reference parameter order, still off the critical path
             ops.unpack_grads(self.sm, self.params[self.na:], gm, self.grad[self.na:self.na + self.nm])
@@ -260,9 +266,9 @@ class TDLearner:
                                      gh=None if self.detach_mixer_hidden else ghid, slabs=slabs_a,
                                      timer=self.timer, hmid=hmid, tape=tape_a)
         # 6. agent grads in reference parameter order
+        main.wait_event(grad_zeroed)
         ops.unpack_grads(self.sa, self.params[:self.na], ga, self.grad[:self.na])
         main.wait_stream(side)
-        self.grad[-1:].copy_(td["loss"][1:2])
         allreduce_grad_and_mask(self.grad, self.pg)
         # 7. clip + Adam
         self.step_count += 1

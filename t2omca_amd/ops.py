@@ -281,22 +281,40 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
     return (contract if defer_contract else contract()), gqv, ghid, ghw0
 
 
+# t2o_td_loss_ex mask element types (include/t2omca.h T2O_DT_*)
+_MASK_DT = {torch.float32: 0, torch.uint8: 1, torch.bool: 1, torch.int32: 2, torch.int64: 3}
+
+
+def _mask_dtype(t):
+    if t is None:
+        return 0
+    if t.dtype not in _MASK_DT:
+        raise TypeError(f"td_loss: unsupported mask dtype {t.dtype}")
+    return _MASK_DT[t.dtype]
+
+
 def td_loss(qtot, qtot_tgt, reward, terminated=None, filled=None, per_weight=None, gamma=0.99,
             td_lambda=0.6, mask_sum=0.0):
     """TD(λ) targets / loss / grads / priorities (PyMARL2 NQLearner contract).
-    qtot [B,T], qtot_tgt [B,T+1]; reward/terminated/filled [B, >=T] float views.
+    qtot [B,T], qtot_tgt [B,T+1]; reward [B, >=T] float view; terminated / filled
+    [B, >=T] views in float32, uint8/bool, int32 or int64 (read in place).
     Returns dict(gq [B,T], targets [B,T], prio [B], loss [2])."""
-    _dev(qtot, qtot_tgt, reward, terminated, filled, per_weight)
+    _dev(qtot, qtot_tgt, reward, per_weight)
+    for m in (terminated, filled):  # any mask dtype of _MASK_DT, device-resident
+        if m is not None and not m.is_cuda:
+            raise RuntimeError("t2omca_amd ops need HIP-device tensors (no CPU fallback)")
+        _mask_dtype(m)
     B, T = qtot.shape
     dev = qtot.device
     assert qtot.is_contiguous() and qtot_tgt.is_contiguous() and qtot_tgt.shape[1] == T + 1
     out = dict(gq=torch.empty(B, T, device=dev), targets=torch.empty(B, T, device=dev),
                prio=torch.empty(B, device=dev), loss=torch.empty(2, device=dev))
     rs, ts, fs = _mstrides(reward), _mstrides(terminated), _mstrides(filled)
-    check(lib().t2o_td_loss(ptr(qtot), ptr(qtot_tgt), ptr(reward), rs[0], rs[1], ptr(terminated),
-                            ts[0], ts[1], ptr(filled), fs[0], fs[1], ptr(per_weight), float(gamma),
-                            float(td_lambda), float(mask_sum), ptr(out["gq"]), ptr(out["targets"]),
-                            ptr(out["prio"]), ptr(out["loss"]), B, T, stream_ptr()), "td_loss")
+    check(lib().t2o_td_loss_ex(ptr(qtot), ptr(qtot_tgt), ptr(reward), rs[0], rs[1], ptr(terminated),
+                               _mask_dtype(terminated), ts[0], ts[1], ptr(filled), _mask_dtype(filled), fs[0],
+                               fs[1], ptr(per_weight), float(gamma), float(td_lambda), float(mask_sum),
+                               ptr(out["gq"]), ptr(out["targets"]), ptr(out["prio"]), ptr(out["loss"]), B, T,
+                               stream_ptr()), "td_loss")
     return out
 
 

@@ -59,3 +59,18 @@ def test_td_loss_matches_oracle(B, T):
                        mask_sum=2.0 * float(msum))
     assert _nw(out2["gq"].cpu().double(), gq / 2) < 1e-5
     assert float(out2["loss"][1]) == float(msum)
+
+
+@pytest.mark.parametrize("tdt,fdt", [(torch.uint8, torch.int64), (torch.bool, torch.int32)])
+def test_td_loss_native_mask_dtypes(tdt, fdt):
+    """terminated / filled read in the EpisodeBatch's own storage types (t2o_td_loss_ex)
+    give exactly the float-mask result (the masks are 0/1)."""
+    from t2omca_amd import ops
+    qtot, qtgt, reward, term, filled, w = _case(37, 23, 5)
+    c = lambda t: t.cuda().contiguous()  # noqa: E731
+    ref = ops.td_loss(c(qtot), c(qtgt), c(reward), c(term), c(filled), c(w), mask_sum=0.0)
+    # [B, T, 1] replay-style tensors viewed as [B, T] (non-unit outer strides)
+    t3, f3 = c(term.to(tdt)[..., None]), c(filled.to(fdt)[..., None])
+    out = ops.td_loss(c(qtot), c(qtgt), c(reward), t3[:, :, 0], f3[:, :, 0], c(w), mask_sum=0.0)
+    for k in ("gq", "targets", "prio", "loss"):
+        assert torch.equal(out[k], ref[k]), k
