@@ -57,8 +57,11 @@ T2O_DEV void put(float* dst, __bf16* dstb, int64_t off, int r, int col, int ld, 
 }
 
 // an E x E operand (row stride ld) into LDS
+// E x E block of g (leading dim ld) into LDS rows of stride E + 1: the
+// products below read both rows and columns, and the odd stride keeps a
+// wave's column reads on distinct banks
 T2O_DEV void stage(float* s, const float* g, int E, int ld) {
-  for (int i = threadIdx.x; i < E * E; i += blockDim.x) s[i] = g[(int64_t)(i / E) * ld + i % E];
+  for (int i = threadIdx.x; i < E * E; i += blockDim.x) s[(i / E) * (E + 1) + i % E] = g[(int64_t)(i / E) * ld + i % E];
 }
 
 __global__ __launch_bounds__(256) void pack_kernel(TaskTable tab, const float* __restrict__ src,
@@ -70,6 +73,7 @@ __global__ __launch_bounds__(256) void pack_kernel(TaskTable tab, const float* _
   const Task tk = tab.t[k];
   const int lb = (int)blockIdx.x - tab.blk[k];
   const int E = tab.E, HE = tab.H * E, h = tk.h;
+  const int LS = E + 1, SQ = E * LS;  // staged matrix row stride / size (stage())
   const bool bf = tk.bf != 0;
   switch (tk.kind) {
     case T_COPY:
@@ -93,14 +97,14 @@ __global__ __launch_bounds__(256) void pack_kernel(TaskTable tab, const float* _
     }
     case T_FOLD_M: {  // a = Wk, b = Wq (params, [HE][E] row-major)
       float* wk = sm;
-      float* wq = sm + E * E;
+      float* wq = sm + SQ;
       stage(wk, src + tk.a + (int64_t)h * E * E, E, E);
       stage(wq, src + tk.b + (int64_t)h * E * E, E, E);
       __syncthreads();
       for (int o = threadIdx.x; o < E * E; o += blockDim.x) {
         const int i = o / E, kk = o % E;
         float acc = 0.f;
-        for (int m = 0; m < E; ++m) acc = fmaf(wk[m * E + i], wq[m * E + kk], acc);
+        for (int m = 0; m < E; ++m) acc = fmaf(wk[m * LS + i], wq[m * LS + kk], acc);
         acc *= tab.scale;
         put(dst, dstb, tk.dst, h * E + i, kk, E, acc, bf);   // M  [HE][E]
         put(dst, dstb, tk.dst2, kk, h * E + i, HE, acc, bf); // MT [E][HE]
@@ -109,14 +113,14 @@ __global__ __launch_bounds__(256) void pack_kernel(TaskTable tab, const float* _
     }
     case T_FOLD_N: {  // a = U ([E][HE]), b = Wv ([HE][E])
       float* u = sm;
-      float* wv = sm + E * E;
+      float* wv = sm + SQ;
       stage(u, src + tk.a + (int64_t)h * E, E, HE);
       stage(wv, src + tk.b + (int64_t)h * E * E, E, E);
       __syncthreads();
       for (int o = threadIdx.x; o < E * E; o += blockDim.x) {
         const int oo = o / E, kk = o % E;
         float acc = 0.f;
-        for (int m = 0; m < E; ++m) acc = fmaf(u[oo * E + m], wv[m * E + kk], acc);
+        for (int m = 0; m < E; ++m) acc = fmaf(u[oo * LS + m], wv[m * LS + kk], acc);
         put(dst, dstb, tk.dst, oo, h * E + kk, HE, acc, bf);   // N  [E][HE]
         put(dst, dstb, tk.dst2, h * E + kk, oo, E, acc, bf);   // NT [HE][E]
       }
@@ -124,8 +128,8 @@ __global__ __launch_bounds__(256) void pack_kernel(TaskTable tab, const float* _
     }
     case T_UNFOLD_QK: {  // a = Wq, b = Wk (params), c = gM (gpack [HE][E]); dst = gWq, dst2 = gWk
       float* wq = sm;
-      float* wk = sm + E * E;
-      float* gm = sm + 2 * E * E;
+      float* wk = sm + SQ;
+      float* gm = sm + 2 * SQ;
       stage(wq, src + tk.a + (int64_t)h * E * E, E, E);
       stage(wk, src + tk.b + (int64_t)h * E * E, E, E);
       stage(gm, src2 + tk.c + (int64_t)h * E * E, E, E);
@@ -134,8 +138,8 @@ __global__ __launch_bounds__(256) void pack_kernel(TaskTable tab, const float* _
         const int m = o / E, kk = o % E;
         float aq = 0.f, ak = 0.f;
         for (int i = 0; i < E; ++i) {
-          aq = fmaf(wk[m * E + i], gm[i * E + kk], aq);  // gWq[m][kk]
-          ak = fmaf(wq[m * E + i], gm[kk * E + i], ak);  // gWk[m][kk] (kk plays i)
+          aq = fmaf(wk[m * LS + i], gm[i * LS + kk], aq);  // gWq[m][kk]
+          ak = fmaf(wq[m * LS + i], gm[kk * LS + i], ak);  // gWk[m][kk] (kk plays i)
         }
         dst[tk.dst + (int64_t)(h * E + m) * E + kk] += aq * tab.scale;
         dst[tk.dst2 + (int64_t)(h * E + m) * E + kk] += ak * tab.scale;
@@ -144,8 +148,8 @@ __global__ __launch_bounds__(256) void pack_kernel(TaskTable tab, const float* _
     }
     case T_UNFOLD_VU: {  // a = U, b = Wv (params), c = gN (gpack [E][HE]); dst = gWv, dst2 = gU
       float* u = sm;
-      float* wv = sm + E * E;
-      float* gn = sm + 2 * E * E;
+      float* wv = sm + SQ;
+      float* gn = sm + 2 * SQ;
       stage(u, src + tk.a + (int64_t)h * E, E, HE);
       stage(wv, src + tk.b + (int64_t)h * E * E, E, E);
       stage(gn, src2 + tk.c + (int64_t)h * E, E, HE);
@@ -154,8 +158,8 @@ __global__ __launch_bounds__(256) void pack_kernel(TaskTable tab, const float* _
         const int m = o / E, kk = o % E;
         float av = 0.f, au = 0.f;
         for (int j = 0; j < E; ++j) {
-          av = fmaf(u[j * E + m], gn[j * E + kk], av);   // gWv[m][kk] = Σ_o U[o][m] gN[o][kk]
-          au = fmaf(gn[m * E + j], wv[kk * E + j], au);  // gU[m][kk] = Σ_k gN[m][k] Wv[kk][k]  (m = o, kk = m')
+          av = fmaf(u[j * LS + m], gn[j * LS + kk], av);   // gWv[m][kk] = Σ_o U[o][m] gN[o][kk]
+          au = fmaf(gn[m * LS + j], wv[kk * LS + j], au);  // gU[m][kk] = Σ_k gN[m][k] Wv[kk][k]  (m = o, kk = m')
         }
         dst[tk.dst + (int64_t)(h * E + m) * E + kk] += av;
         dst[tk.dst2 + (int64_t)m * HE + h * E + kk] += au;
@@ -201,7 +205,7 @@ struct Builder {
   }
   void flush() {
     if (nb > 0 && rc == 0) {
-      const size_t lds = sizeof(float) * 3 * (size_t)tab.E * tab.E;
+      const size_t lds = sizeof(float) * 3 * (size_t)tab.E * (tab.E + 1);
       hipLaunchKernelGGL(pack_kernel, dim3(nb), dim3(256), lds, (hipStream_t)stream, tab, src, src2, dst, dstb);
       rc = (int)hipGetLastError();
     }
