@@ -200,8 +200,12 @@ extern "C" int t2o_td_loss_ex(const float* qtot, const float* qtot_tgt, const fl
            gamma, td_lambda, mask_sum, gq, targets, prio, loss, B, T, term_dtype, filled_dtype};
   hipStream_t s = (hipStream_t)stream;
   const size_t per_ep = sizeof(float) * (5 * (size_t)T + 1);
+  // episodes per workgroup: few enough that the grid covers the CUs (the
+  // staging loads, not the per-episode scan, dominate a fat workgroup)
   int ep = (int)((96 * 1024) / per_ep);
   if (ep > 64) ep = 64;
+  const int ep_fill = (B + 255) / 256;
+  if (ep > ep_fill) ep = ep_fill;
   if (ep < 1) return T2O_EUNSUPPORTED;
   if (hipMemsetAsync(loss, 0, 2 * sizeof(float), s) != hipSuccess) return (int)hipGetLastError();
   (void)hipFuncSetAttribute((const void*)td_loss_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -72,5 +72,8 @@ def test_td_loss_native_mask_dtypes(tdt, fdt):
     # [B, T, 1] replay-style tensors viewed as [B, T] (non-unit outer strides)
     t3, f3 = c(term.to(tdt)[..., None]), c(filled.to(fdt)[..., None])
     out = ops.td_loss(c(qtot), c(qtgt), c(reward), t3[:, :, 0], f3[:, :, 0], c(w), mask_sum=0.0)
-    for k in ("gq", "targets", "prio", "loss"):
+    for k in ("gq", "targets", "prio"):
         assert torch.equal(out[k], ref[k]), k
+    # loss sums workgroup partials with float atomics (order varies); Σ mask is integral
+    assert torch.allclose(out["loss"][:1], ref["loss"][:1], rtol=1e-6, atol=0.0)
+    assert torch.equal(out["loss"][1:], ref["loss"][1:])
