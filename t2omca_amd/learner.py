@@ -231,13 +231,15 @@ class TDLearner:
         with torch.cuda.stream(side):
             self.grad.zero_()
             grad_zeroed = side.record_event()
+            ops.pack_params(self.sm, self.params[self.na:], self.pack_m)  # beside the agent's pack + forward
+            mixer_packed = side.record_event()
         ops.pack_params(self.sa, self.params[:self.na], self.pack_a)
-        ops.pack_params(self.sm, self.params[self.na:], self.pack_m)
         # 1. agents: online + target over t = 0..T
         hmid = self._buf("hmid", (B, T1, self.sa.D - 1, A, self.sa.E)) if self.sa.D > 1 else None
         q_on, h_on, q_tg, h_tg = ops.agent_unroll_fwd(self.sa, self.pack_a, obs, pack_tg=self.pack_at,
                                                       timer=self.timer, hmid_on=hmid)
         # 2. mixers: online on chosen Q (t < T), target on double-Q (t <= T)
+        main.wait_event(mixer_packed)
         o_on, o_tg = ops.mixer_unroll_fwd(self.sm, self.pack_m, state, h_on, qmode_on=1, q_on=q_on,
                                           actions=act, avail=avail, T_on=T, pack_tg=self.pack_mt,
                                           hid_tg=h_tg, qmode_tg=2, q_tg=q_tg, T_tg=T1,
