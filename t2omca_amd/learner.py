@@ -230,9 +230,8 @@ class TDLearner:
         side.wait_stream(main)
         with torch.cuda.stream(side):
             self.grad.zero_()
-            grad_zeroed = side.record_event()
             ops.pack_params(self.sm, self.params[self.na:], self.pack_m)  # beside the agent's pack + forward
-            mixer_packed = side.record_event()
+            mixer_packed = side.record_event()  # (main waits for it before the mixer: grad is clear by then too)
         ops.pack_params(self.sa, self.params[:self.na], self.pack_a)
         # 1. agents: online + target over t = 0..T
         hmid = self._buf("hmid", (B, T1, self.sa.D - 1, A, self.sa.E)) if self.sa.D > 1 else None
@@ -268,7 +267,6 @@ class TDLearner:
                                      gh=None if self.detach_mixer_hidden else ghid, slabs=slabs_a,
                                      timer=self.timer, hmid=hmid, tape=tape_a)
         # 6. agent grads in reference parameter order
-        main.wait_event(grad_zeroed)
         ops.unpack_grads(self.sa, self.params[:self.na], ga, self.grad[:self.na])
         main.wait_stream(side)
         allreduce_grad_and_mask(self.grad, self.pg)
