@@ -693,7 +693,9 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 // wrt the block-1 input (query rows, in R's padding rows)], then the step's
 // total key grads written by the block-0 wave, whose hyper rows the block-1
 // wave reads at its next backward.  Per-step math, records and slab sums are
-// those of mixer_bwd_kernel.
+// those of mixer_bwd_kernel; the block cache is the lean one (MixerCacheLean)
+// so that a wave fits half a register file (two waves per SIMD), and records
+// are written through MaskedRec (tape tiles of exactly the Q query rows).
 template <int E, int A>
 struct MixPipeDims {
   using Dm = MixDims<E, A>;
@@ -713,8 +715,10 @@ inline bool mixer_bwd_single_wave() {
   return single;
 }
 
-// The block-1 wave's per-step inputs (none recurrent), prefetched a phase
-// ahead: the backward's Q selection is qmode 0, so only qvals ride along.
+// The block-1 wave's per-step inputs (none recurrent), loaded at the start of
+// its recompute phase (which has slack under the block-0 backward) and held
+// through its backward phase; the backward's Q selection is qmode 0, so only
+// qvals ride along.
 template <int E, int A>
 struct MixPIn {
   using Dm = MixDims<E, A>;
