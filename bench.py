@@ -253,10 +253,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # T2O_DIST_BACKEND=gloo rehearses the multi-rank path on a box with fewer GPUs
+    # than ranks (ranks share devices round-robin); the default is RCCL, one GPU per rank
+    backend = os.environ.get("T2O_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     from t2omca_amd.learner import TDLearner
     from t2omca_amd.modules import TransformerAgent, TransformerMixer
     from t2omca_amd.perfmodel import ref_order_flops_per_transition, td_update_bytes, td_update_flops
