@@ -59,6 +59,10 @@ def parse():
                          "host-side buffer contract: one device->host copy and sync per update)")
     ap.add_argument("--serial", action="store_true",
                     help="no side-stream overlap: every kernel's HIP-event time is its isolated cost")
+    ap.add_argument("--kernel-timer-every", type=int, default=2,
+                    help="bracket the kernels with HIP events on every k-th timed step (the per-kernel "
+                         "times and the roofline come from those steps; the events cost ~40 us per "
+                         "instrumented update, so every step would inflate ms_per_step ~1.5%%; 0: never)")
     ap.add_argument("--print-workload-tag", action="store_true",
                     help="print the tag that keys profiles/hbm_traffic.json for these args and exit")
     return ap.parse_args()
@@ -298,13 +302,14 @@ def main():
     for i in range(args.warmup):
         step(i)
     timer = KernelTimer()
-    learner.timer = timer
+    every = args.kernel_timer_every
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
+        learner.timer = timer if every > 0 and i % every == 0 else None
         step(i)
     torch.cuda.synchronize()
     if world > 1:
