@@ -409,7 +409,14 @@ __global__ __launch_bounds__(256 * D) void dw_gemm_kernel(DwGemmArgs a) {
     }
   }
   const int w = wave_id();
+  // Waves w and w + 4 share a SIMD.  Roles 2/3 (FFN halves: 32 MFMAs per tile
+  // plus the W1/W2ᵀ reads) weigh about 2.7x roles 0/1 (12 MFMAs), so block 1
+  // rotates its roles by two: every SIMD holds one light and one heavy role.
+#ifndef T2O_DW_NO_ROLE_ROTATE
+  const int d = w >> 2, role = (w + 2 * d) & 3;
+#else
   const int d = w >> 2, role = w & 3;
+#endif
   switch (role) {  // wave-uniform; the four paths issue the same barriers
     case 0: dw_run<0, E, H, FF, D, TT, RT>(a, buf0, buf1, wlds, d); break;
     case 1: dw_run<1, E, H, FF, D, TT, RT>(a, buf0, buf1, wlds, d); break;
