@@ -398,7 +398,14 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
   // wave-uniform by construction; readfirstlane tells the compiler, so the block's
   // layout offsets (L.M[d] ...) are scalar loads, not per-lane global loads
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
-  const int d = w & 1;   // the block this wave owns
+  // the block this wave owns.  Waves w and w + 4 share a SIMD: with four pairs,
+  // pairs 2-3 swap their block roles so every SIMD holds one block-0 and one
+  // block-1 wave (the two phases of a barrier interval differ in cost)
+#ifndef T2O_PIPE_NO_SIMD_MIX
+  const int d = (w ^ (w >> 2)) & 1;
+#else
+  const int d = w & 1;
+#endif
   const int tl = w >> 1; // tile within the workgroup
   const t2o_layout Lb = block_view(L, d), Gb = block_view(G, d);
   float* stage = smem + lds_w + w * STAGE;

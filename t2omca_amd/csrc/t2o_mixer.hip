@@ -1040,7 +1040,14 @@ __global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) 
   const t2o_layout& L = args.f.L;
   const t2o_layout& G = args.G;
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
-  const int d = w & 1;   // the block this wave owns
+  // the block this wave owns.  Waves w and w + 4 share a SIMD: with four pairs,
+  // pairs 2-3 swap their block roles so every SIMD holds one block-0 and one
+  // block-1 wave (the two phases of a barrier interval differ in cost)
+#ifndef T2O_PIPE_NO_SIMD_MIX
+  const int d = (w ^ (w >> 2)) & 1;
+#else
+  const int d = w & 1;
+#endif
   const int pr = w >> 1; // the episode within the workgroup
   float* X0 = smem + args.lds_w + pr * MixPipeDims<E, A>::PAIRF;
   float* R = X0 + Dm::X0F;
