@@ -63,6 +63,8 @@ def parse():
                     help="bracket the kernels with HIP events on every k-th timed step (the per-kernel "
                          "times and the roofline come from those steps; the events cost ~40 us per "
                          "instrumented update, so every step would inflate ms_per_step ~1.5%%; 0: never)")
+    ap.add_argument("--no-fp32-companion", dest="fp32_companion", action="store_false",
+                    help="skip the fp32-precision companion timing of the same workload (bf16 runs)")
     ap.add_argument("--print-workload-tag", action="store_true",
                     help="print the tag that keys profiles/hbm_traffic.json for these args and exit")
     return ap.parse_args()
@@ -120,28 +122,48 @@ def traffic_for(kernel, tag):
     return None if k is None else k.get("hbm_bytes")
 
 
-def cpu_baseline(args):
-    """The oracle's PyTorch-CPU TD update on a bounded sample of the same workload."""
+def _cpu_rate(args, B, threads, seconds):
+    """min-of-N time of the oracle's CPU TD update on B episodes with `threads` threads."""
     from oracle import ref_learner, ref_model
-    A, T, B = args.agents, args.T, args.cpu_sample
+    from t2omca_amd.synthetic import make_batch
+    A, T = args.agents, args.T
     cfg = dict(n_agents=A, n_entities=A, obs_entity_feats=9, emb=32, heads=3, depth=2, ff_hidden_mult=4,
                n_actions=5, state_entity_feats=8, mixer_emb=32, mixer_heads=3, mixer_depth=2)
-    from t2omca_amd.synthetic import make_batch
     batch, w = make_batch(B, T, A, seed=7, device="cpu")
     learner = ref_learner.RefLearner(ref_model.init_params("agent", cfg, 0), ref_model.init_params("mixer", cfg, 1),
                                      cfg)
-    threads = torch.get_num_threads()
-    learner.train(batch, 0, 0, per_weight=w)  # warm-up
-    times = []
-    t_start = time.perf_counter()
-    while len(times) < 3 or (time.perf_counter() - t_start < args.cpu_seconds and len(times) < 20):
-        t0 = time.perf_counter()
-        learner.train(batch, 0, 0, per_weight=w)
-        times.append(time.perf_counter() - t0)
-    best = min(times)
-    return {"value": B * T * A / best, "unit": "agent-transitions/s", "cores": threads, "kind": "port",
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        learner.train(batch, 0, 0, per_weight=w)  # warm-up
+        times = []
+        t_start = time.perf_counter()
+        while len(times) < 3 or (time.perf_counter() - t_start < seconds and len(times) < 20):
+            t0 = time.perf_counter()
+            learner.train(batch, 0, 0, per_weight=w)
+            times.append(time.perf_counter() - t0)
+    finally:
+        torch.set_num_threads(prev)
+    return B * T * A / min(times), len(times)
+
+
+def cpu_baseline(args):
+    """The oracle's PyTorch-CPU TD update (oracle/ref_learner.py, reference op order,
+    fp32) on a bounded sample of the same workload, on this host's cores: all the
+    threads torch runs with (capped by the CPU affinity set) and one thread."""
+    affinity = len(os.sched_getaffinity(0))
+    threads = max(1, min(torch.get_num_threads(), affinity))
+    A, T, B = args.agents, args.T, args.cpu_sample
+    rate, n = _cpu_rate(args, B, threads, args.cpu_seconds)
+    b1 = max(1, B // 4)
+    rate1, n1 = _cpu_rate(args, b1, 1, args.cpu_seconds / 2)
+    return {"value": rate, "unit": "agent-transitions/s", "cores": threads, "kind": "port",
             "sample": f"{B} episodes x T={T} x A={A} (one TD update = {B * T * A} agent-transitions), "
-                      f"min of {len(times)} updates after 1 warm-up, torch CPU fp32, {threads} threads"}
+                      f"min of {n} updates after 1 warm-up, torch CPU fp32, {threads} threads "
+                      f"(sched_getaffinity: {affinity} cores; torch threads: {torch.get_num_threads()})",
+            "affinity_cores": affinity,
+            "single_thread": {"value": rate1, "unit": "agent-transitions/s", "cores": 1,
+                              "sample": f"{b1} episodes x T={T} x A={A}, min of {n1} updates after 1 warm-up"}}
 
 
 def rollout_bench(args, world, rank, dev):
@@ -271,7 +293,8 @@ def main():
             dist.init_process_group(backend)
     from t2omca_amd.learner import TDLearner
     from t2omca_amd.modules import TransformerAgent, TransformerMixer
-    from t2omca_amd.perfmodel import ref_order_flops_per_transition, td_update_bytes, td_update_flops
+    from t2omca_amd.perfmodel import (ref_order_flops_per_transition, ref_order_kernel_flops, td_update_bytes,
+                                      td_update_flops)
     from t2omca_amd.synthetic import make_args, make_batch
 
     A, T, B = args.agents, args.T, args.batch
@@ -279,12 +302,15 @@ def main():
         return rollout_bench(args, world, rank, dev)
     if args.mode == "expand":
         return expand_bench(args, world, rank, dev)
-    torch.manual_seed(0)
-    margs = make_args(A, device=str(dev))
-    agent = TransformerAgent(None, margs).to(dev)
-    mixer = TransformerMixer(margs).to(dev)
-    learner = TDLearner(agent, mixer, target_update_interval=10 ** 9, precision=args.dtype,
-                        overlap=not args.serial, priorities_to_cpu=args.priorities == "cpu")
+    def make_learner(precision):
+        torch.manual_seed(0)
+        margs = make_args(A, device=str(dev))
+        agent = TransformerAgent(None, margs).to(dev)
+        mixer = TransformerMixer(margs).to(dev)
+        return TDLearner(agent, mixer, target_update_interval=10 ** 9, precision=precision,
+                         overlap=not args.serial, priorities_to_cpu=args.priorities == "cpu")
+
+    learner = make_learner(args.dtype)
     batch, w = make_batch(B, T, A, seed=1 + rank, device=dev)
     if args.mode == "forward":
         from t2omca_amd import ops
@@ -297,30 +323,49 @@ def main():
             ops.mixer_unroll_fwd(learner.sm, learner.pack_m, batch["state"], h, qmode_on=1, q_on=q, actions=act,
                                  T_on=T, want_xout=False)
     else:
-        def step(i):
-            learner.train(batch, 0, i, per_weight=w)
-    for i in range(args.warmup):
-        step(i)
+        # the driver's closed step (per_run.py:224-238): the update, then the sampled
+        # episodes' priorities back into the replay buffer.  --priorities device: the
+        # device-resident buffer's update_priorities (t2o_per_update) on the device
+        # |TD errors|; cpu: the learner copies them to the host (4 KB + a sync) and the
+        # host list goes through the same call.  The buffer is sized like PyMARL2's
+        # default (5000 episodes); the batch's episode indices are a fixed sample.
+        from t2omca_amd.replay import PrioritizedReplayBuffer
+        buf = PrioritizedReplayBuffer({"filled": torch.zeros(1, T + 1, 1, device=dev)}, max(5000, B), T + 1,
+                                      0.6, 0.4, 10 ** 6, device=dev, seed=rank)
+        idx = torch.randperm(max(5000, B), generator=torch.Generator().manual_seed(rank))[:B].to(dev)
+
+        def make_step(lr):
+            def step(i):
+                info = lr.train(batch, 0, i, per_weight=w)
+                buf.update_priorities(idx, info["td_errors_abs"].flatten() + 1e-6)
+            return step
+        step = make_step(learner)
+
+    def timed(step, timer=None, every=0):
+        for i in range(args.warmup):
+            step(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            learner.timer = timer if every > 0 and i % every == 0 else None
+            step(i)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        learner.timer = None
+        if world > 1:
+            t = torch.tensor([el], device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t)
+        return el
+
     timer = KernelTimer()
-    every = args.kernel_timer_every
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        learner.timer = timer if every > 0 and i % every == 0 else None
-        step(i)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    learner.timer = None
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t)
+    elapsed = timed(step, timer, args.kernel_timer_every)
     if args.mode == "forward":
         value = world * B * (T + 1) * A * args.steps / elapsed
         out = {"metric": "agent-transitions/sec for agent+mixer forward (inference over a replay batch)",
@@ -340,17 +385,18 @@ def main():
     value = transitions / elapsed
     kern = {k: sum(v) / len(v) for k, v in timer.durations().items()}
     flops = td_update_flops(B, T, A)
+    ref_flops = ref_order_kernel_flops(B, T, A)
     bytes_ = td_update_bytes(B, T, A, elem=2 if args.dtype == "bf16" else 4)
-    # dominant kernel on the critical path (mixer_dw runs on a side stream, hidden
-    # behind agent_bwd, so its event interval includes contention, not its cost)
-    dom = max((k for k in flops if k != "mixer_dw"), key=lambda k: kern.get(k, 0.0))
+    # dominant kernel: the longest of the four network kernels on the critical path
+    # (the tape contractions are part of a backward; mixer_dw runs on a side stream)
+    dom = max(ref_flops, key=lambda k: kern.get(k, 0.0))
     dom_ms = kern.get(dom, float("nan"))
-    hbm_bound = dom.endswith("_dw")  # tape contractions stream their operands once
-    if hbm_bound:
-        achieved, peak, unit = bytes_[dom] / (dom_ms * 1e-3) / 1e9, PEAK_HBM_GBS, "GB/s"
-    else:
-        peak_tf = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_FP32_TFLOPS
-        achieved, peak, unit = flops[dom] / (dom_ms * 1e-3) / 1e12, peak_tf, "TFLOP/s"
+    peak_tf = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_FP32_TFLOPS
+    # SURVEY.md §8(d) basis: the reference-order necessary FLOPs of the kernel's share
+    achieved = ref_flops[dom] / (dom_ms * 1e-3) / 1e12
+    ms_step = elapsed / args.steps * 1e3
+    upd_flops = ref_order_flops_per_transition(A) * B * T * A
+    dw = {"agent_bwd": "agent_dw", "mixer_bwd": "mixer_dw"}.get(dom)
     out = {
         "metric": "agent-transitions/sec for TD update fwd+bwd (whole node)",
         "value": value,
@@ -358,7 +404,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": ms_step,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -368,15 +414,32 @@ def main():
                                f"batch {B} episodes/GPU x T={T}",
                    "global_batch": B * world, "seq_len": T, "agents": A, "emb": 32, "heads": 3, "depth": 2,
                    "parallelism": f"dp{world}", "priorities": args.priorities},
-        "roofline": {"bound": "hbm" if hbm_bound else "mfma", "kernel": dom, "achieved": achieved, "peak": peak,
-                     "unit": unit, "frac": achieved / peak, "traffic": traffic_for(dom, workload_tag(args)),
-                     "algorithmic_flops_per_launch": flops[dom],
-                     "algorithmic_bytes_per_launch": bytes_[dom],
-                     "avg_launch_ms": dom_ms},
+        "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": peak_tf,
+                     "unit": "TFLOP/s", "frac": achieved / peak_tf, "traffic": traffic_for(dom, workload_tag(args)),
+                     "basis": "SURVEY.md §8(d) reference-order necessary FLOPs of the kernel's share "
+                              "(perfmodel.ref_order_kernel_flops)",
+                     "algorithmic_flops_per_launch": ref_flops[dom],
+                     "algorithmic_bytes_per_launch": bytes_.get(dom),
+                     "avg_launch_ms": dom_ms,
+                     "incl_tape_contraction": None if dw is None or dw not in kern else {
+                         "ms": dom_ms + kern[dw],
+                         "frac": ref_flops[dom] / ((dom_ms + kern[dw]) * 1e-3) / 1e12 / peak_tf},
+                     "executed_algorithm": {"flops_per_launch": flops[dom],
+                                            "frac": flops[dom] / (dom_ms * 1e-3) / 1e12 / peak_tf},
+                     "whole_update": {"flops": upd_flops, "ms": ms_step,
+                                      "achieved": upd_flops / (ms_step * 1e-3) / 1e12,
+                                      "frac": upd_flops / (ms_step * 1e-3) / 1e12 / peak_tf}},
         "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items())},
         "flops_per_transition": {"executed_algorithm": sum(flops.values()) / (B * T * A),
                                  "reference_order": ref_order_flops_per_transition(A)},
     }
+    if args.dtype == "bf16" and args.fp32_companion:
+        # the same workload at the reference's own precision (fp32 MFMA operands)
+        lr32 = make_learner("fp32")
+        el32 = timed(make_step(lr32))
+        out["fp32_companion"] = {"value": transitions / el32, "unit": "agent-transitions/s",
+                                 "ms_per_step": el32 / args.steps * 1e3, "dtype": "fp32"}
+        del lr32
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

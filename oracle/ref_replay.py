@@ -12,12 +12,13 @@ segment trees compute it:
     w_k     = (p[idx_k] / sum_tree.sum() * n) ** -beta / max_w
     update: p[idx] = priority ** alpha;  max_priority = max(max_priority, priority)
 
-with u_k = U(seed, k, counter) of the counter-based stream (oracle/ref_mac.py).
+with u_k = U(seed, k, counter) of the counter-based stream (oracle/ref_mac.py),
+seed keyed by STREAM_PER.
 Parity unpinned against the absent module; pinned to PyMARL2's published code.
 """
 import numpy as np
 
-from oracle.ref_mac import _uniform
+from oracle.ref_mac import STREAM_PER, _uniform
 
 
 def sample(p, batch, beta, seed, counter):
@@ -30,7 +31,7 @@ def sample(p, batch, beta, seed, counter):
     w = np.empty(batch, np.float64)
     max_w = (p.min() / total * n) ** (-beta)
     for k in range(batch):
-        mass = _uniform(seed, k, counter) * rng + k * rng
+        mass = _uniform(seed, k, counter, STREAM_PER) * rng + k * rng
         i = int(np.searchsorted(cum, mass, side="right"))
         idx[k] = min(i, n - 1)
         w[k] = (p[idx[k]] / total * n) ** (-beta) / max_w
@@ -40,6 +41,8 @@ def sample(p, batch, beta, seed, counter):
 def update(p, max_priority, idx, priorities, alpha):
     p = np.array(p, np.float64)
     for i, pr in zip(idx, priorities):
+        if not (pr > 0 and np.isfinite(pr)):  # PyMARL2 asserts priority > 0: such values are dropped
+            continue
         p[i] = pr ** alpha
         max_priority = max(max_priority, pr)
     return p, max_priority

@@ -26,6 +26,12 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 #define T2O_DEV __device__ __forceinline__
 
+// Stream keys of the counter-based uniforms (env_spec.uniforms): XOR-ed into the
+// seed of every stream but the env's, so the env, the ε-greedy selector and the
+// PER sampler draw independent sequences from one user seed.
+#define T2O_STREAM_MAC 0x4D41435354524D31ull  // "MACSTRM1"
+#define T2O_STREAM_PER 0x5045525354524D31ull  // "PERSTRM1"
+
 namespace t2o {
 
 T2O_DEV int lane_c() { return threadIdx.x & 15; }
@@ -645,6 +651,7 @@ struct TapeRec {
   static constexpr int GY = XH1 + E;          // dL/dy              (E)   g1, n1
   static constexpr int SIZE = GY + E;
 };
+
 // Layout: tiles of 16 records (one wave's rows at one step), RECORD-major
 // inside a tile: element (record 16·tile + c, feature f) of block d sits at
 // ((d·ntiles + tile)·16 + c)·SIZE + f, in the MFMA operand type (fp32, or

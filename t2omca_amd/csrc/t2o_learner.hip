@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void td_loss_kernel(TDArgs a, int EP) {
       mb += m;
       lb += 0.5f * td * td * m;
     }
-    a.prio[b] = absum / sqrtf(mb);
+    a.prio[b] = mb > 0.f ? absum / sqrtf(mb) : 0.f;  // an all-masked episode: 0, not 0/0
     lsum = lb * w;
     msum = mb;
   }

@@ -17,9 +17,11 @@
 
 namespace {
 
+// the selector's own stream: seed keyed with T2O_STREAM_MAC (t2o_common.hpp), so
+// exploration draws never repeat the env's dynamics draws of the same row
 __device__ double mac_uniform(uint64_t seed, int64_t row, int64_t idx) {
   uint64_t x = ((uint64_t)row << 40) | (uint64_t)idx;
-  x ^= seed * 0xD1B54A32D192ED03ull;
+  x ^= (seed ^ T2O_STREAM_MAC) * 0xD1B54A32D192ED03ull;
   uint64_t z = x + 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;

@@ -18,9 +18,12 @@
 
 namespace {
 
+// PER's draws are their own stream: the seed is keyed with a per-stream constant
+// (env: none, MAC: T2O_STREAM_MAC, PER: T2O_STREAM_PER), so replay sampling never
+// repeats the env's or the action selector's draws for the same seed.
 __device__ double per_uniform(uint64_t seed, int64_t row, int64_t idx) {
   uint64_t x = ((uint64_t)row << 40) | (uint64_t)idx;
-  x ^= seed * 0xD1B54A32D192ED03ull;
+  x ^= (seed ^ T2O_STREAM_PER) * 0xD1B54A32D192ED03ull;
   uint64_t z = x + 0x9E3779B97F4A7C15ull;
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -88,6 +91,9 @@ __global__ void per_update_kernel(float* __restrict__ p, const int64_t* __restri
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= n) return;
   const float v = prio[k] + eps;
+  // PyMARL2 asserts priority > 0; a non-positive or non-finite value (a NaN's bit
+  // pattern would win the unsigned max below for good) leaves the episode as it was
+  if (!(v > 0.f) || !isfinite(v)) return;
   p[idx[k]] = powf(v, alpha);
   atomicMax(reinterpret_cast<unsigned int*>(max_prio), __float_as_uint(v));  // v > 0: bit order = value order
 }

@@ -11,6 +11,11 @@ DP update equal to the full-batch update:
 
 At E = 32 that buffer is 84,007 floats (336 KB): latency-bound over xGMI, so
 no bucketing or overlap machinery is warranted.
+
+Replicas start identical and stay identical: the learner broadcasts its
+parameters, target parameters and Adam moments from rank 0 when it is built
+and after every checkpoint load (``broadcast_state``); after that every rank
+applies the same all-reduced gradient with the same Adam arithmetic.
 """
 import torch.distributed as dist
 
@@ -21,6 +26,12 @@ def world_size(group=None):
     return 1
 
 
+def rank(group=None):
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(group)
+    return 0
+
+
 def allreduce_grad_and_mask(buf, group=None):
     """In-place SUM all-reduce of [grad..., mask_sum]; returns buf."""
     if world_size(group) > 1:
@@ -28,8 +39,23 @@ def allreduce_grad_and_mask(buf, group=None):
     return buf
 
 
+def broadcast_state(tensors, group=None, src=0):
+    """Overwrite every rank's copy of `tensors` (flat device buffers) with rank
+    `src`'s, in place.  One broadcast per tensor; a no-op without a process group."""
+    if world_size(group) > 1:
+        gsrc = src if group is None else dist.get_global_rank(group, src)
+        for t in tensors:
+            dist.broadcast(t, gsrc, group=group)
+
+
 def shard_bounds(n, rank, world):
     """Contiguous episode shard [lo, hi) of rank (weak scaling uses a full batch per rank)."""
     per = (n + world - 1) // world
     lo = min(n, rank * per)
     return lo, min(n, lo + per)
+
+
+def rank_seed(seed, rank):
+    """Per-rank seed for the env / rollout / PER streams, so data-parallel ranks
+    collect and sample different episodes (rank 0 keeps `seed` itself)."""
+    return int(seed) + 0x9E3779B9 * int(rank)

@@ -28,6 +28,7 @@ import ctypes
 import torch
 
 from . import env_spec as S
+from .distributed import rank as dist_rank, rank_seed
 from ._lib import check, lib, stream_ptr
 
 INFO_KEYS = ("delay_reward", "overtime_penalty", "channel_utilization_rate", "conflict_ratio",
@@ -43,15 +44,21 @@ def spec_vector(edge_only=False):
 
 
 class VecEnv:
-    def __init__(self, n_envs, mec_num=2, agv_num=16, num_channels=4, episode_limit=150, seed=0,
+    def __init__(self, n_envs, mec_num=2, agv_num=16, num_channels=4, episode_limit=150, seed=None,
                  edge_only=False, device="cuda", keep_obs64=False, wire=False):
+        """seed None: 0 mixed with the data-parallel rank (distributed.rank_seed), so
+        every rank's shard of envs draws its own episodes."""
+        if seed is None:
+            seed = rank_seed(0, dist_rank())
         device = torch.device(device)
         if device.type != "cuda":
             raise RuntimeError("VecEnv runs on the HIP device only (the numpy restatement in oracle/ is test-only)")
         if device.index is None:
             device = torch.device("cuda", torch.cuda.current_device())
-        if not (1 <= agv_num <= 64 and 1 <= mec_num <= 16 and 1 <= num_channels <= 16):
-            raise ValueError("VecEnv supports agv_num <= 64, mec_num <= 16, num_channels <= 16")
+        # n_actions = num_channels + 1 must fit the agent head (t2o_layout_init: NA <= 16)
+        if not (1 <= agv_num <= 64 and 1 <= mec_num <= 16 and 1 <= num_channels <= 15):
+            raise ValueError("VecEnv supports agv_num <= 64, mec_num <= 16, num_channels <= 15 "
+                             "(n_actions = num_channels + 1 <= 16, the agent head's limit)")
         self.n_envs, self.M, self.A, self.C = n_envs, mec_num, agv_num, num_channels
         self.T, self.seed, self.device = episode_limit, int(seed), device
         self.n_actions = num_channels + 1

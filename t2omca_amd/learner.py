@@ -30,7 +30,7 @@ import torch
 import torch.distributed as dist
 
 from . import ops
-from .distributed import allreduce_grad_and_mask
+from .distributed import allreduce_grad_and_mask, broadcast_state
 
 
 def _bind_flat(modules, device):
@@ -74,13 +74,16 @@ class TDLearner:
         self.exp_avg = torch.zeros_like(self.params)
         self.exp_avg_sq = torch.zeros_like(self.params)
         self.target_params = self.params.clone()
+        self.pg = process_group
+        # data parallel: every replica starts from rank 0's parameters (ranks that
+        # initialised with different seeds would otherwise drift apart silently)
+        broadcast_state([self.params, self.target_params], self.pg)
         self.adam_ws = torch.empty(int(ops.lib().t2o_adam_workspace_floats()), device=dev)
         self.grad_norm = torch.zeros(1, device=dev)
         self.lr, self.betas, self.eps, self.wd = lr, optim_betas, optim_eps, weight_decay
         self.gamma, self.td_lambda, self.clip = gamma, td_lambda, grad_norm_clip
         self.target_update_interval = target_update_interval
         self.detach_mixer_hidden = detach_mixer_hidden
-        self.pg = process_group
         self.priorities_to_cpu = priorities_to_cpu
         self.overlap = overlap  # mixer tape contraction on a side stream beside the agent BPTT
         self.step_count = 0
@@ -175,8 +178,8 @@ class TDLearner:
             self.agent.load_state_dict(load("agent.th"))  # copies into the flat-buffer views
             self.mixer.load_state_dict(load("mixer.th"))
             self.target_params[:self.na].copy_(self.params[:self.na])
-        self._pack_targets()
         if not os.path.exists(os.path.join(path, "opt.th")):
+            self._sync_replicas()
             return
         opt = self._optimiser_view()
         opt.load_state_dict(load("opt.th"))
@@ -192,6 +195,16 @@ class TDLearner:
         if len(steps) > 1:
             raise ValueError(f"opt.th: parameters carry different Adam step counts {sorted(steps)}")
         self.step_count = steps.pop() if steps else 0
+        self._sync_replicas()
+
+    def _sync_replicas(self):
+        """Data parallel: rank 0's params, target params, Adam moments and step
+        count on every rank (after a checkpoint load), then re-pack the targets."""
+        if self._world() > 1:
+            step = torch.tensor([float(self.step_count)], device=self.device)
+            broadcast_state([self.params, self.target_params, self.exp_avg, self.exp_avg_sq, step], self.pg)
+            self.step_count = int(step.item())
+        self._pack_targets()
 
     # -- the TD update -------------------------------------------------------
     def train(self, batch, t_env=0, episode_num=0, per_weight=None):

@@ -9,7 +9,8 @@ count ~5 FLOPs per element.
 SURVEY.md §8(d) also quotes the reference-association-order counts
 (1.793 / 2.608 / 7.833 MFLOP per agent-transition at A = 8 / 16 / 64);
 ``ref_order_flops_per_transition`` reproduces that formula so bench.py can
-report both.  Rooflines are always priced against the executed algorithm.
+report both.  bench.py prices its roofline on the §8(d) reference-order count
+(``ref_order_kernel_flops``) and reports the executed-algorithm count beside it.
 """
 
 
@@ -90,8 +91,9 @@ def td_update_bytes(B, T, A, E=32, F=9, Fs=8, NA=5, elem=4):
     }
 
 
-def ref_order_flops_per_transition(A, E=32, H=3, D=2, F=9, Fs=8, NA=5, FF=None):
-    """SURVEY.md §8(d) formula: 4*F_agent + 4*F_mixer/A (reference association order)."""
+def ref_order_network_flops(A, E=32, H=3, D=2, F=9, Fs=8, NA=5, FF=None):
+    """(F_agent per sequence-step, F_mixer per episode-step), the
+    necessary (token-pruned) forward FLOPs in the reference association order."""
     FF = FF or 4 * E
     HE = H * E
     La, Lm, Lq = A + 1, 2 * A + 3, A + 3
@@ -99,4 +101,20 @@ def ref_order_flops_per_transition(A, E=32, H=3, D=2, F=9, Fs=8, NA=5, FF=None):
         + 2 * E * NA
     f_mixer = 2 * A * Fs * E + D * (4 * Lm * E * HE + 2 * Lq * E * HE + 4 * H * Lq * Lm * E
                                     + 2 * Lq * HE * E + 4 * Lq * E * FF)
+    return f_agent, f_mixer
+
+
+def ref_order_flops_per_transition(A, E=32, H=3, D=2, F=9, Fs=8, NA=5, FF=None):
+    """SURVEY.md §8(d) formula: 4*F_agent + 4*F_mixer/A (reference association order)."""
+    f_agent, f_mixer = ref_order_network_flops(A, E, H, D, F, Fs, NA, FF)
     return 4 * f_agent + 4 * f_mixer / A
+
+
+def ref_order_kernel_flops(B, T, A, **kw):
+    """SURVEY.md §8(d)'s per-kernel shares of one TD update (the basis of the bench's
+    roofline): forward online + target once each, backward = 2x the online forward,
+    recompute excluded, the (T+1)/T factor ignored.  The backward share of a network
+    is charged to its BPTT kernel (the tape contractions are part of that backward)."""
+    f_agent, f_mixer = ref_order_network_flops(A, **kw)
+    return {"agent_fwd": 2 * B * T * A * f_agent, "mixer_fwd": 2 * B * T * f_mixer,
+            "agent_bwd": 2 * B * T * A * f_agent, "mixer_bwd": 2 * B * T * f_mixer}

@@ -22,15 +22,19 @@ import numpy as np
 import torch
 
 from ._lib import check, lib, ptr, stream_ptr
+from .distributed import rank as dist_rank, rank_seed
 
 
 class PrioritizedReplayBuffer:
     # per-episode fields (no time axis): the wire-format obs normaliser snapshot
     EPISODE_KEYS = ("obs_nrm_n", "obs_nrm")
 
-    def __init__(self, example_batch, buffer_size, max_seq_length, alpha, beta, t_max, *, device="cuda", seed=0):
+    def __init__(self, example_batch, buffer_size, max_seq_length, alpha, beta, t_max, *, device="cuda", seed=None):
         """example_batch: a dict of [n, max_seq_length, ...] tensors (e.g. one
-        RolloutRunner batch) giving the scheme (keys, per-step shapes, dtypes)."""
+        RolloutRunner batch) giving the scheme (keys, per-step shapes, dtypes).
+        seed None: 0 mixed with the data-parallel rank (distributed.rank_seed)."""
+        if seed is None:
+            seed = rank_seed(0, dist_rank())
         self.device = torch.device(device)
         self.buffer_size, self.max_seq_length = int(buffer_size), int(max_seq_length)
         self.alpha, self.beta_original, self.beta = float(alpha), float(beta), float(beta)

@@ -36,6 +36,7 @@ TDLearner.train when the batch has no ``obs``) rebuilds the dense obs exactly.
 import torch
 
 from . import ops
+from .distributed import rank as dist_rank, rank_seed
 
 
 class LinearSchedule:
@@ -51,7 +52,10 @@ class LinearSchedule:
 
 class RolloutRunner:
     def __init__(self, agent, env, *, epsilon_start=1.0, epsilon_finish=0.05, epsilon_anneal_time=50000,
-                 seed=0, compact_obs=False):
+                 seed=None, compact_obs=False):
+        # seed None: 0 mixed with the data-parallel rank (distributed.rank_seed)
+        if seed is None:
+            seed = rank_seed(0, dist_rank())
         if compact_obs and getattr(env, "wire", None) is None:
             raise ValueError("compact_obs needs a VecEnv built with wire=True")
         self.compact_obs = bool(compact_obs)

@@ -1,0 +1,164 @@
+"""GPU parity at every BASELINE.json config's real shape (BASELINE.json "configs",
+SURVEY.md §8 scenario mapping), on an episode slice the fp64 CPU oracle finishes
+in seconds:
+
+  configs[0]/[1]  16 AGVs, T = 150 (default scenario): the agent + mixer forward
+                  unroll (configs[1]'s inference workload) and the full TD update
+                  (configs[0]'s), 4 episodes;
+  configs[2]      8 AGVs, T = 60 (the headline): the full TD update in fp32 AND in
+                  bf16 (configs[2] is quoted in bf16), 16 episodes, plus the bf16
+                  agent Q error at every t up to t = 59;
+  configs[3]      64 AGVs, T = 60: the full TD update, 2 episodes (chunked online-
+                  softmax agent, five-tile mixer);
+  configs[4]      the vectorised env, 16 AGVs x 2 MEC servers, a full 150-step
+                  episode, bit-exact against the numpy restatement for 6 envs.
+
+Oracle: oracle/ref_learner.td_forward in fp64 (pinned to the reference modules'
+goldens by tests/test_oracle_golden.py; TD semantics parity-unpinned).
+Bars (normwise max|Δ| / max|ref|):
+  fp32   Q_tot, targets, priorities <= 1e-5; parameter gradients <= 2e-4 at these
+         horizons (3e-5 at the short-horizon tests, tests/test_gpu_learner.py);
+  bf16   Q_tot, targets, priorities <= 2e-2; gradients <= 6e-2; agent Q at every
+         t <= 4e-2 (bf16 MFMA operands, fp32 accumulation / LayerNorm / softmax /
+         recurrent state).  Measured: agent Q 3.4e-3 at t = 0, 1.7e-2 at t = 30,
+         2.3e-2 at t = 59, 2.6e-2 max (the rounding of the recurrent input to bf16
+         operands compounds over the unroll; SURVEY §8c's all-bf16 probe: 4.5e-2).
+Why the fp32 gradient bar is wider over 60-150-step BPTT: an FFN pre-activation
+within fp32 rounding of 0 takes the other ReLU branch than in fp64, and that one
+record's whole gf1 entry (not a rounding-sized amount) enters dW1 and, through the
+recurrence, every earlier step's gradient.  With ~2M ReLU evaluations per update at
+configs[2]'s slice such a flip happens about once per run, in the CPU fp32 path too:
+the reference-order CPU restatement in fp32 vs fp64 gives 1.7e-7 - 3.0e-7 on seeds
+3-9 and 2.9e-5 on seed 10 (same shapes); the GPU path measured 8.6e-7, 2.2e-5 and
+6.0e-5 on seeds 4, 5 and 3.  Q_tot, targets and priorities (forward quantities) stay
+at 2e-7 - 5e-7.
+"""
+import dataclasses
+
+import pytest
+import torch
+
+from oracle import ref_learner, ref_model
+from tests.gpu_util import normwise, require_gpu
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"fp32": dict(q=1e-5, g=2e-4, qt=1e-5), "bf16": dict(q=2e-2, g=6e-2, qt=4e-2)}
+
+
+def _cfg(A):
+    return dict(n_agents=A, n_entities=A, obs_entity_feats=9, emb=32, heads=3, depth=2, ff_hidden_mult=4,
+                n_actions=5, state_entity_feats=8, mixer_emb=32, mixer_heads=3, mixer_depth=2)
+
+
+def _modules(A, seed=0):
+    from t2omca_amd.modules import TransformerAgent, TransformerMixer
+    from t2omca_amd.synthetic import make_args
+    torch.manual_seed(seed)
+    args = make_args(A)
+    return TransformerAgent(None, args).cuda(), TransformerMixer(args).cuda()
+
+
+def _td_vs_oracle(A, B, T, precision, seed=3):
+    from t2omca_amd.learner import TDLearner
+    from t2omca_amd.synthetic import make_batch
+    agent, mixer = _modules(A)
+    pa = {k: v.detach().cpu().double() for k, v in agent.state_dict().items()}
+    pm = {k: v.detach().cpu().double() for k, v in mixer.state_dict().items()}
+    learner = TDLearner(agent, mixer, precision=precision)
+    batch, w = make_batch(B, T, A, seed=seed)
+    cpu = {k: (v.cpu().double() if v.is_floating_point() else v.cpu()) for k, v in batch.items()}
+    pa_g = {k: v.clone().requires_grad_(True) for k, v in pa.items()}
+    pm_g = {k: v.clone().requires_grad_(True) for k, v in pm.items()}
+    loss, prio, ex = ref_learner.td_forward(pa_g, pm_g, pa, pm, cpu, _cfg(A), per_weight=w.cpu().double())
+    loss.backward()
+    info = learner.train(batch, 0, 0, per_weight=w)
+    torch.cuda.synchronize()
+    g = (learner.grad[:-1] / learner.grad[-1]).cpu()
+    ref_g = torch.cat([v.grad.reshape(-1) for v in list(pa_g.values()) + list(pm_g.values())])
+    errs = dict(qtot=normwise(info["qtot"], ex["qtot"]), targets=normwise(info["targets"], ex["targets"]),
+                prio=normwise(info["td_errors_abs"], prio), grad=normwise(g, ref_g))
+    return errs, learner, batch, ex
+
+
+def _check(errs, precision):
+    tol = TOL[precision]
+    print(precision, {k: f"{v:.2e}" for k, v in errs.items()})
+    assert errs["qtot"] < tol["q"] and errs["targets"] < tol["q"] and errs["prio"] < tol["q"], errs
+    assert errs["grad"] < tol["g"], errs
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_config2_headline_td_update_T60(precision):
+    """configs[2]: 8 AGVs x 4 MEC, T = 60, a 16-episode slice of the 1024-episode batch."""
+    require_gpu()
+    errs, learner, batch, ex = _td_vs_oracle(8, 16, 60, precision)
+    _check(errs, precision)
+    # the agent Q of every step (the bf16 drift grows with t): the online
+    # network's unroll with the learner's own pack, vs the oracle's mac_out
+    from t2omca_amd import ops
+    q, _ = ops.agent_unroll_fwd(learner.sa, learner.pack_a, batch["obs"])
+    torch.cuda.synchronize()
+    ref_q = ex["mac_out"]
+    per_t = [normwise(q[:, t], ref_q[:, t]) for t in range(q.shape[1])]
+    print(precision, "agent Q normwise error t=0/30/59/60:", [f"{per_t[t]:.2e}" for t in (0, 30, 59, 60)])
+    assert per_t[59] < TOL[precision]["qt"] and max(per_t) < TOL[precision]["qt"], max(per_t)
+
+
+def test_config1_forward_A16_T150():
+    """configs[1]: agent + mixer forward only (inference over a replay batch), 16 AGVs, T = 150."""
+    require_gpu()
+    from t2omca_amd import ops
+    from t2omca_amd.synthetic import make_batch
+    A, B, T = 16, 4, 150
+    agent, mixer = _modules(A)
+    pa = {k: v.detach().cpu().double() for k, v in agent.state_dict().items()}
+    pm = {k: v.detach().cpu().double() for k, v in mixer.state_dict().items()}
+    batch, _ = make_batch(B, T, A, seed=4)
+    pack_a = ops.pack_params(agent.shape, torch.cat([p.detach().reshape(-1) for p in agent.parameters()]))
+    pack_m = ops.pack_params(mixer.shape, torch.cat([p.detach().reshape(-1) for p in mixer.parameters()]))
+    q, h = ops.agent_unroll_fwd(agent.shape, pack_a, batch["obs"])
+    act = batch["actions"][..., 0]
+    o = ops.mixer_unroll_fwd(mixer.shape, pack_m, batch["state"], h, qmode_on=1, q_on=q, actions=act, T_on=T,
+                             want_xout=False)
+    torch.cuda.synchronize()
+    cfg = _cfg(A)
+    obs = batch["obs"].cpu().double()
+    ref_q, ref_h = ref_model.agent_unroll(pa, obs, torch.zeros(B, A, 32, dtype=torch.float64), cfg=cfg)
+    chosen = torch.gather(ref_q[:, :-1], 3, act[:, :-1].cpu().unsqueeze(3)).squeeze(3)
+    ref_y, ref_hw = ref_model.mixer_unroll(pm, chosen, ref_h[:, :-1], batch["state"][:, :-1].cpu().double(),
+                                           torch.zeros(B, 3, 32, dtype=torch.float64), cfg=cfg)
+    errs = dict(q=normwise(q, ref_q), h=normwise(h, ref_h), y=normwise(o["y"], ref_y), hw=normwise(o["hw"], ref_hw))
+    print("configs[1] forward", errs)
+    assert max(errs.values()) < 1e-5, errs
+
+
+def test_config0_td_update_A16_T150():
+    """configs[0]: the default scenario's TD update, 16 AGVs, T = 150, 4 episodes."""
+    require_gpu()
+    errs, *_ = _td_vs_oracle(16, 4, 150, "fp32")
+    _check(errs, "fp32")
+
+
+def test_config3_td_update_A64_T60():
+    """configs[3]: 64 AGVs x 16 MEC, T = 60, 2 episodes (of the 512 per GPU)."""
+    require_gpu()
+    errs, *_ = _td_vs_oracle(64, 2, 60, "fp32")
+    _check(errs, "fp32")
+
+
+def test_config4_env_full_episode_A16_M2_T150():
+    """configs[4]: the vectorised env over a whole 150-step episode, bit-exact."""
+    require_gpu()
+    from tests.test_gpu_env import _rollout_vs_oracle
+    _rollout_vs_oracle(NE=6, M=2, A=16, T=150, eps=1, seed=21)
+
+
+def test_bf16_mode_is_the_learner_precision():
+    """The bf16 learner really runs the prec-1 kernels (pack carries the bf16 image)."""
+    require_gpu()
+    agent, mixer = _modules(8)
+    from t2omca_amd.learner import TDLearner
+    lr = TDLearner(agent, mixer, precision="bf16")
+    assert lr.sa.prec == 1 and lr.sm.prec == 1
+    assert lr.pack_a.numel() == dataclasses.replace(agent.shape, prec=1).layout().pack_floats

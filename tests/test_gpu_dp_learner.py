@@ -1,0 +1,95 @@
+"""GPU, data parallel on the PRODUCT learner: two ranks (gloo, both on cuda:0, spawned
+before any GPU call in the children) each run TDLearner.train on their episode shard;
+after every update the post-Adam parameters equal a single-rank full-batch TDLearner
+update (<= 1e-6 normwise) and stay identical across ranks.
+
+The ranks deliberately build their modules from different seeds: the learner's
+rank-0 broadcast (distributed.broadcast_state) must make the replicas identical
+before the first update.  Masks are ragged (a terminated step, unfilled tail), so
+the shards carry different Σ mask and only the all-reduced [grad, Σ mask] buffer
+gives the full-batch normalisation (learner.py step 7).
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from tests.gpu_util import normwise, require_gpu
+
+pytestmark = pytest.mark.gpu
+A, B, T, UPDATES = 8, 6, 7, 3
+
+
+def _batch(device):
+    from t2omca_amd.synthetic import make_batch
+    batch, w = make_batch(B, T, A, seed=11, device=device)
+    batch["terminated"][1, 3] = 1  # ragged masks: the shards' Σ mask differ
+    batch["filled"][4, 5:] = 0
+    return batch, w
+
+
+def _learner(seed, device, pg=None):
+    from t2omca_amd.learner import TDLearner
+    from t2omca_amd.modules import TransformerAgent, TransformerMixer
+    from t2omca_amd.synthetic import make_args
+    torch.manual_seed(seed)
+    args = make_args(A, device=str(device))
+    agent = TransformerAgent(None, args).to(device)
+    mixer = TransformerMixer(args).to(device)
+    return TDLearner(agent, mixer, process_group=pg, target_update_interval=2)
+
+
+def _worker(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from t2omca_amd.distributed import shard_bounds
+        learner = _learner(100 + rank, dev)  # different init per rank: the broadcast must fix it
+        batch, w = _batch(dev)
+        lo, hi = shard_bounds(B, rank, world)
+        shard = {k: v[lo:hi] for k, v in batch.items()}
+        hist = [learner.params.detach().cpu().clone()]
+        for u in range(UPDATES):
+            learner.train(shard, 0, u, per_weight=w[lo:hi])
+            torch.cuda.synchronize()
+            hist.append(learner.params.detach().cpu().clone())
+        out.put((rank, torch.stack(hist).numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_two_ranks_equal_full_batch_learner():
+    require_gpu()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=240) for _ in procs)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    for p in procs:
+        assert p.exitcode == 0
+    r0, r1 = torch.from_numpy(res[0]), torch.from_numpy(res[1])
+    # replicas are identical from the start (rank 0's init) and stay identical
+    assert torch.equal(r0, r1)
+    dev = torch.device("cuda", 0)
+    full = _learner(100, dev)  # rank 0's init
+    batch, w = _batch(dev)
+    assert torch.equal(full.params.cpu(), r0[0])
+    for u in range(UPDATES):
+        full.train(batch, 0, u, per_weight=w)
+        torch.cuda.synchronize()
+        err = normwise(r0[u + 1], full.params.cpu())
+        assert err < 1e-6, (u, err)
