@@ -59,7 +59,11 @@ enum {
  * state and every accumulation stay fp32 in both modes. */
 typedef struct {
   int32_t kind, E, H, D, F, NA, FF, n_ent;
-  int32_t prec, reserved_;
+  int32_t prec;
+  int32_t generic;            /* 1: no tuned kernel instance for this shape; the
+                                 runtime-shaped kernels run (t2o_generic.hip) and the
+                                 pack is the reference-order parameters followed by
+                                 transposed copies; compact grads = reference order */
   int64_t WeT, We, be;        /* WeT[16][E], We[E][16], be[E] (F <= 16) */
   int64_t Wo, bo, WoT;        /* agent: q_basic padded Wo[16][E], bo[16], WoT[E][16];
                                  mixer: hyper_b2.weight in Wo row 0, bias in bo[0] */
@@ -74,10 +78,35 @@ typedef struct {
   int64_t grad_total;         /* size of the compact gradient block (no transposes) */
   int64_t vec_lo;             /* first vector element (see above) */
   int64_t pack_floats;        /* buffer size of a pack in floats (prec 1: fp32 + bf16 image) */
+  int32_t n_agents;           /* mixer: agents (hidden tokens, qvals, w1 rows); n_ent = its state
+                                 tokens (n_entities_state, or n_agents * n_entities for the obs
+                                 branch of n_transf_mixer.py:62-63).  agent: = n_ent */
+  int32_t pos_func;           /* mixer head positivity (n_transf_mixer.py:95-103):
+                                 T2O_POS_ABS / _SOFTPLUS / _QUADRATIC / _IDENTITY */
+  float pos_beta;             /* softplus beta (qmix_pos_func_beta) */
+  int32_t reserved_;
 } t2o_layout;
 
-/* Fill *L for a network (prec 0 = fp32, 1 = bf16 MFMA operands); returns 0 or T2O_EINVAL. */
+#define T2O_POS_ABS 0
+#define T2O_POS_SOFTPLUS 1
+#define T2O_POS_QUADRATIC 2
+#define T2O_POS_IDENTITY 3
+
+/* t2o_layout_init_ex flags */
+#define T2O_LAYOUT_FORCE_GENERIC 1  /* use the runtime-shaped kernels even for a tuned shape */
+
+/* Fill *L for a network (prec 0 = fp32, 1 = bf16 MFMA operands); returns 0 or T2O_EINVAL.
+ * Shapes with a tuned kernel instance (E 32 / 3 heads / depth 2 / FF 128 at 3, 8, 16 or
+ * 64 entities; E 16 / 2 heads / depth 1 / FF 64 at 3) get the folded MFMA pack; any
+ * other shape within the runtime-shaped kernels' limits (E <= 64, H <= 8, H*E <= 512,
+ * D <= 4, FF <= 512, F <= 16, NA <= 16, agent entities <= 64, mixer tokens
+ * n_ent + n_agents + 3 <= 192 with n_agents <= 64) gets generic = 1.  The generic
+ * kernels compute in fp32 whatever prec says. */
 int t2o_layout_init(t2o_layout* L, int kind, int E, int H, int D, int F, int NA, int FF, int n_ent, int prec);
+/* t2o_layout_init with the mixer's agent count (n_agents; 0 = n_ent), its head's
+ * positivity function (T2O_POS_*, softplus beta) and flags (T2O_LAYOUT_*). */
+int t2o_layout_init_ex(t2o_layout* L, int kind, int E, int H, int D, int F, int NA, int FF, int n_ent, int prec,
+                       int n_agents, int pos_func, float pos_beta, int flags);
 
 /* sizeof(t2o_layout), for bindings to check their mirror of the struct. */
 int t2o_layout_sizeof(void);

@@ -57,11 +57,13 @@ def td_forward(p_agent, p_mixer, p_agent_tgt, p_mixer_tgt, batch, cfg, *, gamma=
         cur_max = mac_det.max(dim=3, keepdim=True)[1]
         target_max_q = torch.gather(tgt_out, 3, cur_max).squeeze(3)
         hw0 = torch.zeros(B, 3, cfg["mixer_emb"], dtype=obs.dtype)
-        qtot_tgt, _ = ref_model.mixer_unroll(p_mixer_tgt, target_max_q, tgt_hs, state, hw0, cfg=cfg)
+        obs_tok = None if cfg.get("state_entity_mode", True) else obs  # n_transf_mixer.py:60-63
+        qtot_tgt, _ = ref_model.mixer_unroll(p_mixer_tgt, target_max_q, tgt_hs, state, hw0, cfg=cfg, obs=obs_tok)
         targets = build_td_lambda_targets(rewards, terminated, mask, qtot_tgt, gamma, td_lambda)
     hid = hs[:, :-1].detach() if detach_mixer_hidden else hs[:, :-1]
     hw0 = torch.zeros(B, 3, cfg["mixer_emb"], dtype=obs.dtype)
-    qtot, _ = ref_model.mixer_unroll(p_mixer, chosen, hid, state[:, :-1], hw0, cfg=cfg)
+    qtot, _ = ref_model.mixer_unroll(p_mixer, chosen, hid, state[:, :-1], hw0, cfg=cfg,
+                                     obs=None if obs_tok is None else obs[:, :-1])
     td_error = qtot - targets.detach()
     td_error2 = 0.5 * td_error.pow(2)
     masked = td_error2 * mask

@@ -13,8 +13,10 @@ to rounding and the fp32 one is the "reference CPU path" timed by bench.py:
 * ``transformer``    — transformer.py:169-178.
 * ``agent_forward``  — transf_agent.py:54-76 (hidden token first, Q read from
   token 0).
-* ``mixer_forward``  — n_transf_mixer.py:55-91 (w1/b1/w2/b2 from the last A+3
-  output tokens, pos_func = abs, elu hidden layer).
+* ``mixer_forward``  — n_transf_mixer.py:55-103 (w1/b1/w2/b2 from the last A+3
+  output tokens, elu hidden layer; pos_func abs / softplus(beta) / quadratic /
+  identity; state tokens from the state, or from every agent's obs when
+  state_entity_mode is off, :60-63).
 """
 import torch
 import torch.nn.functional as F
@@ -80,10 +82,14 @@ def agent_forward(p, inputs, hidden_state, *, n_entities, feat_dim, emb, heads, 
 
 
 def mixer_forward(p, qvals, hidden_states, hyper_weights, states, *, n_agents, n_entities,
-                  feat_dim, emb, heads, depth, pos_func="abs"):
-    """n_transf_mixer.py:55-91 (custom_space=True branch) -> (y [b,1,1], hw [b,3,E])."""
+                  feat_dim, emb, heads, depth, pos_func="abs", pos_beta=1.0, obs=None):
+    """n_transf_mixer.py:55-103 -> (y [b,1,1], hw [b,3,E]).  obs given: the
+    custom_space=False branch (tokens = obs.reshape(b, n_agents*n_entities, feat_dim))."""
     b, _, _ = qvals.size()
-    inputs = states.reshape(b, n_entities, feat_dim)
+    if obs is None:
+        inputs = states.reshape(b, n_entities, feat_dim)
+    else:
+        inputs = obs.reshape(b, n_agents * n_entities, feat_dim)
     embs = _lin(inputs, p, "feat_embedding")
     x = torch.cat((embs, hidden_states, hyper_weights), 1)
     embs = transformer(p, "transformer.", x, x, heads, depth)
@@ -91,10 +97,12 @@ def mixer_forward(p, qvals, hidden_states, hyper_weights, states, *, n_agents, n
     b1 = embs[:, -3, :].view(-1, 1, emb)
     w2 = embs[:, -2, :].view(-1, emb, 1)
     b2 = F.relu(_lin(embs[:, -1, :], p, "hyper_b2")).view(-1, 1, 1)
-    if pos_func == "abs":
-        w1, w2 = torch.abs(w1), torch.abs(w2)
+    if pos_func == "softplus":
+        w1, w2 = F.softplus(w1, beta=pos_beta), F.softplus(w2, beta=pos_beta)  # nn.Softplus: threshold 20
     elif pos_func == "quadratic":
         w1, w2 = 0.5 * w1 ** 2, 0.5 * w2 ** 2
+    elif pos_func == "abs":
+        w1, w2 = torch.abs(w1), torch.abs(w2)
     hidden = F.elu(torch.matmul(qvals, w1) + b1)
     y = torch.matmul(hidden, w2) + b2
     return y, embs[:, -3:, :]
@@ -107,7 +115,7 @@ def agent_unroll(p, obs, h0, *, cfg):
     qs, hs = [], []
     h = h0
     for t in range(obs.shape[1]):
-        q, h = agent_forward(p, obs[:, t].contiguous(), h, n_entities=cfg["n_entities"],
+        q, h = agent_forward(p, obs[:, t].contiguous(), h, n_entities=cfg.get("n_entities_obs", cfg["n_entities"]),
                              feat_dim=cfg["obs_entity_feats"], emb=cfg["emb"],
                              heads=cfg["heads"], depth=cfg["depth"])
         qs.append(q)
@@ -115,18 +123,21 @@ def agent_unroll(p, obs, h0, *, cfg):
     return torch.stack(qs, 1), torch.stack(hs, 1)
 
 
-def mixer_unroll(p, qvals, hidden, states, hw0, *, cfg):
-    """Unroll the mixer over qvals [b,T,A], hidden [b,T,A,E], states [b,T,S].
+def mixer_unroll(p, qvals, hidden, states, hw0, *, cfg, obs=None):
+    """Unroll the mixer over qvals [b,T,A], hidden [b,T,A,E], states [b,T,S]
+    (or, state_entity_mode False, obs [b,T,A,n_ent*F]).
 
     The 3 hyper-weight tokens are recurrent (n_transf_mixer.py:69,91).
     Returns y [b, T] and hw [b, T, 3, E] (hw[:, t] = hyper tokens after step t)."""
     ys, hws = [], []
     hw = hw0
     for t in range(qvals.shape[1]):
-        y, hw = mixer_forward(p, qvals[:, t:t + 1], hidden[:, t], hw, states[:, t],
-                              n_agents=cfg["n_agents"], n_entities=cfg["n_entities"],
+        y, hw = mixer_forward(p, qvals[:, t:t + 1], hidden[:, t], hw, states[:, t] if states is not None else None,
+                              n_agents=cfg["n_agents"], n_entities=cfg.get("n_entities_state", cfg["n_entities"]),
                               feat_dim=cfg["state_entity_feats"], emb=cfg["mixer_emb"],
-                              heads=cfg["mixer_heads"], depth=cfg["mixer_depth"])
+                              heads=cfg["mixer_heads"], depth=cfg["mixer_depth"],
+                              pos_func=cfg.get("qmix_pos_func", "abs"), pos_beta=cfg.get("qmix_pos_func_beta", 1.0),
+                              obs=None if obs is None else obs[:, t])
         ys.append(y.view(-1))
         hws.append(hw)
     return torch.stack(ys, 1), torch.stack(hws, 1)

@@ -16,16 +16,25 @@ _I64x = ctypes.c_int64 * MAX_DEPTH
 
 class Layout(ctypes.Structure):
     _fields_ = ([(n, ctypes.c_int32) for n in ("kind", "E", "H", "D", "F", "NA", "FF", "n_ent", "prec",
-                                                "reserved_")] +
+                                                "generic")] +
                 [(n, ctypes.c_int64) for n in ("WeT", "We", "be", "Wo", "bo", "WoT")] +
                 [(n, _I64x) for n in ("M", "MT", "N", "NT", "bu", "g1", "n1", "W1", "W1T", "c1",
                                       "W2", "W2T", "c2", "g2", "n2")] +
-                [(n, ctypes.c_int64) for n in ("fwd_total", "total", "grad_total", "vec_lo", "pack_floats")])
+                [(n, ctypes.c_int64) for n in ("fwd_total", "total", "grad_total", "vec_lo", "pack_floats")] +
+                [("n_agents", ctypes.c_int32), ("pos_func", ctypes.c_int32), ("pos_beta", ctypes.c_float),
+                 ("reserved_", ctypes.c_int32)])
+
+
+# mixer head positivity functions (include/t2omca.h T2O_POS_*; n_transf_mixer.py:95-103)
+POS_FUNCS = {"abs": 0, "softplus": 1, "quadratic": 2}  # anything else: identity (3)
+LAYOUT_FORCE_GENERIC = 1
 
 
 EXPORTS = {
     # name: (restype, argtypes)
     "t2o_layout_init": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_int] * 9),
+    "t2o_layout_init_ex": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_int] * 11 + [ctypes.c_float,
+                                                                                       ctypes.c_int]),
     "t2o_param_count": (ctypes.c_int64, [ctypes.c_int] * 7),
     "t2o_layout_sizeof": (ctypes.c_int, []),
     "t2o_pack_params": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_void_p, ctypes.c_void_p,
@@ -126,7 +135,16 @@ def stream_ptr(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
-def make_layout(kind, E, H, D, F, NA, FF, n_ent, prec=0):
+def force_generic():
+    """T2O_GENERIC=1 lays every network out for the runtime-shaped kernels, tuned
+    shapes included (cross-checks of the generic path against the tuned one)."""
+    return os.environ.get("T2O_GENERIC", "0") == "1"
+
+
+def make_layout(kind, E, H, D, F, NA, FF, n_ent, prec=0, n_agents=0, pos_func=0, pos_beta=1.0, flags=None):
+    if flags is None:
+        flags = LAYOUT_FORCE_GENERIC if force_generic() else 0
     L = Layout()
-    check(lib().t2o_layout_init(ctypes.byref(L), kind, E, H, D, F, NA, FF, n_ent, prec), "t2o_layout_init")
+    check(lib().t2o_layout_init_ex(ctypes.byref(L), kind, E, H, D, F, NA, FF, n_ent, prec, n_agents, pos_func,
+                                   float(pos_beta), flags), "t2o_layout_init_ex")
     return L

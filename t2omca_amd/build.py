@@ -41,11 +41,17 @@ def build(force=False, verbose=False, jobs=None, out=None):
     objdir = os.path.join(LIBDIR, "obj" if out is None else "obj_" + os.path.basename(out))
     os.makedirs(objdir, exist_ok=True)
     hipcc = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "bin", "hipcc")
-    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wno-unused-result"]
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++20", "-fPIC", "-Wno-unused-result"]
     objs, procs = [], []
+    headers = glob.glob(os.path.join(CSRC, "*.hpp")) + [os.path.join(os.path.dirname(HERE), "include", "t2omca.h")]
+    newest_header = max(os.path.getmtime(h) for h in headers)
     for src in sources():
         obj = os.path.join(objdir, os.path.basename(src) + ".o")
         objs.append(obj)
+        # an object newer than its source, every header and this file is reused
+        if not force and os.path.exists(obj) and os.path.getmtime(obj) > max(
+                os.path.getmtime(src), newest_header, os.path.getmtime(__file__)):
+            continue
         cmd = [hipcc] + flags + ["-c", "-o", obj, src]
         if verbose:
             print(" ".join(cmd))

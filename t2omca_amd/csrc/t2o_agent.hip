@@ -13,6 +13,7 @@
 #include "t2o_agent_block.hpp"
 #include "t2o_agent_block_ch.hpp"
 #include "t2o_dispatch.hpp"
+#include "t2o_generic.hpp"
 #include "t2o_layout.hpp"
 
 using namespace t2o;
@@ -639,8 +640,11 @@ extern "C" int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, c
                                     const float* h0_tg, float* q_on, float* h_on, float* hmid_on, float* q_tg,
                                     float* h_tg, float* hmid_tg, int B, int T, int A, void* stream) {
   if (!L || L->kind != 0 || !pack_on || !obs || !q_on || !h_on || B < 1 || T < 1 || A < 1 ||
-      L->n_ent != A)
+      (!L->generic && L->n_ent != A))
     return T2O_EINVAL;
+  if (L->generic)
+    return gen_agent_unroll_fwd(L, pack_on, pack_tg, obs, obs_sb, obs_st, h0_on, h0_tg, q_on, h_on, hmid_on, q_tg,
+                                h_tg, hmid_tg, B, T, A, (hipStream_t)stream);
   AgentFwdArgs args{};
   args.L = *L;
   args.net[0] = AgentNet{pack_on, h0_on, q_on, h_on, hmid_on};
@@ -671,8 +675,11 @@ extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, cons
                                     int max_slabs, int* nslab, void* tape, float* gh0, int B, int T, int A,
                                     void* stream) {
   if (!L || L->kind != 0 || !pack || !obs || !h_seq || !gslabs || !nslab || !tape || B < 1 || T < 1 || A < 1 ||
-      L->n_ent != A || h_ts < T || (gchosen && !actions))
+      (!L->generic && L->n_ent != A) || h_ts < T || (gchosen && !actions))
     return T2O_EINVAL;
+  if (L->generic)
+    return gen_agent_unroll_bwd(L, pack, obs, obs_sb, obs_st, h0, h_seq, hmid, h_ts, gq, gchosen, actions, act_sb,
+                                act_st, gh, gslabs, max_slabs, nslab, tape, gh0, B, T, A, (hipStream_t)stream);
   AgentBwdArgs args{};
   args.L = *L;
   grad_layout(*L, args.G);

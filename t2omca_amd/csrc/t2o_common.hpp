@@ -355,6 +355,27 @@ T2O_DEV float rowsum16_fast(float v) {
   return v;
 }
 
+// ---- mixing-head positivity (n_transf_mixer.py:95-103; the generic kernels) --
+// pf = t2o_layout.pos_func (wave-uniform): abs, softplus(beta, torch's threshold
+// 20), quadratic 0.5x², identity; dposf is the derivative torch's backward uses
+// (abs: sign(x), 0 at 0).
+T2O_DEV float posf(float x, int pf, float beta) {
+  if (pf == T2O_POS_ABS) return fabsf(x);
+  if (pf == T2O_POS_SOFTPLUS) return x * beta > 20.f ? x : log1pf(expf(x * beta)) / beta;
+  if (pf == T2O_POS_QUADRATIC) return 0.5f * x * x;
+  return x;
+}
+T2O_DEV float dposf(float x, int pf, float beta) {
+  if (pf == T2O_POS_ABS) return (float)((x > 0.f) - (x < 0.f));
+  if (pf == T2O_POS_SOFTPLUS) {
+    if (x * beta > 20.f) return 1.f;
+    const float z = expf(x * beta);
+    return z / (z + 1.f);
+  }
+  if (pf == T2O_POS_QUADRATIC) return x;
+  return 1.f;
+}
+
 // ---- LayerNorm over E = 16*ET features of each row (eps 1e-5, biased var) --
 template <int ET>
 T2O_DEV void layernorm_fwd(const f4* r, const float* __restrict__ gamma,

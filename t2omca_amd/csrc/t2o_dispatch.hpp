@@ -2,9 +2,8 @@
 //
 // Instantiated shapes: the reference defaults used by BASELINE configs 1-4
 // (emb 32, 3 heads, depth 2, ff_hidden_mult 4, 8, 16 or 64 AGVs) plus the
-// small shapes of the golden fixtures.  (64 AGVs runs the generic code with
-// register spills: correct, not tuned — DESIGN.md §9.)  Anything else returns T2O_EUNSUPPORTED
-// (the Python side raises; there is no fallback path).
+// small shapes of the golden fixtures.  Every other shape is laid out generic
+// (t2o_layout_init) and runs the runtime-shaped kernels of t2o_generic.hip.
 #pragma once
 
 #define T2O_CASE(E, H, D, NE, FF, STMT)                                   \
@@ -13,6 +12,12 @@
     (void)E_; (void)H_; (void)D_; (void)NE_; (void)FF_;                    \
     STMT;                                                                  \
   }
+
+// the same list, for t2o_layout_init (shapes outside it get generic = 1)
+inline bool t2o_tuned_shape(int E, int H, int D, int NE, int FF) {
+  return (E == 16 && H == 2 && D == 1 && NE == 3 && FF == 64) ||
+         (E == 32 && H == 3 && D == 2 && FF == 128 && (NE == 3 || NE == 8 || NE == 16 || NE == 64));
+}
 
 #define T2O_DISPATCH(EV, HV, DV, NEV, FFV, STMT)                          \
   do {                                                                     \

@@ -32,6 +32,7 @@
 
 #include "t2o_common.hpp"
 #include "t2o_dispatch.hpp"
+#include "t2o_generic.hpp"
 #include "t2o_layout.hpp"
 
 namespace t2o {
@@ -456,6 +457,7 @@ using namespace t2o;
 
 extern "C" int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t tiles) {
   if (!L || tiles < 0) return -1;
+  if (L->generic) return gen_tape_floats(L, tiles);
   const int64_t elems = (int64_t)L->D * tiles * tape_tile_records(*L) * (6 * L->E + 2 * L->H * L->E);
   return L->prec ? (elems + 1) / 2 : elems;
 }
@@ -463,6 +465,7 @@ extern "C" int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t tiles) {
 extern "C" int t2o_bwd_tape_contract(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
                                      float* gslabs, int nslab, void* stream) {
   if (!L || !pack || !tape || !gslabs || tiles < 0 || nslab < 1) return T2O_EINVAL;
+  if (L->generic) return gen_tape_contract(L, tape, tiles, gslabs, nslab, (hipStream_t)stream);
   t2o_layout G;
   grad_layout(*L, G);
   int rc = T2O_EUNSUPPORTED;

@@ -1,5 +1,6 @@
 // t2o_layout.hpp — host/device description of parameter, pack and gradient layouts.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/t2omca.h"
@@ -17,7 +18,7 @@ struct ParamOffsets {
   int64_t total;
 };
 
-inline ParamOffsets param_offsets(int kind, int E, int H, int D, int F, int NA, int FF) {
+__host__ __device__ inline ParamOffsets param_offsets(int kind, int E, int H, int D, int F, int NA, int FF) {
   ParamOffsets p{};
   int64_t o = 0;
   const int64_t HE = (int64_t)H * E;
@@ -45,11 +46,75 @@ inline ParamOffsets param_offsets(int kind, int E, int H, int D, int F, int NA, 
   return p;
 }
 
+// ---- runtime-shaped ("generic") networks (t2o_generic.hip) -------------------
+// Pack: the reference-order parameters [0, P.total), then transposed copies, so
+// that every lane-per-feature matrix-vector product of the generic kernels reads
+// its weights coalesced (lane = output feature, consecutive lanes = consecutive
+// addresses): forward q = Wq x, v = Wv z, a = U v, f1 = W1 y, r2 = W2 fr, the
+// entity embedding and the agent head read the transposes; backward products
+// read the originals, except gq = Wk gu (transpose of u = Wkᵀ q) which reads WkT.
+struct GenOffsets {
+  ParamOffsets P;
+  int64_t WqT[T2O_MAX_DEPTH], WkT[T2O_MAX_DEPTH], WvT[T2O_MAX_DEPTH];  // [E][HE]
+  int64_t UT[T2O_MAX_DEPTH];                                          // [HE][E]
+  int64_t W1T[T2O_MAX_DEPTH];                                         // [E][FF]
+  int64_t W2T[T2O_MAX_DEPTH];                                         // [FF][E]
+  int64_t WeT, WoT;                                                   // [F][E], [E][no]
+  int64_t total;
+};
+
+__host__ __device__ inline GenOffsets gen_offsets(int kind, int E, int H, int D, int F, int NA, int FF) {
+  GenOffsets g{};
+  g.P = param_offsets(kind, E, H, D, F, NA, FF);
+  int64_t o = g.P.total;
+  const int64_t HE = (int64_t)H * E;
+  for (int d = 0; d < D; ++d) {
+    g.WqT[d] = o; o += E * HE;
+    g.WkT[d] = o; o += E * HE;
+    g.WvT[d] = o; o += E * HE;
+    g.UT[d] = o; o += HE * E;
+    g.W1T[d] = o; o += (int64_t)E * FF;
+    g.W2T[d] = o; o += (int64_t)FF * E;
+  }
+  g.WeT = o; o += (int64_t)F * E;
+  g.WoT = o; o += (int64_t)E * (kind == 0 ? NA : 1);
+  g.total = o;
+  return g;
+}
+
+// Generic weight-gradient record of one (row, step, block): the operand vectors
+// of dWq = Σ gq⊗x, dWk_h = Σ q_h⊗gu_h, dWv_h = Σ gv_h⊗z_h, dU = Σ ga⊗v,
+// dW1 = Σ gf1⊗y, dW2 = Σ gr2⊗relu(f1) (fp32; contracted by t2o_generic.hip).
+struct GenRec {
+  int X, Q, GQ, GU, Z, GV, V, GA, Y, GF1, GR2, FR, SIZE;
+};
+__host__ __device__ inline GenRec gen_rec(int E, int H, int FF) {
+  GenRec r{};
+  const int HE = H * E;
+  int o = 0;
+  r.X = o; o += E;
+  r.Q = o; o += HE;
+  r.GQ = o; o += HE;
+  r.GU = o; o += HE;
+  r.Z = o; o += HE;
+  r.GV = o; o += HE;
+  r.V = o; o += HE;
+  r.GA = o; o += E;
+  r.Y = o; o += E;
+  r.GF1 = o; o += FF;
+  r.GR2 = o; o += E;
+  r.FR = o; o += FF;
+  r.SIZE = (o + 3) / 4 * 4;
+  return r;
+}
+
 // Records per weight-gradient tape tile (TapeRec, t2o_common.hpp): 16, one
 // wave's rows; a mixer whose A+3 query rows fit one tile stores exactly those
 // rows (no padding records in HBM; the contraction zero-fills them in LDS).
 constexpr int mixer_tape_records(int n_ent) { return n_ent + 3 <= 16 ? n_ent + 3 : 16; }
-inline int tape_tile_records(const t2o_layout& L) { return L.kind == 1 ? mixer_tape_records(L.n_ent) : 16; }
+inline int tape_tile_records(const t2o_layout& L) {
+  return (L.kind == 1 && !L.generic) ? mixer_tape_records(L.n_ent) : 16;
+}
 
 // Compact gradient layout (what the backward kernels accumulate in LDS and
 // write per workgroup): the pack layout without transposed copies.

@@ -10,6 +10,7 @@
 //   qmode 1  chosen-action Q  gather(Q[:, t], actions)  (online mixer)
 //   qmode 2  double-Q         Q_tgt[argmax(Q_on masked by avail)] (target mixer)
 #include "t2o_dispatch.hpp"
+#include "t2o_generic.hpp"
 #include "t2o_layout.hpp"
 #include "t2o_mixer_block.hpp"
 
@@ -212,7 +213,8 @@ T2O_DEV void mix_keys(const Wts<WT>& P, const t2o_layout& L, const In& in, float
   }
 }
 
-// Mixing head (n_transf_mixer.py:75-89) on the final query rows OUT[q][f],
+// Mixing head (n_transf_mixer.py:75-89, pos_func abs: t2o_layout_init lays out
+// every other qmix_pos_func generic) on the final query rows OUT[q][f],
 // lanes = features.  Returns y; writes hyper tokens back into X0.
 template <int E, int A, typename WT>
 T2O_DEV float mixer_head(const Wts<WT>& P, const t2o_layout& L, const float* OUT,
@@ -1129,6 +1131,17 @@ extern "C" int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, c
   if (!L || L->kind != 1 || !pack_on || !states || !hid_on || !y_on || !hw_on || B < 1 || T_on < 1 ||
       L->E > 64)
     return T2O_EINVAL;
+  if (L->generic) {
+    auto ok = [&](int mode, const float* qv, const float* qsel) {
+      return mode == 0 ? qv != nullptr : mode == 1 ? (qsel && actions) : mode == 2 ? (qsel && q_on) : false;
+    };
+    if (!ok(qmode_on, qv_on, q_on) || (pack_tg && (!hid_tg || !y_tg || !hw_tg || T_tg < 1 || !ok(qmode_tg, qv_tg, q_tg))))
+      return T2O_EINVAL;
+    return gen_mixer_unroll_fwd(L, pack_on, pack_tg, states, st_sb, st_st, hid_on, hid_tg, hid_sb, hid_st, hw0_on,
+                                hw0_tg, qmode_on, qmode_tg, qv_on, qv_tg, q_on, q_tg, q_ts, n_actions, actions,
+                                act_sb, act_st, avail, av_sb, av_st, y_on, hw_on, qvo_on, xout_on, xmid_on, y_tg,
+                                hw_tg, qvo_tg, xout_tg, xmid_tg, B, T_on, T_tg, (hipStream_t)stream);
+  }
   MixerFwdArgs a{};
   a.L = *L;
   a.states = states;
@@ -1181,6 +1194,9 @@ extern "C" int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, cons
   if (!L || L->kind != 1 || !pack || !states || !hid || !qv || !hw || !xout || !gy || !gqv || !ghid ||
       !gslabs || !nslab || !tape || B < 1 || T < 1 || L->E > 64)
     return T2O_EINVAL;
+  if (L->generic)
+    return gen_mixer_unroll_bwd(L, pack, states, st_sb, st_st, hid, hid_sb, hid_st, hw0, qv, hw, xout, xmid, gy,
+                                ghw_ext, gqv, ghid, ghw0, gslabs, max_slabs, nslab, tape, B, T, (hipStream_t)stream);
   MixerBwdArgs a{};
   a.f.L = *L;
   a.f.states = states;

@@ -10,6 +10,7 @@
 #include <math.h>
 
 #include "t2o_common.hpp"
+#include "t2o_dispatch.hpp"
 #include "t2o_layout.hpp"
 
 using namespace t2o;
@@ -221,18 +222,47 @@ struct Builder {
 
 extern "C" int t2o_layout_init(t2o_layout* L, int kind, int E, int H, int D, int F, int NA, int FF, int n_ent,
                                int prec) {
-  if (!L || (kind != 0 && kind != 1) || E <= 0 || E % 16 || H < 1 || D < 1 || D > T2O_MAX_DEPTH ||
-      F < 1 || F > 16 || NA < 1 || NA > 16 || FF <= 0 || FF % 16 || n_ent < 1 || (prec != 0 && prec != 1))
+  return t2o_layout_init_ex(L, kind, E, H, D, F, NA, FF, n_ent, prec, 0, T2O_POS_ABS, 1.0f, 0);
+}
+
+extern "C" int t2o_layout_init_ex(t2o_layout* L, int kind, int E, int H, int D, int F, int NA, int FF, int n_ent,
+                                  int prec, int n_agents, int pos_func, float pos_beta, int flags) {
+  if (!L || (kind != 0 && kind != 1) || E <= 0 || H < 1 || D < 1 || D > T2O_MAX_DEPTH || F < 1 || F > 16 ||
+      NA < 1 || NA > 16 || FF <= 0 || n_ent < 1 || (prec != 0 && prec != 1) || pos_func < 0 || pos_func > 3 ||
+      !(pos_beta > 0.f))
     return T2O_EINVAL;
+  if (n_agents <= 0) n_agents = n_ent;
+  if (kind == 0 && n_agents != n_ent) return T2O_EINVAL;  // the agent's rows are its own sequences
   t2o_layout z{};
   *L = z;
   L->kind = kind; L->E = E; L->H = H; L->D = D; L->F = F; L->NA = NA; L->FF = FF; L->n_ent = n_ent;
   L->prec = prec;
-  int64_t o = 0;
-  const int64_t HE = (int64_t)H * E;
+  L->n_agents = n_agents;
+  L->pos_func = pos_func;
+  L->pos_beta = pos_beta;
   for (int d = 0; d < T2O_MAX_DEPTH; ++d)
     L->M[d] = L->MT[d] = L->N[d] = L->NT[d] = L->bu[d] = L->g1[d] = L->n1[d] = L->W1[d] = L->W1T[d] = L->c1[d] =
         L->W2[d] = L->W2T[d] = L->c2[d] = L->g2[d] = L->n2[d] = -1;
+  // the tuned mixer head computes pos_func abs only (the reference default): a
+  // runtime switch there measured slower and, at 64 agents, fell over a compiler
+  // limit; the other functions run the generic kernels
+  if ((flags & T2O_LAYOUT_FORCE_GENERIC) || n_agents != n_ent || !t2o_tuned_shape(E, H, D, n_ent, FF) ||
+      (kind == 1 && pos_func != T2O_POS_ABS)) {
+    // runtime-shaped kernels (t2o_generic.hip): pack = reference-order params +
+    // transposed copies; compact grads = reference order
+    const bool ok = E <= 64 && H <= 8 && H * E <= 512 && FF <= 512 &&
+                    (kind == 0 ? n_ent <= 64 : (n_agents <= 64 && n_ent + n_agents + 3 <= 192));
+    if (!ok) return T2O_EUNSUPPORTED;
+    L->generic = 1;
+    L->WeT = L->We = L->be = L->Wo = L->bo = L->WoT = -1;
+    const GenOffsets g = gen_offsets(kind, E, H, D, F, kind == 0 ? NA : 1, FF);
+    L->vec_lo = 0;
+    L->fwd_total = L->total = L->pack_floats = g.total;
+    L->grad_total = g.P.total;
+    return 0;
+  }
+  int64_t o = 0;
+  const int64_t HE = (int64_t)H * E;
   // forward matrices, then forward vectors (one contiguous LDS copy; in bf16
   // mode the vectors stay fp32), then the backward's transposed copies.  Every
   // size is a multiple of 16 elements, so every section stays 64-B aligned.
@@ -282,6 +312,23 @@ extern "C" int64_t t2o_param_count(int kind, int E, int H, int D, int F, int NA,
 extern "C" int t2o_pack_params(const t2o_layout* L, const float* params, float* pack, void* stream) {
   if (!L || !params || !pack) return T2O_EINVAL;
   const int E = L->E, H = L->H, D = L->D, F = L->F, FF = L->FF;
+  if (L->generic) {  // reference-order params, then the transposed copies (GenOffsets)
+    const int no = L->kind == 0 ? L->NA : 1, HE = H * E;
+    const GenOffsets g = gen_offsets(L->kind, E, H, D, F, no, FF);
+    Builder b(E, H, params, nullptr, pack, nullptr, stream);
+    b.ew(T_COPY, 1, (int)g.P.total, 0, 0);
+    for (int d = 0; d < D; ++d) {
+      b.ew(T_TPAD2D, E, HE, g.WqT[d], g.P.Wq[d], HE, E);
+      b.ew(T_TPAD2D, E, HE, g.WkT[d], g.P.Wk[d], HE, E);
+      b.ew(T_TPAD2D, E, HE, g.WvT[d], g.P.Wv[d], HE, E);
+      b.ew(T_TPAD2D, HE, E, g.UT[d], g.P.U[d], E, HE);
+      b.ew(T_TPAD2D, E, FF, g.W1T[d], g.P.W1[d], FF, E);
+      b.ew(T_TPAD2D, FF, E, g.W2T[d], g.P.W2[d], E, FF);
+    }
+    b.ew(T_TPAD2D, F, E, g.WeT, g.P.We, E, F);
+    b.ew(T_TPAD2D, E, no, g.WoT, g.P.Wo, no, E);
+    return b.finish();
+  }
   if (E > 64) return T2O_EUNSUPPORTED;
   const ParamOffsets P = param_offsets(L->kind, E, H, D, F, L->NA, FF);
   // bf16 mode: every matrix also goes to the swizzled bf16 image after the fp32 pack
@@ -319,6 +366,11 @@ extern "C" int t2o_unpack_grads(const t2o_layout* L, const float* params, const 
                                 void* stream) {
   if (!L || !params || !gpack || !grad) return T2O_EINVAL;
   const int E = L->E, H = L->H, D = L->D, F = L->F, FF = L->FF;
+  if (L->generic) {  // the generic backward's grads are already in reference order
+    Builder b(E, H, params, gpack, grad, nullptr, stream);
+    b.ew(T_ADD, 1, (int)L->grad_total, 0, 0);
+    return b.finish();
+  }
   if (E > 64) return T2O_EUNSUPPORTED;
   const ParamOffsets P = param_offsets(L->kind, E, H, D, F, L->NA, FF);
   t2o_layout G;

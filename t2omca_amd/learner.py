@@ -215,7 +215,9 @@ class TDLearner:
             b, T1, A = wire.shape[:3]
             obs = ops.obs_expand(wire, batch["obs_nrm_n"], batch["obs_nrm"],
                                  out=self._buf("obs", (b, T1, A, 9 * A)))
-        state = batch["state"]
+        # the mixer's tokens: the state (state_entity_mode) or every agent's obs
+        # entities (n_transf_mixer.py:60-63)
+        state = batch["state"] if self.mixer.custom_space else obs.flatten(2)
         actions = batch["actions"]
         avail = batch["avail_actions"]
         B, T1, A, _ = obs.shape

@@ -15,7 +15,7 @@ on the same parameters.  CPU tensors raise — there is no CPU fallback.
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import _lib, ops
 
 
 class MultiHeadAttention(nn.Module):
@@ -58,6 +58,17 @@ class Transformer(nn.Module):
 
 def _flat(module):
     return torch.cat([p.reshape(-1) for p in module.parameters()])
+
+
+def orthogonal_init_(m, gain=1.0):
+    """PyMARL2's utils.th_utils.orthogonal_init_ (imported by n_transf_mixer.py:6,
+    applied to every submodule at :48-50; the module itself is absent from the
+    reference, so this restates its published form): orthogonal Linear weights,
+    zero biases.  Bias-free Linears (the attention projections) keep no bias."""
+    if isinstance(m, nn.Linear):
+        nn.init.orthogonal_(m.weight.data, gain=gain)
+        if m.bias is not None:
+            nn.init.constant_(m.bias.data, 0)
 
 
 class _AgentStep(torch.autograd.Function):
@@ -120,7 +131,7 @@ class _MixerStep(torch.autograd.Function):
     @staticmethod
     def forward(ctx, flat, qvals, hidden_states, hyper_weights, states, shape):
         b = qvals.shape[0]
-        A, E = shape.n_ent, shape.E
+        A, E = shape.agents, shape.E
         pack = ops.pack_params(shape, flat.detach().contiguous())
         qv = qvals.detach().reshape(b, 1, A).contiguous()
         hid = hidden_states.detach().reshape(b, 1, A, E).contiguous()
@@ -149,7 +160,14 @@ class _MixerStep(torch.autograd.Function):
 
 
 class TransformerMixer(nn.Module):
-    """n_transf_mixer.py:12-102 drop-in (HIP forward/backward, pos_func abs)."""
+    """n_transf_mixer.py:12-102 drop-in (HIP forward/backward).
+
+    Every pos_func of the reference (:95-103: softplus with qmix_pos_func_beta,
+    quadratic, abs, anything else = identity), both input branches (:60-63:
+    state_entity_mode -> the n_entities_state state tokens; otherwise the
+    n_agents * n_entities obs tokens, which needs state_entity_feats == the obs
+    feature width), n_entities_state != n_agents and use_orthogonal (:48-50).
+    Shapes without a tuned MFMA instance run the runtime-shaped kernels."""
 
     def __init__(self, args, abs=True):
         super().__init__()
@@ -163,17 +181,17 @@ class TransformerMixer(nn.Module):
                                        args.ff_hidden_mult, args.dropout)
         self.qmix_pos_func = getattr(self.args, "qmix_pos_func", "abs")
         self.custom_space = args.env_args.get("state_entity_mode", True)
-        if self.qmix_pos_func != "abs" or not self.custom_space:
-            raise NotImplementedError("t2omca_amd: only qmix_pos_func='abs' with state_entity_mode=True "
-                                      "(the reference defaults, n_transf_mixer.py:42-43) are fused")
-        if self.n_entities != self.n_agents:
-            raise NotImplementedError("t2omca_amd: n_entities_state must equal n_agents "
-                                      "(environment_multi_mec.py:429)")
         self.hyper_b2 = nn.Linear(self.emb_dim, 1)
         if getattr(args, "use_orthogonal", False):
-            raise NotImplementedError("t2omca_amd: use_orthogonal init is not supported")
+            for m in self.modules():
+                orthogonal_init_(m)
+        pos = _lib.POS_FUNCS.get(self.qmix_pos_func, 3)
+        beta = float(getattr(args, "qmix_pos_func_beta", 1.0)) if self.qmix_pos_func == "softplus" else 1.0
+        # state tokens: the state's entities, or (obs branch) every agent's obs entities
+        n_tok = self.n_entities if self.custom_space else self.n_agents * self.n_entities
         self.shape = ops.NetShape(ops.MIXER, args.mixer_emb, args.mixer_heads, args.mixer_depth, self.feat_dim, 1,
-                                  args.ff_hidden_mult * args.mixer_emb, self.n_agents)
+                                  args.ff_hidden_mult * args.mixer_emb, n_tok, n_agents=self.n_agents,
+                                  pos_func=pos, pos_beta=beta)
 
     def init_hidden(self):
         # n_transf_mixer.py:52-53 (shape [1, A, E] as in the reference)
@@ -182,4 +200,5 @@ class TransformerMixer(nn.Module):
     def forward(self, qvals, hidden_states, hyper_weights, states, obs):
         b = qvals.size(0)
         hyper_weights = hyper_weights.expand(b, 3, self.emb_dim)
-        return _MixerStep.apply(_flat(self), qvals, hidden_states, hyper_weights, states, self.shape)
+        tokens = states if self.custom_space else obs  # n_transf_mixer.py:60-63
+        return _MixerStep.apply(_flat(self), qvals, hidden_states, hyper_weights, tokens, self.shape)

@@ -36,9 +36,21 @@ class NetShape:
     FF: int
     n_ent: int
     prec: int = 0   # 0 fp32, 1 bf16 MFMA operands (fp32 accumulate / LayerNorm / softmax / state)
+    n_agents: int = 0  # mixer: agents (hidden tokens / qvals); 0 = n_ent (its state tokens)
+    pos_func: int = 0  # mixer head positivity (_lib.POS_FUNCS; 3 = identity)
+    pos_beta: float = 1.0
 
     def layout(self):
         return _layout_cached(self)
+
+    @property
+    def generic(self):
+        """True when no tuned kernel instance exists: the runtime-shaped kernels run."""
+        return bool(self.layout().generic)
+
+    @property
+    def agents(self):
+        return self.n_agents or self.n_ent
 
     @property
     def n_params(self):
@@ -49,10 +61,12 @@ _LAYOUTS = {}
 
 
 def _layout_cached(s):
-    L = _LAYOUTS.get(s)
+    key = (s, _lib.force_generic())
+    L = _LAYOUTS.get(key)
     if L is None:
-        L = _lib.make_layout(s.kind, s.E, s.H, s.D, s.F, s.NA, s.FF, s.n_ent, s.prec)
-        _LAYOUTS[s] = L
+        L = _lib.make_layout(s.kind, s.E, s.H, s.D, s.F, s.NA, s.FF, s.n_ent, s.prec, s.n_agents, s.pos_func,
+                             s.pos_beta)
+        _LAYOUTS[key] = L
     return L
 
 

@@ -1,6 +1,17 @@
 """Shared helpers for the -m gpu parity tests (GPU kernels vs the CPU oracle)."""
+import os
+
 import numpy as np
 import torch
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+# golden fixtures of the tuned kernel shapes (make_golden.CONFIGS); the EXTENDED
+# ones (other shapes / options) are exercised by tests/test_gpu_generic.py
+TUNED_TAGS = ("a3_e16_h2_d1", "a8_e32_h3_d2", "a16_e32_h3_d2")
+
+
+def tuned_fixtures(kind, tags=TUNED_TAGS):
+    return [os.path.join(GOLD, f"{kind}_{t}.npz") for t in tags]
 
 
 def flat_from_npz(z):

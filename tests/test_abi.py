@@ -48,7 +48,8 @@ def test_layout_and_param_count(kind, F, NA):
 def test_layout_rejects_bad_shapes():
     from t2omca_amd import _lib
     L = _lib.Layout()
-    assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 30, 3, 2, 9, 5, 128, 8, 0) != 0  # E % 16
+    assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 96, 3, 2, 9, 5, 128, 8, 0) != 0  # E > 64
+    assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 32, 3, 2, 9, 5, 128, 65, 0) != 0  # > 64 entities
     assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 32, 3, 9, 9, 5, 128, 8, 0) != 0  # depth > 4
     assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 32, 3, 2, 20, 5, 128, 8, 0) != 0  # F > 16
     assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 32, 3, 2, 9, 5, 128, 8, 2) != 0  # precision
@@ -96,3 +97,22 @@ def test_dropin_modules_state_dict_matches_reference_keys():
         ref = {k[6:]: z[k].shape for k in z.files if k.startswith("param/")}
         mine = {k: tuple(v.shape) for k, v in m.state_dict().items()}
         assert list(mine) == list(ref) and mine == ref
+
+
+@pytest.mark.parametrize("E,H,D,FF,n,generic", [(32, 3, 2, 128, 8, 0), (32, 3, 2, 128, 5, 1), (30, 3, 2, 120, 8, 1),
+                                                 (64, 4, 2, 256, 8, 1), (16, 1, 3, 32, 6, 1), (16, 2, 1, 64, 3, 0)])
+def test_layout_tuned_or_generic(E, H, D, FF, n, generic):
+    """Shapes with a tuned MFMA instance get the folded pack; every other shape within
+    the runtime-shaped kernels' limits gets generic = 1 and a pack of the reference
+    parameters + transposed copies, with reference-order gradients."""
+    from t2omca_amd import _lib
+    for kind in (0, 1):
+        L = _lib.make_layout(kind, E, H, D, 9, 5, FF, n, flags=0)
+        assert L.generic == generic
+        n_params = _lib.lib().t2o_param_count(kind, E, H, D, 9, 5, FF)
+        if generic:
+            no = 5 if kind == 0 else 1
+            assert L.grad_total == n_params
+            assert L.total == L.pack_floats == n_params + D * (4 * H * E * E + 2 * E * FF) + 9 * E + E * no
+        forced = _lib.make_layout(kind, E, H, D, 9, 5, FF, n, flags=_lib.LAYOUT_FORCE_GENERIC)
+        assert forced.generic == 1

@@ -1,6 +1,5 @@
 """The restructured kernel algorithm (tests/algo_model.py) equals the reference
 (pinned oracle + golden gradients) in fp64: forward and hand-written BPTT."""
-import glob
 import os
 
 import numpy as np
@@ -8,12 +7,13 @@ import pytest
 import torch
 
 from tests import algo_model as am
+from tests.gpu_util import tuned_fixtures
 from tests.test_oracle_golden import _cfg, _rel
 
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 
-@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "agent_*.npz"))))
+@pytest.mark.parametrize("path", tuned_fixtures("agent"))
 def test_agent_algo_fwd_bwd(path):
     z = np.load(path)
     p, cfg = _cfg(z, "agent")
@@ -29,7 +29,7 @@ def test_agent_algo_fwd_bwd(path):
     assert _rel(gh0.numpy(), z["grad_h0"]) < 1e-10
 
 
-@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "mixer_*.npz"))))
+@pytest.mark.parametrize("path", tuned_fixtures("mixer"))
 def test_mixer_algo_fwd_bwd(path):
     z = np.load(path)
     p, cfg = _cfg(z, "mixer")

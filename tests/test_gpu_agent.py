@@ -1,5 +1,4 @@
 """GPU parity: fused agent unroll forward vs the CPU oracle / reference goldens."""
-import glob
 import os
 
 import numpy as np
@@ -7,7 +6,7 @@ import pytest
 import torch
 
 from oracle import ref_model
-from tests.gpu_util import flat_from_dict, flat_from_npz, normwise, require_gpu
+from tests.gpu_util import flat_from_dict, flat_from_npz, normwise, require_gpu, tuned_fixtures
 from tests.test_oracle_golden import _cfg
 
 pytestmark = pytest.mark.gpu
@@ -20,7 +19,7 @@ def _shape(cfg):
     return NetShape(AGENT, cfg["emb"], cfg["heads"], cfg["depth"], 9, 5, 4 * cfg["emb"], cfg["n_entities"])
 
 
-@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "agent_*.npz"))))
+@pytest.mark.parametrize("path", tuned_fixtures("agent"))
 def test_agent_fwd_matches_reference_golden(path):
     require_gpu()
     from t2omca_amd import ops
@@ -79,7 +78,7 @@ def test_agent_fwd_strided_obs_single_step():
     assert normwise(h[:, 0], hr) < TOL_F32
 
 
-@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "agent_*.npz"))))
+@pytest.mark.parametrize("path", tuned_fixtures("agent"))
 def test_agent_bwd_matches_reference_autograd(path):
     """BPTT kernel grads (params, h0) vs the reference modules' autograd (fp64 goldens)."""
     require_gpu()

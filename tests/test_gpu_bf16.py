@@ -7,7 +7,6 @@ propagated through D=2 blocks and the recurrence:
     parameter gradients          <= 6e-2
     agent Q / h over a 4-step unroll <= 2e-2 (reference goldens)
 """
-import glob
 import os
 
 import numpy as np
@@ -15,7 +14,7 @@ import pytest
 import torch
 
 from oracle import ref_learner
-from tests.gpu_util import normwise, require_gpu
+from tests.gpu_util import normwise, require_gpu, tuned_fixtures
 from tests.test_gpu_learner import _cfg_dict, _setup
 
 pytestmark = pytest.mark.gpu
@@ -49,7 +48,7 @@ def test_td_update_bf16_vs_oracle(A, B, T):
     assert errs["grad"] < TOL_G, errs
 
 
-@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "agent_*.npz"))))
+@pytest.mark.parametrize("path", tuned_fixtures("agent"))
 def test_agent_unroll_bf16_vs_reference(path):
     require_gpu()
     import dataclasses

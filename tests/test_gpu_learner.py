@@ -1,5 +1,4 @@
 """GPU: one full TD update (fwd + bwd + Adam) vs the CPU oracle learner; drop-in modules."""
-import glob
 import os
 
 import numpy as np
@@ -7,7 +6,7 @@ import pytest
 import torch
 
 from oracle import ref_learner, ref_model
-from tests.gpu_util import flat_from_npz, normwise, require_gpu
+from tests.gpu_util import flat_from_npz, normwise, require_gpu, tuned_fixtures
 from tests.test_oracle_golden import _cfg
 
 pytestmark = pytest.mark.gpu
@@ -76,7 +75,7 @@ def test_td_update_matches_oracle(A, B, T, lam):
     assert (learner.params.cpu() - ref_p.detach()).abs().max() < 1e-6
 
 
-@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "agent_a8*.npz"))))
+@pytest.mark.parametrize("path", tuned_fixtures("agent", ("a8_e32_h3_d2",)))
 def test_dropin_agent_module_step_and_autograd(path):
     """TransformerAgent.forward (reference signature) per step + autograd through it."""
     require_gpu()
@@ -103,7 +102,7 @@ def test_dropin_agent_module_step_and_autograd(path):
     assert normwise(h.grad, z["grad_h0"]) < 3e-5
 
 
-@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "mixer_a8*.npz"))))
+@pytest.mark.parametrize("path", tuned_fixtures("mixer", ("a8_e32_h3_d2",)))
 def test_dropin_mixer_module_step_and_autograd(path):
     require_gpu()
     from t2omca_amd.modules import TransformerMixer

@@ -1,5 +1,4 @@
 """GPU parity: fused mixer unroll forward/backward vs the reference goldens / oracle."""
-import glob
 import os
 
 import numpy as np
@@ -7,7 +6,7 @@ import pytest
 import torch
 
 from oracle import ref_model
-from tests.gpu_util import flat_from_dict, flat_from_npz, normwise, require_gpu
+from tests.gpu_util import flat_from_dict, flat_from_npz, normwise, require_gpu, tuned_fixtures
 from tests.test_oracle_golden import _cfg
 
 pytestmark = pytest.mark.gpu
@@ -21,7 +20,7 @@ def _shape(cfg):
                     4 * cfg["mixer_emb"], cfg["n_agents"])
 
 
-@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLD, "mixer_*.npz"))))
+@pytest.mark.parametrize("path", tuned_fixtures("mixer"))
 def test_mixer_fwd_bwd_matches_reference(path):
     require_gpu()
     from t2omca_amd import ops

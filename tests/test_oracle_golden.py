@@ -21,10 +21,24 @@ def _cfg(z, kind):
         A = z["obs"].shape[2]
     else:
         A = z["qvals"].shape[2]
+    FF = p["transformer.tblocks.0.ff.0.weight"].shape[0]
     cfg = dict(n_agents=A, n_entities=A, obs_entity_feats=9, emb=E, heads=H, depth=D,
-               ff_hidden_mult=4, n_actions=5, state_entity_feats=8, mixer_emb=E,
+               ff_hidden_mult=FF // E, n_actions=5, state_entity_feats=8, mixer_emb=E,
                mixer_heads=H, mixer_depth=D)
+    # EXTENDED fixtures (make_golden.py): the args fields they override
+    for k in z.files:
+        if k.startswith("meta/"):
+            v = z[k].item()
+            cfg[k[5:]] = v.decode() if isinstance(v, bytes) else v
     return p, cfg
+
+
+def _mixer_inputs(z, dt):
+    """(states, obs) for mixer_unroll: the obs branch (state_entity_mode off) feeds obs."""
+    st = torch.from_numpy(z["states"]).to(dt)
+    if "meta/state_entity_mode" in z.files and not bool(z["meta/state_entity_mode"]):
+        return None, st
+    return st, None
 
 
 def _rel(a, b):
@@ -67,10 +81,10 @@ def test_mixer_oracle_matches_reference(path):
     p, cfg = _cfg(z, "mixer")
     for dt, name, tol in [(torch.float64, "f64", 1e-13), (torch.float32, "f32", 2e-6)]:
         pp = {k: v.to(dt) for k, v in p.items()}
+        st, ob = _mixer_inputs(z, dt)
         y, hw = ref_model.mixer_unroll(pp, torch.from_numpy(z["qvals"]).to(dt),
-                                       torch.from_numpy(z["hidden"]).to(dt),
-                                       torch.from_numpy(z["states"]).to(dt),
-                                       torch.from_numpy(z["hw0"]).to(dt), cfg=cfg)
+                                       torch.from_numpy(z["hidden"]).to(dt), st,
+                                       torch.from_numpy(z["hw0"]).to(dt), cfg=cfg, obs=ob)
         assert _rel(y.numpy(), z[f"y_{name}"]) < tol
         assert _rel(hw.numpy(), z[f"hw_{name}"]) < tol
 
@@ -83,7 +97,8 @@ def test_mixer_oracle_grads_match_reference(path):
     qv = torch.from_numpy(z["qvals"]).requires_grad_(True)
     hd = torch.from_numpy(z["hidden"]).requires_grad_(True)
     hw0 = torch.from_numpy(z["hw0"]).requires_grad_(True)
-    y, hw = ref_model.mixer_unroll(pp, qv, hd, torch.from_numpy(z["states"]), hw0, cfg=cfg)
+    st, ob = _mixer_inputs(z, torch.float64)
+    y, hw = ref_model.mixer_unroll(pp, qv, hd, st, hw0, cfg=cfg, obs=ob)
     loss = (y * torch.from_numpy(z["cy"])).sum() + (hw * torch.from_numpy(z["chw"])).sum()
     loss.backward()
     for k, v in pp.items():

@@ -42,7 +42,6 @@ def run(A, B, T, precision="fp32", seed=3):
 
 
 if __name__ == "__main__":
-    for seed in (3, 4, 5):
-        run(8, 16, 60, seed=seed)
-    for A, B, T in [(16, 4, 150), (64, 2, 60)]:
+    cases = [tuple(int(v) for v in c.split(",")) for c in sys.argv[1:]] or [(8, 16, 60), (16, 4, 150), (64, 2, 60)]
+    for A, B, T in cases:
         run(A, B, T)
