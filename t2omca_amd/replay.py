@@ -22,6 +22,7 @@ import numpy as np
 import torch
 
 from ._lib import check, lib, ptr, stream_ptr
+from .episode_batch import DeviceEpisodeBatch, as_tensor_dict
 from .distributed import rank as dist_rank, rank_seed
 
 
@@ -41,7 +42,7 @@ class PrioritizedReplayBuffer:
         self.beta_increment = (1.0 - self.beta) / float(t_max)
         self.seed = int(seed)
         self.data = {}
-        for k, v in example_batch.items():
+        for k, v in as_tensor_dict(example_batch).items():
             if k not in self.EPISODE_KEYS and v.shape[1] != self.max_seq_length:
                 raise ValueError(f"{k}: time extent {v.shape[1]} != max_seq_length {self.max_seq_length}")
             self.data[k] = torch.zeros((self.buffer_size,) + tuple(v.shape[1:]), dtype=v.dtype, device=self.device)
@@ -55,6 +56,7 @@ class PrioritizedReplayBuffer:
 
     # -- EpisodeBatch ring-buffer insert (new episodes at max priority) --------------
     def insert_episode_batch(self, batch):
+        batch = as_tensor_dict(batch)
         n = next(iter(batch.values())).shape[0]
         done = 0
         while done < n:
@@ -99,8 +101,10 @@ class PrioritizedReplayBuffer:
         return out
 
     def sample(self, batch_size, t):
+        """(episode batch, idx, IS weights): the batch answers the EpisodeBatch calls of
+        per_run.py:228-232 (max_t_filled, [:, :t] slicing, device, to)."""
         idx, w = self.sample_indices(batch_size, t)
-        return self.gather(idx), idx, w
+        return DeviceEpisodeBatch(self.gather(idx)), idx, w
 
     # -- priorities -----------------------------------------------------------------
     def update_priorities(self, idxes, priorities):

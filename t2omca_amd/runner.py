@@ -37,6 +37,7 @@ import torch
 
 from . import ops
 from .distributed import rank as dist_rank, rank_seed
+from .episode_batch import DeviceEpisodeBatch
 
 
 class LinearSchedule:
@@ -69,6 +70,7 @@ class RolloutRunner:
         self.t_env = 0
         self.episode = 0
         self._bufs = None
+        self.last_returns = None
 
     # -- replay batch ---------------------------------------------------------
     def _alloc(self):
@@ -89,8 +91,10 @@ class RolloutRunner:
         )
 
     def run(self, test_mode=False, new_buffers=True):
-        """One episode of every env; returns the batch dict ([n, T+1, ...] views)
-        and the per-env episode return [n] (fp64, on the device)."""
+        """One episode of every env; returns the episode batch ([n, T+1, ...] device
+        views as a DeviceEpisodeBatch, like ParallelRunner.run's EpisodeBatch,
+        parallel_runner.py:221); the per-env episode returns [n] (fp64, on the
+        device) are in self.last_returns."""
         if self._bufs is None or new_buffers:
             self._bufs = self._alloc()
         tm = self._bufs
@@ -119,7 +123,8 @@ class RolloutRunner:
         if self.compact_obs:  # per-episode: the normaliser each episode's obs start from
             batch["obs_nrm_n"] = env.snap_n.clone()
             batch["obs_nrm"] = env.snap.clone()
-        return batch, ret
+        self.last_returns = ret
+        return DeviceEpisodeBatch(batch)
 
     def _dest(self, tm, t):
         if self.compact_obs:

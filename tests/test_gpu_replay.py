@@ -3,6 +3,8 @@
 weights, priority updates with max tracking, ring-buffer insert with wrap, the
 episode gather, and one full rollout -> insert -> sample -> train ->
 update_priorities cycle on the device."""
+import types
+
 import numpy as np
 import pytest
 import torch
@@ -80,10 +82,10 @@ def test_rollout_insert_sample_train_cycle():
     mixer = TransformerMixer(make_args(A)).cuda()
     runner = RolloutRunner(agent, VecEnv(n, mec_num=M, agv_num=A, episode_limit=T, seed=5))
     learner = TDLearner(agent, mixer, priorities_to_cpu=False)
-    batch, _ = runner.run()
+    batch = runner.run()
     buf = PrioritizedReplayBuffer(batch, 16, T + 1, 0.6, 0.4, 10000)
     buf.insert_episode_batch(batch)
-    batch, _ = runner.run()
+    batch = runner.run()
     buf.insert_episode_batch(batch)
     sample, idx, w = buf.sample(4, runner.t_env)
     info = learner.train(sample, runner.t_env, 0, per_weight=w)
@@ -93,3 +95,43 @@ def test_rollout_insert_sample_train_cycle():
     assert torch.isfinite(p).all() and bool((p > 0).all())
     expect = (info["td_errors_abs"].flatten().cpu() + 1e-6) ** 0.6
     assert torch.allclose(p[idx.cpu()], expect, rtol=1e-5) or len(set(idx.tolist())) < 4
+
+
+def test_reference_driver_loop_runs_unchanged():
+    """per_run.py:212-238's training loop, statement for statement, on the device
+    runner / buffer / learner (priorities to the host as the reference buffer wants)."""
+    require_gpu()
+    from t2omca_amd.env import VecEnv
+    from t2omca_amd.learner import TDLearner
+    from t2omca_amd.modules import TransformerAgent, TransformerMixer
+    from t2omca_amd.replay import PrioritizedReplayBuffer
+    from t2omca_amd.runner import RolloutRunner
+    from t2omca_amd.synthetic import make_args
+    A, T, batch_size, batch_size_run = 3, 4, 4, 4
+    args = types.SimpleNamespace(device=torch.device("cuda", torch.cuda.current_device()), t_max=3 * batch_size_run * T)
+    torch.manual_seed(0)
+    mac_agent = TransformerAgent(None, make_args(A)).cuda()
+    learner = TDLearner(mac_agent, TransformerMixer(make_args(A)).cuda())
+    runner = RolloutRunner(mac_agent, VecEnv(batch_size_run, mec_num=2, agv_num=A, episode_limit=T, seed=1))
+    buffer = PrioritizedReplayBuffer(runner.run(), 16, T + 1, 0.6, 0.4, args.t_max)
+    episode, trained = 0, 0
+    while runner.t_env <= args.t_max:
+        with torch.no_grad():
+            episode_batch = runner.run(test_mode=False)
+            buffer.insert_episode_batch(episode_batch)
+        if buffer.can_sample(batch_size):
+            episode_sample, idx, weights = buffer.sample(batch_size, runner.t_env)
+            max_ep_t = episode_sample.max_t_filled()
+            episode_sample = episode_sample[:, :max_ep_t]
+            if episode_sample.device != args.device:
+                episode_sample.to(args.device)
+            info = learner.train(episode_sample, runner.t_env, episode, weights)
+            del episode_sample
+            new_priorities = info["td_errors_abs"].flatten() + 1e-6
+            buffer.update_priorities(idx, new_priorities.numpy().tolist())
+            trained += 1
+        episode += batch_size_run
+    torch.cuda.synchronize()
+    assert trained >= 2 and max_ep_t == T + 1
+    assert torch.isfinite(learner.params).all()
+    assert bool((buffer.p[:buffer.episodes_in_buffer] > 0).all())

@@ -57,7 +57,8 @@ def test_rollout_matches_env_replay_and_agent_unroll(A, M, n, T):
     agent = _agent(A)
     env = VecEnv(n, mec_num=M, agv_num=A, episode_limit=T, seed=11)
     runner = RolloutRunner(agent, env, seed=3)
-    batch, ret = runner.run(test_mode=True)
+    batch = runner.run(test_mode=True)
+    ret = runner.last_returns
     torch.cuda.synchronize()
     # replay the recorded actions on a fresh env
     env2 = VecEnv(n, mec_num=M, agv_num=A, episode_limit=T, seed=11)
@@ -97,7 +98,7 @@ def test_rollout_batch_feeds_learner():
     pm = {k: v.detach().cpu().double() for k, v in mixer.state_dict().items()}
     env = VecEnv(n, mec_num=M, agv_num=A, episode_limit=T, seed=2)
     runner = RolloutRunner(agent, env, seed=4, epsilon_start=0.5)
-    batch, _ = runner.run()
+    batch = runner.run()
     learner = TDLearner(agent, mixer)
     w = torch.linspace(0.5, 1.0, n, device="cuda")
     cfg = dict(n_agents=A, n_entities=A, obs_entity_feats=9, emb=32, heads=3, depth=2, ff_hidden_mult=4,

@@ -104,7 +104,7 @@ def test_wire_rollout_trains_like_dense():
         env = VecEnv(n, mec_num=M, agv_num=A, episode_limit=T, seed=3, wire=compact)
         env.get_env_info()
         runner = RolloutRunner(agent, env, seed=5, compact_obs=compact)
-        batch, _ = runner.run()
+        batch = runner.run()
         if compact:
             assert "obs" not in batch and batch["obs_wire"].shape == (n, T + 1, A, 4)
         buf = PrioritizedReplayBuffer(batch, 32, T + 1, 0.6, 0.4, 1000)

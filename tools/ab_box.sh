@@ -12,7 +12,7 @@ mkdir -p "$OUT"
 for i in 1 2 3; do
   for lib in "${LIBS[@]}"; do
     n=$(basename "$lib" .so)
-    T2O_LIB=$PWD/$lib timeout -k 10 200 python bench.py --no-cpu-baseline --serial --steps 20 "$@" > "$OUT/$n$i.json"
+    T2O_LIB=$PWD/$lib timeout -k 10 200 python bench.py --no-cpu-baseline --no-fp32-companion --serial --steps 20 "$@" > "$OUT/$n$i.json"
   done
 done
 python - "$OUT" "${LIBS[@]}" <<'PY'

@@ -7,7 +7,7 @@ T=$(mktemp -d)
 git -C "$R" archive "$REV" t2omca_amd/csrc include | tar -x -C "$T"
 mkdir -p "$T/obj"
 for f in "$T"/t2omca_amd/csrc/*.hip; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result -c -o "$T/obj/$(basename "$f").o" "$f" &
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++20 -fPIC -Wno-unused-result -c -o "$T/obj/$(basename "$f").o" "$f" &
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$R/t2omca_amd/lib/libt2omca_base.so" "$T"/obj/*.o

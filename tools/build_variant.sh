@@ -6,7 +6,7 @@ NAME=$1; shift
 R=$(cd "$(dirname "$0")/.." && pwd)
 T=$(mktemp -d)
 for f in "$R"/t2omca_amd/csrc/*.hip; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-result "$@" -c -o "$T/$(basename "$f").o" "$f" &
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++20 -fPIC -Wno-unused-result "$@" -c -o "$T/$(basename "$f").o" "$f" &
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$R/t2omca_amd/lib/$NAME.so" "$T"/*.o
