@@ -395,7 +395,7 @@ struct MixBwdIn {
   f4 stT[Dm::ST];  // lane (g, c) reg r: state feature c of entity 16s + 4g + r; column Fs = 1 (bias)
 };
 
-template <int E, int A, int D>
+template <int E, int A, int D, bool XM = true>
 T2O_DEV void mixb_load(const MixerBwdArgs& args, const MixerNet& n, int b, int t, MixBwdIn<E, A, D>& in) {
   using Dm = MixDims<E, A>;
   using In = MixBwdIn<E, A, D>;
@@ -418,7 +418,7 @@ T2O_DEV void mixb_load(const MixerBwdArgs& args, const MixerNet& n, int b, int t
 #pragma unroll
   for (int k = 0; k < 3; ++k) in.ghx[k] = (args.ghw_ext && lane < E) ? args.ghw_ext[(bt * 3 + k) * E + lane] : 0.f;
   in.gy = args.gy[bt];
-  if (D > 1 && args.xmid) {
+  if (XM && D > 1 && args.xmid) {
 #pragma unroll
     for (int qt = 0; qt < Dm::QT; ++qt) {
       const int q = 16 * qt + c;
@@ -501,11 +501,18 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
       for (int t = 0; t < 2 * ET; ++t) ln2[d][t] = zero4();
     float gWo = 0.f, gbo = 0.f;
+    // Multi-tile mixers (A+3 > 16 query rows) hold a register file's worth of
+    // state per step: they use the lean block cache (the forward recompute writes
+    // the record's X / Z / Y fields itself) and load each step's inputs when the
+    // step starts instead of double-buffering them a step ahead — without both,
+    // the 16-AGV kernel spilled ~100 registers to scratch.
+    constexpr bool LEAN = Dm::QT > 1;
     MixBwdIn<E, A, D> cur, nxt;
-    mixb_load<E, A, D>(args, n, b, n.T - 1, cur);
+    if constexpr (!LEAN) mixb_load<E, A, D>(args, n, b, n.T - 1, cur);
     for (int t = n.T - 1; t >= 0; --t) {
       const Wts<WT> P = step_view(P0);
       const size_t bt = (size_t)b * n.T + t;
+      if constexpr (LEAN) mixb_load<E, A, D, false>(args, n, b, t, cur);  // (block inputs: per tile, below)
       mix_keys<E, A>(P, L, cur.m, X0);
 #pragma unroll
       for (int k = 0; k < MixBwdIn<E, A, D>::HW; ++k) {
@@ -518,7 +525,9 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
         const int i = lane + 64 * k;
         if (i < Dm::Q * E) OUT[i] = cur.xo[k];
       }
-      if (t > 0) mixb_load<E, A, D>(args, n, b, t - 1, nxt);  // prefetch step t-1
+      if constexpr (!LEAN) {
+        if (t > 0) mixb_load<E, A, D>(args, n, b, t - 1, nxt);  // prefetch step t-1
+      }
       __builtin_amdgcn_wave_barrier();
       // ---- mixing head backward (lanes = features)
       float qv[A];
@@ -565,7 +574,44 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
       for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft) gX0[kt][ft] = zero4();
-      f4 gq0[Dm::QT][ET];
+      f4 gq0[LEAN ? 1 : Dm::QT][ET];
+      if constexpr (LEAN) {
+        // one query tile at a time, not unrolled: its grads come from and go back
+        // to GOUT (LDS), its block inputs straight from HBM
+#pragma unroll 1
+        for (int qt = 0; qt < Dm::QT; ++qt) {
+          const int q = 16 * qt + c;
+          f4 gx[ET];
+#pragma unroll
+          for (int ft = 0; ft < ET; ++ft) gx[ft] = ld4(GOUT + (16 * qt + c) * E + 16 * ft + 4 * g);
+#pragma unroll
+          for (int d = D - 1; d >= 0; --d) {
+            f4 x[ET];
+#pragma unroll
+            for (int ft = 0; ft < ET; ++ft) x[ft] = q < Dm::Q ? ld4(X0 + (Dm::NS + q) * Dm::LDX + 16 * ft + 4 * g) : zero4();
+            if (d > 0) {
+              if (args.xmid) {
+#pragma unroll
+                for (int ft = 0; ft < ET; ++ft)
+                  x[ft] = q < Dm::Q ? ld4(args.xmid + ((bt * (D - 1) + d - 1) * Dm::Q + q) * E + 16 * ft + 4 * g)
+                                    : zero4();
+              } else {
+                for (int dd = 0; dd < d; ++dd) mixer_block_fwd<E, H, KT, FF, false>(P, L, dd, K, Dm::LK, x, nullptr);
+              }
+            }
+            constexpr int RT = mixer_tape_records(A);
+            WT* tile = static_cast<WT*>(args.tape) +
+                       ((size_t)d * ntiles + ((size_t)t * fa.B + b) * Dm::QT + qt) * Rec::SIZE * RT;
+            MixerCacheLean<E, H, KT, FF> cache;  // whole 16-record tiles (padding records: zero grads)
+            const MaskedRec<WT> rec(tile, RT, Rec::SIZE);
+            mixer_block_fwd_lean<E, H, KT, FF>(P, L, d, K, Dm::LK, x, cache, rec);
+            mixer_block_bwd_lean<E, H, KT, FF>(P, L, gs, rec, stage, d, K, gX0, cache, gx, ln2[d]);
+          }
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int ft = 0; ft < ET; ++ft) st4(GOUT + (16 * qt + c) * E + 16 * ft + 4 * g, q < Dm::Q ? gx[ft] : zero4());
+        }
+      } else {
 #pragma unroll
       for (int qt = 0; qt < Dm::QT; ++qt)
 #pragma unroll
@@ -599,22 +645,22 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
         }
 #pragma unroll
         for (int d = D - 1; d >= 0; --d) {
-          MixerCache<E, H, KT, FF> cache;
           f4 x[ET];
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft) x[ft] = xs[d][ft];
-          mixer_block_fwd<E, H, KT, FF, true>(P, L, d, K, Dm::LK, x, &cache);
           // one tile per (episode, step, query tile); padding rows carry zero gradients
           // tiles are step-major (t, b, qt): at any step the grid writes one contiguous window
           // (a one-tile mixer's tiles hold just its Q rows: mixer_tape_records)
           constexpr int RT = mixer_tape_records(A);
-          WT* rec = c < RT ? static_cast<WT*>(args.tape) +
-                                 ((size_t)d * ntiles + ((size_t)t * fa.B + b) * Dm::QT + qt) * Rec::SIZE * RT
-                           : nullptr;
-          mixer_block_bwd<E, H, KT, FF>(P, L, G, gs, rec, stage, d, K, gX0, cache, gx, ln2[d]);
+          WT* tile = static_cast<WT*>(args.tape) +
+                     ((size_t)d * ntiles + ((size_t)t * fa.B + b) * Dm::QT + qt) * Rec::SIZE * RT;
+          MixerCache<E, H, KT, FF> cache;
+          mixer_block_fwd<E, H, KT, FF, true>(P, L, d, K, Dm::LK, x, &cache);
+          mixer_block_bwd<E, H, KT, FF>(P, L, G, gs, c < RT ? tile : nullptr, stage, d, K, gX0, cache, gx, ln2[d]);
         }
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft) gq0[qt][ft] = q < Dm::Q ? gx[ft] : zero4();
+      }
       }
       // ---- state embedding grads straight from the key-grad registers:
       // dWe[f][fs] (+ d be[f] in column Fs) += Σ_{entity j} gX0[j][f] · [s_j, 1][fs]
@@ -649,7 +695,8 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft) {
             float* dst = GX0 + (Dm::NS + q) * E + 16 * ft + 4 * g;
-            st4(dst, ld4(dst) + gq0[qt][ft]);
+            const f4 gq = LEAN ? ld4(GOUT + q * E + 16 * ft + 4 * g) : gq0[LEAN ? 0 : qt][ft];
+            st4(dst, ld4(dst) + gq);
           }
         }
       }
@@ -659,7 +706,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) ghw[k] = fv ? GX0[(Dm::NS + A + k) * E + f] : 0.f;
       __builtin_amdgcn_wave_barrier();
-      cur = nxt;
+      if constexpr (!LEAN) cur = nxt;
     }
     if (args.ghw0 && fv) {
 #pragma unroll
