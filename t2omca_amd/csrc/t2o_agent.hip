@@ -390,7 +390,9 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
   constexpr bool CHUNK = NE > AG_CHUNK_MIN;
   constexpr int NO = CHUNK ? 1 : NE;
   using Rec = TapeRec<E, H, FF>;
-  using Cache = typename std::conditional<CHUNK, AgentCacheCh<E, H, NE, FF>, AgentCache<E, H, NE, FF>>::type;
+  // lean cache (half the registers of the one-wave kernel's; X, Z, Y records
+  // written by the recompute phase) unless the entities are streamed in chunks
+  using Cache = typename std::conditional<CHUNK, AgentCacheCh<E, H, NE, FF>, AgentCacheLean<E, H, NE, FF>>::type;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const t2o_layout& L = args.L;
   const t2o_layout& G = args.G;
@@ -510,13 +512,15 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
       if (ph == 0) T2O_STAMP(2 * (T - 1 - step), 1);
 #endif
       const Wts<WT> P = step_view(P0);
+      WT* const tile = static_cast<WT*>(args.tape) +
+                       ((size_t)d * ntiles + (size_t)step * tiles_per_step + rt) * Rec::SIZE * 16;
       if (ph == 0) {
 #ifdef T2O_PHASE_PROF
         __builtin_amdgcn_s_waitcnt(0);
 #endif
         T2O_MARK(1);
         if constexpr (CHUNK) agent_block_fwd_ch<E, H, NE, FF, true>(P, Lb, 0, h, ObsRow{ob, F}, xo, &cache);
-        else agent_block_fwd<E, H, NE, FF, true>(P, Lb, 0, h, o, xo, &cache);
+        else agent_block_fwd_lean<E, H, NE, FF>(P, Lb, 0, h, o, xo, cache, MaskedRec<WT>(tile, tile_ok ? 16 : 0, Rec::SIZE));
       } else {
         f4 gx[ET], ghi[ET];
         if (d == 1) {
@@ -550,14 +554,12 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
         __builtin_amdgcn_s_waitcnt(0);
 #endif
         T2O_MARK(1);
-        WT* rec = tile_ok ? static_cast<WT*>(args.tape) +
-                                ((size_t)d * ntiles + (size_t)step * tiles_per_step + rt) * Rec::SIZE * 16
-                          : nullptr;
         if constexpr (CHUNK)
-          agent_block_bwd_ch<E, H, NE, FF>(P, Lb, Gb, gs, rec, stage, 0, h, ObsRow{ob, F}, cache, gx, ghi, gbe, gWe,
-                                           ln2);
+          agent_block_bwd_ch<E, H, NE, FF>(P, Lb, Gb, gs, tile_ok ? tile : nullptr, stage, 0, h, ObsRow{ob, F}, cache,
+                                           gx, ghi, gbe, gWe, ln2);
         else
-          agent_block_bwd<E, H, NE, FF>(P, Lb, Gb, gs, rec, stage, 0, h, o, cache, gx, ghi, gbe, gWe, ln2);
+          agent_block_bwd_lean<E, H, NE, FF>(P, Lb, gs, MaskedRec<WT>(tile, tile_ok ? 16 : 0, Rec::SIZE), stage, 0, h,
+                                             o, cache, gx, ghi, gbe, gWe, ln2);
         if (d == 1) {
           xput(0, gx);
           xput(1, ghi);

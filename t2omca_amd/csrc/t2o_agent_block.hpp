@@ -20,26 +20,31 @@
 
 namespace t2o {
 
-template <int E, int H, int NE, int FF>
-struct AgentCache {
+template <int E, int H, int NE, int FF, bool LEAN>
+struct AgentCacheT {
   static constexpr int ET = E / 16, HET = H * ET;
-  PostCache<E, H, FF> post;
+  typename std::conditional<LEAN, PostCacheLean<E, H, FF>, PostCache<E, H, FF>>::type post;
   f4 u[HET];
   float p[H][NE + 1];
   f4 oh[H];
   float Ps[H];
 };
+template <int E, int H, int NE, int FF>
+using AgentCache = AgentCacheT<E, H, NE, FF, false>;
+// lean (PostCacheLean) cache of the two-wave pipelined BPTT: the record's X, Z, Y
+// fields are written by the recompute, which is the lighter of the two phases
+template <int E, int H, int NE, int FF>
+using AgentCacheLean = AgentCacheT<E, H, NE, FF, true>;
 
-// Forward of block d.  h: hidden token (layer-0 key 0), o: observations,
-// x: in = block input query, out = block output.
-template <int E, int H, int NE, int FF, bool CACHE, typename WT>
-T2O_DEV void agent_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* h,
-                             const f4 (&o)[NE], f4* x, AgentCache<E, H, NE, FF>* cache) {
+// Attention half of block d: u = M x, per head softmax over [h, entities] and
+// z_h = p0 h + We ô_h + P_h b_e.  Caches (u, p, ô, P) when C is non-null.
+template <int E, int H, int NE, int FF, bool LEAN, typename WT>
+T2O_DEV void agent_attn_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* h, const f4 (&o)[NE],
+                            const f4* x, f4* z, AgentCacheT<E, H, NE, FF, LEAN>* cache) {
   constexpr int ET = E / 16, HET = H * ET;
   const float* be = P.v + L.be;
   f4 u[HET];
   matvec<HET, ET>(P.w + L.M[d], E, x, u);
-  f4 z[HET];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
     float p[NE + 1];
@@ -87,38 +92,51 @@ T2O_DEV void agent_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const
     matvec<ET, 1>(P.w + L.We, 16, &oh, zz);
 #pragma unroll
     for (int t = 0; t < ET; ++t) z[hh * ET + t] = zz[t] + p[0] * h[t] + Ps * vec_t(be, t);
-    if constexpr (CACHE) {
+    if (cache) {
       cache->oh[hh] = oh;
       cache->Ps[hh] = Ps;
 #pragma unroll
       for (int j = 0; j <= NE; ++j) cache->p[hh][j] = p[j];
     }
   }
-  if constexpr (CACHE) {
+  if (cache) {
 #pragma unroll
     for (int t = 0; t < HET; ++t) cache->u[t] = u[t];
   }
+}
+
+// Forward of block d.  h: hidden token (layer-0 key 0), o: observations,
+// x: in = block input query, out = block output.
+template <int E, int H, int NE, int FF, bool CACHE, typename WT>
+T2O_DEV void agent_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* h,
+                             const f4 (&o)[NE], f4* x, AgentCache<E, H, NE, FF>* cache) {
+  constexpr int HET = H * (E / 16);
+  f4 z[HET];
+  agent_attn_fwd<E, H, NE, FF, false>(P, L, d, h, o, x, z, CACHE ? cache : nullptr);
   T2O_MARK(2);
   post_fwd<E, H, FF, CACHE>(P, L, d, z, x, CACHE ? &cache->post : nullptr);
 }
 
-// Backward of block d.  gx: in = grad wrt block output, out = grad wrt block
-// input (query path).  gh_in accumulates the grad wrt h through the key/value
-// path (token 0); gbe the grad wrt the embedding bias; gWe (MFMA register
-// block, [E][16] as ET x 1 tiles) the grad wrt the embedding weight.  M's
-// operand pair goes to the tape record (t2o_common.hpp TapeRec).
 template <int E, int H, int NE, int FF, typename WT>
-T2O_DEV void agent_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G,
-                             float* __restrict__ gs, WT* __restrict__ rec, float* __restrict__ stage, int d,
-                             const f4* h, const f4 (&o)[NE], const AgentCache<E, H, NE, FF>& c, f4* gx,
-                             f4* gh_in, f4* gbe, f4 (&gWe)[E / 16][1], f4* ln2) {
-  constexpr int ET = E / 16, HET = H * ET;
+T2O_DEV void agent_block_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d, const f4* h, const f4 (&o)[NE],
+                                  f4* x, AgentCacheLean<E, H, NE, FF>& cache, const MaskedRec<WT>& rec) {
+  constexpr int HET = H * (E / 16);
+  f4 z[HET];
+  agent_attn_fwd<E, H, NE, FF, true>(P, L, d, h, o, x, z, &cache);
+  post_fwd_lean<E, H, FF>(P, L, d, z, x, &cache.post, rec);
+}
+
+// Attention half of the backward: from gz (grad wrt z) to gu (grad wrt u = M x);
+// gh_in accumulates the grad wrt h through the key/value path (token 0), gbe the
+// grad wrt the embedding bias, gWe (MFMA register block, [E][16] as ET x 1 tiles)
+// the grad wrt the embedding weight.
+template <int E, int H, int NE, int FF, bool LEAN, typename WT>
+T2O_DEV void agent_attn_bwd(const Wts<WT>& P, const t2o_layout& L, float* __restrict__ stage, const f4* h,
+                            const f4 (&o)[NE], const AgentCacheT<E, H, NE, FF, LEAN>& c, const f4* gz, f4* gu,
+                            f4* gh_in, f4* gbe, f4 (&gWe)[E / 16][1]) {
+  constexpr int ET = E / 16;
   constexpr bool BF = sizeof(WT) == 2;
   const float* be = P.v + L.be;
-  f4 gz[HET], gres[ET];
-  post_bwd<E, H, FF>(P, L, G, gs, rec, d, c.post, gx, gz, gres, ln2);
-  T2O_MARK(2);
-  f4 gu[HET];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
     const f4* gzh = &gz[hh * ET];
@@ -173,11 +191,44 @@ T2O_DEV void agent_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_la
     }
     dw_accumulate_regs<ET, 1, BF>(gWe, uh, &gw, stage);
   }
+}
+
+// Backward of block d.  gx: in = grad wrt block output, out = grad wrt block
+// input (query path).  M's operand pair goes to the tape record (t2o_common.hpp
+// TapeRec).
+template <int E, int H, int NE, int FF, typename WT>
+T2O_DEV void agent_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G,
+                             float* __restrict__ gs, WT* __restrict__ rec, float* __restrict__ stage, int d,
+                             const f4* h, const f4 (&o)[NE], const AgentCache<E, H, NE, FF>& c, f4* gx,
+                             f4* gh_in, f4* gbe, f4 (&gWe)[E / 16][1], f4* ln2) {
+  constexpr int ET = E / 16, HET = H * ET;
+  f4 gz[HET], gres[ET];
+  post_bwd<E, H, FF>(P, L, G, gs, rec, d, c.post, gx, gz, gres, ln2);
+  T2O_MARK(2);
+  f4 gu[HET];
+  agent_attn_bwd<E, H, NE, FF, false>(P, L, stage, h, o, c, gz, gu, gh_in, gbe, gWe);
   // u = M x
   if (rec) {
     rec_store<TapeRec<E, H, FF>::SIZE, HET>(rec, TapeRec<E, H, FF>::GU, gu);
     rec_store<TapeRec<E, H, FF>::SIZE, ET>(rec, TapeRec<E, H, FF>::X, c.post.x);
   }
+  f4 gxp[ET];
+  matvec_tr<ET, HET>(P, L.M[d], E, L.MT[d], H * E, gu, gxp);
+#pragma unroll
+  for (int t = 0; t < ET; ++t) gx[t] = gxp[t] + gres[t];
+}
+
+template <int E, int H, int NE, int FF, typename WT>
+T2O_DEV void agent_block_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restrict__ gs,
+                                  const MaskedRec<WT>& rec, float* __restrict__ stage, int d, const f4* h,
+                                  const f4 (&o)[NE], const AgentCacheLean<E, H, NE, FF>& c, f4* gx, f4* gh_in,
+                                  f4* gbe, f4 (&gWe)[E / 16][1], f4* ln2) {
+  constexpr int ET = E / 16, HET = H * ET;
+  f4 gz[HET], gres[ET];
+  post_bwd_lean<E, H, FF>(P, L, gs, rec, d, c.post, gx, gz, gres, ln2);
+  f4 gu[HET];
+  agent_attn_bwd<E, H, NE, FF, true>(P, L, stage, h, o, c, gz, gu, gh_in, gbe, gWe);
+  rec.template store<HET>(TapeRec<E, H, FF>::GU, gu);
   f4 gxp[ET];
   matvec_tr<ET, HET>(P, L.M[d], E, L.MT[d], H * E, gu, gxp);
 #pragma unroll

@@ -605,7 +605,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
             MixerCacheLean<E, H, KT, FF> cache;  // whole 16-record tiles (padding records: zero grads)
             const MaskedRec<WT> rec(tile, RT, Rec::SIZE);
             mixer_block_fwd_lean<E, H, KT, FF>(P, L, d, K, Dm::LK, x, cache, rec);
-            mixer_block_bwd_lean<E, H, KT, FF>(P, L, gs, rec, stage, d, K, gX0, cache, gx, ln2[d]);
+            mixer_block_bwd_lean<E, H, KT, FF>(P, L, gs, rec, stage, d, K, Dm::LK, gX0, cache, gx, ln2[d]);
           }
           __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -948,7 +948,7 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
       for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft) gX0[kt][ft] = zero4();
-      mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, gX0, cache, gx, ln2);
+      mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, Dm::LK, gX0, cache, gx, ln2);
       __builtin_amdgcn_wave_barrier();
       // hand-over to the block-0 wave
 #pragma unroll
@@ -1027,7 +1027,7 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) gx[ft] = c < Dm::Q ? ld4(R + Pd::XCH + c * E + 16 * ft + 4 * g) : zero4();
       __builtin_amdgcn_wave_barrier();
-      mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, gX0, cache, gx, ln2);
+      mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, Dm::LK, gX0, cache, gx, ln2);
       // state embedding grads from the key-grad registers (as mixer_bwd_kernel)
 #pragma unroll
       for (int s = 0; s < Dm::ST; ++s)

@@ -190,14 +190,45 @@ T2O_DEV void mixer_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_la
 }
 
 // Lean cache (PostCacheLean) versions for the two-wave pipelined backward:
-// the forward recompute writes the record's X, Z, Y fields itself.
+// the forward recompute writes the record's X, Z, Y fields itself.  With many
+// key tiles (KT > 4: 64 agents) the attention probabilities are not cached but
+// recomputed from u in the backward (KT MFMAs per head against 12·KT registers
+// per head held across the post-attention backward).
 template <int E, int H, int KT, int FF>
 struct MixerCacheLean {
   static constexpr int ET = E / 16, HET = H * ET;
+  static constexpr bool PC = KT <= 4;
   PostCacheLean<E, H, FF> post;
   f4 u[HET];
-  f4 p[H][KT];
+  f4 p[PC ? H : 1][PC ? KT : 1];
 };
+
+// softmax over the Lk valid keys of one head's scores: s[kt] (keys 16kt+4g+r, query c)
+template <int E, int KT, bool BF>
+T2O_DEV void attn_probs(const KeyFrags<E, KT, BF>& K, const f4* u, int Lk, f4* s) {
+  const int g = lane_g();
+  keys_dot<E, KT, BF>(K, u, s);
+  float m = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (16 * kt + 4 * g + r >= Lk) s[kt][r] = -INFINITY;
+      m = fmaxf(m, s[kt][r]);
+    }
+  m = allmax4(m);
+  float l = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s[kt][r] = exp_fast(s[kt][r] - m);
+      l += s[kt][r];
+    }
+  const float il = rcp_fast(allsum4(l));
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) s[kt] *= il;
+}
 
 template <int E, int H, int KT, int FF, typename WT>
 T2O_DEV void mixer_block_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d,
@@ -205,35 +236,15 @@ T2O_DEV void mixer_block_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d,
                                   MixerCacheLean<E, H, KT, FF>& cache, const MaskedRec<WT>& rec) {
   constexpr int ET = E / 16, HET = H * ET;
   constexpr bool BF = sizeof(WT) == 2;
-  const int g = lane_g();
   matvec<HET, ET>(P.w + L.M[d], E, x, cache.u);
   f4 z[HET];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
     f4 s[KT];
-    keys_dot<E, KT, BF>(K, &cache.u[hh * ET], s);
-    float m = -INFINITY;
+    attn_probs<E, KT, BF>(K, &cache.u[hh * ET], Lk, s);
+    if constexpr (MixerCacheLean<E, H, KT, FF>::PC) {
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (16 * kt + 4 * g + r >= Lk) s[kt][r] = -INFINITY;
-        m = fmaxf(m, s[kt][r]);
-      }
-    m = allmax4(m);
-    float l = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < KT; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        s[kt][r] = exp_fast(s[kt][r] - m);
-        l += s[kt][r];
-      }
-    const float il = rcp_fast(allsum4(l));
-#pragma unroll
-    for (int kt = 0; kt < KT; ++kt) {
-      s[kt] *= il;
-      cache.p[hh][kt] = s[kt];
+      for (int kt = 0; kt < KT; ++kt) cache.p[hh][kt] = s[kt];
     }
     keys_combine<E, KT, BF>(K, s, &z[hh * ET]);
   }
@@ -243,7 +254,7 @@ T2O_DEV void mixer_block_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d,
 template <int E, int H, int KT, int FF, typename WT>
 T2O_DEV void mixer_block_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restrict__ gs,
                                   const MaskedRec<WT>& rec, float* __restrict__ stage, int d,
-                                  const KeyFrags<E, KT, sizeof(WT) == 2>& K, f4 (&gX0)[KT][E / 16],
+                                  const KeyFrags<E, KT, sizeof(WT) == 2>& K, int Lk, f4 (&gX0)[KT][E / 16],
                                   const MixerCacheLean<E, H, KT, FF>& c, f4* gx, f4* ln2) {
   constexpr int ET = E / 16, HET = H * ET;
   constexpr bool BF = sizeof(WT) == 2;
@@ -252,19 +263,26 @@ T2O_DEV void mixer_block_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* 
   f4 gu[HET];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
+    f4 p[KT];
+    if constexpr (MixerCacheLean<E, H, KT, FF>::PC) {
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) p[kt] = c.p[hh][kt];
+    } else {
+      attn_probs<E, KT, BF>(K, &c.u[hh * ET], Lk, p);
+    }
     f4 gp[KT];
     keys_dot<E, KT, BF>(K, &gz[hh * ET], gp);
     float dot = 0.f;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) dot += c.p[hh][kt][r] * gp[kt][r];
+      for (int r = 0; r < 4; ++r) dot += p[kt][r] * gp[kt][r];
     dot = allsum4(dot);
     f4 gsc[KT];
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) gsc[kt] = c.p[hh][kt] * (gp[kt] - dot);
+    for (int kt = 0; kt < KT; ++kt) gsc[kt] = p[kt] * (gp[kt] - dot);
     keys_combine<E, KT, BF>(K, gsc, &gu[hh * ET]);
-    dw_accumulate_regs<KT, ET, BF>(gX0, c.p[hh], &gz[hh * ET], stage);
+    dw_accumulate_regs<KT, ET, BF>(gX0, p, &gz[hh * ET], stage);
     dw_accumulate_regs<KT, ET, BF>(gX0, gsc, &c.u[hh * ET], stage);
   }
   rec.template store<HET>(TapeRec<E, H, FF>::GU, gu);
