@@ -450,8 +450,7 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
   // barrier"; the block-0 wave starts one barrier late, so its recompute of a
   // step overlaps the block-1 backward of the same step and its backward the
   // block-1 recompute of the next (earlier) one.  The cache lives within one
-  // iteration.  (Loading the next step's inputs a phase ahead measured no
-  // faster: the loads' latency is not on the barrier-paced critical path.)
+  // iteration.
   auto load_fwd_inputs = [&](int step, f4* hh, f4 (&oo)[NO], f4* xx) {
     const float* hp = step == 0 ? (args.h0 ? args.h0 + (size_t)row * E : nullptr)
                                 : args.h_seq + (((size_t)b * args.h_ts + step - 1) * A + a) * E;
@@ -467,27 +466,24 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
           oo[j][r] = f < F ? obp[j * F + f] : 0.f;
         }
     }
-    if (d == 0) {
-#pragma unroll
-      for (int t = 0; t < ET; ++t) xx[t] = hh[t];
-    } else {
+    if (d == 1) {  // (block 0's input is h itself: copied where used, never here —
+                   // touching a register with a load in flight waits for it)
       const float* hm = args.hmid + (((size_t)b * args.h_ts + step) * (D - 1) * A + a) * E;
 #pragma unroll
       for (int t = 0; t < ET; ++t) xx[t] = ld4(hm + 16 * t + 4 * g);
     }
   };
-  if (d == 0) __syncthreads();
-  for (int step = T - 1; step >= 0; --step) {
-#ifdef T2O_TIMELINE
-    T2O_STAMP(2 * (T - 1 - step), 0);
-#endif
-    Cache cache;
-    f4 h[ET], o[NO], xo[ET];
+  // A step's inputs are loaded at the end of the previous (later) step's
+  // backward phase, after its last use of them: the loads are then in flight
+  // through the barrier wait instead of stalling the start of the recompute.
+  // The block-1 wave's output grads (dL/dh_t from the mixer, dL/dq_t; the
+  // recurrent part of dL/dh_t comes from block 0) are loaded raw with them and
+  // combined where the backward uses them.
+  f4 h[ET], o[NO], xo[ET], ghx[ET], gqv = zero4();
+  float gc = 0.f;
+  int64_t act = -1;
+  auto load_step = [&](int step) {
     load_fwd_inputs(step, h, o, xo);
-    const float* ob = args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * NE * F;
-    // this step's grads arriving at the stack output (block-1 wave): dL/dh_t from
-    // the mixer and dL/dq_t (the recurrent part of dL/dh_t comes from block 0)
-    f4 ghx[ET], gq = zero4();
     if (d == 1) {
       const size_t sidx = ((size_t)b * T + step) * A + a;
 #pragma unroll
@@ -495,16 +491,22 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
       if (args.gq) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          if (4 * g + r < L.NA) gq[r] = args.gq[sidx * L.NA + 4 * g + r];
+          if (4 * g + r < L.NA) gqv[r] = args.gq[sidx * L.NA + 4 * g + r];
       }
       if (args.gchosen) {
-        const int64_t act = args.actions[b * args.act_sb + step * args.act_st + a];
-        const float gc = args.gchosen[sidx];
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (4 * g + r == act) gq[r] += gc;
+        act = args.actions[b * args.act_sb + step * args.act_st + a];
+        gc = args.gchosen[sidx];
       }
     }
+  };
+  load_step(T - 1);
+  if (d == 0) __syncthreads();
+  for (int step = T - 1; step >= 0; --step) {
+#ifdef T2O_TIMELINE
+    T2O_STAMP(2 * (T - 1 - step), 0);
+#endif
+    Cache cache;
+    const float* ob = args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * NE * F;
 #pragma unroll
     for (int ph = 0; ph < 2; ++ph) {
       T2O_MARK(0);
@@ -519,11 +521,19 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
         __builtin_amdgcn_s_waitcnt(0);
 #endif
         T2O_MARK(1);
+        if (d == 0) {
+#pragma unroll
+          for (int t = 0; t < ET; ++t) xo[t] = h[t];
+        }
         if constexpr (CHUNK) agent_block_fwd_ch<E, H, NE, FF, true>(P, Lb, 0, h, ObsRow{ob, F}, xo, &cache);
         else agent_block_fwd_lean<E, H, NE, FF>(P, Lb, 0, h, o, xo, cache, MaskedRec<WT>(tile, tile_ok ? 16 : 0, Rec::SIZE));
       } else {
         f4 gx[ET], ghi[ET];
         if (d == 1) {
+          f4 gq = gqv;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (4 * g + r == act) gq[r] += gc;
           if (step < T - 1) xget(2, gx);
           else {
 #pragma unroll
@@ -573,6 +583,7 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
             for (int t = 0; t < ET; ++t) st4(args.gh0 + (size_t)row * E + 16 * t + 4 * g, grec[t]);
           }
         }
+        if (step > 0) load_step(step - 1);
       }
       T2O_MARK(3);
 #ifdef T2O_TIMELINE

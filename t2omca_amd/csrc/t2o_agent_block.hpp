@@ -123,6 +123,7 @@ T2O_DEV void agent_block_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d, 
   constexpr int HET = H * (E / 16);
   f4 z[HET];
   agent_attn_fwd<E, H, NE, FF, true>(P, L, d, h, o, x, z, &cache);
+  T2O_MARK(2);
   post_fwd_lean<E, H, FF>(P, L, d, z, x, &cache.post, rec);
 }
 
@@ -154,7 +155,9 @@ T2O_DEV void agent_attn_bwd(const Wts<WT>& P, const t2o_layout& L, float* __rest
     }
     f4 goh;
     matvec_tr<1, ET>(P, L.We, 16, L.WeT, E, gzh, &goh);
+#ifndef T2O_ABL_NODW  // ablation builds only: wrong gradients
     dw_accumulate_regs<ET, 1, BF>(gWe, gzh, &c.oh[hh], stage);
+#endif
     // softmax backward over [token 0, entities]; [gP, gp_0, goh·o_j] reduced in one batch
     float red[NE + 2];
     red[0] = gPp;
@@ -189,7 +192,9 @@ T2O_DEV void agent_attn_bwd(const Wts<WT>& P, const t2o_layout& L, float* __rest
       gh_in[t] += gs0 * uh[t];
       gbe[t] += gc * uh[t];
     }
+#ifndef T2O_ABL_NODW
     dw_accumulate_regs<ET, 1, BF>(gWe, uh, &gw, stage);
+#endif
   }
 }
 
@@ -226,6 +231,7 @@ T2O_DEV void agent_block_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* 
   constexpr int ET = E / 16, HET = H * ET;
   f4 gz[HET], gres[ET];
   post_bwd_lean<E, H, FF>(P, L, gs, rec, d, c.post, gx, gz, gres, ln2);
+  T2O_MARK(2);
   f4 gu[HET];
   agent_attn_bwd<E, H, NE, FF, true>(P, L, stage, h, o, c, gz, gu, gh_in, gbe, gWe);
   rec.template store<HET>(TapeRec<E, H, FF>::GU, gu);
