@@ -96,6 +96,7 @@ struct MixIn {
   f4 st[Dm::ST];
   f4 hid[HV];
   float qs[MIX_MAXNA], qa[MIX_MAXNA];
+  int av[MIX_MAXNA];
   int act;
 };
 
@@ -103,71 +104,65 @@ template <int E, int A>
 T2O_DEV void mix_load(const MixerFwdArgs& a, const MixerNet& n, int b, int t, MixIn<E, A>& in) {
   using Dm = MixDims<E, A>;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
+  // Every load is unconditional (in-bounds duplicates for padding lanes / rows /
+  // action slots) and its register is left alone until the step that uses it:
+  // a select right after a load would wait for it — and, the vector-memory
+  // counter being in order, for every store issued before it — defeating the
+  // prefetch.  Padding is harmless where it lands: state features past Fs meet
+  // the zero-padded embedding columns, rows past NS / hidden lanes past A·E/4
+  // are never stored (mix_keys), action slots past NA are masked in mix_qv.
   const float* st = a.states + b * a.st_sb + t * a.st_st;
 #pragma unroll
   for (int s = 0; s < Dm::ST; ++s) {
-    const int j = 16 * s + c;
+    const int j = min(16 * s + c, Dm::NS - 1);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int f = 4 * g + r;
-      in.st[s][r] = ld_or0(st, j * a.Fs + f, j < Dm::NS && f < a.Fs);
-    }
+    for (int r = 0; r < 4; ++r) in.st[s][r] = st[j * a.Fs + min(4 * g + r, a.Fs - 1)];
   }
   const float* hd = n.hid + b * n.hid_sb + t * n.hid_st;
 #pragma unroll
-  for (int k = 0; k < MixIn<E, A>::HV; ++k) {
-    const int i = lane + 64 * k;
-    in.hid[k] = i < A * E / 4 ? ld4(hd + 4 * i) : zero4();
-  }
-  // per-agent inputs, lane a < A holds agent a's; branch-free: lanes >= A and
-  // action slots >= NA load an in-bounds duplicate and discard it (selects, not
-  // exec-masked loads — this runs every step on the recurrence's critical path)
+  for (int k = 0; k < MixIn<E, A>::HV; ++k) in.hid[k] = ld4(hd + 4 * min(lane + 64 * k, A * E / 4 - 1));
+  // per-agent inputs, lane a < A holds agent a's.  No branch on the Q-selection
+  // mode either (a branch makes the loop-carried registers phis, and the
+  // compiler then copies them — waiting for the loads — right after issuing):
+  // fields a mode does not use load an in-bounds dummy.
   const int la = lane < A ? lane : A - 1;
-  if (n.qmode == 0) {
-    in.qs[0] = n.qv_in[((size_t)b * n.T + t) * A + la];
-  } else {
-    const int NA = a.n_actions;
-    const size_t qrow = (((size_t)b * a.q_ts + t) * A + la) * NA;
+  const int NA = a.n_actions > 0 ? a.n_actions : 1;
+  const bool q0 = n.qmode == 0;
+  const size_t qrow = q0 ? ((size_t)b * n.T + t) * A + la : (((size_t)b * a.q_ts + t) * A + la) * NA;
+  const float* qsrc = q0 ? n.qv_in : n.qsel;
 #pragma unroll
-    for (int k = 0; k < MIX_MAXNA; ++k) {
-      const float v = n.qsel[qrow + (k < NA ? k : NA - 1)];
-      in.qs[k] = k < NA ? v : 0.f;
-    }
-    if (n.qmode == 1) {
-      in.act = (int)a.actions[b * a.act_sb + t * a.act_st + la];
-    } else if (a.avail) {
-      const int32_t* av = a.avail + b * a.av_sb + t * a.av_st + la * NA;
+  for (int k = 0; k < MIX_MAXNA; ++k) in.qs[k] = qsrc[qrow + (q0 ? 0 : (k < NA ? k : NA - 1))];
+  const bool q2 = n.qmode == 2, q1 = n.qmode == 1;
+  const float* qa = q2 ? a.qarg + qrow : qsrc + qrow;
 #pragma unroll
-      for (int k = 0; k < MIX_MAXNA; ++k) {
-        const int kk = k < NA ? k : NA - 1;
-        const float q = a.qarg[qrow + kk];
-        const int ok = av[kk];
-        in.qa[k] = k < NA ? (ok == 0 ? -9999999.0f : q) : -INFINITY;
-      }
-    } else {
+  for (int k = 0; k < MIX_MAXNA; ++k) in.qa[k] = qa[q2 ? (k < NA ? k : NA - 1) : 0];
+  const int32_t* av = (q2 && a.avail) ? a.avail + b * a.av_sb + t * a.av_st + la * NA
+                                      : reinterpret_cast<const int32_t*>(qsrc + qrow);
 #pragma unroll
-      for (int k = 0; k < MIX_MAXNA; ++k) {
-        const float q = a.qarg[qrow + (k < NA ? k : NA - 1)];
-        in.qa[k] = k < NA ? q : -INFINITY;
-      }
-    }
-  }
+  for (int k = 0; k < MIX_MAXNA; ++k) in.av[k] = av[(q2 && a.avail) ? (k < NA ? k : NA - 1) : 0];
+  const int32_t* ap = q1 ? reinterpret_cast<const int32_t*>(a.actions + b * a.act_sb + t * a.act_st + la)
+                         : reinterpret_cast<const int32_t*>(qsrc + qrow);
+  in.act = *ap;  // (low word of the int64 action)
 }
 
 // This lane's agent's mixer input (lane a < A): chosen-action Q (qmode 1) or
 // the target Q at the avail-masked online argmax (qmode 2, first max wins).
 template <int E, int A>
-T2O_DEV float mix_qv(const MixerNet& n, const MixIn<E, A>& in) {
+T2O_DEV float mix_qv(const MixerNet& n, const MixIn<E, A>& in, int NA, bool avail) {
   if (n.qmode == 0) return in.qs[0];
   int act = 0;
   if (n.qmode == 1) {
     act = in.act;
   } else {
-    float best = in.qa[0];
+    float qa[MIX_MAXNA];
+#pragma unroll
+    for (int k = 0; k < MIX_MAXNA; ++k)
+      qa[k] = k < NA ? (avail && in.av[k] == 0 ? -9999999.0f : in.qa[k]) : -INFINITY;
+    float best = qa[0];
 #pragma unroll
     for (int k = 1; k < MIX_MAXNA; ++k)
-      if (in.qa[k] > best) {
-        best = in.qa[k];
+      if (qa[k] > best) {
+        best = qa[k];
         act = k;
       }
   }
@@ -267,7 +262,8 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
     T2O_MARK(0);
     const Wts<WT> P = step_view(P0);
     mix_keys<E, A>(P, L, in, X0);
-    const float myq = mix_qv<E, A>(n, in);
+    const float myq = mix_qv<E, A>(n, in, args.n_actions, args.avail != nullptr);
+    __builtin_amdgcn_sched_barrier(0);  // every read of this step's inputs issued before they are reloaded
     if (t + 1 < n.T) mix_load<E, A>(args, n, b, t + 1, in);  // prefetch step t+1 (in is consumed)
     __builtin_amdgcn_wave_barrier();
     KeyFrags<E, Dm::KT, sizeof(WT) == 2> K;
