@@ -517,7 +517,7 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
       WT* const tile = static_cast<WT*>(args.tape) +
                        ((size_t)d * ntiles + (size_t)step * tiles_per_step + rt) * Rec::SIZE * 16;
       if (ph == 0) {
-#ifdef T2O_PHASE_PROF
+#if defined(T2O_PHASE_PROF) && !defined(T2O_TIMELINE)  // (timelines: no forced drain)
         __builtin_amdgcn_s_waitcnt(0);
 #endif
         T2O_MARK(1);
@@ -560,7 +560,7 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
           xget(0, gx);
           xget(1, ghi);
         }
-#ifdef T2O_PHASE_PROF
+#if defined(T2O_PHASE_PROF) && !defined(T2O_TIMELINE)  // (timelines: no forced drain)
         __builtin_amdgcn_s_waitcnt(0);
 #endif
         T2O_MARK(1);
