@@ -18,7 +18,11 @@ SHORT = {"agent_fwd_kernel": "agent_fwd", "mixer_fwd_kernel": "mixer_fwd", "mixe
          "env_kernel": "env_step", "reduce_slabs_kernel": "reduce_slabs", "seg_kernel": "pack"}
 
 
-def per_kernel(d, counter):
+def _is_bf16(name):
+    return "DF16b" in name or "__bf16" in name
+
+
+def per_kernel(d, counter, want_bf16=None):
     vals = {}
     for path in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as f:
@@ -26,6 +30,8 @@ def per_kernel(d, counter):
                 if row.get("Counter_Name") != counter:
                     continue
                 name = row["Kernel_Name"]
+                if want_bf16 is not None and _is_bf16(name) != want_bf16:
+                    continue  # the other operand type's instance (e.g. an fp32 companion run)
                 m = re.search(r"dw_gemm_kernel(?:<\d+, *\d+, *\d+, *\d+, *|ILi\d+ELi\d+ELi\d+ELi\d+ELi)(\d)", name)
                 short = ("agent_dw", "mixer_dw")[int(m.group(1))] if m else \
                     next((v for k, v in SHORT.items() if k in name), None)
@@ -38,7 +44,8 @@ def per_kernel(d, counter):
 def main():
     fdir, wdir, out = sys.argv[1:4]
     tag = sys.argv[4] if len(sys.argv) > 4 else ""
-    fetch, write = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
+    want = True if tag.endswith("_bf16") else False if tag.endswith("_fp32") else None
+    fetch, write = per_kernel(fdir, "FETCH_SIZE", want), per_kernel(wdir, "WRITE_SIZE", want)
     res = {"workload": tag, "units": "bytes per launch (FETCH_SIZE x2 x1024, WRITE_SIZE x1024)", "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f = fetch.get(k, [])

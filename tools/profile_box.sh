@@ -11,11 +11,11 @@ mkdir -p "$OUT"
 cd /tmp
 export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run \
-  -- python3 "$R/bench.py" --no-cpu-baseline "$@" > "$OUT/trace.log" 2>&1
+  -- python3 "$R/bench.py" --no-cpu-baseline --no-fp32-companion "$@" > "$OUT/trace.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run \
-  -- python3 "$R/bench.py" --no-cpu-baseline --steps 3 --warmup 1 "$@" > "$OUT/fetch.log" 2>&1
+  -- python3 "$R/bench.py" --no-cpu-baseline --no-fp32-companion --steps 3 --warmup 1 "$@" > "$OUT/fetch.log" 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run \
-  -- python3 "$R/bench.py" --no-cpu-baseline --steps 3 --warmup 1 "$@" > "$OUT/write.log" 2>&1
+  -- python3 "$R/bench.py" --no-cpu-baseline --no-fp32-companion --steps 3 --warmup 1 "$@" > "$OUT/write.log" 2>&1
 python3 "$R/tools/pmc_traffic.py" "$OUT/fetch" "$OUT/write" "$OUT/hbm_traffic.json" \
   "$(python3 "$R/bench.py" --print-workload-tag "$@")" > /dev/null
 find "$OUT/trace" -name '*kernel_stats.csv' -exec cp {} "$OUT/kernel_stats.csv" \;
