@@ -204,9 +204,8 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const t2o_layout& L = args.L;
   const t2o_layout& G = args.G;
-  // fp32 reads the forward matrices transposed in place; bf16 stages the
-  // whole pack (its transposed copies included)
-  const int64_t nw = sizeof(WT) == 4 ? L.fwd_total : L.total;
+  // the forward section of the pack; transposed products read it transposed (matvec_tr)
+  const int64_t nw = L.fwd_total;
   const int lds_w = (int)((lds_weight_floats<WT>(L, nw) + 15) / 16 * 16);
   float* stage = smem + lds_w + wave_id() * STAGE;
   float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
@@ -396,7 +395,7 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const t2o_layout& L = args.L;
   const t2o_layout& G = args.G;
-  const int64_t nw = sizeof(WT) == 4 ? L.fwd_total : L.total;
+  const int64_t nw = L.fwd_total;
   const int lds_w = (int)((lds_weight_floats<WT>(L, nw) + 15) / 16 * 16);
   // wave-uniform by construction; readfirstlane tells the compiler, so the block's
   // layout offsets (L.M[d] ...) are scalar loads, not per-lane global loads
@@ -613,7 +612,7 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
 
 template <int E, int H, int D, int NE, int FF, typename WT>
 size_t bwd_pipe_lds_bytes(const t2o_layout& L) {
-  const int64_t nw = sizeof(WT) == 4 ? L.fwd_total : L.total;
+  const int64_t nw = L.fwd_total;
   return sizeof(float) * ((size_t)(lds_weight_floats<WT>(L, nw) + 15) / 16 * 16 +
                           2 * AGP_TILES * StageDims<1>::FLOATS + AGP_TILES * agp_xch_floats<E>());
 }
@@ -635,7 +634,7 @@ int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream
       return (int)hipGetLastError();
     }
   }
-  const int64_t nw = sizeof(WT) == 4 ? args.L.fwd_total : args.L.total;
+  const int64_t nw = args.L.fwd_total;
   const size_t lds =
       sizeof(float) * ((size_t)(lds_weight_floats<WT>(args.L, nw) + 15) / 16 * 16 + AG_BWD_WAVES * StageDims<1>::FLOATS);
   auto kern = agent_bwd_kernel<E, H, D, NE, FF, WT>;

@@ -175,7 +175,10 @@ T2O_DEV f4 mfma_b32(bf4 a0, bf4 a1, bf4 b0, bf4 b1, f4 acc) {
 // image stores element (r, col) at r*ld + (col ^ bf_swz(r, ld)) — an XOR of
 // whole 8-element groups, so the 4 (or 8) consecutive K values a lane loads
 // stay contiguous — and the readers apply the same XOR.  Only the row's lane
-// index c matters: bf_swz(16o + c, ld) == bf_swz(c, ld).
+// index c matters: bf_swz(16o + c, ld) == bf_swz(c, ld).  (The transposed reads
+// of matvec_tr see 2-way conflicts on 64-B-periodic rows with this XOR; an XOR
+// that frees both read kinds measured 20 more spilled registers in the mixer's
+// pipelined BPTT, whose address registers it multiplies.)
 __host__ __device__ inline int bf_swz(int row, int ld) {
   return ld % 32 == 0 ? 8 * ((row >> 2) & 3) : 8 * ((row >> 3) & 1);
 }
@@ -211,18 +214,57 @@ template <typename WT>
 struct Wts {
   const WT* w;
   const float* v;
+  // bf16: transposed products read the forward image transposed from LDS
+  // (ds_read_b64_tr_b16) — else the pack's transposed copies (global memory, or
+  // an LDS copy that includes them)
+  bool tr;
   T2O_DEV float s(int64_t off) const { return (float)w[off]; }  // row 0 of a matrix (unswizzled row)
 };
 
-// y = Wᵀ x: fp32 reads W transposed in place (matvec_t); bf16 uses the pack's
-// transposed copy WT [16*OT rows][ldT] with the plain product.
+// y = Wᵀ x.  fp32 reads W transposed in place (matvec_t).  bf16 from LDS reads
+// the forward image transposed with ds_read_b64_tr_b16: the A fragment of
+// output tile o, K tile i is Wᵀ[16o + c][16i + 4g .. +3] = W[16i + 4g .. +3][16o + c],
+// i.e. column 16o + c of the 4 rows 16i + 4g + q — exactly what the transposed
+// read delivers to lane c of group g when lane 4q + p addresses row 16i + 4g + q,
+// columns 16o + 4p .. +3.  The same bf16 values as the pack's transposed copy
+// and the same K pairing, so the product is bit-identical to reading WT
+// (which bf16 weights read through L2 still do).
 template <int OT, int IT>
 T2O_DEV void matvec_tr(const Wts<float>& P, int64_t off, int ld, int64_t offT, int ldT, const f4* x, f4* y);
+T2O_DEV bf4 ld_tr_b16(const __bf16* p) {
+  typedef __attribute__((address_space(3))) s4v lds_s4v;
+  return __builtin_bit_cast(bf4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(p)));
+}
 template <int OT, int IT>
 T2O_DEV void matvec_tr(const Wts<__bf16>& P, int64_t off, int ld, int64_t offT, int ldT, const f4* x, f4* y) {
-  (void)off;
-  (void)ld;
-  matvec<OT, IT>(P.w + offT, ldT, x, y);
+  if (!P.tr) {
+    matvec<OT, IT>(P.w + offT, ldT, x, y);
+    return;
+  }
+  // the lane's row q = 4g + (c >> 2) within a 16-row K tile and its column
+  // offset, derived per product from an opaque lane id: hoisted out of the step
+  // loop they would keep one register per matrix live
+  int l = threadIdx.x;
+  asm volatile("" : "+v"(l));
+  const int c = l & 15, q = ((l >> 2) & 12) | (c >> 2);
+  const int sw = bf_swz(q, ld);
+  const __bf16* W = P.w + off + q * ld + ((4 * (c & 3)) ^ sw);
+  const int xs16 = sw & 16;  // the swizzle's tile bit: odd output tiles read the other half
+  bf4 xb[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) xb[i] = to_bf4(x[i]);
+#pragma unroll
+  for (int o = 0; o < OT; ++o) {
+    // (16o + 4p) ^ s = 4p ^ s + 16o, except that the tile bit of s flips o's lowest bit
+    const int col = xs16 ? 16 * (o ^ 1) - 16 : 16 * o;
+    f4 acc = zero4();
+#pragma unroll
+    for (int i = 0; i + 1 < IT; i += 2)
+      acc = mfma_b32(ld_tr_b16(W + (size_t)16 * i * ld + col), ld_tr_b16(W + (size_t)16 * (i + 1) * ld + col), xb[i],
+                     xb[i + 1], acc);
+    if constexpr (IT & 1) acc = mfma_b16(ld_tr_b16(W + (size_t)16 * (IT - 1) * ld + col), xb[IT - 1], acc);
+    y[o] = acc;
+  }
 }
 
 // Weights staged in LDS are invariant across a kernel's step loop, so LICM
@@ -238,7 +280,7 @@ template <typename WT>
 T2O_DEV Wts<WT> step_view(const Wts<WT>& p) {
   int off = 0;
   asm volatile("" : "+s"(off));
-  return Wts<WT>{p.w + off, p.v + off};
+  return Wts<WT>{p.w + off, p.v + off, p.tr};
 }
 
 template <int OT, int IT>
@@ -435,20 +477,25 @@ T2O_DEV void copy_to_lds(float* __restrict__ dst, const float* __restrict__ src,
 // fp32: the first n elements of the pack, copied as is.  bf16: the bf16 image of
 // the first n elements (matrices; vector slots ride along unused) followed by
 // the fp32 vector range [vec_lo, fwd_total).  Vectors are addressed with the
-// pack's own offsets through a shifted base.
-T2O_DEV Wts<float> stage_weights(float* smem, const float* pack, const t2o_layout& L, int64_t n, float) {
+// pack's own offsets through a shifted base.  bf16: tr_reads (a compile-time
+// constant at every call) — transposed products read the forward section
+// transposed (matvec_tr), so n = fwd_total suffices; false: n = total also
+// stages the pack's transposed copies, which they read instead.
+T2O_DEV Wts<float> stage_weights(float* smem, const float* pack, const t2o_layout& L, int64_t n, float,
+                                 bool = true) {
   copy_to_lds(smem, pack, n);
-  return Wts<float>{smem, smem};
+  return Wts<float>{smem, smem, false};
 }
-T2O_DEV Wts<__bf16> stage_weights(float* smem, const float* pack, const t2o_layout& L, int64_t n, __bf16) {
+T2O_DEV Wts<__bf16> stage_weights(float* smem, const float* pack, const t2o_layout& L, int64_t n, __bf16,
+                                  bool tr_reads = true) {
   copy_to_lds(smem, pack + L.total, n / 2);
   float* v = smem + n / 2;
   copy_to_lds(v, pack + L.vec_lo, L.fwd_total - L.vec_lo);
-  return Wts<__bf16>{reinterpret_cast<const __bf16*>(smem), v - L.vec_lo};
+  return Wts<__bf16>{reinterpret_cast<const __bf16*>(smem), v - L.vec_lo, tr_reads};
 }
-T2O_DEV Wts<float> global_weights(const float* pack, const t2o_layout&, float) { return Wts<float>{pack, pack}; }
+T2O_DEV Wts<float> global_weights(const float* pack, const t2o_layout&, float) { return Wts<float>{pack, pack, false}; }
 T2O_DEV Wts<__bf16> global_weights(const float* pack, const t2o_layout& L, __bf16) {
-  return Wts<__bf16>{reinterpret_cast<const __bf16*>(pack + L.total), pack};
+  return Wts<__bf16>{reinterpret_cast<const __bf16*>(pack + L.total), pack, false};
 }
 // LDS floats taken by stage_weights
 template <typename WT>

@@ -471,9 +471,9 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   float* GOUTB = Bd::GOUT ? WORK : WORK;        // head grads (rows of OUT layout)
   float* stage = WORK + Bd::GOUT;               // staging / gX0 region
   float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
-  // the pack (its transposed copies included in bf16 mode) in LDS when it fits
+  // the forward section of the pack in LDS when it fits
   // beside the per-wave buffers, else read through L2 (large mixers)
-  const Wts<WT> P0 = WLDS ? stage_weights(smem, n.pack, L, sizeof(WT) == 4 ? L.fwd_total : L.total, WT{})
+  const Wts<WT> P0 = WLDS ? stage_weights(smem, n.pack, L, L.fwd_total, WT{})
                           : global_weights(n.pack, L, WT{});
   for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) gs[i] = 0.f;
   __syncthreads();
@@ -1076,6 +1076,11 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
   (void)fv;
 }
 
+template <typename WT>
+inline __host__ __device__ int64_t mixp_weight_elems(const t2o_layout& L) {
+  return sizeof(WT) == 4 ? L.fwd_total : L.total;
+}
+
 template <int E, int H, int D, int A, int FF, typename WT>
 __global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) {
   static_assert(D == 2 && MixPipeDims<E, A>::OK, "one wave per block of a depth-2 stack, one query tile");
@@ -1097,7 +1102,9 @@ __global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) 
   float* X0 = smem + args.lds_w + pr * MixPipeDims<E, A>::PAIRF;
   float* R = X0 + Dm::X0F;
   float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
-  const Wts<WT> P0 = stage_weights(smem, args.f.net[0].pack, L, sizeof(WT) == 4 ? L.fwd_total : L.total, WT{});
+  // bf16: with the transposed copies (the pipelined kernel is register-bound at two
+  // waves per SIMD; transposed reads of the forward image cost it spills)
+  const Wts<WT> P0 = stage_weights(smem, args.f.net[0].pack, L, mixp_weight_elems<WT>(L), WT{}, false);
   for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) gs[i] = 0.f;
   if (d == 1)
     for (int i = threadIdx.x & 63; i < Dm::X0F; i += 64) X0[i] = 0.f;
@@ -1115,13 +1122,15 @@ template <int E, int H, int D, int A, int FF, typename WT>
 int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
   constexpr int PERW = MixBwdDims<E, A>::PERW;
   const t2o_layout& L = args.f.L;
-  args.lds_w = (int)((lds_weight_floats<WT>(L, sizeof(WT) == 4 ? L.fwd_total : L.total) + 15) / 16 * 16);
+  args.lds_w = (int)((lds_weight_floats<WT>(L, L.fwd_total) + 15) / 16 * 16);
   if constexpr (D == 2 && MixPipeDims<E, A>::OK) {
     if (args.xmid && !mixer_bwd_single_wave()) {
+      const int lds_w = (int)((lds_weight_floats<WT>(L, mixp_weight_elems<WT>(L)) + 15) / 16 * 16);
       for (int pairs = 4; pairs >= 1; pairs >>= 1) {
-        const size_t lds = sizeof(float) * ((size_t)args.lds_w + (size_t)pairs * MixPipeDims<E, A>::PAIRF);
+        const size_t lds = sizeof(float) * ((size_t)lds_w + (size_t)pairs * MixPipeDims<E, A>::PAIRF);
         if (lds > 160 * 1024 || args.f.B % pairs) continue;
         args.waves = pairs;
+        args.lds_w = lds_w;
         const int grid = args.f.B / pairs;
         if (grid > max_slabs) return T2O_EINVAL;
         auto kern = mixer_bwd_pipe_kernel<E, H, D, A, FF, WT>;

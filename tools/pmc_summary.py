@@ -21,6 +21,8 @@ def short(name):
         return ("agent_dw", "mixer_dw")[int(m.group(1))]
     if "agent_bwd_pipe_kernel" in name:
         return "agent_bwd"
+    if "mixer_bwd_pipe_kernel" in name:
+        return "mixer_bwd"
     for n in NAMES:
         if n in name:
             return n.replace("_kernel", "")
