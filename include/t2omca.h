@@ -264,17 +264,18 @@ int t2o_reduce_slabs(const float* slabs, int nslab, int64_t n, float* out, void*
 /* ---- vectorised MEC-offloading environment -------------
  * Replaces MultiAgvOffloadingEnv (environment_multi_mec.py:12-439) driven by
  * parallel_runner.py's env_worker (:224-270): NE envs advance in lock-step, one
- * wave per env, state resident in HBM.  All arrays are device pointers.
+ * wave per env, state resident in HBM.  All arrays but spec are device pointers.
  *
  * mode 0  construction (:12-59: mec_index + positions, zeroed queues/normaliser)
  * mode 1  worker 'reset'  (:257-263 -> reset() :219-227, get_state, get_avail_actions, get_obs)
  * mode 2  worker 'step'   (:239-256 -> step() :309-366, get_state, get_avail_actions, get_obs)
  * mode 3  get_env_info's two get_obs calls (:421-439; normaliser updates only)
  *
- * spec[15] (fp64): mec_radius, computation_cycles, bandwidth, noise_power,
+ * spec[15] (fp64, host memory): mec_radius, computation_cycles, bandwidth, noise_power,
  *   path_loss, channel_gain_linear, mec_compute_cap, agv_transmit_power,
  *   agv_compute_cap, latency_max, t_length, job_size_min, job_size_max,
- *   job_arrival_p, edge_only (0/1)  (t2omca_amd/env_spec.py).
+ *   job_arrival_p, edge_only (0/1)  (t2omca_amd/env_spec.py).  Entity
+ *   observations (obs_entity_mode = True).
  * state[17]: mec_index i32[NE][A], x f64[NE][A], y f64[NE][A],
  *   q_size i32[NE][A][QMAX], q_thr i32[NE][A][QMAX], q_head i32[NE][A],
  *   q_len i32[NE][A], task_num i32[NE][A], task_success i32[NE][A],
@@ -293,7 +294,11 @@ int t2o_env_run(int mode, const double* spec, void* const* state, void* const* o
                 const int64_t* actions, int64_t act_se, int NE, int A, int M, int C, int QMAX, int T,
                 uint64_t seed, void* stream);
 
-/* t2o_env_run with n_out = 8 (as above) or 11 output pointers; the extra three
+/* t2o_env_run with spec[16] (host memory): spec[15] = obs_entity_mode (1: the
+ * entity observation [A][9A] above; 0: get_obs_agent's flat branch, :172-182,
+ * obs f32/f64[NE][A][6] = [last_ack, get_agent_inf], normalised by the env's
+ * 6-long running normaliser, which keeps its [9A] row stride in state[14..16]),
+ * and n_out = 8 (as above) or 11 output pointers; the extra three
  * carry the compact observation wire format (replaces storing
  * get_obs's dense [A][9A] output, environment_multi_mec.py:148-186):
  *   out[8]  wire i32[NE][A][4], written with every obs the worker returns
@@ -304,7 +309,8 @@ int t2o_env_run(int mode, const double* spec, void* const* state, void* const* o
  *   out[9]  snap_n i64[NE], out[10] snap f64[NE][2][9A]: the normaliser's
  *           count, mean and S right before the worker's get_obs in mode 1 (the
  *           state the episode's first returned obs is normalised from).
- * out[9] / out[10] are both set or both NULL.  Needs latency_max <= 65535. */
+ * out[9] / out[10] are both set or both NULL.  Needs latency_max <= 65535.
+ * The wire format needs entity observations (spec[15] = 1). */
 int t2o_env_run_ex(int mode, const double* spec, void* const* state, void* const* out, int n_out,
                    const int64_t* actions, int64_t act_se, int NE, int A, int M, int C, int QMAX, int T,
                    uint64_t seed, void* stream);

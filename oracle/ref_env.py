@@ -28,9 +28,10 @@ ACK_ONEHOT = {-1: (1.0, 0.0, 0.0), 0: (0.0, 1.0, 0.0), 1: (0.0, 0.0, 1.0)}
 
 
 class RefEnv:
-    def __init__(self, M, A, T, seed, env_id, num_channels=4, edge_only=False):
+    def __init__(self, M, A, T, seed, env_id, num_channels=4, edge_only=False, obs_entity_mode=True):
         self.M, self.A, self.T, self.C = M, A, T, num_channels
         self.edge_only = edge_only
+        self.obs_entity_mode = obs_entity_mode
         self.nA = num_channels + 1
         self.seed, self.env_id = seed, env_id
         self.draw = 0
@@ -49,7 +50,7 @@ class RefEnv:
         self.remain_delay = [0] * A
         self.last_ack = np.zeros(A, dtype=np.int64)
         self.time_slot = 0
-        n = 9 * A
+        n = len(self.obs_agent(0))  # Normalization(shape=len(self.get_obs_agent(0))) (:59)
         self.nrm_n, self.nrm_mean, self.nrm_S, self.nrm_std = 0, np.zeros(n), np.zeros(n), np.zeros(n)
 
     # -- random draws / stand-ins --------------------------------------------------
@@ -91,7 +92,9 @@ class RefEnv:
         return np.array([0, 0, 0, 0, 0])
 
     def obs_agent(self, i):
-        """get_obs_agent (:148-182, obs_entity_mode)."""
+        """get_obs_agent (:148-182): entity mode, or the flat [last_ack, get_agent_inf] (:172-182)."""
+        if not self.obs_entity_mode:
+            return np.concatenate(([self.last_ack[i]], self.agent_inf(i)))
         parts = []
         for j in range(self.A):
             if self.mec_index[i] == self.mec_index[j]:
@@ -130,11 +133,13 @@ class RefEnv:
         return np.array([busy if self.queue[a] else [1] + [0] * (self.nA - 1) for a in range(self.A)])
 
     def get_env_info(self):
-        """get_env_info (:421-439): two get_obs calls (normaliser updates)."""
+        """get_env_info (:421-439): two get_obs calls (normaliser updates), one without entity obs."""
         obs_shape = len(self.get_obs()[0])
-        feats = int(len(self.get_obs()[0]) / self.A)
-        return dict(state_shape=8 * self.A, obs_shape=obs_shape, n_actions=self.nA, n_agents=self.A,
-                    episode_limit=self.T, n_entities=self.A, obs_entity_feats=feats, state_entity_feats=8)
+        info = dict(state_shape=8 * self.A, obs_shape=obs_shape, n_actions=self.nA, n_agents=self.A,
+                    episode_limit=self.T, n_entities=self.A, state_entity_feats=8)
+        if self.obs_entity_mode:  # the second get_obs call happens in entity mode only (:431-434)
+            info["obs_entity_feats"] = int(len(self.get_obs()[0]) / self.A)
+        return info
 
     def reset(self):
         """reset (:219-227) incl. its own get_obs call."""

@@ -579,13 +579,18 @@ T2O_DEV void dw_accumulate_regs(f4 (&acc)[OT][IT], const f4* dY, const f4* X, fl
     // 8-byte write per lane) and read back transposed with one
     // ds_read_b64_tr_b16 — lane (g, c) gets feature c of rows 4g..4g+3, the
     // 16x16x16 K-slice over rows.  The X side is staged whole, dY one tile at
-    // a time (so the stage holds IT + 1 tiles).
+    // a time (so the stage holds IT + 1 tiles).  Row r keeps its four 8-byte
+    // chunks in the order chunk ^ ((r >> 2) & 3): the 16 writes of a lane group
+    // (rows 0..15, one chunk) then cover 32 distinct store banks (unswizzled:
+    // 4-way), and every transposed read still takes whole 32-B rows.
     static_assert((IT + 1) * 128 <= StageDims<NS>::FLOATS, "stage too small");
     __bf16* sb = reinterpret_cast<__bf16*>(stage);
     typedef __attribute__((address_space(3))) s4v lds_s4v;
-    auto stw = [&](int j, f4 v) { *reinterpret_cast<bf4*>(sb + j * 256 + c * 16 + 4 * g) = to_bf4(v); };
+    const int wo = c * 16 + 4 * (g ^ ((c >> 2) & 3));  // this lane's write: row c, chunk g
+    const int ro = (4 * g + (c >> 2)) * 16 + 4 * ((c & 3) ^ g);  // transposed read: row 4g + c/4, chunk c & 3
+    auto stw = [&](int j, f4 v) { *reinterpret_cast<bf4*>(sb + j * 256 + wo) = to_bf4(v); };
     auto trk = [&](int j) {
-      const __bf16* p = sb + j * 256 + (4 * g + (c >> 2)) * 16 + 4 * (c & 3);
+      const __bf16* p = sb + j * 256 + ro;
       return __builtin_bit_cast(bf4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(p)));
     };
 #pragma unroll

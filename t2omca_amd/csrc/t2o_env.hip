@@ -29,7 +29,12 @@ struct EnvSpec {
   int latency_max, t_length, size_min, size_max;
   double arrival_p;
   int edge_only;  // get_avail_agent_actions' edge_only variant (:63-68)
+  int obs_entity;  // obs_entity_mode (:148-182): 1 entity obs [A][9A], 0 flat [A][6]
 };
+
+// get_obs_agent's length: entity mode 9 features per entity, else
+// [last_ack, get_agent_inf(5)] (:172-182); the normaliser has the same length (:59)
+__host__ __device__ inline int obs_len(int obs_entity, int A) { return obs_entity ? 9 * A : 6; }
 
 struct EnvState {
   int32_t* mec_index;   // [NE][A]
@@ -201,19 +206,24 @@ __device__ void write_wire(const EnvArgs& a, int e, const EnvLds& L) {
 // The update count n is kept in a register by every lane (the caller loads and
 // stores it once), so no lane ever reads another lane's global store.
 __device__ void get_obs(const EnvArgs& a, int e, EnvLds& L, bool out, int64_t& n) {
-  const int A = a.A, n9 = 9 * A, lane = threadIdx.x & 63;
+  // normaliser rows keep their [9A] stride in both modes (state[14..16])
+  const int A = a.A, n9 = 9 * A, no = obs_len(a.sp.obs_entity, A), lane = threadIdx.x & 63;
   double* mean = a.s.nrm_mean + (size_t)e * n9;
   double* S = a.s.nrm_S + (size_t)e * n9;
   double* sd = a.s.nrm_std + (size_t)e * n9;
   for (int i = 0; i < A; ++i) {
     ++n;
-    for (int p = lane; p < n9; p += 64) {
-      const int j = p / 9, f = p % 9;
+    for (int p = lane; p < no; p += 64) {
       double x = 0.0;
-      if (L.mec[i] == L.mec[j]) {
-        if (f < 3) x = (f == L.ack[j] + 1) ? 1.0 : 0.0;  // ack_mapping: -1 -> [1,0,0], 0 -> [0,1,0], 1 -> [0,0,1]
-        else if (f < 8) x = L.inf[j][f - 3];
-        else x = (i == j) ? 1.0 : 0.0;
+      if (!a.sp.obs_entity) {
+        x = p == 0 ? (double)L.ack[i] : L.inf[i][p - 1];  // [last_ack (raw -1/0/1), get_agent_inf]
+      } else {
+        const int j = p / 9, f = p % 9;
+        if (L.mec[i] == L.mec[j]) {
+          if (f < 3) x = (f == L.ack[j] + 1) ? 1.0 : 0.0;  // ack_mapping: -1 -> [1,0,0], 0 -> [0,1,0], 1 -> [0,0,1]
+          else if (f < 8) x = L.inf[j][f - 3];
+          else x = (i == j) ? 1.0 : 0.0;
+        }
       }
       double m, s, d;
       if (n == 1) {
@@ -231,7 +241,7 @@ __device__ void get_obs(const EnvArgs& a, int e, EnvLds& L, bool out, int64_t& n
       sd[p] = d;
       if (out) {
         const double v = (x - m) / (d + 1e-8);
-        const size_t o = ((size_t)e * A + i) * n9 + p;
+        const size_t o = ((size_t)e * A + i) * no + p;
         if (a.o.obs) a.o.obs[o] = (float)v;
         if (a.o.obs64) a.o.obs64[o] = v;
       }
@@ -315,11 +325,11 @@ __global__ __launch_bounds__(64) void env_kernel(EnvArgs a) {
     }
     return;
   }
-  if (a.mode == 3) {  // get_env_info (:421-439): two get_obs calls
+  if (a.mode == 3) {  // get_env_info (:421-439): two get_obs calls (one without entity obs, :425,431-434)
     int64_t n = a.s.nrm_n[e];
     fill_lds(a, e, L);
     get_obs(a, e, L, false, n);
-    get_obs(a, e, L, false, n);
+    if (a.sp.obs_entity) get_obs(a, e, L, false, n);
     if (lane == 0) a.s.nrm_n[e] = n;
     return;
   }
@@ -583,14 +593,16 @@ extern "C" int t2o_env_run_ex(int mode, const double* spec, void* const* state, 
                               const int64_t* actions, int64_t act_se, int NE, int A, int M, int C, int QMAX, int T,
                               uint64_t seed, void* stream) {
   if ((out && n_out != 8 && n_out != 11) || (n_out == 11 && out && (out[9] == nullptr) != (out[10] == nullptr)) ||
-      (spec && (int)spec[9] > 0xFFFF) || QMAX > 255)
+      (spec && (int)spec[9] > 0xFFFF) || QMAX > 255 ||
+      (spec && spec[15] == 0.0 && n_out == 11 && out && (out[8] || out[9])))  // wire format: entity obs only
     return T2O_EINVAL;
   if (NE < 1 || A < 1 || A > MAXA || M < 1 || M > 16 || C < 1 || C > 16 || QMAX < 1 || !spec || !state ||
       (mode == 2 && (!actions || !out)) || (mode == 1 && !out) || mode < 0 || mode > 3)
     return T2O_EINVAL;
   EnvArgs a{};
   a.sp = EnvSpec{spec[0], spec[1], spec[2], spec[3], spec[4], spec[5], spec[6], spec[7], spec[8],
-                 (int)spec[9], (int)spec[10], (int)spec[11], (int)spec[12], spec[13], spec[14] != 0.0};
+                 (int)spec[9], (int)spec[10], (int)spec[11], (int)spec[12], spec[13], spec[14] != 0.0,
+                 spec[15] != 0.0};
   a.s = EnvState{(int32_t*)state[0], (double*)state[1], (double*)state[2], (int32_t*)state[3],
                  (int32_t*)state[4], (int32_t*)state[5], (int32_t*)state[6], (int32_t*)state[7],
                  (int32_t*)state[8], (double*)state[9], (int32_t*)state[10], (int32_t*)state[11],
@@ -622,7 +634,10 @@ extern "C" int t2o_env_run(int mode, const double* spec, void* const* state, voi
                            const int64_t* actions, int64_t act_se, int NE, int A, int M, int C, int QMAX, int T,
                            uint64_t seed, void* stream) {
   if (!spec) return T2O_EINVAL;
-  return t2o_env_run_ex(mode, spec, state, out, 8, actions, act_se, NE, A, M, C, QMAX, T, seed, stream);
+  double sp16[16];
+  for (int i = 0; i < 15; ++i) sp16[i] = spec[i];
+  sp16[15] = 1.0;  // entity observations
+  return t2o_env_run_ex(mode, sp16, state, out, 8, actions, act_se, NE, A, M, C, QMAX, T, seed, stream);
 }
 
 extern "C" int t2o_obs_expand(const int32_t* wire, int64_t w_sb, int64_t w_st, const int64_t* snap_n,

@@ -481,6 +481,16 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
   const size_t ntiles = (size_t)fa.B * n.T * Dm::QT;
   using Rec = TapeRec<E, H, FF>;
+  // multi-tile mixers: 16-record tiles over each block's compact record stream
+  // (mixer_tape_tiles); the last tile's records past the stream's end are zeros
+  const size_t nrec = (size_t)fa.B * n.T * Dm::Q, ctiles = (nrec + 15) / 16;
+  if (Dm::QT > 1 && blockIdx.x == 0 && w == 0) {
+    const int tail = (int)(ctiles * 16 - nrec) * Rec::SIZE;  // elements
+    for (int d = 0; d < D; ++d) {
+      WT* z = static_cast<WT*>(args.tape) + ((size_t)d * ctiles * 16 + nrec) * Rec::SIZE;
+      for (int i = lane_c() + 16 * lane_g(); i < tail; i += 64) z[i] = WT(0.f);
+    }
+  }
   if (b < fa.B) {
     for (int i = lane; i < Dm::X0F; i += 64) X0[i] = 0.f;
     float ghw[3] = {0.f, 0.f, 0.f};  // grad wrt this step's hyper outputs, lane = feature
@@ -595,11 +605,13 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
                 for (int dd = 0; dd < d; ++dd) mixer_block_fwd<E, H, KT, FF, false>(P, L, dd, K, Dm::LK, x, nullptr);
               }
             }
-            constexpr int RT = mixer_tape_records(A);
+            // one compact record stream per block, (t, b, query row) in order: a
+            // tile's 16 records, or the Q - 16·qt real ones of the last (no
+            // padding records in HBM; the stream's tail is zeroed below)
             WT* tile = static_cast<WT*>(args.tape) +
-                       ((size_t)d * ntiles + ((size_t)t * fa.B + b) * Dm::QT + qt) * Rec::SIZE * RT;
-            MixerCacheLean<E, H, KT, FF> cache;  // whole 16-record tiles (padding records: zero grads)
-            const MaskedRec<WT> rec(tile, RT, Rec::SIZE);
+                       ((size_t)d * ctiles * 16 + ((size_t)t * fa.B + b) * Dm::Q + 16 * qt) * Rec::SIZE;
+            MixerCacheLean<E, H, KT, FF> cache;
+            const MaskedRec<WT> rec(tile, min(16, Dm::Q - 16 * qt), Rec::SIZE);
             mixer_block_fwd_lean<E, H, KT, FF>(P, L, d, K, Dm::LK, x, cache, rec);
             mixer_block_bwd_lean<E, H, KT, FF>(P, L, gs, rec, stage, d, K, Dm::LK, gX0, cache, gx, ln2[d]);
           }

@@ -15,7 +15,8 @@ only) written in the compact wire format of SURVEY.md §8 f3: ``wire``
 [n_envs, A, 4] int32 per step plus the normaliser snapshot ``snap_n`` /
 ``snap`` taken at reset; ``ops.obs_expand`` rebuilds the dense obs exactly.
 
-Shapes: obs [n_envs, A, 9A] f32, state [n_envs, 8A] f32, avail
+Shapes: obs [n_envs, A, 9A] f32 (obs_entity_mode=False: [n_envs, A, 6], the
+flat [last_ack, get_agent_inf] branch of get_obs_agent :172-182), state [n_envs, 8A] f32, avail
 [n_envs, A, nA] i32, reward [n_envs] f64, terminated [n_envs] bool, info a dict
 of [n_envs] f64 tensors (task_completion_* are NaN except on the terminal step).
 Every launch goes on the current HIP stream; nothing synchronises with the host.
@@ -35,19 +36,28 @@ INFO_KEYS = ("delay_reward", "overtime_penalty", "channel_utilization_rate", "co
              "task_completion_rate", "task_completion_delay")
 
 
-def spec_vector(edge_only=False):
-    """The fp64 spec[15] of t2o_env_run from env_spec's constants."""
+def spec_vector(edge_only=False, obs_entity_mode=True):
+    """The fp64 spec[16] of t2o_env_run_ex from env_spec's constants."""
     return [S.MEC_RADIUS, float(S.COMPUTATION_CYCLES), S.BANDWIDTH, S.NOISE_POWER, float(S.PATH_LOSS),
             10 ** (S.CHANNEL_GAIN / 10), S.MEC_COMPUTE_CAP, S.AGV_TRANSMIT_POWER, S.AGV_COMPUTE_CAP,
             float(S.LATENCY_MAX), float(S.T_LENGTH), float(S.JOB_SIZE_MIN), float(S.JOB_SIZE_MAX),
-            S.JOB_ARRIVAL_P, 1.0 if edge_only else 0.0]
+            S.JOB_ARRIVAL_P, 1.0 if edge_only else 0.0, 1.0 if obs_entity_mode else 0.0]
+
+
+def obs_len(A, obs_entity_mode=True):
+    """get_obs_agent's length (environment_multi_mec.py:148-182)."""
+    return 9 * A if obs_entity_mode else 6
 
 
 class VecEnv:
     def __init__(self, n_envs, mec_num=2, agv_num=16, num_channels=4, episode_limit=150, seed=None,
-                 edge_only=False, device="cuda", keep_obs64=False, wire=False):
+                 edge_only=False, device="cuda", keep_obs64=False, wire=False, obs_entity_mode=True,
+                 state_entity_mode=True):
         """seed None: 0 mixed with the data-parallel rank (distributed.rank_seed), so
-        every rank's shard of envs draws its own episodes."""
+        every rank's shard of envs draws its own episodes.  obs_entity_mode /
+        state_entity_mode as the reference constructor's (:10-11; the transformer
+        path uses both, the defaults here); state_entity_mode only changes
+        get_env_info's keys (:431-438)."""
         if seed is None:
             seed = rank_seed(0, dist_rank())
         device = torch.device(device)
@@ -59,6 +69,10 @@ class VecEnv:
         if not (1 <= agv_num <= 64 and 1 <= mec_num <= 16 and 1 <= num_channels <= 15):
             raise ValueError("VecEnv supports agv_num <= 64, mec_num <= 16, num_channels <= 15 "
                              "(n_actions = num_channels + 1 <= 16, the agent head's limit)")
+        if wire and not obs_entity_mode:
+            raise ValueError("the compact wire format encodes entity observations (obs_entity_mode=True)")
+        self.obs_entity_mode, self.state_entity_mode = bool(obs_entity_mode), bool(state_entity_mode)
+        self.n_obs = obs_len(agv_num, obs_entity_mode)
         self.n_envs, self.M, self.A, self.C = n_envs, mec_num, agv_num, num_channels
         self.T, self.seed, self.device = episode_limit, int(seed), device
         self.n_actions = num_channels + 1
@@ -74,9 +88,9 @@ class VecEnv:
             torch.zeros(NE, dtype=torch.int64, device=device), torch.zeros(NE, dtype=torch.int64, device=device),
             torch.zeros(NE, 9 * A, **f64), torch.zeros(NE, 9 * A, **f64), torch.zeros(NE, 9 * A, **f64),
         ]
-        self._spec = torch.tensor(spec_vector(edge_only), dtype=torch.float64, device=device)
-        self.obs = torch.empty(NE, A, 9 * A, dtype=torch.float32, device=device)
-        self.obs64 = torch.empty(NE, A, 9 * A, **f64) if keep_obs64 else None
+        self._spec = (ctypes.c_double * 16)(*spec_vector(edge_only, obs_entity_mode))  # host array
+        self.obs = torch.empty(NE, A, self.n_obs, dtype=torch.float32, device=device)
+        self.obs64 = torch.empty(NE, A, self.n_obs, **f64) if keep_obs64 else None
         self.state = torch.empty(NE, 8 * A, dtype=torch.float32, device=device)
         self.avail = torch.empty(NE, A, self.n_actions, **i32)
         self.reward = torch.empty(NE, **f64)
@@ -105,7 +119,7 @@ class VecEnv:
         act_p, act_se = None, 0
         if actions is not None:
             act_p, act_se = ctypes.c_void_p(actions.data_ptr()), actions.stride(0)
-        rc = lib().t2o_env_run_ex(mode, ctypes.c_void_p(self._spec.data_ptr()), self._ptrs(self._state),
+        rc = lib().t2o_env_run_ex(mode, ctypes.cast(self._spec, ctypes.c_void_p), self._ptrs(self._state),
                                   self._ptrs(outs), len(outs), act_p, act_se, n_envs or self.n_envs, self.A, self.M,
                                   self.C, self.qmax, self.T, ctypes.c_uint64(self.seed & ((1 << 64) - 1)),
                                   stream_ptr(self.device))
@@ -134,9 +148,13 @@ class VecEnv:
         """get_env_info (:421-439) on env 0, as the runner does once at start-up (:34);
         all_envs=True calls it on every env (as a standalone env object per env would)."""
         self._run(3, n_envs=None if all_envs else 1)
-        return dict(state_shape=8 * self.A, obs_shape=9 * self.A, n_actions=self.n_actions,
-                    n_agents=self.A, episode_limit=self.T, n_entities=self.A, obs_entity_feats=9,
-                    state_entity_feats=8)
+        info = dict(state_shape=8 * self.A, obs_shape=self.n_obs, n_actions=self.n_actions,
+                    n_agents=self.A, episode_limit=self.T, n_entities=self.A)
+        if self.obs_entity_mode:
+            info["obs_entity_feats"] = 9
+        if self.state_entity_mode:
+            info["state_entity_feats"] = 8
+        return info
 
     def reset(self, dest=None):
         """dest: optional dict of output buffers {"obs", "state", "avail", "wire"}

@@ -264,7 +264,7 @@ class TDLearner:
                          td_lambda=self.td_lambda, mask_sum=1.0)
         # 4. mixer BPTT.  Its weight-grad tape contraction (HBM-bound) runs on a
         #    side stream, overlapping the agent BPTT (latency-bound, half the SIMDs)
-        tape_m = self._slab("tape_m", ops.tape_floats(self.sm, ops.mixer_tape_tiles(B, T, A)))
+        tape_m = self._slab("tape_m", ops.tape_floats(self.sm, ops.mixer_tape_tiles(B, T, A, self.sm)))
         tape_a = self._slab("tape_a", ops.tape_floats(self.sa, ops.agent_tape_tiles(B, T, A)))
         slabs_m = self._slab("m", int(ops.lib().t2o_mixer_bwd_max_slabs(B)) * self.sm.layout().grad_total)
         contract_m, gqv, ghid, _ = ops.mixer_unroll_bwd(self.sm, self.pack_m, state, h_on, o_on, td["gq"],

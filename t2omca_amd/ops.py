@@ -144,8 +144,15 @@ def agent_tape_tiles(B, T, A):
     return T * ((B * A + 15) // 16)
 
 
-def mixer_tape_tiles(B, T, A):
-    return B * T * ((A + 3 + 15) // 16)
+def mixer_tape_tiles(B, T, A, shape: NetShape = None):
+    """Weight-gradient tape tiles per block of a mixer BPTT over B episodes x T
+    steps: one tile of the A+3 query rows per (episode, step) when they fit 16
+    records; tuned multi-tile mixers store each block's query-row records as one
+    compact stream cut into 16-record tiles (t2o_mixer.hip)."""
+    Q = A + 3
+    if Q > 16 and shape is not None and not shape.generic:
+        return (B * T * Q + 15) // 16
+    return B * T * ((Q + 15) // 16)
 
 
 def _tape(shape, tiles, tape, device):
@@ -281,7 +288,7 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
     gqv = torch.empty(B, T, A, device=dev)
     ghid = torch.empty(B, T, A, E, device=dev)
     ghw0 = torch.empty(B, 3, E, device=dev) if want_ghw0 else None
-    tiles = mixer_tape_tiles(B, T, A)
+    tiles = mixer_tape_tiles(B, T, A, shape)
     tape = _tape(shape, tiles, tape, dev)
     nslab = ctypes.c_int(0)
     _mark(timer, "begin:mixer_bwd")

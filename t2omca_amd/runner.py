@@ -57,6 +57,8 @@ class RolloutRunner:
         # seed None: 0 mixed with the data-parallel rank (distributed.rank_seed)
         if seed is None:
             seed = rank_seed(0, dist_rank())
+        if not getattr(env, "obs_entity_mode", True):
+            raise ValueError("the transformer agent reads entity observations (VecEnv obs_entity_mode=True)")
         if compact_obs and getattr(env, "wire", None) is None:
             raise ValueError("compact_obs needs a VecEnv built with wire=True")
         self.compact_obs = bool(compact_obs)

@@ -36,10 +36,12 @@ from t2omca_amd import env_spec as S  # noqa: E402
 REF = "/root/reference"
 SEED = 1234
 CONFIGS = {
-    # tag: (M, A, T, episodes, n_envs)
+    # tag: (M, A, T, episodes, n_envs[, obs_entity_mode])
     "m2_a16_t10": (2, 16, 10, 2, 2),
     "m4_a8_t8": (4, 8, 8, 2, 2),
     "m2_a3_t6": (2, 3, 6, 3, 2),
+    # get_obs_agent's flat branch (:172-182): obs = [last_ack, get_agent_inf] per agent
+    "m2_a8_t8_flat": (2, 8, 8, 2, 2, False),
 }
 
 
@@ -131,15 +133,15 @@ def build_pkg():
     return mod
 
 
-def run_env(mod, M, A, T, episodes, env_id, rng):
+def run_env(mod, M, A, T, episodes, env_id, rng, obs_entity_mode=True):
     STREAM[0] = Stream(env_id)
     env = mod.MultiAgvOffloadingEnv(mec_num=M, agv_num=A, num_channels=4, episode_limit=T, seed=0,
-                                    obs_entity_mode=True, state_entity_mode=True)
+                                    obs_entity_mode=obs_entity_mode, state_entity_mode=True)
     out = {"mec_index": np.array([ag.mec_index for ag in env.agents])}
     info0 = env.get_env_info()
     out["env_info"] = np.array([info0["state_shape"], info0["obs_shape"], info0["n_actions"],
                                 info0["n_agents"], info0["episode_limit"], info0["n_entities"],
-                                info0["obs_entity_feats"], info0["state_entity_feats"]])
+                                info0.get("obs_entity_feats", -1), info0["state_entity_feats"]])
     obs, state, avail, actions, reward, ack = [], [], [], [], [], []
     term, util, confl, dreward, overtime, tc_rate, tc_delay = [], [], [], [], [], [], []
     for ep in range(episodes):
@@ -174,18 +176,25 @@ def run_env(mod, M, A, T, episodes, env_id, rng):
     return out
 
 
-def main():
+def main(tags=None):
+    """tags: the CONFIGS to (re)write (default all)."""
     mod = build_pkg()
-    for tag, (M, A, T, episodes, n_envs) in CONFIGS.items():
+    for tag, cfg in CONFIGS.items():
+        if tags and tag not in tags:
+            continue
+        M, A, T, episodes, n_envs = cfg[:5]
+        ent = cfg[5] if len(cfg) > 5 else True
         rng = np.random.default_rng(7)
         res = {"M": np.array(M), "A": np.array(A), "T": np.array(T), "episodes": np.array(episodes),
                "seed": np.array(SEED)}
+        if not ent:
+            res["obs_entity_mode"] = np.array(0)
         for e in range(n_envs):
-            for k, v in run_env(mod, M, A, T, episodes, e, rng).items():
+            for k, v in run_env(mod, M, A, T, episodes, e, rng, ent).items():
                 res[f"env{e}/{k}"] = v
         np.savez_compressed(os.path.join(HERE, f"env_{tag}.npz"), **res)
         print("wrote", tag)
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

@@ -14,12 +14,13 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 
 def replay(z, e):
     M, A, T, eps, seed = (int(z[k]) for k in ("M", "A", "T", "episodes", "seed"))
-    env = RefEnv(M, A, T, seed, e)
+    ent = bool(z["obs_entity_mode"]) if "obs_entity_mode" in z.files else True
+    env = RefEnv(M, A, T, seed, e, obs_entity_mode=ent)
     out = {"mec_index": env.mec_index.copy()}
     info = env.get_env_info()
-    out["env_info"] = np.array([info[k] for k in ("state_shape", "obs_shape", "n_actions", "n_agents",
-                                                  "episode_limit", "n_entities", "obs_entity_feats",
-                                                  "state_entity_feats")])
+    out["env_info"] = np.array([info.get(k, -1) for k in ("state_shape", "obs_shape", "n_actions", "n_agents",
+                                                          "episode_limit", "n_entities", "obs_entity_feats",
+                                                          "state_entity_feats")])
     acts = z[f"env{e}/actions"]
     rec = {k: [] for k in ("obs", "state", "avail", "reward", "ack", "terminated", "utilization",
                            "conflict_ratio", "delay_reward", "overtime_penalty", "task_completion_rate",

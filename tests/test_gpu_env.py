@@ -40,8 +40,9 @@ def test_env_matches_reference_trajectories(path):
     from t2omca_amd.env import VecEnv
     z = np.load(path)
     M, A, T, eps, seed = (int(z[k]) for k in ("M", "A", "T", "episodes", "seed"))
+    ent = bool(z["obs_entity_mode"]) if "obs_entity_mode" in z.files else True  # flat obs branch (:172-182)
     NE = len({k.split("/")[0] for k in z.files if k.startswith("env")})
-    env = VecEnv(NE, mec_num=M, agv_num=A, episode_limit=T, seed=seed, keep_obs64=True)
+    env = VecEnv(NE, mec_num=M, agv_num=A, episode_limit=T, seed=seed, keep_obs64=True, obs_entity_mode=ent)
     _eq(env.mec_index.cpu().numpy(), np.stack([z[f"env{e}/mec_index"] for e in range(NE)]), "mec_index")
     env.get_env_info(all_envs=True)
     gold = {k: np.stack([z[f"env{e}/{k}"] for e in range(NE)]) for k in
@@ -70,13 +71,13 @@ def test_env_matches_reference_trajectories(path):
     _eq(env.draws.cpu().numpy(), gold["draws"], "draws")
 
 
-def _rollout_vs_oracle(NE, M, A, T, eps, seed, edge_only=False, runner_info=True):
+def _rollout_vs_oracle(NE, M, A, T, eps, seed, edge_only=False, runner_info=True, obs_entity_mode=True):
     from t2omca_amd.env import VecEnv
-    env = VecEnv(NE, mec_num=M, agv_num=A, episode_limit=T, seed=seed, edge_only=edge_only, keep_obs64=True)
-    refs = [RefEnv(M, A, T, seed, e, edge_only=edge_only) for e in range(NE)]
+    env = VecEnv(NE, mec_num=M, agv_num=A, episode_limit=T, seed=seed, edge_only=edge_only, keep_obs64=True,
+                 obs_entity_mode=obs_entity_mode)
+    refs = [RefEnv(M, A, T, seed, e, edge_only=edge_only, obs_entity_mode=obs_entity_mode) for e in range(NE)]
     if runner_info:  # the runner's get_env_info touches env 0 only (parallel_runner.py:34)
-        env.get_env_info()
-        refs[0].get_env_info()
+        assert env.get_env_info() == refs[0].get_env_info()
     rng = np.random.default_rng(seed)
     for _ in range(eps):
         st, av, _ = env.reset()
@@ -118,3 +119,10 @@ def test_env_rollout_edge_only_vs_oracle():
 def test_env_single_agent_and_channel_extremes():
     _rollout_vs_oracle(NE=4, M=1, A=1, T=12, eps=2, seed=11)
     _rollout_vs_oracle(NE=4, M=3, A=5, T=12, eps=1, seed=12)
+
+
+def test_env_flat_obs_mode_vs_oracle():
+    """obs_entity_mode=False: get_obs_agent's flat branch (:172-182), 6 features per agent
+    normalised by a 6-long running normaliser; get_env_info makes one get_obs call."""
+    _rollout_vs_oracle(NE=6, M=2, A=8, T=10, eps=2, seed=21, obs_entity_mode=False)
+    _rollout_vs_oracle(NE=3, M=4, A=64, T=4, eps=1, seed=22, obs_entity_mode=False)

@@ -1,5 +1,5 @@
 set -eu
-OUT=gpurun_out/r2_tr
+OUT=gpurun_out/${1:-r2_tr}
 mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -40 $OUT/pytest.log; exit 1; }
 tail -2 $OUT/pytest.log
