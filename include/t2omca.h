@@ -162,6 +162,12 @@ int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack,
                          float* gslabs, int max_slabs, int* nslab, void* tape, float* gh0,
                          int B, int T, int A, void* stream);
 int t2o_agent_bwd_max_slabs(int B, int A);
+/* The record format t2o_agent_unroll_bwd writes to its tape for this layout
+ * (has_hmid: the call passes hmid): 0 the full record; 1 (bf16, the pipelined
+ * kernel, up to 8 entities) the lean record — dM and dN were accumulated in
+ * registers and flushed into the slabs, the tape holds only the FFN / LN1 /
+ * unify-bias operands.  Pass it to t2o_bwd_tape_contract_ex. */
+int t2o_agent_bwd_tape_format(const t2o_layout* L, int has_hmid);
 
 /* Mixer unroll forward for up to two networks (online + target) in one
  * launch; one wave per episode.  states[b][t][n_ent*F] (element strides
@@ -213,6 +219,12 @@ int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t tiles);
  * t2o_*_unroll_bwd call that wrote the tape. */
 int t2o_bwd_tape_contract(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
                           float* gslabs, int nslab, void* stream);
+/* t2o_bwd_tape_contract for a tape in record format rec_format
+ * (t2o_agent_bwd_tape_format; 0 = the full record, what the mixer writes).
+ * Format 1 adds only the FFN / LN1 / bu grads: the backward call already put
+ * dM / dN into the slabs. */
+int t2o_bwd_tape_contract_ex(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
+                             float* gslabs, int nslab, int rec_format, void* stream);
 
 /* TD(λ) targets, masked PER-weighted loss, dL/dQtot and priorities
  * (PyMARL2 NQLearner semantics; see t2o_learner.hip).  qtot [B][T] (online

@@ -66,6 +66,10 @@ EXPORTS = {
     "t2o_bwd_tape_floats": (ctypes.c_int64, [ctypes.POINTER(Layout), ctypes.c_int64]),
     "t2o_bwd_tape_contract": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                              ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
+    "t2o_bwd_tape_contract_ex": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_void_p]),
+    "t2o_agent_bwd_tape_format": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_int]),
     "t2o_td_loss": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_int64] * 2 + [ctypes.c_void_p] +
                     [ctypes.c_int64] * 2 + [ctypes.c_void_p] + [ctypes.c_int64] * 2 +
                     [ctypes.c_void_p] + [ctypes.c_float] * 3 + [ctypes.c_void_p] * 4 +

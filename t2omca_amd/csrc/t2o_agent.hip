@@ -380,15 +380,27 @@ constexpr int AGP_TILES = AG_BWD_WAVES;  // tiles per workgroup (same slab count
 template <int E>
 constexpr int agp_xch_floats() { return 3 * (E / 16) * 64 * 4; }
 
+// the pipelined kernel keeps dM / dN in registers (tape record TapeRecA) in bf16
+// up to 8 entities (beyond, 96 more accumulator registers spill); otherwise it
+// tapes the full record
+template <int E, int H, int NE, typename WT>
+constexpr bool agp_acc() { return sizeof(WT) == 2 && NE <= 8; }
+template <int E, int H, int NE, typename WT>
+constexpr int agp_stage_floats() {
+  return agp_acc<E, H, NE, WT>() ? AgentAccTiles<E, H>::N * 128 : StageDims<1>::FLOATS;
+}
+
 template <int E, int H, int D, int NE, int FF, typename WT>
 __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(AgentBwdArgs args) {
   static_assert(D == 2, "one wave per block of a depth-2 stack");
-  constexpr int ET = E / 16;
-  constexpr int STAGE = StageDims<1>::FLOATS;
+  constexpr int ET = E / 16, HET = H * ET;
   constexpr bool BF = sizeof(WT) == 2;
   constexpr bool CHUNK = NE > AG_CHUNK_MIN;
   constexpr int NO = CHUNK ? 1 : NE;
-  using Rec = TapeRec<E, H, FF>;
+  // bf16, entities in registers: dM / dN accumulate in registers (lean record)
+  constexpr bool ACC = agp_acc<E, H, NE, WT>();
+  constexpr int STAGE = agp_stage_floats<E, H, NE, WT>();
+  using Rec = typename std::conditional<ACC, TapeRecA<E, H, FF>, TapeRec<E, H, FF>>::type;
   // lean cache (half the registers of the one-wave kernel's; X, Z, Y records
   // written by the recompute phase) unless the entities are streamed in chunks
   using Cache = typename std::conditional<CHUNK, AgentCacheCh<E, H, NE, FF>, AgentCacheLean<E, H, NE, FF>>::type;
@@ -445,6 +457,11 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
     gWe[t][0] = gWo[0][t] = gbe[t] = zero4();
     ln2[t] = ln2[ET + t] = zero4();
   }
+  f4 gM[HET][ET], gN[ET][HET];  // ACC: this wave's block's dM, dN over its tile and the unroll
+#pragma unroll
+  for (int i = 0; i < HET; ++i)
+#pragma unroll
+    for (int t = 0; t < ET; ++t) gM[i][t] = gN[t][i] = zero4();
   // Both roles run the same loop body "recompute step; barrier; backward step;
   // barrier"; the block-0 wave starts one barrier late, so its recompute of a
   // step overlaps the block-1 backward of the same step and its backward the
@@ -525,6 +542,9 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
           for (int t = 0; t < ET; ++t) xo[t] = h[t];
         }
         if constexpr (CHUNK) agent_block_fwd_ch<E, H, NE, FF, true>(P, Lb, 0, h, ObsRow{ob, F}, xo, &cache);
+        else if constexpr (ACC)
+          agent_block_fwd_acc<E, H, NE, FF>(P, Lb, 0, h, o, xo, cache, MaskedRec<WT>(tile, tile_ok ? 16 : 0, Rec::SIZE),
+                                            stage);
         else agent_block_fwd_lean<E, H, NE, FF>(P, Lb, 0, h, o, xo, cache, MaskedRec<WT>(tile, tile_ok ? 16 : 0, Rec::SIZE));
       } else {
         f4 gx[ET], ghi[ET];
@@ -566,6 +586,9 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
         if constexpr (CHUNK)
           agent_block_bwd_ch<E, H, NE, FF>(P, Lb, Gb, gs, tile_ok ? tile : nullptr, stage, 0, h, ObsRow{ob, F}, cache,
                                            gx, ghi, gbe, gWe, ln2);
+        else if constexpr (ACC)
+          agent_block_bwd_acc<E, H, NE, FF>(P, Lb, gs, MaskedRec<WT>(tile, tile_ok ? 16 : 0, Rec::SIZE), stage, 0, h,
+                                            o, cache, gx, ghi, gbe, gWe, ln2, gM, gN);
         else
           agent_block_bwd_lean<E, H, NE, FF>(P, Lb, gs, MaskedRec<WT>(tile, tile_ok ? 16 : 0, Rec::SIZE), stage, 0, h,
                                              o, cache, gx, ghi, gbe, gWe, ln2);
@@ -599,6 +622,10 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
   }
   if (d == 1) __syncthreads();
   if (tile_ok) {
+    if constexpr (ACC) {
+      flush_tiles_g<HET, ET>(gs + Gb.M[0], E, gM);
+      flush_tiles_g<ET, HET>(gs + Gb.N[0], H * E, gN);
+    }
     flush_tiles_g<ET, 1>(gs + G.We, 16, gWe);
     vec_accumulate_g<ET>(gs + G.be, gbe);
     vec_accumulate_g<ET>(gs + Gb.g2[0], &ln2[0]);
@@ -614,7 +641,20 @@ template <int E, int H, int D, int NE, int FF, typename WT>
 size_t bwd_pipe_lds_bytes(const t2o_layout& L) {
   const int64_t nw = L.fwd_total;
   return sizeof(float) * ((size_t)(lds_weight_floats<WT>(L, nw) + 15) / 16 * 16 +
-                          2 * AGP_TILES * StageDims<1>::FLOATS + AGP_TILES * agp_xch_floats<E>());
+                          2 * AGP_TILES * agp_stage_floats<E, H, NE, WT>() + AGP_TILES * agp_xch_floats<E>());
+}
+
+// which BPTT kernel launch_bwd picks: the pipelined one (depth 2, block inputs
+// stored by the forward, LDS fits, no T2O_AGENT_BWD=single)
+template <int E, int H, int D, int NE, int FF, typename WT>
+bool bwd_uses_pipe(const t2o_layout& L, bool has_hmid) {
+  if constexpr (D == 2) return has_hmid && bwd_pipe_lds_bytes<E, H, D, NE, FF, WT>(L) <= 160 * 1024 && !agent_bwd_single_wave();
+  return false;
+}
+
+template <int E, int H, int D, int NE, int FF, typename WT>
+int bwd_tape_format(const t2o_layout& L, bool has_hmid) {
+  return bwd_uses_pipe<E, H, D, NE, FF, WT>(L, has_hmid) && agp_acc<E, H, NE, WT>() ? 1 : 0;
 }
 
 template <int E, int H, int D, int NE, int FF, typename WT>
@@ -626,7 +666,7 @@ int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream
   if (grid > max_slabs) return T2O_EINVAL;
   if constexpr (D == 2) {
     const size_t lds = bwd_pipe_lds_bytes<E, H, D, NE, FF, WT>(args.L);
-    if (args.hmid && lds <= 160 * 1024 && !agent_bwd_single_wave()) {
+    if (bwd_uses_pipe<E, H, D, NE, FF, WT>(args.L, args.hmid != nullptr)) {
       auto kern = agent_bwd_pipe_kernel<E, H, D, NE, FF, WT>;
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * 2 * AGP_TILES), lds, stream, args);
@@ -725,6 +765,16 @@ extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, cons
 
 // diagnostic builds only (-DT2O_PHASE_PROF, tools/phase_prof.py)
 T2O_PROF_READER(t2o_prof_read_agent)
+
+extern "C" int t2o_agent_bwd_tape_format(const t2o_layout* L, int has_hmid) {
+  if (!L || L->kind != 0) return T2O_EINVAL;
+  if (L->generic) return 0;
+  int fmt = 0;
+  T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
+               fmt = (L->prec ? bwd_tape_format<E_, H_, D_, NE_, FF_, __bf16>(*L, has_hmid != 0)
+                              : bwd_tape_format<E_, H_, D_, NE_, FF_, float>(*L, has_hmid != 0)));
+  return fmt;
+}
 
 extern "C" int t2o_agent_bwd_max_slabs(int B, int A) {
   const int rpw = rows_per_wave(B * A);

@@ -127,6 +127,35 @@ T2O_DEV void agent_block_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d, 
   post_fwd_lean<E, H, FF>(P, L, d, z, x, &cache.post, rec);
 }
 
+// Register-accumulating variant of the lean pair (the pipelined bf16 BPTT):
+// dM = Σ gu ⊗ x and dN = Σ gres ⊗ z stay in MFMA accumulator registers over the
+// whole unroll instead of going to the tape (record TapeRecA).  Their row
+// operands known in the recompute phase — the block input x and the head
+// outputs z — are staged there (bf16 tiles of the wave's stage, transposed-read
+// ready), so the backward phase only streams gres / gu against them.  Stage
+// tiles: 0 streamed operand, 1..ET the head / embedding grads' staging
+// (dw_accumulate_regs), then z, then x.
+template <int E, int H>
+struct AgentAccTiles {
+  static constexpr int ET = E / 16, HET = H * ET;
+  static constexpr int ZT = 1 + ET, XT = ZT + HET, N = XT + ET;  // N: tiles per wave
+};
+
+template <int E, int H, int NE, int FF, typename WT>
+T2O_DEV void agent_block_fwd_acc(const Wts<WT>& P, const t2o_layout& L, int d, const f4* h, const f4 (&o)[NE],
+                                 f4* x, AgentCacheLean<E, H, NE, FF>& cache, const MaskedRec<WT>& rec,
+                                 float* __restrict__ stage) {
+  using Tl = AgentAccTiles<E, H>;
+  __bf16* sb = reinterpret_cast<__bf16*>(stage);
+#pragma unroll
+  for (int t = 0; t < Tl::ET; ++t) stage_tile_bf(sb, Tl::XT + t, x[t]);
+  f4 z[Tl::HET];
+  agent_attn_fwd<E, H, NE, FF, true>(P, L, d, h, o, x, z, &cache);
+#pragma unroll
+  for (int t = 0; t < Tl::HET; ++t) stage_tile_bf(sb, Tl::ZT + t, z[t]);
+  post_fwd_lean<E, H, FF, WT, TapeRecA<E, H, FF>>(P, L, d, z, x, &cache.post, rec);
+}
+
 // Attention half of the backward: from gz (grad wrt z) to gu (grad wrt u = M x);
 // gh_in accumulates the grad wrt h through the key/value path (token 0), gbe the
 // grad wrt the embedding bias, gWe (MFMA register block, [E][16] as ET x 1 tiles)
@@ -235,6 +264,27 @@ T2O_DEV void agent_block_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* 
   f4 gu[HET];
   agent_attn_bwd<E, H, NE, FF, true>(P, L, stage, h, o, c, gz, gu, gh_in, gbe, gWe);
   rec.template store<HET>(TapeRec<E, H, FF>::GU, gu);
+  f4 gxp[ET];
+  matvec_tr<ET, HET>(P, L.M[d], E, L.MT[d], H * E, gu, gxp);
+#pragma unroll
+  for (int t = 0; t < ET; ++t) gx[t] = gxp[t] + gres[t];
+}
+
+template <int E, int H, int NE, int FF, typename WT>
+T2O_DEV void agent_block_bwd_acc(const Wts<WT>& P, const t2o_layout& L, float* __restrict__ gs,
+                                 const MaskedRec<WT>& rec, float* __restrict__ stage, int d, const f4* h,
+                                 const f4 (&o)[NE], const AgentCacheLean<E, H, NE, FF>& c, f4* gx, f4* gh_in,
+                                 f4* gbe, f4 (&gWe)[E / 16][1], f4* ln2, f4 (&gM)[H * (E / 16)][E / 16],
+                                 f4 (&gN)[E / 16][H * (E / 16)]) {
+  using Tl = AgentAccTiles<E, H>;
+  constexpr int ET = E / 16, HET = H * ET;
+  f4 gz[HET], gres[ET];
+  post_bwd_lean<E, H, FF, WT, TapeRecA<E, H, FF>>(P, L, gs, rec, d, c.post, gx, gz, gres, ln2);
+  dw_accumulate_prestaged<ET, HET>(gN, gres, stage, Tl::ZT, 0);  // dN += gres ⊗ z
+  T2O_MARK(2);
+  f4 gu[HET];
+  agent_attn_bwd<E, H, NE, FF, true>(P, L, stage, h, o, c, gz, gu, gh_in, gbe, gWe);
+  dw_accumulate_prestaged<HET, ET>(gM, gu, stage, Tl::XT, 0);  // dM += gu ⊗ x
   f4 gxp[ET];
   matvec_tr<ET, HET>(P, L.M[d], E, L.MT[d], H * E, gu, gxp);
 #pragma unroll

@@ -133,13 +133,14 @@ struct PostCacheLean {
   float rs2;
 };
 
-template <int E, int H, int FF, typename WT>
+// R: the tape record (TapeRec; TapeRecA has no X / Z fields — its writer keeps
+// dN's operands itself).
+template <int E, int H, int FF, typename WT, typename R = TapeRec<E, H, FF>>
 T2O_DEV void post_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d, const f4* z, f4* x,
                            PostCacheLean<E, H, FF>* c, const MaskedRec<WT>& rec) {
   constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
-  using R = TapeRec<E, H, FF>;
-  rec.template store<ET>(R::X, x);
-  rec.template store<HET>(R::Z, z);
+  if constexpr (R::X >= 0) rec.template store<ET>(R::X, x);
+  if constexpr (R::Z >= 0) rec.template store<HET>(R::Z, z);
   f4 r1[ET];
   matvec<ET, HET>(P.w + L.N[d], H * E, z, r1);
 #pragma unroll
@@ -168,11 +169,10 @@ T2O_DEV void post_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d, const f
 }
 
 // post_bwd for the lean cache (the X, Z, Y record fields were written forward)
-template <int E, int H, int FF, typename WT>
+template <int E, int H, int FF, typename WT, typename R = TapeRec<E, H, FF>>
 T2O_DEV void post_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restrict__ gs, const MaskedRec<WT>& rec,
                            int d, const PostCacheLean<E, H, FF>& c, const f4* gx, f4* gz, f4* gres, f4* ln2) {
   constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
-  using R = TapeRec<E, H, FF>;
 #pragma unroll
   for (int t = 0; t < ET; ++t) {
     ln2[t] += gx[t] * c.xh2[t];

@@ -567,6 +567,44 @@ T2O_DEV void dw_accumulate(float* __restrict__ ldsW, int ldw, const f4* dY, cons
   }
 }
 
+// bf16 staging tiles of the register-block contractions: tile j of a wave's
+// stage is [16 rows][16 features] bf16; a lane writes its T-layout f4 (row c,
+// features 4g..4g+3: one 8-byte store) and reads back the K-slice over rows
+// (feature c of rows 4g..4g+3) with one ds_read_b64_tr_b16.  Row r keeps its
+// four 8-byte chunks in the order chunk ^ ((r >> 2) & 3): the 16 writes of a
+// lane group (rows 0..15, one chunk) then cover 32 distinct store banks
+// (unswizzled: 4-way), and every transposed read still takes whole 32-B rows.
+T2O_DEV void stage_tile_bf(__bf16* sb, int j, f4 v) {
+  const int c = lane_c(), g = lane_g();
+  *reinterpret_cast<bf4*>(sb + j * 256 + c * 16 + 4 * (g ^ ((c >> 2) & 3))) = to_bf4(v);
+}
+T2O_DEV bf4 kslice_tile_bf(const __bf16* sb, int j) {
+  typedef __attribute__((address_space(3))) s4v lds_s4v;
+  const int c = lane_c(), g = lane_g();
+  const __bf16* p = sb + j * 256 + (4 * g + (c >> 2)) * 16 + 4 * ((c & 3) ^ g);
+  return __builtin_bit_cast(bf4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(p)));
+}
+
+// acc[o][i] += Σ_rows dY[o] ⊗ X[i] with X already staged (stage_tile_bf) in
+// tiles xt .. xt+IT-1 of the wave's stage — e.g. by an earlier phase of the
+// same wave — and dY streamed through tile yt.
+template <int OT, int IT>
+T2O_DEV void dw_accumulate_prestaged(f4 (&acc)[OT][IT], const f4* dY, float* stage, int xt, int yt) {
+  __bf16* sb = reinterpret_cast<__bf16*>(stage);
+  bf4 xb[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) xb[i] = kslice_tile_bf(sb, xt + i);
+#pragma unroll
+  for (int o = 0; o < OT; ++o) {
+    stage_tile_bf(sb, yt, dY[o]);
+    asm volatile("" ::: "memory");
+    const bf4 ab = kslice_tile_bf(sb, yt);
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < IT; ++i) acc[o][i] = mfma_b16(ab, xb[i], acc[o][i]);
+  }
+}
+
 // Same contraction, accumulated into MFMA accumulator registers acc[o][i]
 // (a wave-private gradient block that stays in registers across calls).
 // BF: bf16 operands, one 16x16x16 MFMA over the 16 rows per tile pair.
@@ -585,26 +623,18 @@ T2O_DEV void dw_accumulate_regs(f4 (&acc)[OT][IT], const f4* dY, const f4* X, fl
     // 4-way), and every transposed read still takes whole 32-B rows.
     static_assert((IT + 1) * 128 <= StageDims<NS>::FLOATS, "stage too small");
     __bf16* sb = reinterpret_cast<__bf16*>(stage);
-    typedef __attribute__((address_space(3))) s4v lds_s4v;
-    const int wo = c * 16 + 4 * (g ^ ((c >> 2) & 3));  // this lane's write: row c, chunk g
-    const int ro = (4 * g + (c >> 2)) * 16 + 4 * ((c & 3) ^ g);  // transposed read: row 4g + c/4, chunk c & 3
-    auto stw = [&](int j, f4 v) { *reinterpret_cast<bf4*>(sb + j * 256 + wo) = to_bf4(v); };
-    auto trk = [&](int j) {
-      const __bf16* p = sb + j * 256 + ro;
-      return __builtin_bit_cast(bf4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4v*)(p)));
-    };
 #pragma unroll
-    for (int i = 0; i < IT; ++i) stw(1 + i, X[i]);
+    for (int i = 0; i < IT; ++i) stage_tile_bf(sb, 1 + i, X[i]);
     bf4 xb[IT];
 #pragma unroll
     for (int o = 0; o < OT; ++o) {
-      stw(0, dY[o]);
+      stage_tile_bf(sb, 0, dY[o]);
       asm volatile("" ::: "memory");  // a wave's LDS accesses complete in order; keep the compiler's order too
       if (o == 0) {
 #pragma unroll
-        for (int i = 0; i < IT; ++i) xb[i] = trk(1 + i);
+        for (int i = 0; i < IT; ++i) xb[i] = kslice_tile_bf(sb, 1 + i);
       }
-      const bf4 ab = trk(0);
+      const bf4 ab = kslice_tile_bf(sb, 0);
       asm volatile("" ::: "memory");
 #pragma unroll
       for (int i = 0; i < IT; ++i) acc[o][i] = mfma_b16(ab, xb[i], acc[o][i]);
@@ -722,6 +752,20 @@ struct TapeRec {
   static constexpr int GR2 = Y + E;           // dL/d(W2 f + c2 + y)(E)   W2: dY, gf1, c2
   static constexpr int XH1 = GR2 + E;         // LN1 x̂             (E)   g1
   static constexpr int GY = XH1 + E;          // dL/dy              (E)   g1, n1
+  static constexpr int SIZE = GY + E;
+};
+
+// The agent's pipelined bf16 BPTT accumulates dM and dN in registers
+// (dw_accumulate_prestaged) and tapes only the rest: the lean agent record.
+// X, GU, Z are absent (negative offsets).
+template <int E, int H, int FF>
+struct TapeRecA {
+  static constexpr int X = -1, GU = -1, Z = -1;
+  static constexpr int GRES = 0;
+  static constexpr int Y = GRES + E;
+  static constexpr int GR2 = Y + E;
+  static constexpr int XH1 = GR2 + E;
+  static constexpr int GY = XH1 + E;
   static constexpr int SIZE = GY + E;
 };
 

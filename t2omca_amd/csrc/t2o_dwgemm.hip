@@ -74,9 +74,12 @@ template <typename TT> struct DwTraits;
 template <> struct DwTraits<__bf16> { static constexpr int TG = 2, PADC = 2; };  // tiles per group, pad chunks
 template <> struct DwTraits<float> { static constexpr int TG = 1, PADC = 1; };
 
-template <int E, int H, int FF, int D, typename TT, int RT = 16>
+// FMT 0: the full record (TapeRec); 1: the lean agent record (TapeRecA: dM and
+// dN were accumulated by the BPTT kernel, roles 0 / 1 keep only their vectors)
+template <int E, int H, int FF, int D, typename TT, int RT = 16, int FMT = 0>
 struct DwDims {
-  using R = TapeRec<E, H, FF>;
+  using R = typename std::conditional<FMT == 1, TapeRecA<E, H, FF>, TapeRec<E, H, FF>>::type;
+  static constexpr bool MN = R::GU >= 0;  // dM / dN operands on the tape
   static constexpr int ET = E / 16, HET = H * ET, FT = FF / 16, FH = FT / 2;
   static constexpr bool BF = sizeof(TT) == 2;
   static constexpr int TG = DwTraits<TT>::TG;
@@ -167,12 +170,12 @@ T2O_DEV f4 kmma(f4 a, f4 b, f4 acc) {
 
 // Role state: the accumulators of one wave.  ROLE 0 dM (+ g1, n1), 1 dN (+ bu),
 // 2/3 FFN half 0/1 (+ c1 of the half; role 2 also c2).
-template <int ROLE, int E, int H, int FF, int D, typename TT>
+template <int ROLE, int E, int H, int FF, int D, typename TT, int FMT>
 struct DwRole;
 
-template <int E, int H, int FF, int D, typename TT>
-struct DwRole<0, E, H, FF, D, TT> {
-  using Dm = DwDims<E, H, FF, D, TT>;
+template <int E, int H, int FF, int D, typename TT, int FMT>
+struct DwRole<0, E, H, FF, D, TT, FMT> {
+  using Dm = DwDims<E, H, FF, D, TT, 16, FMT>;
   using R = typename Dm::R;
   using Frag = typename std::conditional<Dm::BF, bf4, f4>::type;
   f4 acc[Dm::HET][Dm::ET];  // dM[gu feature][x feature]
@@ -187,14 +190,16 @@ struct DwRole<0, E, H, FF, D, TT> {
   }
   T2O_DEV void tile(const TT* t) {
     constexpr int S = Dm::RSTR;
-    Frag xb[Dm::ET];
+    if constexpr (Dm::MN) {
+      Frag xb[Dm::ET];
 #pragma unroll
-    for (int i = 0; i < Dm::ET; ++i) xb[i] = kslice<S>(t, R::X + 16 * i);
+      for (int i = 0; i < Dm::ET; ++i) xb[i] = kslice<S>(t, R::X + 16 * i);
 #pragma unroll
-    for (int o = 0; o < Dm::HET; ++o) {
-      const Frag ab = kslice<S>(t, R::GU + 16 * o);
+      for (int o = 0; o < Dm::HET; ++o) {
+        const Frag ab = kslice<S>(t, R::GU + 16 * o);
 #pragma unroll
-      for (int i = 0; i < Dm::ET; ++i) acc[o][i] = kmma(ab, xb[i], acc[o][i]);
+        for (int i = 0; i < Dm::ET; ++i) acc[o][i] = kmma(ab, xb[i], acc[o][i]);
+      }
     }
 #pragma unroll
     for (int i = 0; i < Dm::ET; ++i) {
@@ -204,15 +209,15 @@ struct DwRole<0, E, H, FF, D, TT> {
     }
   }
   T2O_DEV void finish(const DwGemmArgs& a, float* slab, int d) {
-    dw_tiles_store<Dm::HET, Dm::ET>(slab + a.G.M[d], E, acc);
+    if constexpr (Dm::MN) dw_tiles_store<Dm::HET, Dm::ET>(slab + a.G.M[d], E, acc);
     dw_vec_store<Dm::ET>(slab + a.G.n1[d], vn1);
     dw_vec_store<Dm::ET>(slab + a.G.g1[d], vg1);
   }
 };
 
-template <int E, int H, int FF, int D, typename TT>
-struct DwRole<1, E, H, FF, D, TT> {
-  using Dm = DwDims<E, H, FF, D, TT>;
+template <int E, int H, int FF, int D, typename TT, int FMT>
+struct DwRole<1, E, H, FF, D, TT, FMT> {
+  using Dm = DwDims<E, H, FF, D, TT, 16, FMT>;
   using R = typename Dm::R;
   using Frag = typename std::conditional<Dm::BF, bf4, f4>::type;
   f4 acc[Dm::ET][Dm::HET];  // dN[gres feature][z feature]
@@ -233,15 +238,17 @@ struct DwRole<1, E, H, FF, D, TT> {
       gb[o] = kslice<S>(t, R::GRES + 16 * o);
       vbu[o] += bsum4(gb[o]);
     }
+    if constexpr (Dm::MN) {
 #pragma unroll
-    for (int i = 0; i < Dm::HET; ++i) {
-      const Frag zb = kslice<S>(t, R::Z + 16 * i);
+      for (int i = 0; i < Dm::HET; ++i) {
+        const Frag zb = kslice<S>(t, R::Z + 16 * i);
 #pragma unroll
-      for (int o = 0; o < Dm::ET; ++o) acc[o][i] = kmma(gb[o], zb, acc[o][i]);
+        for (int o = 0; o < Dm::ET; ++o) acc[o][i] = kmma(gb[o], zb, acc[o][i]);
+      }
     }
   }
   T2O_DEV void finish(const DwGemmArgs& a, float* slab, int d) {
-    dw_tiles_store<Dm::ET, Dm::HET>(slab + a.G.N[d], H * E, acc);
+    if constexpr (Dm::MN) dw_tiles_store<Dm::ET, Dm::HET>(slab + a.G.N[d], H * E, acc);
     dw_vec_store<Dm::ET>(slab + a.G.bu[d], vbu);
   }
 };
@@ -252,9 +259,9 @@ struct DwRole<1, E, H, FF, D, TT> {
 // contraction), then dW2[e][J] += gr2 ⊗ relu(f1), dW1[J][e] += gf1 ⊗ y.
 // Weight fragments: bf16 from the workgroup's LDS copy of the pack's
 // (swizzled) bf16 image; fp32 straight from the pack (L2-resident).
-template <int HALF, int E, int H, int FF, int D, typename TT>
+template <int HALF, int E, int H, int FF, int D, typename TT, int FMT>
 struct DwFfn {
-  using Dm = DwDims<E, H, FF, D, TT>;
+  using Dm = DwDims<E, H, FF, D, TT, 16, FMT>;
   using R = typename Dm::R;
   static constexpr int ET = Dm::ET, FH = Dm::FH;
   using Frag = typename std::conditional<Dm::BF, bf4, f4>::type;
@@ -342,20 +349,20 @@ struct DwFfn {
     if (HALF == 0) dw_vec_store<ET>(slab + a.G.c2[d], vc2);
   }
 };
-template <int E, int H, int FF, int D, typename TT>
-struct DwRole<2, E, H, FF, D, TT> : DwFfn<0, E, H, FF, D, TT> {};
-template <int E, int H, int FF, int D, typename TT>
-struct DwRole<3, E, H, FF, D, TT> : DwFfn<1, E, H, FF, D, TT> {};
+template <int E, int H, int FF, int D, typename TT, int FMT>
+struct DwRole<2, E, H, FF, D, TT, FMT> : DwFfn<0, E, H, FF, D, TT, FMT> {};
+template <int E, int H, int FF, int D, typename TT, int FMT>
+struct DwRole<3, E, H, FF, D, TT, FMT> : DwFfn<1, E, H, FF, D, TT, FMT> {};
 
 // One wave's whole launch for its role (every role runs the same pipeline and
 // the same barrier sequence; the roles only differ in what they read).
 // Pipeline: LDS double buffer, register ring of two, prefetch distance 2.
-template <int ROLE, int E, int H, int FF, int D, typename TT, int RT>
+template <int ROLE, int E, int H, int FF, int D, typename TT, int RT, int FMT>
 T2O_DEV void dw_run(const DwGemmArgs& a, TT* buf0, TT* buf1, const TT* wlds, int d) {
-  using Dm = DwDims<E, H, FF, D, TT, RT>;
+  using Dm = DwDims<E, H, FF, D, TT, RT, FMT>;
   const int64_t ngroups = (a.ntiles + Dm::TG - 1) / Dm::TG;
   const int64_t nj = (int64_t)blockIdx.x < ngroups ? (ngroups - 1 - blockIdx.x) / gridDim.x + 1 : 0;
-  DwRole<ROLE, E, H, FF, D, TT> st;
+  DwRole<ROLE, E, H, FF, D, TT, FMT> st;
   st.init(a, d, wlds);
   auto compute = [&](const TT* buf) {
 #pragma unroll
@@ -386,9 +393,9 @@ T2O_DEV void dw_run(const DwGemmArgs& a, TT* buf0, TT* buf1, const TT* wlds, int
   st.finish(a, a.slabs + (size_t)blockIdx.x * a.slab_stride, d);
 }
 
-template <int E, int H, int FF, int D, int KIND, typename TT, int RT>
+template <int E, int H, int FF, int D, int KIND, typename TT, int RT, int FMT>
 __global__ __launch_bounds__(256 * D) void dw_gemm_kernel(DwGemmArgs a) {
-  using Dm = DwDims<E, H, FF, D, TT, RT>;
+  using Dm = DwDims<E, H, FF, D, TT, RT, FMT>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   TT* const buf0 = reinterpret_cast<TT*>(smem);
   TT* const buf1 = buf0 + Dm::GELEM;
@@ -422,17 +429,17 @@ __global__ __launch_bounds__(256 * D) void dw_gemm_kernel(DwGemmArgs a) {
   // gaps (A/B: mixer_dw 0.256 -> 0.249 ms; prioritising the light roles: no gain)
   if (role >= 2) __builtin_amdgcn_s_setprio(1);
   switch (role) {  // wave-uniform; the four paths issue the same barriers
-    case 0: dw_run<0, E, H, FF, D, TT, RT>(a, buf0, buf1, wlds, d); break;
-    case 1: dw_run<1, E, H, FF, D, TT, RT>(a, buf0, buf1, wlds, d); break;
-    case 2: dw_run<2, E, H, FF, D, TT, RT>(a, buf0, buf1, wlds, d); break;
-    default: dw_run<3, E, H, FF, D, TT, RT>(a, buf0, buf1, wlds, d); break;
+    case 0: dw_run<0, E, H, FF, D, TT, RT, FMT>(a, buf0, buf1, wlds, d); break;
+    case 1: dw_run<1, E, H, FF, D, TT, RT, FMT>(a, buf0, buf1, wlds, d); break;
+    case 2: dw_run<2, E, H, FF, D, TT, RT, FMT>(a, buf0, buf1, wlds, d); break;
+    default: dw_run<3, E, H, FF, D, TT, RT, FMT>(a, buf0, buf1, wlds, d); break;
   }
 }
 
-template <int E, int H, int FF, int D, int NE, typename TT>
+template <int E, int H, int FF, int D, int NE, typename TT, int FMT>
 int launch_dw_gemm(int kind, const void* tape, int64_t ntiles, const float* pack, float* slabs, const t2o_layout& L,
                    const t2o_layout& G, int nslab, hipStream_t stream) {
-  using Dm = DwDims<E, H, FF, D, TT>;
+  using Dm = DwDims<E, H, FF, D, TT, 16, FMT>;
   if (nslab < 1) return T2O_EINVAL;
   DwGemmArgs a{};
   a.tape = tape;
@@ -444,7 +451,7 @@ int launch_dw_gemm(int kind, const void* tape, int64_t ntiles, const float* pack
   a.G = G;
   const size_t lds = sizeof(TT) * ((size_t)2 * Dm::GELEM + (Dm::BF ? (size_t)D * 2 * FF * E : 0));
   constexpr int RTM = mixer_tape_records(NE);  // the mixer's query rows per tape tile
-  auto kern = kind == 0 ? dw_gemm_kernel<E, H, FF, D, 0, TT, 16> : dw_gemm_kernel<E, H, FF, D, 1, TT, RTM>;
+  auto kern = kind == 0 ? dw_gemm_kernel<E, H, FF, D, 0, TT, 16, FMT> : dw_gemm_kernel<E, H, FF, D, 1, TT, RTM, 0>;
   if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(nslab), dim3(256 * D), lds, stream, a);
@@ -462,17 +469,30 @@ extern "C" int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t tiles) {
   return L->prec ? (elems + 1) / 2 : elems;
 }
 
-extern "C" int t2o_bwd_tape_contract(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
-                                     float* gslabs, int nslab, void* stream) {
-  if (!L || !pack || !tape || !gslabs || tiles < 0 || nslab < 1) return T2O_EINVAL;
+extern "C" int t2o_bwd_tape_contract_ex(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
+                                        float* gslabs, int nslab, int rec_format, void* stream) {
+  if (!L || !pack || !tape || !gslabs || tiles < 0 || nslab < 1 || rec_format < 0 || rec_format > 1 ||
+      (rec_format == 1 && (L->kind != 0 || !L->prec || L->generic)))
+    return T2O_EINVAL;
   if (L->generic) return gen_tape_contract(L, tape, tiles, gslabs, nslab, (hipStream_t)stream);
   t2o_layout G;
   grad_layout(*L, G);
   int rc = T2O_EUNSUPPORTED;
+  if (rec_format == 1) {
+    T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
+                 rc = (launch_dw_gemm<E_, H_, FF_, D_, NE_, __bf16, 1>(0, tape, tiles, pack, gslabs, *L, G, nslab,
+                                                                      (hipStream_t)stream)));
+    return rc;
+  }
   T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
-               rc = (L->prec ? launch_dw_gemm<E_, H_, FF_, D_, NE_, __bf16>(L->kind, tape, tiles, pack, gslabs, *L, G,
-                                                                       nslab, (hipStream_t)stream)
-                             : launch_dw_gemm<E_, H_, FF_, D_, NE_, float>(L->kind, tape, tiles, pack, gslabs, *L, G,
-                                                                      nslab, (hipStream_t)stream)));
+               rc = (L->prec ? launch_dw_gemm<E_, H_, FF_, D_, NE_, __bf16, 0>(L->kind, tape, tiles, pack, gslabs, *L,
+                                                                          G, nslab, (hipStream_t)stream)
+                             : launch_dw_gemm<E_, H_, FF_, D_, NE_, float, 0>(L->kind, tape, tiles, pack, gslabs, *L, G,
+                                                                         nslab, (hipStream_t)stream)));
   return rc;
+}
+
+extern "C" int t2o_bwd_tape_contract(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
+                                     float* gslabs, int nslab, void* stream) {
+  return t2o_bwd_tape_contract_ex(L, pack, tape, tiles, gslabs, nslab, 0, stream);
 }

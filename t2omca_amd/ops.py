@@ -194,7 +194,8 @@ def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchose
                                      ctypes.byref(nslab), ptr(tape), ptr(gh0), B, T, A, stream_ptr()),
           "agent_unroll_bwd")
     _mark(timer, "end:agent_bwd")
-    return tape_contract(shape, pack, tape, tiles, slabs, nslab.value, timer, "agent_dw"), gh0
+    fmt = int(lib().t2o_agent_bwd_tape_format(ctypes.byref(L), int(hmid is not None)))
+    return tape_contract(shape, pack, tape, tiles, slabs, nslab.value, timer, "agent_dw", fmt), gh0
 
 
 def _mstrides(t):
@@ -255,14 +256,15 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
     return (o_on, o_tg) if pack_tg is not None else o_on
 
 
-def tape_contract(shape: NetShape, pack, tape, tiles, slabs, nslab, timer=None, tag="dw"):
+def tape_contract(shape: NetShape, pack, tape, tiles, slabs, nslab, timer=None, tag="dw", fmt=0):
     """Fill the M/N/W1/W2 regions of the backward's slabs from its tape (pack =
-    the pack the backward used), then sum the slabs.  Returns the compact
+    the pack the backward used; fmt = the tape's record format,
+    t2o_agent_bwd_tape_format), then sum the slabs.  Returns the compact
     gradient block (on the current stream)."""
     L = shape.layout()
     _mark(timer, "begin:" + tag)
-    check(lib().t2o_bwd_tape_contract(ctypes.byref(L), ptr(pack), ptr(tape), int(tiles), ptr(slabs), int(nslab),
-                                      stream_ptr()), "bwd_tape_contract")
+    check(lib().t2o_bwd_tape_contract_ex(ctypes.byref(L), ptr(pack), ptr(tape), int(tiles), ptr(slabs), int(nslab),
+                                         int(fmt), stream_ptr()), "bwd_tape_contract")
     _mark(timer, "end:" + tag)
     gpack = torch.empty(L.grad_total, device=slabs.device)
     reduce_slabs(slabs, nslab, gpack)
