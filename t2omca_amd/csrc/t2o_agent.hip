@@ -462,6 +462,9 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
   for (int i = 0; i < HET; ++i)
 #pragma unroll
     for (int t = 0; t < ET; ++t) gM[i][t] = gN[t][i] = zero4();
+  if constexpr (ACC) {  // the first recompute's deferred contractions then add zeros
+    for (int i = lane; i < STAGE; i += 64) stage[i] = 0.f;
+  }
   // Both roles run the same loop body "recompute step; barrier; backward step;
   // barrier"; the block-0 wave starts one barrier late, so its recompute of a
   // step overlaps the block-1 backward of the same step and its backward the
@@ -544,7 +547,7 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
         if constexpr (CHUNK) agent_block_fwd_ch<E, H, NE, FF, true>(P, Lb, 0, h, ObsRow{ob, F}, xo, &cache);
         else if constexpr (ACC)
           agent_block_fwd_acc<E, H, NE, FF>(P, Lb, 0, h, o, xo, cache, MaskedRec<WT>(tile, tile_ok ? 16 : 0, Rec::SIZE),
-                                            stage);
+                                            stage, gM, gN, gWe);
         else agent_block_fwd_lean<E, H, NE, FF>(P, Lb, 0, h, o, xo, cache, MaskedRec<WT>(tile, tile_ok ? 16 : 0, Rec::SIZE));
       } else {
         f4 gx[ET], ghi[ET];
@@ -621,6 +624,7 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
     }
   }
   if (d == 1) __syncthreads();
+  if constexpr (ACC) agent_dw_deferred<E, H>(stage, gM, gN, gWe);  // the last backward phase's
   if (tile_ok) {
     if constexpr (ACC) {
       flush_tiles_g<HET, ET>(gs + Gb.M[0], E, gM);

@@ -129,23 +129,71 @@ T2O_DEV void agent_block_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d, 
 
 // Register-accumulating variant of the lean pair (the pipelined bf16 BPTT):
 // dM = Σ gu ⊗ x and dN = Σ gres ⊗ z stay in MFMA accumulator registers over the
-// whole unroll instead of going to the tape (record TapeRecA).  Their row
-// operands known in the recompute phase — the block input x and the head
-// outputs z — are staged there (bf16 tiles of the wave's stage, transposed-read
-// ready), so the backward phase only streams gres / gu against them.  Stage
-// tiles: 0 streamed operand, 1..ET the head / embedding grads' staging
-// (dw_accumulate_regs), then z, then x.
+// whole unroll instead of going to the tape (record TapeRecA), and no weight
+// gradient is contracted on the dependent chain: the backward phase only
+// stages its operands (bf16 tiles of the wave's stage, transposed-read ready:
+// gres, gu and per head gz_h, ô_h, u_h, gw_h), and the wave's next phase — a
+// recompute, which has slack under the other wave's backward — contracts them
+// into dN, dM and dWe (agent_dw_deferred) before staging its own x and z.
+// Stage tiles per wave: 0..ET the head's gWo staging (dw_accumulate_regs), z,
+// x, gres, gu, then 2(ET+1) per head for dWe.
 template <int E, int H>
 struct AgentAccTiles {
   static constexpr int ET = E / 16, HET = H * ET;
-  static constexpr int ZT = 1 + ET, XT = ZT + HET, N = XT + ET;  // N: tiles per wave
+  static constexpr int ZT = 1 + ET, XT = ZT + HET, GREST = XT + ET, GUT = GREST + ET, WET = GUT + HET;
+  static constexpr int WEH = 2 * (ET + 1);  // per head: gz_h (ET), ô_h (1), u_h (ET), gw_h (1)
+  static constexpr int N = WET + H * WEH;    // tiles per wave
 };
+
+// the weight-grad contractions the previous backward phase of this wave staged
+template <int E, int H>
+T2O_DEV void agent_dw_deferred(float* __restrict__ stage, f4 (&gM)[H * (E / 16)][E / 16],
+                               f4 (&gN)[E / 16][H * (E / 16)], f4 (&gWe)[E / 16][1]) {
+  using Tl = AgentAccTiles<E, H>;
+  constexpr int ET = Tl::ET, HET = Tl::HET;
+  const __bf16* sb = reinterpret_cast<const __bf16*>(stage);
+  {  // dN += gres ⊗ z
+    bf4 zb[HET];
+#pragma unroll
+    for (int i = 0; i < HET; ++i) zb[i] = kslice_tile_bf(sb, Tl::ZT + i);
+#pragma unroll
+    for (int o = 0; o < ET; ++o) {
+      const bf4 a = kslice_tile_bf(sb, Tl::GREST + o);
+#pragma unroll
+      for (int i = 0; i < HET; ++i) gN[o][i] = mfma_b16(a, zb[i], gN[o][i]);
+    }
+  }
+  {  // dM += gu ⊗ x
+    bf4 xb[ET];
+#pragma unroll
+    for (int i = 0; i < ET; ++i) xb[i] = kslice_tile_bf(sb, Tl::XT + i);
+#pragma unroll
+    for (int o = 0; o < HET; ++o) {
+      const bf4 a = kslice_tile_bf(sb, Tl::GUT + o);
+#pragma unroll
+      for (int i = 0; i < ET; ++i) gM[o][i] = mfma_b16(a, xb[i], gM[o][i]);
+    }
+  }
+#pragma unroll
+  for (int hh = 0; hh < H; ++hh) {  // dWe += gz_h ⊗ ô_h + u_h ⊗ gw_h
+    const int b = Tl::WET + hh * Tl::WEH;
+    const bf4 ob = kslice_tile_bf(sb, b + ET), wb = kslice_tile_bf(sb, b + 2 * ET + 1);
+#pragma unroll
+    for (int t = 0; t < ET; ++t) {
+      gWe[t][0] = mfma_b16(kslice_tile_bf(sb, b + t), ob, gWe[t][0]);
+      gWe[t][0] = mfma_b16(kslice_tile_bf(sb, b + ET + 1 + t), wb, gWe[t][0]);
+    }
+  }
+}
 
 template <int E, int H, int NE, int FF, typename WT>
 T2O_DEV void agent_block_fwd_acc(const Wts<WT>& P, const t2o_layout& L, int d, const f4* h, const f4 (&o)[NE],
                                  f4* x, AgentCacheLean<E, H, NE, FF>& cache, const MaskedRec<WT>& rec,
-                                 float* __restrict__ stage) {
+                                 float* __restrict__ stage, f4 (&gM)[H * (E / 16)][E / 16],
+                                 f4 (&gN)[E / 16][H * (E / 16)], f4 (&gWe)[E / 16][1]) {
   using Tl = AgentAccTiles<E, H>;
+  agent_dw_deferred<E, H>(stage, gM, gN, gWe);
+  asm volatile("" ::: "memory");  // the staged operands are read before x / z overwrite theirs
   __bf16* sb = reinterpret_cast<__bf16*>(stage);
 #pragma unroll
   for (int t = 0; t < Tl::ET; ++t) stage_tile_bf(sb, Tl::XT + t, x[t]);
@@ -160,12 +208,15 @@ T2O_DEV void agent_block_fwd_acc(const Wts<WT>& P, const t2o_layout& L, int d, c
 // gh_in accumulates the grad wrt h through the key/value path (token 0), gbe the
 // grad wrt the embedding bias, gWe (MFMA register block, [E][16] as ET x 1 tiles)
 // the grad wrt the embedding weight.
-template <int E, int H, int NE, int FF, bool LEAN, typename WT>
+// DEFER: stage the dWe operands (AgentAccTiles) for agent_dw_deferred instead.
+template <int E, int H, int NE, int FF, bool LEAN, typename WT, bool DEFER = false>
 T2O_DEV void agent_attn_bwd(const Wts<WT>& P, const t2o_layout& L, float* __restrict__ stage, const f4* h,
                             const f4 (&o)[NE], const AgentCacheT<E, H, NE, FF, LEAN>& c, const f4* gz, f4* gu,
                             f4* gh_in, f4* gbe, f4 (&gWe)[E / 16][1]) {
   constexpr int ET = E / 16;
   constexpr bool BF = sizeof(WT) == 2;
+  using Tl = AgentAccTiles<E, H>;
+  __bf16* const sb = reinterpret_cast<__bf16*>(stage);
   const float* be = P.v + L.be;
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
@@ -185,7 +236,17 @@ T2O_DEV void agent_attn_bwd(const Wts<WT>& P, const t2o_layout& L, float* __rest
     f4 goh;
     matvec_tr<1, ET>(P, L.We, 16, L.WeT, E, gzh, &goh);
 #ifndef T2O_ABL_NODW  // ablation builds only: wrong gradients
-    dw_accumulate_regs<ET, 1, BF>(gWe, gzh, &c.oh[hh], stage);
+    if constexpr (DEFER) {
+      const int b = Tl::WET + hh * Tl::WEH;
+#pragma unroll
+      for (int t = 0; t < ET; ++t) {
+        stage_tile_bf(sb, b + t, gzh[t]);
+        stage_tile_bf(sb, b + ET + 1 + t, uh[t]);
+      }
+      stage_tile_bf(sb, b + ET, c.oh[hh]);
+    } else {
+      dw_accumulate_regs<ET, 1, BF>(gWe, gzh, &c.oh[hh], stage);
+    }
 #endif
     // softmax backward over [token 0, entities]; [gP, gp_0, goh·o_j] reduced in one batch
     float red[NE + 2];
@@ -222,7 +283,8 @@ T2O_DEV void agent_attn_bwd(const Wts<WT>& P, const t2o_layout& L, float* __rest
       gbe[t] += gc * uh[t];
     }
 #ifndef T2O_ABL_NODW
-    dw_accumulate_regs<ET, 1, BF>(gWe, uh, &gw, stage);
+    if constexpr (DEFER) stage_tile_bf(sb, Tl::WET + hh * Tl::WEH + 2 * ET + 1, gw);
+    else dw_accumulate_regs<ET, 1, BF>(gWe, uh, &gw, stage);
 #endif
   }
 }
@@ -278,13 +340,16 @@ T2O_DEV void agent_block_bwd_acc(const Wts<WT>& P, const t2o_layout& L, float* _
                                  f4 (&gN)[E / 16][H * (E / 16)]) {
   using Tl = AgentAccTiles<E, H>;
   constexpr int ET = E / 16, HET = H * ET;
+  __bf16* const sb = reinterpret_cast<__bf16*>(stage);
   f4 gz[HET], gres[ET];
   post_bwd_lean<E, H, FF, WT, TapeRecA<E, H, FF>>(P, L, gs, rec, d, c.post, gx, gz, gres, ln2);
-  dw_accumulate_prestaged<ET, HET>(gN, gres, stage, Tl::ZT, 0);  // dN += gres ⊗ z
+#pragma unroll
+  for (int t = 0; t < ET; ++t) stage_tile_bf(sb, Tl::GREST + t, gres[t]);  // dN += gres ⊗ z, deferred
   T2O_MARK(2);
   f4 gu[HET];
-  agent_attn_bwd<E, H, NE, FF, true>(P, L, stage, h, o, c, gz, gu, gh_in, gbe, gWe);
-  dw_accumulate_prestaged<HET, ET>(gM, gu, stage, Tl::XT, 0);  // dM += gu ⊗ x
+  agent_attn_bwd<E, H, NE, FF, true, WT, true>(P, L, stage, h, o, c, gz, gu, gh_in, gbe, gWe);
+#pragma unroll
+  for (int t = 0; t < HET; ++t) stage_tile_bf(sb, Tl::GUT + t, gu[t]);  // dM += gu ⊗ x, deferred
   f4 gxp[ET];
   matvec_tr<ET, HET>(P, L.M[d], E, L.MT[d], H * E, gu, gxp);
 #pragma unroll
