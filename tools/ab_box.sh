@@ -1,6 +1,6 @@
 #!/bin/bash
 # Run ON THE GPU BOX: interleaved A/B(/C...) bench of several builds of the library,
-# serial mode, 3 rounds.   tools/ab_box.sh <tag> <lib1.so> <lib2.so> ... [-- bench args]
+# serial mode (AB_SERIAL= for the overlapped default), 3 rounds.   tools/ab_box.sh <tag> <lib1.so> <lib2.so> ... [-- bench args]
 #   -> gpurun_out/<tag>/<name><round>.json and a median summary on stdout
 set -eu
 TAG=$1; shift
@@ -12,7 +12,7 @@ mkdir -p "$OUT"
 for i in 1 2 3; do
   for lib in "${LIBS[@]}"; do
     n=$(basename "$lib" .so)
-    T2O_LIB=$PWD/$lib timeout -k 10 200 python bench.py --no-cpu-baseline --no-fp32-companion --serial --steps 20 "$@" > "$OUT/$n$i.json"
+    T2O_LIB=$PWD/$lib timeout -k 10 200 python bench.py --no-cpu-baseline --no-fp32-companion ${AB_SERIAL---serial} --steps 20 "$@" > "$OUT/$n$i.json"
   done
 done
 python - "$OUT" "${LIBS[@]}" <<'PY'
