@@ -358,12 +358,13 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
 // one 16-row tile per wave (8,192 rows = 512 waves) it leaves half the SIMDs
 // idle.  Here each tile gets two waves: wave "d" owns block d (its forward
 // recompute, cache and backward) and the two interleave so that one's recompute
-// overlaps the other's backward (phases separated by workgroup barriers):
+// overlaps the other's backward (phases separated by the pair's barrier,
+// t2o_common.hpp PairBarrier):
 //   block-1 wave:  fwd(T-1) | bwd(T-1) | fwd(T-2) | bwd(T-2) | ...
 //   block-0 wave:     -     | fwd(T-1) | bwd(T-1) | fwd(T-2) | ...
 // Per step the dependent work is bwd1 -> bwd0 -> bwd1 ..., exchanged through
 // LDS (per lane: grad wrt the block-1 input and the block-1 key/value grad of h,
-// 1 -> 0; the recurrent grad wrt h_{t-1}, 0 -> 1), one workgroup barrier per
+// 1 -> 0; the recurrent grad wrt h_{t-1}, 0 -> 1), one pair barrier per
 // phase.  The backward of a block is the same code as in the single-wave
 // kernel, so records, slabs and the head grads are identical in meaning.
 // T2O_AGENT_BWD=single selects the single-wave kernel (A/B timing, parity cross-check)
@@ -428,7 +429,11 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
   float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
   const Wts<WT> P0 = stage_weights(smem, args.pack, L, nw, WT{});
   for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) gs[i] = 0.f;
+  int* const flags = reinterpret_cast<int*>(smem + lds_w + 2 * AGP_TILES * STAGE + AGP_TILES * agp_xch_floats<E>());
+  if (threadIdx.x < PAIR_FLAG_FLOATS) flags[threadIdx.x] = 0;
   __syncthreads();
+  // the tile's two waves synchronise pairwise (t2o_common.hpp PairBarrier)
+  PairBarrier pb = PairBarrier::make(flags, w);
 
   const int A = args.A, F = args.F, T = args.T;
   const int R = args.B * A;
@@ -519,7 +524,7 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
     }
   };
   load_step(T - 1);
-  if (d == 0) __syncthreads();
+  if (d == 0) pb.sync();
   for (int step = T - 1; step >= 0; --step) {
 #ifdef T2O_TIMELINE
     T2O_STAMP(2 * (T - 1 - step), 0);
@@ -614,7 +619,7 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
 #ifdef T2O_TIMELINE
       T2O_STAMP(2 * (T - 1 - step) + ph, 2 * (1 - ph));
 #endif
-      __syncthreads();
+      pb.sync();
       T2O_MARK(4);
 #ifdef T2O_TIMELINE
       T2O_STAMP(2 * (T - 1 - step) + ph, 3 - 2 * ph);
@@ -623,7 +628,7 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
 #endif
     }
   }
-  if (d == 1) __syncthreads();
+  if (d == 1) pb.sync();
   if constexpr (ACC) agent_dw_deferred<E, H>(stage, gM, gN, gWe);  // the last backward phase's
   if (tile_ok) {
     if constexpr (ACC) {
@@ -645,7 +650,8 @@ template <int E, int H, int D, int NE, int FF, typename WT>
 size_t bwd_pipe_lds_bytes(const t2o_layout& L) {
   const int64_t nw = L.fwd_total;
   return sizeof(float) * ((size_t)(lds_weight_floats<WT>(L, nw) + 15) / 16 * 16 +
-                          2 * AGP_TILES * agp_stage_floats<E, H, NE, WT>() + AGP_TILES * agp_xch_floats<E>());
+                          2 * AGP_TILES * agp_stage_floats<E, H, NE, WT>() + AGP_TILES * agp_xch_floats<E>() +
+                          PAIR_FLAG_FLOATS);
 }
 
 // which BPTT kernel launch_bwd picks: the pipelined one (depth 2, block inputs

@@ -503,6 +503,51 @@ __host__ __device__ inline int64_t lds_weight_floats(const t2o_layout& L, int64_
   return sizeof(WT) == 4 ? n : n / 2 + (L.fwd_total - L.vec_lo);
 }
 
+// Phase barrier of the two waves of one pipelined recurrence (the BPTT
+// kernels' block-1 / block-0 wave pairs: an episode of the mixer, a 16-row tile
+// of the agent).  Their only cross-wave dependencies run through the pair's
+// own LDS region, so each wave writes a phase counter in LDS and polls its
+// partner's instead of waiting for the whole workgroup: the other pairs' waves
+// keep issuing while this pair waits (mixer BPTT 0.666 -> 0.652 ms).  Both waves
+// of a pair must pass the same number of phases.  The wait is one inline-asm
+// block (this wave's LDS ops drained, its counter written, the partner's polled
+// with s_sleep between reads): a C++ spin loop kept values live across it and
+// doubled the mixer kernel's register spills.  -DT2O_PIPE_WG_BARRIER:
+// workgroup barriers instead (A/B).
+constexpr int PAIR_FLAG_FLOATS = 16;  // LDS counters, one per wave (<= 16 waves)
+struct PairBarrier {
+  uint32_t mine, other;  // LDS byte addresses of the two counters (wave-uniform)
+  int k;
+  // counters at `flags` (zeroed before a workgroup barrier); partner = wave w ^ 1
+  T2O_DEV static PairBarrier make(int* flags, int w) {
+    typedef __attribute__((address_space(3))) int lds_int;
+    const uint32_t fl = (uint32_t)(uintptr_t)(lds_int*)(flags);  // LDS byte address
+    return PairBarrier{fl + 4u * w, fl + 4u * (w ^ 1), 0};
+  }
+  T2O_DEV void sync() {
+#ifdef T2O_PIPE_WG_BARRIER
+    __syncthreads();
+#else
+    ++k;
+    int t;
+    asm volatile(
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "ds_write_b32 %[a], %[kv]\n\t"
+        "1:\n\t"
+        "ds_read_b32 %[t], %[b]\n\t"
+        "s_waitcnt lgkmcnt(0)\n\t"
+        "v_cmp_gt_i32 vcc, %[k], %[t]\n\t"
+        "s_cbranch_vccz 2f\n\t"
+        "s_sleep 1\n\t"
+        "s_branch 1b\n"
+        "2:"
+        : [t] "=&v"(t)
+        : [a] "v"(mine), [b] "v"(other), [kv] "v"(k), [k] "s"(k)
+        : "vcc", "memory");
+#endif
+  }
+};
+
 // ---- weight-gradient accumulation -------------------------------------------
 // dW[16*OT x 16*IT] += Σ_rows dY[row]ᵀ ⊗ X[row] over the wave's 16 rows, added
 // into an LDS accumulator (row-major, leading dim ldw) with ds_add_f32.

@@ -738,7 +738,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 // As the agent's pipelined BPTT (t2o_agent.hip, agent_bwd_pipe_kernel): each
 // wave of a pair owns one transformer block of one episode, and the two
 // interleave so that one's recompute overlaps the other's backward (phases
-// separated by workgroup barriers):
+// separated by the pair's barrier, t2o_common.hpp PairBarrier):
 //   block-1 wave: keys+fwd1(T-1) | head+bwd1(T-1) | keys+fwd1(T-2) | head+bwd1(T-2) | ...
 //   block-0 wave:        -       |   fwd0(T-1)    |  bwd0+X0(T-1)  |   fwd0(T-2)    | ...
 // The dependent chain per step is head -> bwd1 -> bwd0 -> hyper-token grads ->
@@ -855,7 +855,7 @@ T2O_DEV void mixp_load_stT(const MixerFwdArgs& fa, int b, int t, f4 (&stT)[MixDi
 // block-1 wave: key block + block-1 recompute, then head + block-1 backward
 template <int E, int H, int A, int FF, typename WT>
 T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_layout& L, const t2o_layout& Lb,
-                         const t2o_layout& Gb, float* __restrict__ gs, float* X0, float* R, int b) {
+                         const t2o_layout& Gb, float* __restrict__ gs, float* X0, float* R, int b, PairBarrier& pb) {
   using Dm = MixDims<E, A>;
   using Pd = MixPipeDims<E, A>;
   using In = MixPIn<E, A>;
@@ -899,7 +899,7 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
       for (int ft = 0; ft < ET; ++ft) x[ft] = cur.xm[ft];
       mixer_block_fwd_lean<E, H, KT, FF>(P, Lb, 0, K, Dm::LK, x, cache, rec);
     }
-    __syncthreads();
+    pb.sync();
     {  // ---- backward: mixing head, block 1
       const Wts<WT> P = step_view(P0);
       float ghw[3];
@@ -973,9 +973,9 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
         for (int ft = 0; ft < ET; ++ft) st4(R + Pd::XCH + c * E + 16 * ft + 4 * g, gx[ft]);
       }
     }
-    __syncthreads();
+    pb.sync();
   }
-  __syncthreads();  // the block-0 wave's last backward phase
+  pb.sync();  // the block-0 wave's last backward phase
   vec_accumulate_g<ET>(gs + Gb.g2[0], &ln2[0]);
   vec_accumulate_g<ET>(gs + Gb.n2[0], &ln2[ET]);
   if (fv) unsafeAtomicAdd(gs + Gb.Wo + f, gWo);
@@ -985,7 +985,7 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
 // block-0 wave: block-0 recompute, then block-0 backward and the step's key grads
 template <int E, int H, int A, int FF, typename WT>
 T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_layout& Lb, const t2o_layout& Gb,
-                         float* __restrict__ gs, const float* X0, float* R, int b) {
+                         float* __restrict__ gs, const float* X0, float* R, int b, PairBarrier& pb) {
   using Dm = MixDims<E, A>;
   using Pd = MixPipeDims<E, A>;
   using Rec = TapeRec<E, H, FF>;
@@ -1002,7 +1002,7 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
 #pragma unroll
   for (int i = 0; i < ET; ++i) ln2[i] = ln2[ET + i] = gWe[i] = zero4();
   f4 stT[Dm::ST];
-  __syncthreads();  // one phase behind the block-1 wave
+  pb.sync();  // one phase behind the block-1 wave
   for (int t = T - 1; t >= 0; --t) {
     const size_t bt = (size_t)b * T + t;
     // tape tiles of exactly the Q query rows (mixer_tape_records)
@@ -1019,7 +1019,7 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
       for (int ft = 0; ft < ET; ++ft) x[ft] = c < Dm::Q ? ld4(X0 + (Dm::NS + c) * Dm::LDX + 16 * ft + 4 * g) : zero4();
       mixer_block_fwd_lean<E, H, KT, FF>(P, Lb, 0, K, Dm::LK, x, cache, rec);
     }
-    __syncthreads();
+    pb.sync();
     {  // ---- backward: block 0, then the step's key-token grads
       const Wts<WT> P = step_view(P0);
       f4 gX0[KT][ET], gx[ET];
@@ -1073,7 +1073,7 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
         for (int k = 0; k < 3; ++k) args.ghw0[((size_t)b * 3 + k) * E + f] = R[(Dm::NS + A + k) * E + f];
       }
     }
-    __syncthreads();
+    pb.sync();
   }
 #pragma unroll
   for (int ft = 0; ft < ET; ++ft)
@@ -1120,14 +1120,17 @@ __global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) 
   for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) gs[i] = 0.f;
   if (d == 1)
     for (int i = threadIdx.x & 63; i < Dm::X0F; i += 64) X0[i] = 0.f;
+  int* const flags = reinterpret_cast<int*>(smem + args.lds_w + args.waves * MixPipeDims<E, A>::PAIRF);
+  if (threadIdx.x < PAIR_FLAG_FLOATS) flags[threadIdx.x] = 0;
   __syncthreads();
+  PairBarrier pb = PairBarrier::make(flags, w);  // partner: the pair's other wave
   const int b = blockIdx.x * args.waves + pr;  // the launcher makes every pair valid
   const t2o_layout Lb = block_view(L, d), Gb = block_view(G, d);
   // the block-0 wave issues first on its SIMD (A/B: mixer_bwd 0.663 -> 0.654 ms;
   // prioritising the block-1 wave instead costs +0.011 ms)
   if (d == 0) __builtin_amdgcn_s_setprio(1);
-  if (d == 1) mixp_block1<E, H, A, FF, WT>(args, P0, L, Lb, Gb, gs, X0, R, b);
-  else mixp_block0<E, H, A, FF, WT>(args, P0, Lb, Gb, gs, X0, R, b);
+  if (d == 1) mixp_block1<E, H, A, FF, WT>(args, P0, L, Lb, Gb, gs, X0, R, b, pb);
+  else mixp_block0<E, H, A, FF, WT>(args, P0, Lb, Gb, gs, X0, R, b, pb);
 }
 
 template <int E, int H, int D, int A, int FF, typename WT>
@@ -1139,7 +1142,8 @@ int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t 
     if (args.xmid && !mixer_bwd_single_wave()) {
       const int lds_w = (int)((lds_weight_floats<WT>(L, mixp_weight_elems<WT>(L)) + 15) / 16 * 16);
       for (int pairs = 4; pairs >= 1; pairs >>= 1) {
-        const size_t lds = sizeof(float) * ((size_t)lds_w + (size_t)pairs * MixPipeDims<E, A>::PAIRF);
+        const size_t lds =
+            sizeof(float) * ((size_t)lds_w + (size_t)pairs * MixPipeDims<E, A>::PAIRF + PAIR_FLAG_FLOATS);
         if (lds > 160 * 1024 || args.f.B % pairs) continue;
         args.waves = pairs;
         args.lds_w = lds_w;
