@@ -515,6 +515,11 @@ __host__ __device__ inline int64_t lds_weight_floats(const t2o_layout& L, int64_
 // doubled the mixer kernel's register spills.  -DT2O_PIPE_WG_BARRIER:
 // workgroup barriers instead (A/B).
 constexpr int PAIR_FLAG_FLOATS = 16;  // LDS counters, one per wave (<= 16 waves)
+#ifndef T2O_PAIR_SLEEP  // s_sleep argument between polls (64 cycles per unit)
+#define T2O_PAIR_SLEEP 1
+#endif
+#define T2O_STR2(x) #x
+#define T2O_STR(x) T2O_STR2(x)
 struct PairBarrier {
   uint32_t mine, other;  // LDS byte addresses of the two counters (wave-uniform)
   int k;
@@ -538,7 +543,7 @@ struct PairBarrier {
         "s_waitcnt lgkmcnt(0)\n\t"
         "v_cmp_gt_i32 vcc, %[k], %[t]\n\t"
         "s_cbranch_vccz 2f\n\t"
-        "s_sleep 1\n\t"
+        "s_sleep " T2O_STR(T2O_PAIR_SLEEP) "\n\t"
         "s_branch 1b\n"
         "2:"
         : [t] "=&v"(t)
