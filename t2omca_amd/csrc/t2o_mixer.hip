@@ -1126,9 +1126,15 @@ __global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) 
   PairBarrier pb = PairBarrier::make(flags, w);  // partner: the pair's other wave
   const int b = blockIdx.x * args.waves + pr;  // the launcher makes every pair valid
   const t2o_layout Lb = block_view(L, d), Gb = block_view(G, d);
-  // the block-0 wave issues first on its SIMD (A/B: mixer_bwd 0.663 -> 0.654 ms;
-  // prioritising the block-1 wave instead costs +0.011 ms)
-  if (d == 0) __builtin_amdgcn_s_setprio(1);
+  // the block-1 wave issues first on its SIMD.  With pair barriers (each pair
+  // waits only for itself) that is the head + bwd1 end of the dependent chain:
+  // A/B, overlapped, 3 rounds: block 1 mixer_bwd 0.596 ms / update 2.556 ms,
+  // block 0 0.634 / 2.602, none 0.637 / 2.586 (profiles/r2_pb/r2_prio_ovl/).
+  // (Under workgroup barriers block 0 had measured better: 0.654 vs 0.665.)
+#ifndef T2O_MIXP_PRIO_BLOCK  // the block whose waves issue first on their SIMD (-1: none; A/B builds)
+#define T2O_MIXP_PRIO_BLOCK 1
+#endif
+  if (T2O_MIXP_PRIO_BLOCK >= 0 && d == T2O_MIXP_PRIO_BLOCK) __builtin_amdgcn_s_setprio(1);
   if (d == 1) mixp_block1<E, H, A, FF, WT>(args, P0, L, Lb, Gb, gs, X0, R, b, pb);
   else mixp_block0<E, H, A, FF, WT>(args, P0, Lb, Gb, gs, X0, R, b, pb);
 }
