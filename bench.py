@@ -10,6 +10,10 @@ in HBM (t2omca_amd.synthetic, SURVEY.md §8 d).  One agent-transition = one
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
+`--gpus N` with N > 1 from a plain process starts the N ranks itself
+(torch.distributed.run on 127.0.0.1, one process per GPU, RCCL); under a
+launcher (WORLD_SIZE set) each process is one rank.
+
 Data parallel (weak scaling): every rank trains on its own 1024-episode shard
 and the flat gradient (+ Σ mask) is all-reduced over RCCL once per update.
 Rank 0 prints ONE JSON line.  Per-kernel times come from HIP events recorded
@@ -271,12 +275,53 @@ def expand_bench(args, world, rank, dev):
         dist.destroy_process_group()
 
 
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(argv, n, port):
+    """The command that runs this bench as `n` ranks, one process per GPU, over
+    torch.distributed.run on 127.0.0.1 (the driver's own N > 1 invocation)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def needs_launch(args, environ):
+    """`--gpus N` (N > 1) started as a plain process: this process starts the N
+    ranks itself instead of timing one GPU."""
+    return args.gpus > 1 and "WORLD_SIZE" not in environ
+
+
+def launch(args, argv):
+    """Run the N ranks as child processes (nothing in this parent has touched the
+    GPU: torch.cuda.device_count() does not initialise it on this image) and exit
+    with their status.  Each child binds cuda:<LOCAL_RANK>; rank 0 prints the line."""
+    import subprocess
+    backend = os.environ.get("T2O_DIST_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and ndev < args.gpus:
+        sys.exit(f"bench.py --gpus {args.gpus}: only {ndev} HIP devices visible (RCCL needs one GPU per rank; "
+                 f"T2O_DIST_BACKEND=gloo rehearses the ranks on fewer devices)")
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    r = subprocess.run(launcher_cmd(argv, args.gpus, free_port()), env=env)
+    sys.exit(r.returncode)
+
+
 def main():
     args = parse()
     if args.print_workload_tag:
         print(workload_tag(args))
         return
+    if needs_launch(args, os.environ):
+        return launch(args, sys.argv[1:])
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}; reporting the real world size",
+              file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # T2O_DIST_BACKEND=gloo rehearses the multi-rank path on a box with fewer GPUs

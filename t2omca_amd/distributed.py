@@ -10,7 +10,11 @@ DP update equal to the full-batch update:
     loss = Σ_b w_b Σ_t ½ td² m / Σ_all m   ->   grad = Σ_r g_r / Σ_r M_r
 
 At E = 32 that buffer is 84,007 floats (336 KB): latency-bound over xGMI, so
-no bucketing or overlap machinery is warranted.
+it is not bucketed further.  It is split in two at the agent / mixer boundary
+only because the mixer half is final a whole kernel (the agent BPTT) earlier:
+that half's all-reduce is issued from the side stream as soon as it is
+unfolded and runs under the agent BPTT (``allreduce_async``), so only the
+agent half's latency stays on the critical path.
 
 Replicas start identical and stay identical: the learner broadcasts its
 parameters, target parameters and Adam moments from rank 0 when it is built
@@ -37,6 +41,24 @@ def allreduce_grad_and_mask(buf, group=None):
     if world_size(group) > 1:
         dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group)
     return buf
+
+
+def allreduce_async(buf, group=None):
+    """Start an in-place SUM all-reduce of `buf` ordered after the work already
+    queued on the CURRENT stream; returns a handle for ``wait_all`` (None
+    without a process group).  The learner issues the mixer half of the
+    gradient (+ Σ mask) from the side stream as soon as it is unfolded, so it
+    runs under the agent BPTT, and the agent half after the agent's unfold."""
+    if world_size(group) > 1:
+        return dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group, async_op=True)
+    return None
+
+
+def wait_all(works):
+    """Make the current stream wait for every started all-reduce."""
+    for w in works:
+        if w is not None:
+            w.wait()
 
 
 def broadcast_state(tensors, group=None, src=0):

@@ -19,7 +19,9 @@ priorities are copied out):
   mixer BPTT -> dL/dq_chosen, dL/dhidden           t2o_mixer_unroll_bwd + slab reduce
   agent BPTT                                       t2o_agent_unroll_bwd + slab reduce
   unfold grads into the reference parameter order  t2o_unpack_grads x2
-  [data parallel: one all_reduce of the flat grad + Σ mask over RCCL]
+  [data parallel: all_reduce of the flat grad + Σ mask over RCCL, in two
+   halves: the mixer's (+ Σ mask) from the side stream under the agent BPTT,
+   the agent's after its unfold]
   clip_grad_norm_ + Adam                           t2o_adam_step
 """
 import dataclasses
@@ -30,7 +32,7 @@ import torch
 import torch.distributed as dist
 
 from . import ops
-from .distributed import allreduce_grad_and_mask, broadcast_state
+from .distributed import allreduce_async, broadcast_state, wait_all
 
 
 def _bind_flat(modules, device):
@@ -276,6 +278,9 @@ class TDLearner:
             gm = contract_m()
             # mixer grads in reference parameter order, still off the critical path
             ops.unpack_grads(self.sm, self.params[self.na:], gm, self.grad[self.na:self.na + self.nm])
+            # data parallel: the mixer half (+ Σ mask) is final now; its all-reduce
+            # runs under the agent BPTT
+            work_m = allreduce_async(self.grad[self.na:], self.pg)
         # 5. agent BPTT (grads of the chosen Q and, unless detached, of the hidden states)
         slabs_a = self._slab("a", int(ops.lib().t2o_agent_bwd_max_slabs(B, A)) * self.sa.layout().grad_total)
         ga, _ = ops.agent_unroll_bwd(self.sa, self.pack_a, obs, h_on, gchosen=gqv, actions=act,
@@ -283,8 +288,9 @@ class TDLearner:
                                      timer=self.timer, hmid=hmid, tape=tape_a)
         # 6. agent grads in reference parameter order
         ops.unpack_grads(self.sa, self.params[:self.na], ga, self.grad[:self.na])
+        work_a = allreduce_async(self.grad[:self.na], self.pg)
         main.wait_stream(side)
-        allreduce_grad_and_mask(self.grad, self.pg)
+        wait_all((work_m, work_a))
         # 7. clip + Adam
         self.step_count += 1
         ops.adam_step(self.params, self.grad[:-1], self.exp_avg, self.exp_avg_sq, self.step_count, lr=self.lr,
