@@ -56,6 +56,10 @@ def parse():
                          "unroll only (configs[1], inference over a replay batch); rollout: closed-loop "
                          "env step + agent step + ε-greedy over --envs envs per GPU (configs[4])")
     ap.add_argument("--envs", type=int, default=8192, help="rollout mode: envs per GPU")
+    ap.add_argument("--compact-obs", action="store_true",
+                    help="rollout mode: store obs in the compact wire format (SURVEY.md §8 f3)")
+    ap.add_argument("--no-cpu-configs0", action="store_true",
+                    help="skip the configs[0]-shape (16 AGVs, T=150) CPU-baseline figure")
     ap.add_argument("--mecs", type=int, default=2, help="rollout mode: MEC servers")
     ap.add_argument("--priorities", choices=("device", "cpu"), default="device",
                     help="where each update's |TD errors| go: device (consumed by the device-resident "
@@ -75,6 +79,8 @@ def parse():
 
 
 def workload_tag(args):
+    if args.mode == "rollout":
+        return rollout_tag(args)
     return f"b{args.batch}_t{args.T}_a{args.agents}_{args.dtype}"
 
 
@@ -126,11 +132,10 @@ def traffic_for(kernel, tag):
     return None if k is None else k.get("hbm_bytes")
 
 
-def _cpu_rate(args, B, threads, seconds):
+def _cpu_rate(A, T, B, threads, seconds):
     """min-of-N time of the oracle's CPU TD update on B episodes with `threads` threads."""
     from oracle import ref_learner, ref_model
     from t2omca_amd.synthetic import make_batch
-    A, T = args.agents, args.T
     cfg = dict(n_agents=A, n_entities=A, obs_entity_feats=9, emb=32, heads=3, depth=2, ff_hidden_mult=4,
                n_actions=5, state_entity_feats=8, mixer_emb=32, mixer_heads=3, mixer_depth=2)
     batch, w = make_batch(B, T, A, seed=7, device="cpu")
@@ -153,64 +158,163 @@ def _cpu_rate(args, B, threads, seconds):
 
 def cpu_baseline(args):
     """The oracle's PyTorch-CPU TD update (oracle/ref_learner.py, reference op order,
-    fp32) on a bounded sample of the same workload, on this host's cores: all the
-    threads torch runs with (capped by the CPU affinity set) and one thread."""
+    fp32) on a bounded sample of the same workload, on this host's cores.
+    BASELINE.md's rule: torch.set_num_threads(len(os.sched_getaffinity(0))) — the
+    figure of record; beside it the same sample at the thread count torch picks by
+    itself (the box's CPU share: OMP_NUM_THREADS), one thread, and configs[0]'s own
+    shape (16 AGVs, T = 150) at the affinity thread count."""
     affinity = len(os.sched_getaffinity(0))
-    threads = max(1, min(torch.get_num_threads(), affinity))
+    share = max(1, min(torch.get_num_threads(), affinity))
     A, T, B = args.agents, args.T, args.cpu_sample
-    rate, n = _cpu_rate(args, B, threads, args.cpu_seconds)
+    sec = args.cpu_seconds
+    rate, n = _cpu_rate(A, T, B, affinity, sec)
+    out = {"value": rate, "unit": "agent-transitions/s", "cores": affinity, "kind": "port",
+           "sample": f"{B} episodes x T={T} x A={A} (one TD update = {B * T * A} agent-transitions), "
+                     f"min of {n} updates after 1 warm-up, torch CPU fp32, "
+                     f"torch.set_num_threads(len(sched_getaffinity(0))) = {affinity} threads (BASELINE.md)",
+           "affinity_cores": affinity}
+    if share != affinity:
+        r2, n2 = _cpu_rate(A, T, B, share, sec / 2)
+        out["share_threads"] = {"value": r2, "unit": "agent-transitions/s", "cores": share,
+                                "sample": f"same sample, {share} threads (torch's default here: "
+                                          f"OMP_NUM_THREADS / the box's CPU share), min of {n2} updates"}
     b1 = max(1, B // 4)
-    rate1, n1 = _cpu_rate(args, b1, 1, args.cpu_seconds / 2)
-    return {"value": rate, "unit": "agent-transitions/s", "cores": threads, "kind": "port",
-            "sample": f"{B} episodes x T={T} x A={A} (one TD update = {B * T * A} agent-transitions), "
-                      f"min of {n} updates after 1 warm-up, torch CPU fp32, {threads} threads "
-                      f"(sched_getaffinity: {affinity} cores; torch threads: {torch.get_num_threads()})",
-            "affinity_cores": affinity,
-            "single_thread": {"value": rate1, "unit": "agent-transitions/s", "cores": 1,
-                              "sample": f"{b1} episodes x T={T} x A={A}, min of {n1} updates after 1 warm-up"}}
+    rate1, n1 = _cpu_rate(A, T, b1, 1, sec / 3)
+    out["single_thread"] = {"value": rate1, "unit": "agent-transitions/s", "cores": 1,
+                            "sample": f"{b1} episodes x T={T} x A={A}, min of {n1} updates after 1 warm-up"}
+    if not args.no_cpu_configs0:
+        b0 = 2
+        r0, n0 = _cpu_rate(16, 150, b0, affinity, sec / 2)
+        out["configs0"] = {"value": r0, "unit": "agent-transitions/s", "cores": affinity,
+                           "sample": f"configs[0]'s shape (16 AGVs, T=150; the config quotes 32 episodes): "
+                                     f"{b0} episodes, min of {n0} updates after 1 warm-up, {affinity} threads"}
+    return out
+
+
+def _cpu_rollout_rate(A, M, T, n_env, threads, seconds):
+    """The CPU path configs[4] replaces, on a sample of n_env envs: per timestep the
+    agent forward on torch CPU (oracle/ref_model.agent_forward, transf_agent.py:54-76)
+    for all n_env x A agents, ε-greedy (oracle/ref_mac), then each env's worker step
+    (oracle/ref_env.RefEnv.worker_step = env.step + get_state + get_avail_actions +
+    get_obs, parallel_runner.py:239-256, environment_multi_mec.py:309-366) in one
+    process.  Returns agent-transitions/s over whole steps until `seconds` elapse."""
+    import numpy as np
+    from oracle import ref_mac, ref_model
+    from oracle.ref_env import RefEnv
+    cfg = dict(n_agents=A, n_entities=A, obs_entity_feats=9, emb=32, heads=3, depth=2, ff_hidden_mult=4,
+               n_actions=5)
+    p = ref_model.init_params("agent", cfg, 0)
+    envs = [RefEnv(M, A, T, 1, e) for e in range(n_env)]
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        obs = np.stack([e.worker_reset()[2] for e in envs])
+        avail = np.stack([e.get_avail_actions() for e in envs])
+        h = torch.zeros(n_env, A, 32)
+        steps, t0 = 0, time.perf_counter()
+        while steps < T and (steps < 3 or time.perf_counter() - t0 < seconds):
+            with torch.no_grad():
+                q, h = ref_model.agent_forward(p, torch.as_tensor(obs, dtype=torch.float32), h, n_entities=A,
+                                               feat_dim=9, emb=32, heads=3, depth=2)
+            act = ref_mac.select_actions(q.reshape(-1, 5).numpy(), avail.reshape(-1, 5), 0.05, 3, steps)
+            act = act.reshape(n_env, A)
+            res = [e.worker_step(act[i]) for i, e in enumerate(envs)]
+            obs = np.stack([r[5] for r in res])
+            avail = np.stack([np.asarray(r[4]) for r in res])
+            steps += 1
+        el = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev)
+    return n_env * A * steps / el, steps
 
 
 def rollout_bench(args, world, rank, dev):
     """configs[4]: every rank steps its own shard of envs (no collective)."""
     from t2omca_amd.env import VecEnv
     from t2omca_amd.modules import TransformerAgent
+    from t2omca_amd.perfmodel import env_step_bytes, ref_order_network_flops
     from t2omca_amd.runner import RolloutRunner
     from t2omca_amd.synthetic import make_args
     A, T, n = args.agents, args.T, args.envs
     torch.manual_seed(0)
     agent = TransformerAgent(None, make_args(A, device=str(dev))).to(dev)
-    env = VecEnv(n, mec_num=args.mecs, agv_num=A, episode_limit=T, seed=1 + rank, device=dev)
-    runner = RolloutRunner(agent, env, seed=rank)
+    env = VecEnv(n, mec_num=args.mecs, agv_num=A, episode_limit=T, seed=1, device=dev, wire=args.compact_obs)
+    runner = RolloutRunner(agent, env, seed=0, compact_obs=args.compact_obs)
     for _ in range(args.warmup):
         runner.run(new_buffers=False)
+    timer = KernelTimer()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for i in range(args.steps):
+        # HIP events around every 10th timestep's launches on every 2nd rollout
+        runner.timer = timer if args.kernel_timer_every > 0 and i % args.kernel_timer_every == 0 else None
         runner.run(new_buffers=False)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    runner.timer = None
     if world > 1:
         t = torch.tensor([elapsed], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     env_steps = world * n * T * args.steps
+    kern = {k: sum(v) / len(v) for k, v in timer.durations().items()}
+    # the rollout's two hot kernels and their bounds: the env step (HBM: SURVEY §8(d)'s
+    # bytes per agent-step x n x A per launch) and the one-step agent forward (MFMA:
+    # §8(d)'s F_agent per sequence x n x A); the dominant one carries `roofline`
+    env_bytes = env_step_bytes(A) * n * A
+    agent_flops = ref_order_network_flops(A)[0] * n * A
+    rl = {}
+    if "env_step" in kern:
+        ach = env_bytes / (kern["env_step"] * 1e-3) / 1e9
+        rl["env_step"] = {"bound": "hbm", "kernel": "env_step", "achieved": ach, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                          "frac": ach / PEAK_HBM_GBS, "traffic": traffic_for("env_step", rollout_tag(args)),
+                          "algorithmic_bytes_per_launch": env_bytes, "avg_launch_ms": kern["env_step"],
+                          "basis": "SURVEY.md §8(d): (16+4+64+4 + 9A*4) B per agent-step (perfmodel.env_step_bytes)"}
+    if "agent_fwd" in kern:
+        ach = agent_flops / (kern["agent_fwd"] * 1e-3) / 1e12
+        rl["agent_fwd"] = {"bound": "mfma", "kernel": "agent_fwd", "achieved": ach, "peak": PEAK_FP32_TFLOPS,
+                           "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS,
+                           "traffic": traffic_for("agent_fwd", rollout_tag(args)),
+                           "algorithmic_flops_per_launch": agent_flops, "avg_launch_ms": kern["agent_fwd"],
+                           "basis": "SURVEY.md §8(d) F_agent per sequence-step (reference order, token-pruned), "
+                                    "fp32 MFMA peak (the rollout agent runs fp32)"}
+    dom = max(rl, key=lambda k: rl[k]["avg_launch_ms"]) if rl else None
     out = {"metric": "agent-transitions/sec for closed-loop rollout (env step + agent step + eps-greedy)",
            "value": env_steps * A / elapsed, "unit": "agent-transitions/s", "env_steps_per_s": env_steps / elapsed,
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
            "vs_baseline": None, "dtype": "fp32 agent, fp64 env", "data": "simulated (VecEnv, env_spec stand-ins)",
            "config": {"workload": f"configs[4]: {n} envs/GPU x {A} AGVs x {args.mecs} MEC, episode {T} steps, "
-                                  "one rollout per step", "global_envs": n * world, "agents": A}}
+                                  "one rollout per step" + (", compact obs wire format" if args.compact_obs else ""),
+                      "global_envs": n * world, "agents": A, "compact_obs": bool(args.compact_obs)},
+           "roofline": rl.get(dom), "roofline_other": {k: v for k, v in rl.items() if k != dom},
+           "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items())},
+           "per_env_step_ms": elapsed / args.steps / T * 1e3}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        affinity = len(os.sched_getaffinity(0))
+        ne = 8
+        r, st = _cpu_rollout_rate(A, args.mecs, T, ne, affinity, args.cpu_seconds)
+        out["cpu_baseline"] = {"value": r, "unit": "agent-transitions/s", "cores": affinity, "kind": "port",
+                               "sample": f"{ne} envs x {A} AGVs x {args.mecs} MEC, {st} steps of one episode: "
+                                         f"agent forward on torch CPU ({affinity} threads, "
+                                         f"len(sched_getaffinity(0))), eps-greedy and the numpy env "
+                                         f"(oracle/ref_env, environment_multi_mec.py:309-366) serially in one "
+                                         f"process (the reference runs one process per env, "
+                                         f"parallel_runner.py:18-32)", "affinity_cores": affinity}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def rollout_tag(args):
+    return f"rollout_n{args.envs}_t{args.T}_a{args.agents}_m{args.mecs}" + ("_wire" if args.compact_obs else "")
 
 
 def expand_bench(args, world, rank, dev):
@@ -338,7 +442,8 @@ def main():
             dist.init_process_group(backend)
     from t2omca_amd.learner import TDLearner
     from t2omca_amd.modules import TransformerAgent, TransformerMixer
-    from t2omca_amd.perfmodel import (ref_order_flops_per_transition, ref_order_kernel_flops, td_update_bytes,
+    from t2omca_amd.perfmodel import (ref_order_flops_per_transition, ref_order_kernel_flops, td_tape_bytes,
+                                      td_update_bytes,
                                       td_update_flops)
     from t2omca_amd.synthetic import make_args, make_batch
 
@@ -432,6 +537,7 @@ def main():
     flops = td_update_flops(B, T, A)
     ref_flops = ref_order_kernel_flops(B, T, A)
     bytes_ = td_update_bytes(B, T, A, elem=2 if args.dtype == "bf16" else 4)
+    tape_ = td_tape_bytes(B, T, A, elem=2 if args.dtype == "bf16" else 4)
     # dominant kernel: the longest of the four network kernels on the critical path
     # (the tape contractions are part of a backward; mixer_dw runs on a side stream)
     dom = max(ref_flops, key=lambda k: kern.get(k, 0.0))
@@ -465,6 +571,7 @@ def main():
                               "(perfmodel.ref_order_kernel_flops)",
                      "algorithmic_flops_per_launch": ref_flops[dom],
                      "algorithmic_bytes_per_launch": bytes_.get(dom),
+                     "tape_bytes_per_update": tape_,
                      "avg_launch_ms": dom_ms,
                      "incl_tape_contraction": None if dw is None or dw not in kern else {
                          "ms": dom_ms + kern[dw],

@@ -151,8 +151,8 @@ int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, const float*
  * layout, overwritten; *nslab = number written, at most max_slabs =
  * t2o_agent_bwd_max_slabs(B, A)); gh0[b][a][E] = dL/dh0 (may be NULL).
  * Workspace: tape, t2o_bwd_tape_floats(L, tiles) floats with tiles =
- * T * ceil(B*A/16) — the per-record operand pairs of the M/N/W1/W2 weight
- * grads; the slabs are complete only after t2o_bwd_tape_contract(L, pack,
+ * t2o_bwd_tape_tiles(L, B, T, A) — the per-record operand pairs of the M/N/W1/W2
+ * weight grads; the slabs are complete only after t2o_bwd_tape_contract(L, pack,
  * tape, tiles, gslabs, *nslab) on the same stream. */
 int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack,
                          const float* obs, int64_t obs_sb, int64_t obs_st,
@@ -199,7 +199,9 @@ int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, const float*
  * extra grad on the hyper outputs.  Outputs: gqv[B][T][A] (dL/dqvals),
  * ghid[B][T][A][E] (dL/dhidden states), ghw0[B][3][E] (may be NULL), partial
  * weight-grad slabs as for the agent (max_slabs = t2o_mixer_bwd_max_slabs(B)),
- * tape workspace of t2o_bwd_tape_floats(L, tiles) floats, tiles = B*T*ceil((A+3)/16). */
+ * tape workspace of t2o_bwd_tape_floats(L, tiles) floats with
+ * tiles = t2o_bwd_tape_tiles(L, B, T, A); pass the same `tiles` to the contraction
+ * (it is the per-block stride of the tape). */
 int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, const float* states,
                          int64_t st_sb, int64_t st_st, const float* hid, int64_t hid_sb,
                          int64_t hid_st, const float* hw0, const float* qv, const float* hw,
@@ -207,6 +209,13 @@ int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, const float* st
                          float* ghid, float* ghw0, float* gslabs, int max_slabs, int* nslab, void* tape,
                          int B, int T, void* stream);
 int t2o_mixer_bwd_max_slabs(int B);
+
+/* Tiles of 16 weight-gradient records per block that one backward call writes
+ * (agent: T * ceil(B*A/16); mixer, A = L->n_agents: B*T*ceil((A+3)/16), or for
+ * a tuned mixer with A+3 > 16 query rows, whose records form one compact stream
+ * per block, ceil(B*T*(A+3)/16)).  -1 on a bad argument.  Both the tape size
+ * (t2o_bwd_tape_floats) and the contraction's `tiles` argument take this count. */
+int64_t t2o_bwd_tape_tiles(const t2o_layout* L, int B, int T, int A);
 
 /* Floats of backward tape workspace for `tiles` tiles of 16 records:
  * D * tiles * 16 * (6E + 2HE) elements of 4 (fp32) or 2 (bf16) bytes. */

@@ -64,6 +64,7 @@ EXPORTS = {
                              [ctypes.c_void_p] + [ctypes.c_int] * 2 + [ctypes.c_void_p]),
     "t2o_mixer_bwd_max_slabs": (ctypes.c_int, [ctypes.c_int]),
     "t2o_bwd_tape_floats": (ctypes.c_int64, [ctypes.POINTER(Layout), ctypes.c_int64]),
+    "t2o_bwd_tape_tiles": (ctypes.c_int64, [ctypes.POINTER(Layout), ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     "t2o_bwd_tape_contract": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                              ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]),
     "t2o_bwd_tape_contract_ex": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_void_p, ctypes.c_void_p,

@@ -469,6 +469,18 @@ extern "C" int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t tiles) {
   return L->prec ? (elems + 1) / 2 : elems;
 }
 
+extern "C" int64_t t2o_bwd_tape_tiles(const t2o_layout* L, int B, int T, int A) {
+  if (!L || B < 1 || T < 1 || A < 1) return -1;
+  if (L->kind == 0) return (int64_t)T * (((int64_t)B * A + 15) / 16);
+  if (A != L->n_agents) return -1;
+  const int64_t Q = A + 3;  // the mixer's query rows: A weight rows + 3 hyper tokens
+  // tuned multi-tile mixers write each block's records as one compact stream
+  // (t2o_mixer.hip, mixer_bwd_kernel); a one-tile or generic mixer, one tile-set
+  // per (episode, step)
+  if (Q > 16 && !L->generic) return ((int64_t)B * T * Q + 15) / 16;
+  return (int64_t)B * T * ((Q + 15) / 16);
+}
+
 extern "C" int t2o_bwd_tape_contract_ex(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
                                         float* gslabs, int nslab, int rec_format, void* stream) {
   if (!L || !pack || !tape || !gslabs || tiles < 0 || nslab < 1 || rec_format < 0 || rec_format > 1 ||

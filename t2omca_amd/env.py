@@ -53,13 +53,14 @@ class VecEnv:
     def __init__(self, n_envs, mec_num=2, agv_num=16, num_channels=4, episode_limit=150, seed=None,
                  edge_only=False, device="cuda", keep_obs64=False, wire=False, obs_entity_mode=True,
                  state_entity_mode=True):
-        """seed None: 0 mixed with the data-parallel rank (distributed.rank_seed), so
+        """seed (None = 0) mixed with the data-parallel rank (distributed.rank_seed), so
         every rank's shard of envs draws its own episodes.  obs_entity_mode /
         state_entity_mode as the reference constructor's (:10-11; the transformer
         path uses both, the defaults here); state_entity_mode only changes
         get_env_info's keys (:431-438)."""
-        if seed is None:
-            seed = rank_seed(0, dist_rank())
+        # the data-parallel rank is always mixed in (rank 0 keeps `seed`), so ranks given
+        # the same explicit seed still draw different streams
+        seed = rank_seed(0 if seed is None else seed, dist_rank())
         device = torch.device(device)
         if device.type != "cuda":
             raise RuntimeError("VecEnv runs on the HIP device only (the numpy restatement in oracle/ is test-only)")

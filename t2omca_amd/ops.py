@@ -140,19 +140,20 @@ def tape_floats(shape: NetShape, tiles):
     return int(lib().t2o_bwd_tape_floats(ctypes.byref(shape.layout()), int(tiles)))
 
 
-def agent_tape_tiles(B, T, A):
+def agent_tape_tiles(B, T, A, shape: NetShape = None):
     return T * ((B * A + 15) // 16)
 
 
-def mixer_tape_tiles(B, T, A, shape: NetShape = None):
+def mixer_tape_tiles(B, T, A, shape: NetShape):
     """Weight-gradient tape tiles per block of a mixer BPTT over B episodes x T
-    steps: one tile of the A+3 query rows per (episode, step) when they fit 16
-    records; tuned multi-tile mixers store each block's query-row records as one
-    compact stream cut into 16-record tiles (t2o_mixer.hip)."""
-    Q = A + 3
-    if Q > 16 and shape is not None and not shape.generic:
-        return (B * T * Q + 15) // 16
-    return B * T * ((Q + 15) // 16)
+    steps (include/t2omca.h t2o_bwd_tape_tiles: one tile of the A+3 query rows
+    per (episode, step) when they fit 16 records; tuned multi-tile mixers store
+    each block's query-row records as one compact stream cut into 16-record
+    tiles, t2o_mixer.hip)."""
+    n = int(lib().t2o_bwd_tape_tiles(ctypes.byref(shape.layout()), int(B), int(T), int(A)))
+    if n < 0:
+        raise ValueError(f"mixer_tape_tiles: bad shape B={B} T={T} A={A} for a mixer of {shape.agents} agents")
+    return n
 
 
 def _tape(shape, tiles, tape, device):
@@ -213,6 +214,8 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
     _dev(pack_on, states, hid_on, qv_on, q_on, hw0_on, pack_tg, hid_tg, qv_tg, q_tg, hw0_tg)
     B = states.shape[0]
     A, E = hid_on.shape[2], shape.E
+    if A != shape.agents:
+        raise ValueError(f"mixer_unroll_fwd: hidden states carry {A} agents, the mixer was built for {shape.agents}")
     L = shape.layout()
     dev = states.device
     T_on = T_on or (qv_on.shape[1] if qv_on is not None else hid_on.shape[1])
@@ -281,6 +284,8 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
     _dev(pack, states, hid, gy, hw0, ghw_ext)
     B, T = gy.shape
     A, E = hid.shape[2], shape.E
+    if A != shape.agents:
+        raise ValueError(f"mixer_unroll_bwd: hidden states carry {A} agents, the mixer was built for {shape.agents}")
     L = shape.layout()
     dev = gy.device
     assert gy.is_contiguous() and fwd["xout"] is not None

@@ -74,21 +74,36 @@ def td_update_flops(B, T, A, E=32, H=3, D=2, F=9, Fs=8, NA=5):
 
 
 def td_update_bytes(B, T, A, E=32, F=9, Fs=8, NA=5, elem=4):
-    """Compulsory HBM bytes per kernel (fp32 inputs read / outputs written once; the
-    weight-gradient tape in the MFMA operand type, `elem` bytes, valid records only)."""
+    """Compulsory HBM bytes per kernel: its inputs read and outputs written once
+    (the replay batch's obs / state in fp32, Q / hidden rows, the mixer's per-step
+    outputs).  The weight-gradient tape is the implementation's own intermediate,
+    not algorithmic traffic: it is reported apart, by ``td_tape_bytes``."""
     obs = B * (T + 1) * A * A * F * 4
     st = B * (T + 1) * A * Fs * 4
     qh = B * (T + 1) * A * (NA + E) * 4
-    tape_a = B * T * A * dw_record_bytes(E, elem=elem)
-    tape_m = B * T * (A + 3) * dw_record_bytes(E, elem=elem)
     return {
         "agent_fwd": obs + 2 * qh,
         "mixer_fwd": st + 2 * qh + 2 * B * (T + 1) * ((A + 3) * E + 3 * E + A + 1) * 4,
-        "mixer_bwd": st + B * T * ((A + 3) * E + 3 * E + 2 * A + A * E + 2) * 4 + tape_m,
-        "mixer_dw": tape_m,
-        "agent_bwd": obs + B * T * A * (2 * E + 2) * 4 + tape_a,
-        "agent_dw": tape_a,
+        "mixer_bwd": st + B * T * ((A + 3) * E + 3 * E + 2 * A + A * E + 2) * 4,
+        "agent_bwd": obs + B * T * A * (2 * E + 2) * 4,
     }
+
+
+def td_tape_bytes(B, T, A, E=32, elem=4):
+    """Weight-gradient tape bytes per update (valid records only, in the MFMA operand
+    type): written by the BPTT kernel, read back by its contraction (agent_dw /
+    mixer_dw).  The mixer's record is always the full one; the agent's pipelined
+    bf16 kernel writes the lean record (160 of 384 features) at up to 8 entities."""
+    full = dw_record_bytes(E, elem=elem)
+    agent_rec = full * 160 // 384 if (elem == 2 and A <= 8) else full
+    return {"agent": B * T * A * agent_rec, "mixer": B * T * (A + 3) * full}
+
+
+def env_step_bytes(A):
+    """algorithmic HBM bytes per agent per env step — the agent's
+    state (position 16 B, MEC index 4 B, job queue <= ~64 B, ack 4 B) plus its
+    observation row written once (9A fp32)."""
+    return 16 + 4 + 64 + 4 + 9 * A * 4
 
 
 def ref_order_network_flops(A, E=32, H=3, D=2, F=9, Fs=8, NA=5, FF=None):

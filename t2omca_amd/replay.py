@@ -33,9 +33,10 @@ class PrioritizedReplayBuffer:
     def __init__(self, example_batch, buffer_size, max_seq_length, alpha, beta, t_max, *, device="cuda", seed=None):
         """example_batch: a dict of [n, max_seq_length, ...] tensors (e.g. one
         RolloutRunner batch) giving the scheme (keys, per-step shapes, dtypes).
-        seed None: 0 mixed with the data-parallel rank (distributed.rank_seed)."""
-        if seed is None:
-            seed = rank_seed(0, dist_rank())
+        seed (None = 0) is mixed with the data-parallel rank (distributed.rank_seed)."""
+        # the data-parallel rank is always mixed in (rank 0 keeps `seed`), so ranks given
+        # the same explicit seed still draw different streams
+        seed = rank_seed(0 if seed is None else seed, dist_rank())
         self.device = torch.device(device)
         self.buffer_size, self.max_seq_length = int(buffer_size), int(max_seq_length)
         self.alpha, self.beta_original, self.beta = float(alpha), float(beta), float(beta)

@@ -54,9 +54,10 @@ class LinearSchedule:
 class RolloutRunner:
     def __init__(self, agent, env, *, epsilon_start=1.0, epsilon_finish=0.05, epsilon_anneal_time=50000,
                  seed=None, compact_obs=False):
-        # seed None: 0 mixed with the data-parallel rank (distributed.rank_seed)
-        if seed is None:
-            seed = rank_seed(0, dist_rank())
+        # seed (None = 0) mixed with the data-parallel rank (distributed.rank_seed)
+        # the data-parallel rank is always mixed in (rank 0 keeps `seed`), so ranks given
+        # the same explicit seed still draw different streams
+        seed = rank_seed(0 if seed is None else seed, dist_rank())
         if not getattr(env, "obs_entity_mode", True):
             raise ValueError("the transformer agent reads entity observations (VecEnv obs_entity_mode=True)")
         if compact_obs and getattr(env, "wire", None) is None:
@@ -73,6 +74,10 @@ class RolloutRunner:
         self.episode = 0
         self._bufs = None
         self.last_returns = None
+        # optional callable(tag) recording HIP events around the step's three launches
+        # (agent step, action selection, env step) on every timer_every-th timestep
+        self.timer = None
+        self.timer_every = 10
 
     # -- replay batch ---------------------------------------------------------
     def _alloc(self):
@@ -107,15 +112,21 @@ class RolloutRunner:
         ret = torch.zeros(self.n, dtype=torch.float64, device=self.device)
         h = None
         for t in range(self.T + 1):
+            timer = self.timer if self.timer is not None and t % self.timer_every == 0 else None
+            mark = timer or (lambda tag: None)
             obs_t = self._obs_step if self.compact_obs else tm["obs"][t]
-            q, h_seq = ops.agent_unroll_fwd(shape, pack, obs_t.unsqueeze(1), h0_on=h)
+            q, h_seq = ops.agent_unroll_fwd(shape, pack, obs_t.unsqueeze(1), h0_on=h, timer=timer)
             h = h_seq.view(self.n * self.A, shape.E)
             counter = (self.episode * (self.T + 1) + t)
+            mark("begin:select_actions")
             ops.select_actions(q[:, 0], tm["avail_actions"][t], eps, self.seed, counter,
                                out=tm["actions"][t, :, :, 0])
+            mark("end:select_actions")
             if t == self.T:
                 break
+            mark("begin:env_step")
             reward, _, _, _, _, _ = env.step(tm["actions"][t, :, :, 0], dest=self._dest(tm, t + 1))
+            mark("end:env_step")
             tm["reward"][t, :, 0].copy_(reward)
             ret += reward
         if not test_mode:

@@ -116,3 +116,26 @@ def test_layout_tuned_or_generic(E, H, D, FF, n, generic):
             assert L.total == L.pack_floats == n_params + D * (4 * H * E * E + 2 * E * FF) + 9 * E + E * no
         forced = _lib.make_layout(kind, E, H, D, 9, 5, FF, n, flags=_lib.LAYOUT_FORCE_GENERIC)
         assert forced.generic == 1
+
+
+def test_bwd_tape_tiles_host_logic():
+    """t2o_bwd_tape_tiles (host-only): the per-block tile count a C caller sizes the
+    tape by and passes to the contraction."""
+    import ctypes as C
+
+    from t2omca_amd import _lib
+    lib = _lib.lib()
+    B, T = 5, 7
+    La = _lib.make_layout(0, 32, 3, 2, 9, 5, 128, 8)
+    assert lib.t2o_bwd_tape_tiles(C.byref(La), B, T, 8) == T * ((B * 8 + 15) // 16)
+    Lm8 = _lib.make_layout(1, 32, 3, 2, 8, 1, 128, 8)
+    assert lib.t2o_bwd_tape_tiles(C.byref(Lm8), B, T, 8) == B * T  # 11 query rows: one tile each
+    for A in (16, 64):
+        Lm = _lib.make_layout(1, 32, 3, 2, 8, 1, 128, A)
+        assert Lm.generic == 0
+        assert lib.t2o_bwd_tape_tiles(C.byref(Lm), B, T, A) == (B * T * (A + 3) + 15) // 16
+        assert lib.t2o_bwd_tape_tiles(C.byref(Lm), B, T, A - 1) == -1
+    Lg = _lib.make_layout(1, 32, 3, 2, 8, 1, 128, 32)  # generic: one tile-set per (episode, step)
+    assert Lg.generic == 1
+    assert lib.t2o_bwd_tape_tiles(C.byref(Lg), B, T, 32) == B * T * 3
+    assert lib.t2o_bwd_tape_tiles(C.byref(Lg), 0, T, 32) == -1

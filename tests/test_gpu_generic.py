@@ -151,6 +151,9 @@ def _cfg_of(A, E=32, H=3, D=2, ff=4, **kw):
     ("E16H1D3", _cfg_of(6, E=16, H=1, D=3, ff=2), 3, 5),
     ("softplus", _cfg_of(8, qmix_pos_func="softplus", qmix_pos_func_beta=0.5), 3, 5),
     ("quadratic", _cfg_of(4, qmix_pos_func="quadratic"), 3, 5),
+    # the mixer's obs-token branch through the learner (state = obs.flatten(2),
+    # n_tok = A * n_entities; n_transf_mixer.py:60-63), target mixer included
+    ("obsbranch", _cfg_of(4, state_entity_mode=False, state_entity_feats=9), 3, 5),
 ])
 def test_generic_td_update_matches_oracle(tag, cfg, B, T):
     require_gpu()

@@ -36,7 +36,7 @@ def main():
     gy = torch.randn(B, T, device="cuda") * 1e-3
     gq = torch.randn(B, T, A, device="cuda") * 1e-3
     gh = torch.randn(B, T, A, 32, device="cuda") * 1e-3
-    tape_m = torch.empty(ops.tape_floats(lr.sm, ops.mixer_tape_tiles(B, T, A)), device="cuda")
+    tape_m = torch.empty(ops.tape_floats(lr.sm, ops.mixer_tape_tiles(B, T, A, lr.sm)), device="cuda")
     tape_a = torch.empty(ops.tape_floats(lr.sa, ops.agent_tape_tiles(B, T, A)), device="cuda")
     s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
 

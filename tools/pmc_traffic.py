@@ -15,7 +15,8 @@ import sys
 
 SHORT = {"agent_fwd_kernel": "agent_fwd", "mixer_fwd_kernel": "mixer_fwd", "mixer_bwd_kernel": "mixer_bwd",
          "agent_bwd_kernel": "agent_bwd", "agent_bwd_pipe_kernel": "agent_bwd", "mixer_bwd_pipe_kernel": "mixer_bwd", "td_loss_kernel": "td_loss", "adam_kernel": "adam",
-         "env_kernel": "env_step", "reduce_slabs_kernel": "reduce_slabs", "seg_kernel": "pack"}
+         "env_kernel": "env_step", "reduce_slabs_kernel": "reduce_slabs", "seg_kernel": "pack",
+         "select_actions_kernel": "select_actions", "obs_expand_kernel": "obs_expand"}
 
 
 def _is_bf16(name):
