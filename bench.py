@@ -42,9 +42,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=1024, help="episodes per GPU")
-    ap.add_argument("--T", type=int, default=60)
-    ap.add_argument("--agents", type=int, default=8)
+    ap.add_argument("--batch", type=int, default=None,
+                    help="episodes per GPU (default: 1024 train = configs[2]; 128 forward = configs[1])")
+    ap.add_argument("--T", type=int, default=None,
+                    help="episode length (default: 60 train = configs[2]; 150 forward / rollout, the default "
+                         "scenario of configs[1] / configs[4])")
+    ap.add_argument("--agents", type=int, default=None, help="AGVs (default: 8 train; 16 forward / rollout)")
     ap.add_argument("--dtype", choices=("bf16", "fp32"), default="bf16",
                     help="MFMA operand precision (BASELINE configs[2] is quoted in bf16; accumulation, "
                          "LayerNorm, softmax, recurrent state, TD targets and Adam stay fp32 either way)")
@@ -75,7 +78,16 @@ def parse():
                     help="skip the fp32-precision companion timing of the same workload (bf16 runs)")
     ap.add_argument("--print-workload-tag", action="store_true",
                     help="print the tag that keys profiles/hbm_traffic.json for these args and exit")
-    return ap.parse_args()
+    a = ap.parse_args()
+    # per-mode defaults: each mode's BASELINE config (SURVEY.md §8 scenario mapping)
+    scen = a.mode in ("forward", "rollout")
+    if a.agents is None:
+        a.agents = 16 if scen else 8
+    if a.T is None:
+        a.T = 150 if scen else 60
+    if a.batch is None:
+        a.batch = 128 if a.mode == "forward" else 1024
+    return a
 
 
 def workload_tag(args):
@@ -156,38 +168,64 @@ def _cpu_rate(A, T, B, threads, seconds):
     return B * T * A / min(times), len(times)
 
 
+def host_cpus():
+    """The host cores this process may really run on: its CPU affinity set, capped
+    by a cgroup CPU quota (v2 cpu.max, v1 cpu.cfs_quota_us) and, when no quota is
+    visible, by OMP_NUM_THREADS (the GPU box sets it to the box's CPU share: its
+    affinity set spans the whole machine).  Oversubscribing the share is not a
+    baseline: 256 torch threads on a 16-CPU share ran the rollout's CPU path at
+    11 agent-transitions/s (profiles/r3_c/rollout.json) against 2.3 K/s on 8."""
+    import math
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = math.ceil(int(q) / int(per))
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f1, open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f2:
+                q, per = int(f1.read()), int(f2.read())
+                if q > 0:
+                    quota = math.ceil(q / per)
+        except (OSError, ValueError):
+            pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    omp = int(omp) if omp and omp.isdigit() and int(omp) > 0 else None
+    usable = min(affinity, quota) if quota else (min(affinity, omp) if omp else affinity)
+    return {"usable": max(1, usable), "affinity": affinity, "cgroup_quota": quota, "omp_num_threads": omp}
+
+
 def cpu_baseline(args):
     """The oracle's PyTorch-CPU TD update (oracle/ref_learner.py, reference op order,
     fp32) on a bounded sample of the same workload, on this host's cores.
-    BASELINE.md's rule: torch.set_num_threads(len(os.sched_getaffinity(0))) — the
-    figure of record; beside it the same sample at the thread count torch picks by
-    itself (the box's CPU share: OMP_NUM_THREADS), one thread, and configs[0]'s own
-    shape (16 AGVs, T = 150) at the affinity thread count."""
-    affinity = len(os.sched_getaffinity(0))
-    share = max(1, min(torch.get_num_threads(), affinity))
+    BASELINE.md: torch.set_num_threads(n) with n = the host cores available —
+    len(os.sched_getaffinity(0)), capped by the CPU share the process really has
+    (host_cpus: on the GPU box the affinity set is the whole 256-core machine but
+    the share is 16).  Beside it: one thread, and configs[0]'s own shape (16 AGVs,
+    T = 150) at n threads."""
+    hc = host_cpus()
+    n_thr = hc["usable"]
     A, T, B = args.agents, args.T, args.cpu_sample
     sec = args.cpu_seconds
-    rate, n = _cpu_rate(A, T, B, affinity, sec)
-    out = {"value": rate, "unit": "agent-transitions/s", "cores": affinity, "kind": "port",
+    rate, n = _cpu_rate(A, T, B, n_thr, sec)
+    out = {"value": rate, "unit": "agent-transitions/s", "cores": n_thr, "kind": "port",
            "sample": f"{B} episodes x T={T} x A={A} (one TD update = {B * T * A} agent-transitions), "
-                     f"min of {n} updates after 1 warm-up, torch CPU fp32, "
-                     f"torch.set_num_threads(len(sched_getaffinity(0))) = {affinity} threads (BASELINE.md)",
-           "affinity_cores": affinity}
-    if share != affinity:
-        r2, n2 = _cpu_rate(A, T, B, share, sec / 2)
-        out["share_threads"] = {"value": r2, "unit": "agent-transitions/s", "cores": share,
-                                "sample": f"same sample, {share} threads (torch's default here: "
-                                          f"OMP_NUM_THREADS / the box's CPU share), min of {n2} updates"}
+                     f"min of {n} updates after 1 warm-up, torch CPU fp32, torch.set_num_threads({n_thr}): "
+                     f"the host cores available (sched_getaffinity {hc['affinity']}, cgroup quota "
+                     f"{hc['cgroup_quota']}, OMP_NUM_THREADS {hc['omp_num_threads']})",
+           "affinity_cores": hc["affinity"], "host_cpus": hc}
     b1 = max(1, B // 4)
     rate1, n1 = _cpu_rate(A, T, b1, 1, sec / 3)
     out["single_thread"] = {"value": rate1, "unit": "agent-transitions/s", "cores": 1,
                             "sample": f"{b1} episodes x T={T} x A={A}, min of {n1} updates after 1 warm-up"}
     if not args.no_cpu_configs0:
         b0 = 2
-        r0, n0 = _cpu_rate(16, 150, b0, affinity, sec / 2)
-        out["configs0"] = {"value": r0, "unit": "agent-transitions/s", "cores": affinity,
+        r0, n0 = _cpu_rate(16, 150, b0, n_thr, sec / 2)
+        out["configs0"] = {"value": r0, "unit": "agent-transitions/s", "cores": n_thr,
                            "sample": f"configs[0]'s shape (16 AGVs, T=150; the config quotes 32 episodes): "
-                                     f"{b0} episodes, min of {n0} updates after 1 warm-up, {affinity} threads"}
+                                     f"{b0} episodes, min of {n0} updates after 1 warm-up, {n_thr} threads"}
     return out
 
 
@@ -232,7 +270,7 @@ def rollout_bench(args, world, rank, dev):
     """configs[4]: every rank steps its own shard of envs (no collective)."""
     from t2omca_amd.env import VecEnv
     from t2omca_amd.modules import TransformerAgent
-    from t2omca_amd.perfmodel import env_step_bytes, ref_order_network_flops
+    from t2omca_amd.perfmodel import agent_row_step_flops, env_step_bytes, ref_order_network_flops
     from t2omca_amd.runner import RolloutRunner
     from t2omca_amd.synthetic import make_args
     A, T, n = args.agents, args.T, args.envs
@@ -268,7 +306,8 @@ def rollout_bench(args, world, rank, dev):
     # bytes per agent-step x n x A per launch) and the one-step agent forward (MFMA:
     # §8(d)'s F_agent per sequence x n x A); the dominant one carries `roofline`
     env_bytes = env_step_bytes(A) * n * A
-    agent_flops = ref_order_network_flops(A)[0] * n * A
+    agent_flops = agent_row_step_flops(n=A) * n * A  # what the fp32 kernel executes per launch
+    agent_ref_flops = ref_order_network_flops(A)[0] * n * A
     rl = {}
     if "env_step" in kern:
         ach = env_bytes / (kern["env_step"] * 1e-3) / 1e9
@@ -282,8 +321,14 @@ def rollout_bench(args, world, rank, dev):
                            "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS,
                            "traffic": traffic_for("agent_fwd", rollout_tag(args)),
                            "algorithmic_flops_per_launch": agent_flops, "avg_launch_ms": kern["agent_fwd"],
-                           "basis": "SURVEY.md §8(d) F_agent per sequence-step (reference order, token-pruned), "
-                                    "fp32 MFMA peak (the rollout agent runs fp32)"}
+                           "basis": "executed algorithm (perfmodel.agent_row_step_flops: folded projections, "
+                                    "observation-space attention, token 0 only) vs the fp32 MFMA peak (the rollout "
+                                    "agent runs fp32)",
+                           "reference_order": {"flops_per_launch": agent_ref_flops,
+                                               "achieved": agent_ref_flops / (kern["agent_fwd"] * 1e-3) / 1e12,
+                                               "note": "SURVEY.md §8(d) F_agent: the reference association order "
+                                                       "counts more work than the kernel issues, so it is not "
+                                                       "priced against the peak"}}
     dom = max(rl, key=lambda k: rl[k]["avg_launch_ms"]) if rl else None
     out = {"metric": "agent-transitions/sec for closed-loop rollout (env step + agent step + eps-greedy)",
            "value": env_steps * A / elapsed, "unit": "agent-transitions/s", "env_steps_per_s": env_steps / elapsed,
@@ -297,16 +342,17 @@ def rollout_bench(args, world, rank, dev):
            "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items())},
            "per_env_step_ms": elapsed / args.steps / T * 1e3}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        affinity = len(os.sched_getaffinity(0))
+        hc = host_cpus()
         ne = 8
-        r, st = _cpu_rollout_rate(A, args.mecs, T, ne, affinity, args.cpu_seconds)
-        out["cpu_baseline"] = {"value": r, "unit": "agent-transitions/s", "cores": affinity, "kind": "port",
+        r, st = _cpu_rollout_rate(A, args.mecs, T, ne, hc["usable"], args.cpu_seconds)
+        out["cpu_baseline"] = {"value": r, "unit": "agent-transitions/s", "cores": hc["usable"], "kind": "port",
                                "sample": f"{ne} envs x {A} AGVs x {args.mecs} MEC, {st} steps of one episode: "
-                                         f"agent forward on torch CPU ({affinity} threads, "
-                                         f"len(sched_getaffinity(0))), eps-greedy and the numpy env "
+                                         f"agent forward on torch CPU ({hc['usable']} threads: the host cores "
+                                         f"available, see host_cpus), eps-greedy and the numpy env "
                                          f"(oracle/ref_env, environment_multi_mec.py:309-366) serially in one "
                                          f"process (the reference runs one process per env, "
-                                         f"parallel_runner.py:18-32)", "affinity_cores": affinity}
+                                         f"parallel_runner.py:18-32)", "affinity_cores": hc["affinity"],
+                               "host_cpus": hc}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -279,6 +279,11 @@ int t2o_adam_workspace_floats(void);
  * (tests/test_gpu_primitives.py). */
 int t2o_probe_lane_ops(const float* in, float* out, void* stream);
 
+/* Diagnostic: the XOR (in bf16 elements, a multiple of 8) applied to the
+ * columns of row `row` of a bf16 weight-image matrix with row length ld: element
+ * (r, col) of the image sits at r*ld + (col ^ t2o_bf_swz(r, ld)). */
+int t2o_bf_swz(int row, int ld);
+
 /* Sum nslab partial gradient slabs [nslab][n] into out[n] (out = sum, overwritten). */
 int t2o_reduce_slabs(const float* slabs, int nslab, int64_t n, float* out, void* stream);
 

@@ -84,6 +84,7 @@ EXPORTS = {
                       [ctypes.c_float] * 3 + [ctypes.c_int64] + [ctypes.c_void_p] * 3),
     "t2o_adam_workspace_floats": (ctypes.c_int, []),
     "t2o_probe_lane_ops": (ctypes.c_int, [ctypes.c_void_p] * 3),
+    "t2o_bf_swz": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
     "t2o_env_run": (ctypes.c_int, [ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_int64] +
                     [ctypes.c_int] * 6 + [ctypes.c_uint64, ctypes.c_void_p]),
     "t2o_env_run_ex": (ctypes.c_int, [ctypes.c_int] + [ctypes.c_void_p] * 3 + [ctypes.c_int, ctypes.c_void_p,

@@ -170,17 +170,33 @@ T2O_DEV f4 mfma_b32(bf4 a0, bf4 a1, bf4 b0, bf4 b1, f4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
 }
 
-// Bank-conflict-free bf16 weight rows: a weight row is only 64 B at E=32, so
-// the 16 rows a wave reads at once would pile onto 4 bank groups.  The bf16
-// image stores element (r, col) at r*ld + (col ^ bf_swz(r, ld)) — an XOR of
-// whole 8-element groups, so the 4 (or 8) consecutive K values a lane loads
-// stay contiguous — and the readers apply the same XOR.  Only the row's lane
-// index c matters: bf_swz(16o + c, ld) == bf_swz(c, ld).  (The transposed reads
-// of matvec_tr see 2-way conflicts on 64-B-periodic rows with this XOR; an XOR
-// that frees both read kinds measured 20 more spilled registers in the mixer's
-// pipelined BPTT, whose address registers it multiplies.)
+// Bank-conflict-free bf16 weight rows.  The bf16 image stores element
+// (r, col) at r*ld + (col ^ bf_swz(r, ld)) — an XOR of whole 8-element groups,
+// so the 4 (or 8) consecutive K values a lane loads stay contiguous — and the
+// readers apply the same XOR.  Only the row's lane index matters:
+// bf_swz(16o + c, ld) == bf_swz(c, ld).  The group index x(r) (sw = 8·x) is
+// chosen per row length so that BOTH read kinds are conflict-free
+// (MI355X_MICROARCH.md §LDS: ds_read_b64 and ds_read_b64_tr_b16 bank = dword
+// address mod 64, lanes 0-31 and 32-63 separately):
+//  * matvec (ds_read_b64): lane (g, c) reads 2 dwords of row c at group
+//    (2i + g/2) ^ x(c): x must be a bijection over the rows that share a bank
+//    base (row r starts at dword r·ld/2 mod 64);
+//  * matvec_tr (ds_read_b64_tr_b16): lane (g, c) reads 8 B of row
+//    q = 4g + (c >> 2) in output tile o, i.e. one 8-dword window per row, at
+//    window (o ^ (x >> 1)) of the row: x >> 1 must separate the rows q of a
+//    32-lane half that share a bank base.
+//  ld ≡ 0 mod 128 (one bank base, 16 groups): x = (r & 7) << 1 | r >> 3 & 1
+//  ld ≡ 64 mod 128 (two bases, 8 groups):     x = (r >> 1 & 3) << 1 | r >> 3 & 1
+//  ld ≡ 32 mod 64  (four bases, 4 groups):    x = (r >> 2 & 1) << 1 | r >> 3 & 1
+//  ld = 16         (eight bases, 2 groups):   x = r >> 3 & 1
+// (Round 2 used x = r >> 2 & 3 for every ld ≡ 0 mod 32: fine for ld = 32 / 96
+// matvec reads, but 4-way conflicted at ld = 128 (the FFN's W2 and W1ᵀ) and
+// 2-way / 8-way on the transposed reads at ld = 32 / 128.)
 __host__ __device__ inline int bf_swz(int row, int ld) {
-  return ld % 32 == 0 ? 8 * ((row >> 2) & 3) : 8 * ((row >> 3) & 1);
+  if (ld % 128 == 0) return 8 * (((row & 7) << 1) | ((row >> 3) & 1));
+  if (ld % 64 == 0) return 8 * ((((row >> 1) & 3) << 1) | ((row >> 3) & 1));
+  if (ld % 32 == 0) return 8 * ((((row >> 2) & 1) << 1) | ((row >> 3) & 1));
+  return 8 * ((row >> 3) & 1);
 }
 
 T2O_DEV f4 mma_tile(const __bf16* __restrict__ W, int ldw, int o, int i, f4 x, f4 acc) {
@@ -191,7 +207,11 @@ T2O_DEV f4 mma_tile(const __bf16* __restrict__ W, int ldw, int o, int i, f4 x, f
 // y[0..OT) = W · x[0..IT), bf16 weights and operands, fp32 accumulate
 template <int OT, int IT>
 T2O_DEV void matvec(const __bf16* __restrict__ W, int ldw, const f4* x, f4* y) {
-  const int c = lane_c(), g = lane_g();
+  // the lane's row swizzle derived per product from an opaque lane id: hoisted
+  // out of a step loop, one register per distinct row length would stay live
+  int l = threadIdx.x;
+  asm volatile("" : "+v"(l));
+  const int c = l & 15, g = (l >> 4) & 3;
   bf4 xb[IT];
 #pragma unroll
   for (int i = 0; i < IT; ++i) xb[i] = to_bf4(x[i]);
@@ -248,15 +268,17 @@ T2O_DEV void matvec_tr(const Wts<__bf16>& P, int64_t off, int ld, int64_t offT, 
   asm volatile("" : "+v"(l));
   const int c = l & 15, q = ((l >> 2) & 12) | (c >> 2);
   const int sw = bf_swz(q, ld);
-  const __bf16* W = P.w + off + q * ld + ((4 * (c & 3)) ^ sw);
-  const int xs16 = sw & 16;  // the swizzle's tile bit: odd output tiles read the other half
+  // (16o + 4p) ^ sw = (4p ^ (sw & 15)) + 16·(o ^ (sw >> 4)): the swizzle's low
+  // bit permutes 4-element halves inside the lane's 8-element group, its high
+  // bits permute whole 16-column output tiles
+  const __bf16* W = P.w + off + q * ld + ((4 * (c & 3)) ^ (sw & 15));
+  const int hi = sw >> 4;
   bf4 xb[IT];
 #pragma unroll
   for (int i = 0; i < IT; ++i) xb[i] = to_bf4(x[i]);
 #pragma unroll
   for (int o = 0; o < OT; ++o) {
-    // (16o + 4p) ^ s = 4p ^ s + 16o, except that the tile bit of s flips o's lowest bit
-    const int col = xs16 ? 16 * (o ^ 1) - 16 : 16 * o;
+    const int col = 16 * (o ^ hi);
     f4 acc = zero4();
 #pragma unroll
     for (int i = 0; i + 1 < IT; i += 2)

@@ -437,3 +437,6 @@ extern "C" int t2o_reduce_slabs(const float* slabs, int nslab, int64_t n, float*
   hipLaunchKernelGGL(reduce_slabs_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slabs, nslab, n, out);
   return (int)hipGetLastError();
 }
+
+// diagnostic: the bf16 image swizzle (tests check the image and its bank model)
+extern "C" int t2o_bf_swz(int row, int ld) { return t2o::bf_swz(row, ld); }

@@ -78,8 +78,9 @@ def test_pack_and_unpack(kind):
 
 
 def _bf_swz(r, ld):
-    """include/t2omca.h bf16 image swizzle (t2o_common.hpp bf_swz)."""
-    return 8 * ((r >> 2) & 3) if ld % 32 == 0 else 8 * ((r >> 3) & 1)
+    """The bf16 image swizzle (t2o_common.hpp bf_swz, exported as t2o_bf_swz)."""
+    from t2omca_amd import _lib
+    return int(_lib.lib().t2o_bf_swz(r, ld))
 
 
 @pytest.mark.parametrize("kind", [0, 1])
