@@ -104,6 +104,9 @@ EXPORTS = {
                                                                  ctypes.c_uint64, ctypes.c_int64, ctypes.c_void_p]),
 }
 
+# exports only tests / tools call (never on the product path)
+_DIAGNOSTIC = {"t2o_bf_swz", "t2o_probe_lane_ops"}
+
 _lib = None
 
 
@@ -118,6 +121,8 @@ def lib():
                                "(there is no CPU fallback)")
         h = ctypes.CDLL(path)
         for name, (res, args) in EXPORTS.items():
+            if name in _DIAGNOSTIC and path != LIB and not hasattr(h, name):
+                continue  # an older build under A/B (T2O_LIB) may lack a diagnostic export
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args

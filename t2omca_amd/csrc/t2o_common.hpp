@@ -170,6 +170,10 @@ T2O_DEV f4 mfma_b32(bf4 a0, bf4 a1, bf4 b0, bf4 b1, f4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
 }
 
+#ifndef T2O_SWZ_HOIST  // see matvec (bf16)
+#define T2O_SWZ_HOIST 1
+#endif
+
 // Bank-conflict-free bf16 weight rows.  The bf16 image stores element
 // (r, col) at r*ld + (col ^ bf_swz(r, ld)) — an XOR of whole 8-element groups,
 // so the 4 (or 8) consecutive K values a lane loads stay contiguous — and the
@@ -207,10 +211,14 @@ T2O_DEV f4 mma_tile(const __bf16* __restrict__ W, int ldw, int o, int i, f4 x, f
 // y[0..OT) = W · x[0..IT), bf16 weights and operands, fp32 accumulate
 template <int OT, int IT>
 T2O_DEV void matvec(const __bf16* __restrict__ W, int ldw, const f4* x, f4* y) {
-  // the lane's row swizzle derived per product from an opaque lane id: hoisted
-  // out of a step loop, one register per distinct row length would stay live
+  // T2O_SWZ_HOIST 0 (the mixer kernels, register-bound at two waves per SIMD):
+  // the lane's row swizzle is derived per product from an opaque lane id, since
+  // hoisted out of the step loop one register per distinct row length stays
+  // live (mixer BPTT spills 26 -> 4 VGPRs).  1 (default; the agent kernels,
+  // issue-bound at one wave per SIMD): computed once, hoisted — per product it
+  // costs them ~7 % (interleaved A/B, profiles/r3_ab_swz/).
   int l = threadIdx.x;
-  asm volatile("" : "+v"(l));
+  if (!T2O_SWZ_HOIST) asm volatile("" : "+v"(l));
   const int c = l & 15, g = (l >> 4) & 3;
   bf4 xb[IT];
 #pragma unroll

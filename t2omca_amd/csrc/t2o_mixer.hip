@@ -9,6 +9,8 @@
 //   qmode 0  qvals given directly                      [b][t][a]
 //   qmode 1  chosen-action Q  gather(Q[:, t], actions)  (online mixer)
 //   qmode 2  double-Q         Q_tgt[argmax(Q_on masked by avail)] (target mixer)
+// per-product weight swizzle (t2o_common.hpp matvec): these kernels are register-bound
+#define T2O_SWZ_HOIST 0
 #include "t2o_dispatch.hpp"
 #include "t2o_generic.hpp"
 #include "t2o_layout.hpp"
