@@ -508,6 +508,10 @@ def main():
 
     learner = make_learner(args.dtype)
     batch, w = make_batch(B, T, A, seed=1 + rank, device=dev)
+    # which kernels run (include/t2omca.h t2o_layout_instance): the runtime-shaped
+    # generic kernels compute in fp32 whatever precision is asked, and say so
+    kernels = {"agent": learner.sa.instance, "mixer": learner.sm.instance}
+    dtype = "fp32" if "generic" in kernels.values() else args.dtype
     if args.mode == "forward":
         from t2omca_amd import ops
         act = batch["actions"][..., 0]
@@ -567,11 +571,11 @@ def main():
         out = {"metric": "agent-transitions/sec for agent+mixer forward (inference over a replay batch)",
                "value": value, "unit": "agent-transitions/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+               "scaling": "weak", "vs_baseline": None, "dtype": dtype,
                "data": "synthetic (SURVEY.md §8 d distributions, resident in HBM)",
                "config": {"workload": f"configs[1]-style: online agent (t=0..T) + online mixer (t<T) unroll, "
                                       f"{A} AGVs, batch {B} episodes/GPU x T={T}",
-                          "global_batch": B * world, "seq_len": T, "agents": A}}
+                          "global_batch": B * world, "seq_len": T, "agents": A, "kernels": kernels}}
         if rank == 0:
             print(json.dumps(out), flush=True)
         if world > 1:
@@ -588,7 +592,7 @@ def main():
     # (the tape contractions are part of a backward; mixer_dw runs on a side stream)
     dom = max(ref_flops, key=lambda k: kern.get(k, 0.0))
     dom_ms = kern.get(dom, float("nan"))
-    peak_tf = PEAK_BF16_TFLOPS if args.dtype == "bf16" else PEAK_FP32_TFLOPS
+    peak_tf = PEAK_BF16_TFLOPS if dtype == "bf16" else PEAK_FP32_TFLOPS
     # SURVEY.md §8(d) basis: the reference-order necessary FLOPs of the kernel's share
     achieved = ref_flops[dom] / (dom_ms * 1e-3) / 1e12
     ms_step = elapsed / args.steps * 1e3
@@ -605,12 +609,12 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": args.dtype,
+        "dtype": dtype,
         "data": "synthetic (SURVEY.md §8 d distributions, seeded per rank, resident in HBM)",
         "config": {"workload": f"{train_config_name(A, B, T)}: full TD update fwd+bwd+Adam, {A} AGVs, "
                                f"batch {B} episodes/GPU x T={T}",
                    "global_batch": B * world, "seq_len": T, "agents": A, "emb": 32, "heads": 3, "depth": 2,
-                   "parallelism": f"dp{world}", "priorities": args.priorities},
+                   "parallelism": f"dp{world}", "priorities": args.priorities, "kernels": kernels},
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": peak_tf,
                      "unit": "TFLOP/s", "frac": achieved / peak_tf, "traffic": traffic_for(dom, workload_tag(args)),
                      "basis": "SURVEY.md §8(d) reference-order necessary FLOPs of the kernel's share "
@@ -631,7 +635,7 @@ def main():
         "flops_per_transition": {"executed_algorithm": sum(flops.values()) / (B * T * A),
                                  "reference_order": ref_order_flops_per_transition(A)},
     }
-    if args.dtype == "bf16" and args.fp32_companion:
+    if dtype == "bf16" and args.fp32_companion:
         # the same workload at the reference's own precision (fp32 MFMA operands)
         lr32 = make_learner("fp32")
         el32 = timed(make_step(lr32))

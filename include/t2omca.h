@@ -96,17 +96,29 @@ typedef struct {
 #define T2O_LAYOUT_FORCE_GENERIC 1  /* use the runtime-shaped kernels even for a tuned shape */
 
 /* Fill *L for a network (prec 0 = fp32, 1 = bf16 MFMA operands); returns 0 or T2O_EINVAL.
- * Shapes with a tuned kernel instance (E 32 / 3 heads / depth 2 / FF 128 at 3, 8, 16 or
- * 64 entities; E 16 / 2 heads / depth 1 / FF 64 at 3) get the folded MFMA pack; any
- * other shape within the runtime-shaped kernels' limits (E <= 64, H <= 8, H*E <= 512,
- * D <= 4, FF <= 512, F <= 16, NA <= 16, agent entities <= 64, mixer tokens
- * n_ent + n_agents + 3 <= 192 with n_agents <= 64) gets generic = 1.  The generic
- * kernels compute in fp32 whatever prec says. */
+ * Shapes with a tuned MFMA kernel instance get the folded MFMA pack: the default
+ * network (E 32 / 3 heads / depth 2 / FF 128) at any entity count 1..64 — exact
+ * instances at 3, 8, 16 and 64, runtime-entity instances of capacity 8 / 16 / 64
+ * (agent) and 8 / 13 / 16 / 32 / 64 (mixer) otherwise (t2o_layout_instance) — and
+ * E 16 / 2 heads / depth 1 / FF 64 at 3 (a fixture shape).  Any other shape within
+ * the runtime-shaped kernels' limits (E <= 64, H <= 8, H*E <= 512, D <= 4, FF <= 512,
+ * F <= 16, NA <= 16, agent entities <= 64, mixer tokens n_ent + n_agents + 3 <= 192
+ * with n_agents <= 64), a mixer head other than abs, or n_agents != n_ent, gets
+ * generic = 1.  The generic kernels compute in fp32 whatever prec says. */
 int t2o_layout_init(t2o_layout* L, int kind, int E, int H, int D, int F, int NA, int FF, int n_ent, int prec);
 /* t2o_layout_init with the mixer's agent count (n_agents; 0 = n_ent), its head's
  * positivity function (T2O_POS_*, softplus beta) and flags (T2O_LAYOUT_*). */
 int t2o_layout_init_ex(t2o_layout* L, int kind, int E, int H, int D, int F, int NA, int FF, int n_ent, int prec,
                        int n_agents, int pos_func, float pos_beta, int flags);
+
+/* Which kernels a layout runs: T2O_INSTANCE_EXACT (MFMA instance compiled for its
+ * entity count), T2O_INSTANCE_RUNTIME (MFMA instance of a capacity class, entity
+ * count read at run time), T2O_INSTANCE_GENERIC (runtime-shaped fp32 kernels);
+ * negative on a null layout. */
+#define T2O_INSTANCE_EXACT 0
+#define T2O_INSTANCE_RUNTIME 1
+#define T2O_INSTANCE_GENERIC 2
+int t2o_layout_instance(const t2o_layout* L);
 
 /* sizeof(t2o_layout), for bindings to check their mirror of the struct. */
 int t2o_layout_sizeof(void);

@@ -37,6 +37,7 @@ EXPORTS = {
                                                                                        ctypes.c_int]),
     "t2o_param_count": (ctypes.c_int64, [ctypes.c_int] * 7),
     "t2o_layout_sizeof": (ctypes.c_int, []),
+    "t2o_layout_instance": (ctypes.c_int, [ctypes.POINTER(Layout)]),
     "t2o_pack_params": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_void_p]),
     "t2o_unpack_grads": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_void_p, ctypes.c_void_p,

@@ -51,7 +51,9 @@ constexpr int AG_FWD_WAVES = 4;  // waves per workgroup sharing one LDS copy of 
 template <int NE>
 constexpr int agent_fwd_waves_per_eu() { return NE <= 8 ? 2 : 1; }
 
-template <int E, int H, int D, int NE, int FF, bool WLDS, typename WT>
+// RT: runtime-entity instance (t2o_dispatch.hpp) — NE is a capacity, the real
+// entity count is args.A (n_entities = n_agents on the tuned path)
+template <int E, int H, int D, int NE, int FF, bool RT, bool WLDS, typename WT>
 __global__ __launch_bounds__(64 * AG_FWD_WAVES) __attribute__((amdgpu_waves_per_eu(agent_fwd_waves_per_eu<NE>())))
 void agent_fwd_kernel(AgentFwdArgs args) {
   constexpr int ET = E / 16;
@@ -67,6 +69,7 @@ void agent_fwd_kernel(AgentFwdArgs args) {
     P0 = global_weights(net.pack, L, WT{});
   }
   const int A = args.A, F = args.F;
+  const int ne = RT ? A : NE;
   const int R = args.B * A;
   const int rt = blockIdx.x * AG_FWD_WAVES + wave_id();
   if (rt * args.rpw >= R) return;  // wave-uniform: no barriers after this point
@@ -86,7 +89,7 @@ void agent_fwd_kernel(AgentFwdArgs args) {
   constexpr bool CHUNK = NE > AG_CHUNK_MIN;
   constexpr int NO = CHUNK ? 1 : NE;
   auto row_obs = [&](int step) {
-    return args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * NE * F;
+    return args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * ne * F;
   };
   auto load_obs = [&](int step, f4 (&o)[NO]) {
     const float* ob = row_obs(step);
@@ -95,7 +98,7 @@ void agent_fwd_kernel(AgentFwdArgs args) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int f = 4 * g + r;
-        o[j][r] = f < F ? ob[j * F + f] : 0.f;
+        o[j][r] = (f < F && j < ne) ? ob[j * F + f] : 0.f;
       }
   };
   f4 on[NO];
@@ -108,7 +111,7 @@ void agent_fwd_kernel(AgentFwdArgs args) {
       for (int j = 0; j < NE; ++j) o[j] = on[j];
       if (step + 1 < args.T) load_obs(step + 1, on);
     }
-    const ObsRow orow{row_obs(step), F};
+    const ObsRow orow{row_obs(step), F, ne, RT && ne % AG_CHUNK != 0};
     f4 x[ET];
 #pragma unroll
     for (int t = 0; t < ET; ++t) x[t] = h[t];
@@ -123,7 +126,7 @@ void agent_fwd_kernel(AgentFwdArgs args) {
         agent_block_fwd_ch<E, H, NE, FF, false>(P, L, d, h, orow, x, nullptr);
       } else {
         (void)orow;
-        agent_block_fwd<E, H, NE, FF, false>(P, L, d, h, o, x, nullptr);
+        agent_block_fwd<E, H, NE, FF, false>(P, L, d, h, o, ne, x, nullptr);
       }
     }
     f4 q = zero4();
@@ -145,7 +148,7 @@ void agent_fwd_kernel(AgentFwdArgs args) {
   }
 }
 
-template <int E, int H, int D, int NE, int FF, typename WT>
+template <int E, int H, int D, int NE, int FF, bool RT, typename WT>
 int launch_fwd(const AgentFwdArgs& args, int nnet, hipStream_t stream) {
   const int R = args.B * args.A;
   AgentFwdArgs a = args;
@@ -155,7 +158,7 @@ int launch_fwd(const AgentFwdArgs& args, int nnet, hipStream_t stream) {
   size_t lds = sizeof(float) * (size_t)lds_weight_floats<WT>(args.L, args.L.fwd_total);
   a.wlds = lds <= 160 * 1024;
   if (!a.wlds) lds = 0;
-  auto kern = a.wlds ? agent_fwd_kernel<E, H, D, NE, FF, true, WT> : agent_fwd_kernel<E, H, D, NE, FF, false, WT>;
+  auto kern = a.wlds ? agent_fwd_kernel<E, H, D, NE, FF, RT, true, WT> : agent_fwd_kernel<E, H, D, NE, FF, RT, false, WT>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, grid, dim3(64 * AG_FWD_WAVES), lds, stream, a);
   return (int)hipGetLastError();
@@ -196,7 +199,7 @@ struct AgentBwdArgs {
 
 constexpr int AG_BWD_WAVES = 2;  // (each wave needs a SIMD's full 512-register file)
 
-template <int E, int H, int D, int NE, int FF, typename WT>
+template <int E, int H, int D, int NE, int FF, bool RT, typename WT>
 __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdArgs args) {
   constexpr int ET = E / 16;
   constexpr int STAGE = StageDims<1>::FLOATS;
@@ -214,6 +217,7 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
   __syncthreads();
 
   const int A = args.A, F = args.F, T = args.T;
+  const int ne = RT ? A : NE;
   const int R = args.B * A;
   const int rt = blockIdx.x * AG_BWD_WAVES + wave_id();
   const int c = lane_c(), g = lane_g();
@@ -247,10 +251,10 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
       if (step == 0 && args.h0) hp = args.h0 + (size_t)row * E;
 #pragma unroll
       for (int t = 0; t < ET; ++t) h[t] = hp ? ld4(hp + 16 * t + 4 * g) : zero4();
-      const float* ob = args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * NE * F;
+      const float* ob = args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * ne * F;
       constexpr bool CHUNK = NE > AG_CHUNK_MIN;  // many entities: streamed per block (t2o_agent_block_ch.hpp)
       constexpr int NO = CHUNK ? 1 : NE;
-      const ObsRow orow{ob, F};
+      const ObsRow orow{ob, F, ne, RT && ne % AG_CHUNK != 0};
       f4 o[NO];
       if constexpr (!CHUNK) {
 #pragma unroll
@@ -258,7 +262,7 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int f = 4 * g + r;
-            o[j][r] = f < F ? ob[j * F + f] : 0.f;
+            o[j][r] = (f < F && j < ne) ? ob[j * F + f] : 0.f;
           }
       }
       // external grads of this step
@@ -305,7 +309,7 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
 #pragma unroll
           for (int t = 0; t < ET; ++t) x[t] = xs[d][t];
           if constexpr (CHUNK) agent_block_fwd_ch<E, H, NE, FF, false>(P, L, d, h, orow, x, nullptr);
-          else agent_block_fwd<E, H, NE, FF, false>(P, L, d, h, o, x, nullptr);
+          else agent_block_fwd<E, H, NE, FF, false>(P, L, d, h, o, ne, x, nullptr);
 #pragma unroll
           for (int t = 0; t < ET; ++t) xs[d + 1][t] = x[t];
         }
@@ -320,7 +324,7 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
 #pragma unroll
         for (int t = 0; t < ET; ++t) x[t] = xs[d][t];
         if constexpr (CHUNK) agent_block_fwd_ch<E, H, NE, FF, true>(P, L, d, h, orow, x, &cache);
-        else agent_block_fwd<E, H, NE, FF, true>(P, L, d, h, o, x, &cache);
+        else agent_block_fwd<E, H, NE, FF, true>(P, L, d, h, o, ne, x, &cache);
         if (d == D - 1) {  // q = Wo x + bo
           dw_accumulate_regs<1, ET, sizeof(WT) == 2>(gWo, &gq, x, stage);
           gbo += gq;
@@ -391,7 +395,7 @@ constexpr int agp_stage_floats() {
   return agp_acc<E, H, NE, WT>() ? AgentAccTiles<E, H>::N * 128 : StageDims<1>::FLOATS;
 }
 
-template <int E, int H, int D, int NE, int FF, typename WT>
+template <int E, int H, int D, int NE, int FF, bool RT, typename WT>
 __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(AgentBwdArgs args) {
   static_assert(D == 2, "one wave per block of a depth-2 stack");
   constexpr int ET = E / 16, HET = H * ET;
@@ -436,6 +440,8 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
   PairBarrier pb = PairBarrier::make(flags, w);
 
   const int A = args.A, F = args.F, T = args.T;
+  const int ne = RT ? A : NE;
+  const bool tail = RT && ne % AG_CHUNK != 0;
   const int R = args.B * A;
   const int rt = blockIdx.x * AGP_TILES + tl;
   const int c = lane_c(), g = lane_g();
@@ -481,13 +487,13 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
 #pragma unroll
     for (int t = 0; t < ET; ++t) hh[t] = hp ? ld4(hp + 16 * t + 4 * g) : zero4();
     if constexpr (!CHUNK) {
-      const float* obp = args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * NE * F;
+      const float* obp = args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * ne * F;
 #pragma unroll
       for (int j = 0; j < NE; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int f = 4 * g + r;
-          oo[j][r] = f < F ? obp[j * F + f] : 0.f;
+          oo[j][r] = (f < F && j < ne) ? obp[j * F + f] : 0.f;
         }
     }
     if (d == 1) {  // (block 0's input is h itself: copied where used, never here —
@@ -530,7 +536,7 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
     T2O_STAMP(2 * (T - 1 - step), 0);
 #endif
     Cache cache;
-    const float* ob = args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * NE * F;
+    const float* ob = args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * ne * F;
 #pragma unroll
     for (int ph = 0; ph < 2; ++ph) {
       T2O_MARK(0);
@@ -549,11 +555,12 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
 #pragma unroll
           for (int t = 0; t < ET; ++t) xo[t] = h[t];
         }
-        if constexpr (CHUNK) agent_block_fwd_ch<E, H, NE, FF, true>(P, Lb, 0, h, ObsRow{ob, F}, xo, &cache);
+        if constexpr (CHUNK) agent_block_fwd_ch<E, H, NE, FF, true>(P, Lb, 0, h, ObsRow{ob, F, ne, tail}, xo, &cache);
         else if constexpr (ACC)
-          agent_block_fwd_acc<E, H, NE, FF>(P, Lb, 0, h, o, xo, cache, MaskedRec<WT>(tile, tile_ok ? 16 : 0, Rec::SIZE),
-                                            stage, gM, gN, gWe);
-        else agent_block_fwd_lean<E, H, NE, FF>(P, Lb, 0, h, o, xo, cache, MaskedRec<WT>(tile, tile_ok ? 16 : 0, Rec::SIZE));
+          agent_block_fwd_acc<E, H, NE, FF>(P, Lb, 0, h, o, ne, xo, cache,
+                                            MaskedRec<WT>(tile, tile_ok ? 16 : 0, Rec::SIZE), stage, gM, gN, gWe);
+        else agent_block_fwd_lean<E, H, NE, FF>(P, Lb, 0, h, o, ne, xo, cache,
+                                                MaskedRec<WT>(tile, tile_ok ? 16 : 0, Rec::SIZE));
       } else {
         f4 gx[ET], ghi[ET];
         if (d == 1) {
@@ -592,7 +599,7 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
 #endif
         T2O_MARK(1);
         if constexpr (CHUNK)
-          agent_block_bwd_ch<E, H, NE, FF>(P, Lb, Gb, gs, tile_ok ? tile : nullptr, stage, 0, h, ObsRow{ob, F}, cache,
+          agent_block_bwd_ch<E, H, NE, FF>(P, Lb, Gb, gs, tile_ok ? tile : nullptr, stage, 0, h, ObsRow{ob, F, ne, tail}, cache,
                                            gx, ghi, gbe, gWe, ln2);
         else if constexpr (ACC)
           agent_block_bwd_acc<E, H, NE, FF>(P, Lb, gs, MaskedRec<WT>(tile, tile_ok ? 16 : 0, Rec::SIZE), stage, 0, h,
@@ -656,18 +663,18 @@ size_t bwd_pipe_lds_bytes(const t2o_layout& L) {
 
 // which BPTT kernel launch_bwd picks: the pipelined one (depth 2, block inputs
 // stored by the forward, LDS fits, no T2O_AGENT_BWD=single)
-template <int E, int H, int D, int NE, int FF, typename WT>
+template <int E, int H, int D, int NE, int FF, bool RT, typename WT>
 bool bwd_uses_pipe(const t2o_layout& L, bool has_hmid) {
   if constexpr (D == 2) return has_hmid && bwd_pipe_lds_bytes<E, H, D, NE, FF, WT>(L) <= 160 * 1024 && !agent_bwd_single_wave();
   return false;
 }
 
-template <int E, int H, int D, int NE, int FF, typename WT>
+template <int E, int H, int D, int NE, int FF, bool RT, typename WT>
 int bwd_tape_format(const t2o_layout& L, bool has_hmid) {
-  return bwd_uses_pipe<E, H, D, NE, FF, WT>(L, has_hmid) && agp_acc<E, H, NE, WT>() ? 1 : 0;
+  return bwd_uses_pipe<E, H, D, NE, FF, RT, WT>(L, has_hmid) && agp_acc<E, H, NE, WT>() ? 1 : 0;
 }
 
-template <int E, int H, int D, int NE, int FF, typename WT>
+template <int E, int H, int D, int NE, int FF, bool RT, typename WT>
 int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
   const int R = args.B * args.A;
   args.rpw = rows_per_wave(R);
@@ -676,8 +683,8 @@ int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream
   if (grid > max_slabs) return T2O_EINVAL;
   if constexpr (D == 2) {
     const size_t lds = bwd_pipe_lds_bytes<E, H, D, NE, FF, WT>(args.L);
-    if (bwd_uses_pipe<E, H, D, NE, FF, WT>(args.L, args.hmid != nullptr)) {
-      auto kern = agent_bwd_pipe_kernel<E, H, D, NE, FF, WT>;
+    if (bwd_uses_pipe<E, H, D, NE, FF, RT, WT>(args.L, args.hmid != nullptr)) {
+      auto kern = agent_bwd_pipe_kernel<E, H, D, NE, FF, RT, WT>;
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
       hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * 2 * AGP_TILES), lds, stream, args);
       *nslab = grid;
@@ -687,7 +694,7 @@ int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream
   const int64_t nw = args.L.fwd_total;
   const size_t lds =
       sizeof(float) * ((size_t)(lds_weight_floats<WT>(args.L, nw) + 15) / 16 * 16 + AG_BWD_WAVES * StageDims<1>::FLOATS);
-  auto kern = agent_bwd_kernel<E, H, D, NE, FF, WT>;
+  auto kern = agent_bwd_kernel<E, H, D, NE, FF, RT, WT>;
   if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * AG_BWD_WAVES), lds, stream, args);
@@ -724,9 +731,9 @@ extern "C" int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, c
   args.A = A;
   args.F = L->F;
   int rc = T2O_EUNSUPPORTED;
-  T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
-               rc = (L->prec ? launch_fwd<E_, H_, D_, NE_, FF_, __bf16>(args, nnet, (hipStream_t)stream)
-                             : launch_fwd<E_, H_, D_, NE_, FF_, float>(args, nnet, (hipStream_t)stream)));
+  T2O_DISPATCH_AGENT(L->E, L->H, L->D, L->n_ent, L->FF,
+                     rc = (L->prec ? launch_fwd<E_, H_, D_, NE_, FF_, RT_, __bf16>(args, nnet, (hipStream_t)stream)
+                                   : launch_fwd<E_, H_, D_, NE_, FF_, RT_, float>(args, nnet, (hipStream_t)stream)));
   return rc;
 }
 
@@ -767,9 +774,9 @@ extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, cons
   args.A = A;
   args.F = L->F;
   int rc = T2O_EUNSUPPORTED;
-  T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
-               rc = (L->prec ? launch_bwd<E_, H_, D_, NE_, FF_, __bf16>(args, max_slabs, nslab, (hipStream_t)stream)
-                             : launch_bwd<E_, H_, D_, NE_, FF_, float>(args, max_slabs, nslab, (hipStream_t)stream)));
+  T2O_DISPATCH_AGENT(L->E, L->H, L->D, L->n_ent, L->FF,
+                     rc = (L->prec ? launch_bwd<E_, H_, D_, NE_, FF_, RT_, __bf16>(args, max_slabs, nslab, (hipStream_t)stream)
+                                   : launch_bwd<E_, H_, D_, NE_, FF_, RT_, float>(args, max_slabs, nslab, (hipStream_t)stream)));
   return rc;
 }
 
@@ -780,9 +787,9 @@ extern "C" int t2o_agent_bwd_tape_format(const t2o_layout* L, int has_hmid) {
   if (!L || L->kind != 0) return T2O_EINVAL;
   if (L->generic) return 0;
   int fmt = 0;
-  T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
-               fmt = (L->prec ? bwd_tape_format<E_, H_, D_, NE_, FF_, __bf16>(*L, has_hmid != 0)
-                              : bwd_tape_format<E_, H_, D_, NE_, FF_, float>(*L, has_hmid != 0)));
+  T2O_DISPATCH_AGENT(L->E, L->H, L->D, L->n_ent, L->FF,
+                     fmt = (L->prec ? bwd_tape_format<E_, H_, D_, NE_, FF_, RT_, __bf16>(*L, has_hmid != 0)
+                                    : bwd_tape_format<E_, H_, D_, NE_, FF_, RT_, float>(*L, has_hmid != 0)));
   return fmt;
 }
 

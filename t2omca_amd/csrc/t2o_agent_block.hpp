@@ -38,8 +38,10 @@ using AgentCacheLean = AgentCacheT<E, H, NE, FF, true>;
 
 // Attention half of block d: u = M x, per head softmax over [h, entities] and
 // z_h = p0 h + We ô_h + P_h b_e.  Caches (u, p, ô, P) when C is non-null.
+// ne: the entity count (NE, or fewer in a runtime-entity instance: entities
+// j >= ne are padding — zero observations, score -inf, probability 0).
 template <int E, int H, int NE, int FF, bool LEAN, typename WT>
-T2O_DEV void agent_attn_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* h, const f4 (&o)[NE],
+T2O_DEV void agent_attn_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* h, const f4 (&o)[NE], int ne,
                             const f4* x, f4* z, AgentCacheT<E, H, NE, FF, LEAN>* cache) {
   constexpr int ET = E / 16, HET = H * ET;
   const float* be = P.v + L.be;
@@ -68,7 +70,7 @@ T2O_DEV void agent_attn_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const 
     const float cval = red[0];
     p[0] = red[1];
 #pragma unroll
-    for (int j = 0; j < NE; ++j) p[j + 1] = red[j + 2] + cval;
+    for (int j = 0; j < NE; ++j) p[j + 1] = j < ne ? red[j + 2] + cval : -INFINITY;
     float m = p[0];
 #pragma unroll
     for (int j = 1; j <= NE; ++j) m = fmaxf(m, p[j]);
@@ -109,20 +111,20 @@ T2O_DEV void agent_attn_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const 
 // x: in = block input query, out = block output.
 template <int E, int H, int NE, int FF, bool CACHE, typename WT>
 T2O_DEV void agent_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* h,
-                             const f4 (&o)[NE], f4* x, AgentCache<E, H, NE, FF>* cache) {
+                             const f4 (&o)[NE], int ne, f4* x, AgentCache<E, H, NE, FF>* cache) {
   constexpr int HET = H * (E / 16);
   f4 z[HET];
-  agent_attn_fwd<E, H, NE, FF, false>(P, L, d, h, o, x, z, CACHE ? cache : nullptr);
+  agent_attn_fwd<E, H, NE, FF, false>(P, L, d, h, o, ne, x, z, CACHE ? cache : nullptr);
   T2O_MARK(2);
   post_fwd<E, H, FF, CACHE>(P, L, d, z, x, CACHE ? &cache->post : nullptr);
 }
 
 template <int E, int H, int NE, int FF, typename WT>
 T2O_DEV void agent_block_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d, const f4* h, const f4 (&o)[NE],
-                                  f4* x, AgentCacheLean<E, H, NE, FF>& cache, const MaskedRec<WT>& rec) {
+                                  int ne, f4* x, AgentCacheLean<E, H, NE, FF>& cache, const MaskedRec<WT>& rec) {
   constexpr int HET = H * (E / 16);
   f4 z[HET];
-  agent_attn_fwd<E, H, NE, FF, true>(P, L, d, h, o, x, z, &cache);
+  agent_attn_fwd<E, H, NE, FF, true>(P, L, d, h, o, ne, x, z, &cache);
   T2O_MARK(2);
   post_fwd_lean<E, H, FF>(P, L, d, z, x, &cache.post, rec);
 }
@@ -188,7 +190,7 @@ T2O_DEV void agent_dw_deferred(float* __restrict__ stage, f4 (&gM)[H * (E / 16)]
 
 template <int E, int H, int NE, int FF, typename WT>
 T2O_DEV void agent_block_fwd_acc(const Wts<WT>& P, const t2o_layout& L, int d, const f4* h, const f4 (&o)[NE],
-                                 f4* x, AgentCacheLean<E, H, NE, FF>& cache, const MaskedRec<WT>& rec,
+                                 int ne, f4* x, AgentCacheLean<E, H, NE, FF>& cache, const MaskedRec<WT>& rec,
                                  float* __restrict__ stage, f4 (&gM)[H * (E / 16)][E / 16],
                                  f4 (&gN)[E / 16][H * (E / 16)], f4 (&gWe)[E / 16][1]) {
   using Tl = AgentAccTiles<E, H>;
@@ -198,7 +200,7 @@ T2O_DEV void agent_block_fwd_acc(const Wts<WT>& P, const t2o_layout& L, int d, c
 #pragma unroll
   for (int t = 0; t < Tl::ET; ++t) stage_tile_bf(sb, Tl::XT + t, x[t]);
   f4 z[Tl::HET];
-  agent_attn_fwd<E, H, NE, FF, true>(P, L, d, h, o, x, z, &cache);
+  agent_attn_fwd<E, H, NE, FF, true>(P, L, d, h, o, ne, x, z, &cache);
 #pragma unroll
   for (int t = 0; t < Tl::HET; ++t) stage_tile_bf(sb, Tl::ZT + t, z[t]);
   post_fwd_lean<E, H, FF, WT, TapeRecA<E, H, FF>>(P, L, d, z, x, &cache.post, rec);

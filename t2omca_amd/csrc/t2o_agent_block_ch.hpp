@@ -26,9 +26,13 @@ constexpr int AG_CHUNK_MIN = T2O_AG_CHUNK_MIN;
 
 // One row's observation vector in memory: entity j, feature f at ob[j*F + f];
 // a lane loads the T-layout slice (features 4g .. 4g+3, zero-padded past F).
+// ne entities; `tail` when ne is not a multiple of the chunk (a runtime-entity
+// instance): the last chunk's entities j >= ne load zeros and score -inf.
 struct ObsRow {
   const float* ob;
   int F;
+  int ne;
+  bool tail;
   template <int CH>
   T2O_DEV void load(int j0, f4 (&o)[CH]) const {
     const int g = lane_g();
@@ -37,9 +41,10 @@ struct ObsRow {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int f = 4 * g + r;
-        o[j][r] = f < F ? ob[(j0 + j) * F + f] : 0.f;
+        o[j][r] = (f < F && (!tail || j0 + j < ne)) ? ob[(j0 + j) * F + f] : 0.f;
       }
   }
+  T2O_DEV bool pad(int j) const { return tail && j >= ne; }
 };
 
 template <int E, int H, int NE, int FF>
@@ -60,7 +65,6 @@ template <int E, int H, int NE, int FF, bool CACHE, typename WT>
 T2O_DEV void agent_block_fwd_ch(const Wts<WT>& P, const t2o_layout& L, int d, const f4* h, const ObsRow& orow,
                                 f4* x, AgentCacheCh<E, H, NE, FF>* cache) {
   constexpr int ET = E / 16, HET = H * ET, CH = AG_CHUNK;
-  static_assert(NE % CH == 0, "entity count must be a multiple of the chunk");
   const float* be = P.v + L.be;
   f4 u[HET];
   matvec<HET, ET>(P.w + L.M[d], E, x, u);
@@ -87,9 +91,10 @@ T2O_DEV void agent_block_fwd_ch(const Wts<WT>& P, const t2o_layout& L, int d, co
   }
   f4 o[CH];
   orow.load<CH>(0, o);
-  for (int j0 = 0; j0 < NE; j0 += CH) {
+  const int ne = orow.ne;
+  for (int j0 = 0; j0 < ne; j0 += CH) {
     f4 on[CH];
-    if (j0 + CH < NE) orow.load<CH>(j0 + CH, on);  // next chunk in flight while this one computes
+    if (j0 + CH < ne) orow.load<CH>(j0 + CH, on);  // next chunk in flight while this one computes
 #pragma unroll
     for (int hh = 0; hh < H; ++hh) {
       float s[CH];
@@ -98,6 +103,7 @@ T2O_DEV void agent_block_fwd_ch(const Wts<WT>& P, const t2o_layout& L, int d, co
       for (int j = 0; j < CH; ++j) {
         const f4 wv = w[hh];
         s[j] = allsum4((wv[0] * o[j][0] + wv[1] * o[j][1]) + (wv[2] * o[j][2] + wv[3] * o[j][3])) + cval[hh];
+        if (orow.pad(j0 + j)) s[j] = -INFINITY;
         mc = fmaxf(mc, s[j]);
       }
       const float sc = exp_fast(m[hh] - mc);
@@ -114,7 +120,7 @@ T2O_DEV void agent_block_fwd_ch(const Wts<WT>& P, const t2o_layout& L, int d, co
       }
       m[hh] = mc;
     }
-    if (j0 + CH < NE) {
+    if (j0 + CH < ne) {
 #pragma unroll
       for (int j = 0; j < CH; ++j) o[j] = on[j];
     }
@@ -187,16 +193,18 @@ T2O_DEV void agent_block_bwd_ch(const Wts<WT>& P, const t2o_layout& L, const t2o
   // entities, chunk by chunk: p recomputed from the cached (w, c, max, 1/sum)
   f4 o[CH];
   orow.load<CH>(0, o);
-  for (int j0 = 0; j0 < NE; j0 += CH) {
+  const int ne = orow.ne;
+  for (int j0 = 0; j0 < ne; j0 += CH) {
     f4 on[CH];
-    if (j0 + CH < NE) orow.load<CH>(j0 + CH, on);
+    if (j0 + CH < ne) orow.load<CH>(j0 + CH, on);
 #pragma unroll
     for (int hh = 0; hh < H; ++hh) {
       const f4 wv = c.w[hh], go = goh[hh];
 #pragma unroll
       for (int j = 0; j < CH; ++j) {
-        const float s = allsum4((wv[0] * o[j][0] + wv[1] * o[j][1]) + (wv[2] * o[j][2] + wv[3] * o[j][3])) +
-                        c.cval[hh];
+        float s = allsum4((wv[0] * o[j][0] + wv[1] * o[j][1]) + (wv[2] * o[j][2] + wv[3] * o[j][3])) +
+                  c.cval[hh];
+        if (orow.pad(j0 + j)) s = -INFINITY;
         const float p = exp_fast(s - c.m[hh]) * c.il[hh];
         const float gp =
             allsum4((go[0] * o[j][0] + go[1] * o[j][1]) + (go[2] * o[j][2] + go[3] * o[j][3])) + gP[hh];
@@ -205,7 +213,7 @@ T2O_DEV void agent_block_bwd_ch(const Wts<WT>& P, const t2o_layout& L, const t2o
         gc[hh] += gsj;
       }
     }
-    if (j0 + CH < NE) {
+    if (j0 + CH < ne) {
 #pragma unroll
       for (int j = 0; j < CH; ++j) o[j] = on[j];
     }

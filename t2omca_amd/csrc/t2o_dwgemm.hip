@@ -436,7 +436,7 @@ __global__ __launch_bounds__(256 * D) void dw_gemm_kernel(DwGemmArgs a) {
   }
 }
 
-template <int E, int H, int FF, int D, int NE, typename TT, int FMT>
+template <int E, int H, int FF, int D, typename TT, int FMT>
 int launch_dw_gemm(int kind, const void* tape, int64_t ntiles, const float* pack, float* slabs, const t2o_layout& L,
                    const t2o_layout& G, int nslab, hipStream_t stream) {
   using Dm = DwDims<E, H, FF, D, TT, 16, FMT>;
@@ -450,8 +450,8 @@ int launch_dw_gemm(int kind, const void* tape, int64_t ntiles, const float* pack
   a.L = L;
   a.G = G;
   const size_t lds = sizeof(TT) * ((size_t)2 * Dm::GELEM + (Dm::BF ? (size_t)D * 2 * FF * E : 0));
-  constexpr int RTM = mixer_tape_records(NE);  // the mixer's query rows per tape tile
-  auto kern = kind == 0 ? dw_gemm_kernel<E, H, FF, D, 0, TT, 16, FMT> : dw_gemm_kernel<E, H, FF, D, 1, TT, RTM, 0>;
+  // (every tuned mixer writes its records as one compact stream of 16-record tiles)
+  auto kern = kind == 0 ? dw_gemm_kernel<E, H, FF, D, 0, TT, 16, FMT> : dw_gemm_kernel<E, H, FF, D, 1, TT, 16, 0>;
   if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(nslab), dim3(256 * D), lds, stream, a);
@@ -474,10 +474,10 @@ extern "C" int64_t t2o_bwd_tape_tiles(const t2o_layout* L, int B, int T, int A) 
   if (L->kind == 0) return (int64_t)T * (((int64_t)B * A + 15) / 16);
   if (A != L->n_agents) return -1;
   const int64_t Q = A + 3;  // the mixer's query rows: A weight rows + 3 hyper tokens
-  // tuned multi-tile mixers write each block's records as one compact stream
-  // (t2o_mixer.hip, mixer_bwd_kernel); a one-tile or generic mixer, one tile-set
-  // per (episode, step)
-  if (Q > 16 && !L->generic) return ((int64_t)B * T * Q + 15) / 16;
+  // tuned mixers write each block's records as one compact stream, (step,
+  // episode, query row) in order, cut into 16-record tiles (t2o_mixer.hip); a
+  // generic mixer, one tile-set per (episode, step)
+  if (!L->generic) return ((int64_t)B * T * Q + 15) / 16;
   return (int64_t)B * T * ((Q + 15) / 16);
 }
 
@@ -491,15 +491,15 @@ extern "C" int t2o_bwd_tape_contract_ex(const t2o_layout* L, const float* pack, 
   grad_layout(*L, G);
   int rc = T2O_EUNSUPPORTED;
   if (rec_format == 1) {
-    T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
-                 rc = (launch_dw_gemm<E_, H_, FF_, D_, NE_, __bf16, 1>(0, tape, tiles, pack, gslabs, *L, G, nslab,
+    T2O_DISPATCH_NET(L->E, L->H, L->D, L->FF,
+                 rc = (launch_dw_gemm<E_, H_, FF_, D_, __bf16, 1>(0, tape, tiles, pack, gslabs, *L, G, nslab,
                                                                       (hipStream_t)stream)));
     return rc;
   }
-  T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
-               rc = (L->prec ? launch_dw_gemm<E_, H_, FF_, D_, NE_, __bf16, 0>(L->kind, tape, tiles, pack, gslabs, *L,
+  T2O_DISPATCH_NET(L->E, L->H, L->D, L->FF,
+               rc = (L->prec ? launch_dw_gemm<E_, H_, FF_, D_, __bf16, 0>(L->kind, tape, tiles, pack, gslabs, *L,
                                                                           G, nslab, (hipStream_t)stream)
-                             : launch_dw_gemm<E_, H_, FF_, D_, NE_, float, 0>(L->kind, tape, tiles, pack, gslabs, *L, G,
+                             : launch_dw_gemm<E_, H_, FF_, D_, float, 0>(L->kind, tape, tiles, pack, gslabs, *L, G,
                                                                          nslab, (hipStream_t)stream)));
   return rc;
 }

@@ -108,13 +108,10 @@ __host__ __device__ inline GenRec gen_rec(int E, int H, int FF) {
   return r;
 }
 
-// Records per weight-gradient tape tile (TapeRec, t2o_common.hpp): 16, one
-// wave's rows; a mixer whose A+3 query rows fit one tile stores exactly those
-// rows (no padding records in HBM; the contraction zero-fills them in LDS).
-constexpr int mixer_tape_records(int n_ent) { return n_ent + 3 <= 16 ? n_ent + 3 : 16; }
-inline int tape_tile_records(const t2o_layout& L) {
-  return (L.kind == 1 && !L.generic) ? mixer_tape_records(L.n_ent) : 16;
-}
+// Records per weight-gradient tape tile (TapeRec, t2o_common.hpp): 16 — one
+// wave's rows (agent), or 16 consecutive records of a tuned mixer's compact
+// per-block stream of query-row records (no padding records in HBM).
+inline int tape_tile_records(const t2o_layout&) { return 16; }
 
 // Compact gradient layout (what the backward kernels accumulate in LDS and
 // write per workgroup): the pack layout without transposed copies.

@@ -47,17 +47,25 @@ struct MixerFwdArgs {
   const int32_t* avail;  // [b][t][a][NA]
   int64_t av_sb, av_st;
   int B, Fs;
+  int na;           // agents = state entities (n_entities = n_agents)
   int waves, wlds;  // set by the launcher
 };
 
+// Compile-time dims of an instance for A agents — the exact count, or the
+// capacity of a runtime-agent instance (t2o_dispatch.hpp), which sizes its
+// register arrays and LDS buffers for A and runs na <= A agents: the kernel
+// code indexes with the runtime counts
+//   na (state entities = agents), nq = na + 3 (query rows read out: A weight
+//   rows + 3 hyper tokens), lk = 2 na + 3 (keys; padding keys score -inf),
+// X0 rows [0, na) state entities, [na, 2na) agent hidden tokens, [2na, 2na+3)
+// hyper tokens; query row q is X0 row na + q.
 template <int E, int A>
 struct MixDims {
-  static constexpr int NS = A;              // state entities (n_entities = n_agents)
-  static constexpr int Q = A + 3;           // query rows read out
-  static constexpr int LK = 2 * A + 3;      // keys
-  static constexpr int KT = (LK + 15) / 16;
-  static constexpr int QT = (Q + 15) / 16;
-  static constexpr int ST = (NS + 15) / 16;
+  static constexpr int QCAP = A + 3;        // query rows
+  static constexpr int LKCAP = 2 * A + 3;   // keys
+  static constexpr int KT = (LKCAP + 15) / 16;
+  static constexpr int QT = (QCAP + 15) / 16;
+  static constexpr int ST = (A + 15) / 16;
   static constexpr int LDX = E + 4;
   static constexpr int X0F = KT * 16 * LDX;
   static constexpr int OUTF = QT * 16 * E;
@@ -103,7 +111,7 @@ struct MixIn {
 };
 
 template <int E, int A>
-T2O_DEV void mix_load(const MixerFwdArgs& a, const MixerNet& n, int b, int t, MixIn<E, A>& in) {
+T2O_DEV void mix_load(const MixerFwdArgs& a, const MixerNet& n, int b, int t, MixIn<E, A>& in, int na) {
   using Dm = MixDims<E, A>;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
   // Every load is unconditional (in-bounds duplicates for padding lanes / rows /
@@ -116,21 +124,21 @@ T2O_DEV void mix_load(const MixerFwdArgs& a, const MixerNet& n, int b, int t, Mi
   const float* st = a.states + b * a.st_sb + t * a.st_st;
 #pragma unroll
   for (int s = 0; s < Dm::ST; ++s) {
-    const int j = min(16 * s + c, Dm::NS - 1);
+    const int j = min(16 * s + c, na - 1);
 #pragma unroll
     for (int r = 0; r < 4; ++r) in.st[s][r] = st[j * a.Fs + min(4 * g + r, a.Fs - 1)];
   }
   const float* hd = n.hid + b * n.hid_sb + t * n.hid_st;
 #pragma unroll
-  for (int k = 0; k < MixIn<E, A>::HV; ++k) in.hid[k] = ld4(hd + 4 * min(lane + 64 * k, A * E / 4 - 1));
+  for (int k = 0; k < MixIn<E, A>::HV; ++k) in.hid[k] = ld4(hd + 4 * min(lane + 64 * k, na * E / 4 - 1));
   // per-agent inputs, lane a < A holds agent a's.  No branch on the Q-selection
   // mode either (a branch makes the loop-carried registers phis, and the
   // compiler then copies them — waiting for the loads — right after issuing):
   // fields a mode does not use load an in-bounds dummy.
-  const int la = lane < A ? lane : A - 1;
+  const int la = lane < na ? lane : na - 1;
   const int NA = a.n_actions > 0 ? a.n_actions : 1;
   const bool q0 = n.qmode == 0;
-  const size_t qrow = q0 ? ((size_t)b * n.T + t) * A + la : (((size_t)b * a.q_ts + t) * A + la) * NA;
+  const size_t qrow = q0 ? ((size_t)b * n.T + t) * na + la : (((size_t)b * a.q_ts + t) * na + la) * NA;
   const float* qsrc = q0 ? n.qv_in : n.qsel;
 #pragma unroll
   for (int k = 0; k < MIX_MAXNA; ++k) in.qs[k] = qsrc[qrow + (q0 ? 0 : (k < NA ? k : NA - 1))];
@@ -189,7 +197,7 @@ T2O_DEV void bcast_agents(float mine, float (&qv)[A]) {
 // Key block X0 rows for one step from the prefetched inputs: state-entity
 // embeddings and agent hidden tokens (the hyper-token rows are carried in X0).
 template <int E, int A, typename WT, typename In>
-T2O_DEV void mix_keys(const Wts<WT>& P, const t2o_layout& L, const In& in, float* X0) {
+T2O_DEV void mix_keys(const Wts<WT>& P, const t2o_layout& L, const In& in, float* X0, int na) {
   using Dm = MixDims<E, A>;
   constexpr int ET = E / 16;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
@@ -198,7 +206,7 @@ T2O_DEV void mix_keys(const Wts<WT>& P, const t2o_layout& L, const In& in, float
     const int j = 16 * s + c;
     f4 emb[ET];
     matvec<ET, 1>(P.w + L.We, 16, &in.st[s], emb);
-    if (j < Dm::NS) {
+    if (j < na) {
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) st4(X0 + j * Dm::LDX + 16 * ft + 4 * g, emb[ft] + vec_t(P.v + L.be, ft));
     }
@@ -206,32 +214,35 @@ T2O_DEV void mix_keys(const Wts<WT>& P, const t2o_layout& L, const In& in, float
 #pragma unroll
   for (int k = 0; k < MixIn<E, A>::HV; ++k) {
     const int i = lane + 64 * k;
-    if (i < A * E / 4) st4(X0 + (Dm::NS + (4 * i) / E) * Dm::LDX + (4 * i) % E, in.hid[k]);
+    if (i < na * E / 4) st4(X0 + (na + (4 * i) / E) * Dm::LDX + (4 * i) % E, in.hid[k]);
   }
 }
 
 // Mixing head (n_transf_mixer.py:75-89, pos_func abs: t2o_layout_init lays out
 // every other qmix_pos_func generic) on the final query rows OUT[q][f],
 // lanes = features.  Returns y; writes hyper tokens back into X0.
+// (qv: capacity-sized; entries ag >= na are not read)
 template <int E, int A, typename WT>
 T2O_DEV float mixer_head(const Wts<WT>& P, const t2o_layout& L, const float* OUT,
-                         const float (&qv)[A], float& pre_h, float& pre2) {
+                         const float (&qv)[A], float& pre_h, float& pre2, int na) {
   const int f = threadIdx.x & 63;
   const bool fv = f < E;
   const int fc = fv ? f : 0;
-  float ph = OUT[A * E + fc];
+  float ph = OUT[na * E + fc];
 #pragma unroll
-  for (int ag = 0; ag < A; ++ag) ph += qv[ag] * fabsf(OUT[ag * E + fc]);
+  for (int ag = 0; ag < A; ++ag)
+    if (ag < na) ph += qv[ag] * fabsf(OUT[ag * E + fc]);
   pre_h = ph;
   const float hidden = elu1(ph);
-  const float w2 = fabsf(OUT[(A + 1) * E + fc]);
+  const float w2 = fabsf(OUT[(na + 1) * E + fc]);
   const float yv = feat_sum<E>(fv ? hidden * w2 : 0.f);
-  const float p2 = feat_sum<E>(fv ? P.s(L.Wo + fc) * OUT[(A + 2) * E + fc] : 0.f) + P.v[L.bo];
+  const float p2 = feat_sum<E>(fv ? P.s(L.Wo + fc) * OUT[(na + 2) * E + fc] : 0.f) + P.v[L.bo];
   pre2 = p2;
   return yv + fmaxf(p2, 0.f);
 }
 
-template <int E, int H, int D, int A, int FF, bool WLDS, typename WT>
+// RT: runtime-agent instance (A is a capacity, args.na the agent count)
+template <int E, int H, int D, int A, int FF, bool RT, bool WLDS, typename WT>
 __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
   using Dm = MixDims<E, A>;
   constexpr int ET = E / 16;
@@ -239,6 +250,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
   const int w = wave_id();
   const MixerNet n = args.net[blockIdx.y];
   const t2o_layout& L = args.L;
+  const int na = RT ? args.na : A, nq = na + 3, lk = 2 * na + 3;
   // forward weights in LDS for the unroll when they fit beside the per-wave buffers
   const int lds_w = WLDS ? (int)((lds_weight_floats<WT>(L, L.fwd_total) + 15) / 16 * 16) : 0;
   Wts<WT> P0;
@@ -256,37 +268,38 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
   for (int i = lane; i < Dm::X0F; i += 64) X0[i] = 0.f;
   for (int i = lane; i < 3 * E; i += 64) {
     const int k = i / E, f = i % E;
-    X0[(Dm::NS + A + k) * Dm::LDX + f] = n.hw0 ? n.hw0[(size_t)b * 3 * E + i] : 0.f;
+    X0[(2 * na + k) * Dm::LDX + f] = n.hw0 ? n.hw0[(size_t)b * 3 * E + i] : 0.f;
   }
   MixIn<E, A> in;
-  mix_load<E, A>(args, n, b, 0, in);
+  mix_load<E, A>(args, n, b, 0, in, na);
   for (int t = 0; t < n.T; ++t) {
     T2O_MARK(0);
     const Wts<WT> P = step_view(P0);
-    mix_keys<E, A>(P, L, in, X0);
+    mix_keys<E, A>(P, L, in, X0, na);
     const float myq = mix_qv<E, A>(n, in, args.n_actions, args.avail != nullptr);
     __builtin_amdgcn_sched_barrier(0);  // every read of this step's inputs issued before they are reloaded
-    if (t + 1 < n.T) mix_load<E, A>(args, n, b, t + 1, in);  // prefetch step t+1 (in is consumed)
+    if (t + 1 < n.T) mix_load<E, A>(args, n, b, t + 1, in, na);  // prefetch step t+1 (in is consumed)
     __builtin_amdgcn_wave_barrier();
     KeyFrags<E, Dm::KT, sizeof(WT) == 2> K;
     K.template load<Dm::LDX>(X0);
     T2O_MARK(1);
 #pragma unroll
     for (int qt = 0; qt < Dm::QT; ++qt) {
+      if (RT && 16 * qt >= nq) break;  // (wave-uniform) query tiles past the real rows
       const int q = 16 * qt + c;
       f4 x[ET];
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft)
-        x[ft] = q < Dm::Q ? ld4(X0 + (Dm::NS + q) * Dm::LDX + 16 * ft + 4 * g) : zero4();
+        x[ft] = q < nq ? ld4(X0 + (na + q) * Dm::LDX + 16 * ft + 4 * g) : zero4();
       __builtin_amdgcn_wave_barrier();  // every X0 read done before OUT (may alias X0) is written
 #pragma unroll
       for (int d = 0; d < D; ++d) {
-        if (d > 0 && n.xmid && q < Dm::Q) {
-          float* xm = n.xmid + ((((size_t)b * n.T + t) * (D - 1) + d - 1) * Dm::Q + q) * E;
+        if (d > 0 && n.xmid && q < nq) {
+          float* xm = n.xmid + ((((size_t)b * n.T + t) * (D - 1) + d - 1) * nq + q) * E;
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft) st4(xm + 16 * ft + 4 * g, x[ft]);
         }
-        mixer_block_fwd<E, H, Dm::KT, FF, false>(P, L, d, K, Dm::LK, x, nullptr);
+        mixer_block_fwd<E, H, Dm::KT, FF, false>(P, L, d, K, lk, x, nullptr);
         if (qt == 0) T2O_MARK(2 + d);
       }
 #pragma unroll
@@ -296,25 +309,25 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
     float qv[A];
     bcast_agents<A>(myq, qv);
     float pre_h, pre2;
-    const float y = mixer_head<E, A>(P, L, OUT, qv, pre_h, pre2);
+    const float y = mixer_head<E, A>(P, L, OUT, qv, pre_h, pre2, na);
     const size_t bt = (size_t)b * n.T + t;
     if (lane == 0) n.y[bt] = y;
-    if (n.qv && lane < A) n.qv[bt * A + lane] = myq;
+    if (n.qv && lane < na) n.qv[bt * na + lane] = myq;
     float hv[(3 * E + 63) / 64];
 #pragma unroll
     for (int k = 0; k < (3 * E + 63) / 64; ++k) {
       const int i = lane + 64 * k;
-      hv[k] = i < 3 * E ? OUT[(A + i / E) * E + i % E] : 0.f;
+      hv[k] = i < 3 * E ? OUT[(na + i / E) * E + i % E] : 0.f;
       if (i < 3 * E) n.hw[bt * 3 * E + i] = hv[k];
     }
     if (n.xout) {
-      for (int i = lane; i < Dm::Q * E; i += 64) n.xout[bt * Dm::Q * E + i] = OUT[i];
+      for (int i = lane; i < nq * E; i += 64) n.xout[bt * nq * E + i] = OUT[i];
     }
     __builtin_amdgcn_wave_barrier();  // OUT (may alias X0) fully read before the hyper rows change
 #pragma unroll
     for (int k = 0; k < (3 * E + 63) / 64; ++k) {
       const int i = lane + 64 * k;
-      if (i < 3 * E) X0[(Dm::NS + A + i / E) * Dm::LDX + i % E] = hv[k];
+      if (i < 3 * E) X0[(2 * na + i / E) * Dm::LDX + i % E] = hv[k];
     }
     __builtin_amdgcn_wave_barrier();
     T2O_MARK(2 + D);
@@ -322,7 +335,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
   }
 }
 
-template <int E, int H, int D, int A, int FF, typename WT>
+template <int E, int H, int D, int A, int FF, bool RT, typename WT>
 int launch_mixer_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
   using Dm = MixDims<E, A>;
   MixerFwdArgs a = args;
@@ -339,7 +352,7 @@ int launch_mixer_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
     lds = sizeof(float) * 4 * perw;
     if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
   }
-  auto kern = a.wlds ? mixer_fwd_kernel<E, H, D, A, FF, true, WT> : mixer_fwd_kernel<E, H, D, A, FF, false, WT>;
+  auto kern = a.wlds ? mixer_fwd_kernel<E, H, D, A, FF, RT, true, WT> : mixer_fwd_kernel<E, H, D, A, FF, RT, false, WT>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid((args.B + a.waves - 1) / a.waves, nnet);
   hipLaunchKernelGGL(kern, grid, dim3(64 * a.waves), lds, stream, a);
@@ -383,7 +396,7 @@ struct MixBwdIn {
   using Dm = MixDims<E, A>;
   static constexpr int ET = E / 16;
   static constexpr int HW = (3 * E + 63) / 64;
-  static constexpr int XO = (Dm::Q * E + 63) / 64;
+  static constexpr int XO = (Dm::QCAP * E + 63) / 64;
   MixIn<E, A> m;
   float hwp[HW];  // X0 hyper rows: hyper outputs of step t-1 (hw0 / zeros at t = 0)
   float xo[XO];   // forward final query rows of step t
@@ -394,12 +407,13 @@ struct MixBwdIn {
 };
 
 template <int E, int A, int D, bool XM = true>
-T2O_DEV void mixb_load(const MixerBwdArgs& args, const MixerNet& n, int b, int t, MixBwdIn<E, A, D>& in) {
+T2O_DEV void mixb_load(const MixerBwdArgs& args, const MixerNet& n, int b, int t, MixBwdIn<E, A, D>& in, int na) {
   using Dm = MixDims<E, A>;
   using In = MixBwdIn<E, A, D>;
   const MixerFwdArgs& fa = args.f;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
-  mix_load<E, A>(fa, n, b, t, in.m);
+  const int nq = na + 3;
+  mix_load<E, A>(fa, n, b, t, in.m, na);
   const size_t bt = (size_t)b * n.T + t;
 #pragma unroll
   for (int k = 0; k < In::HW; ++k) {
@@ -411,7 +425,7 @@ T2O_DEV void mixb_load(const MixerBwdArgs& args, const MixerNet& n, int b, int t
 #pragma unroll
   for (int k = 0; k < In::XO; ++k) {
     const int i = lane + 64 * k;
-    in.xo[k] = i < Dm::Q * E ? args.xout[bt * Dm::Q * E + i] : 0.f;
+    in.xo[k] = i < nq * E ? args.xout[bt * nq * E + i] : 0.f;
   }
 #pragma unroll
   for (int k = 0; k < 3; ++k) in.ghx[k] = (args.ghw_ext && lane < E) ? args.ghw_ext[(bt * 3 + k) * E + lane] : 0.f;
@@ -425,7 +439,7 @@ T2O_DEV void mixb_load(const MixerBwdArgs& args, const MixerNet& n, int b, int t
 #pragma unroll
         for (int ft = 0; ft < In::ET; ++ft)
           in.xm[qt][d - 1][ft] =
-              q < Dm::Q ? ld4(args.xmid + ((bt * (D - 1) + d - 1) * Dm::Q + q) * E + 16 * ft + 4 * g) : zero4();
+              q < nq ? ld4(args.xmid + ((bt * (D - 1) + d - 1) * nq + q) * E + 16 * ft + 4 * g) : zero4();
     }
   }
   const float* st = fa.states + b * fa.st_sb + t * fa.st_st;
@@ -435,8 +449,8 @@ T2O_DEV void mixb_load(const MixerBwdArgs& args, const MixerNet& n, int b, int t
     for (int r = 0; r < 4; ++r) {
       const int j = 16 * s + 4 * g + r;
       float v = 0.f;
-      v = ld_or0(st, j * fa.Fs + c, j < Dm::NS && c < fa.Fs);
-      if (j < Dm::NS && c == fa.Fs) v = 1.f;
+      v = ld_or0(st, j * fa.Fs + c, j < na && c < fa.Fs);
+      if (j < na && c == fa.Fs) v = 1.f;
       in.stT[s][r] = v;
     }
 }
@@ -457,7 +471,57 @@ struct MixBwdDims {
   static constexpr int PERW = Dm::X0F + WORK;
 };
 
-template <int E, int H, int D, int A, int FF, bool WLDS, typename WT>
+// Mixing-head backward of one (episode, step), lanes = features
+// (n_transf_mixer.py:75-89, pos_func abs): from the final query rows OUT (rows
+// [0, nq), stride E) and dL/dy, writes the grads wrt those rows to GOUT (may
+// alias OUT), lane a < na's dL/dqvals[a] to gqv, and accumulates the hyper_b2
+// grads.  ghw: grads wrt the step's hyper outputs (carried + external).
+template <int E, int A, typename WT>
+T2O_DEV void mixer_head_bwd(const Wts<WT>& P, const t2o_layout& L, const float* OUT, float* GOUT, float myq,
+                            float gyv, const float (&ghw)[3], float* gqv, float& gWo, float& gbo, int na) {
+  const int lane = threadIdx.x & 63;
+  const int f = lane < E ? lane : 0;
+  const bool fv = lane < E;
+  float qv[A];
+  bcast_agents<A>(myq, qv);
+  float pre_h, pre2;
+  (void)mixer_head<E, A>(P, L, OUT, qv, pre_h, pre2, na);
+  const float hidden = elu1(pre_h);
+  const float xw2 = OUT[(na + 1) * E + f];
+  const float sgn_w2 = (xw2 > 0.f) - (xw2 < 0.f);
+  const float gpre = gyv * fabsf(xw2) * (pre_h > 0.f ? 1.f : expf(pre_h));
+  const float gpre2 = pre2 > 0.f ? gyv : 0.f;
+  // gout[0, A): the agents' weight rows (entries >= na unused); gout[A + k]: hyper row na + k
+  float gout[A + 3];
+  float gqm = 0.f;  // lane a < na: dL/dqvals[a]
+#pragma unroll
+  for (int ag = 0; ag < A; ++ag) {
+    if (ag < na) {
+      const float xa = OUT[ag * E + f];
+      gout[ag] = qv[ag] * gpre * ((xa > 0.f) - (xa < 0.f));
+      const float gq = feat_sum<E>(fv ? gpre * fabsf(xa) : 0.f);
+      gqm = lane == ag ? gq : gqm;
+    }
+  }
+  if (lane < na) *gqv = gqm;
+  gout[A] = gpre + ghw[0];
+  gout[A + 1] = gyv * hidden * sgn_w2 + ghw[1];
+  const float x2 = OUT[(na + 2) * E + f];
+  gout[A + 2] = gpre2 * P.s(L.Wo + f) + ghw[2];
+  gWo += gpre2 * x2;
+  gbo += gpre2;
+  __builtin_amdgcn_wave_barrier();  // every OUT read done (GOUT may alias it)
+  if (fv) {
+#pragma unroll
+    for (int q = 0; q < A + 3; ++q) {
+      if (q < na) GOUT[q * E + f] = gout[q];
+      else if (q >= A) GOUT[(q - A + na) * E + f] = gout[q];
+    }
+  }
+}
+
+// RT: runtime-agent instance (A is a capacity, args.f.na the agent count)
+template <int E, int H, int D, int A, int FF, bool RT, bool WLDS, typename WT>
 __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   using Dm = MixDims<E, A>;
   using Bd = MixBwdDims<E, A>;
@@ -467,6 +531,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   const MixerNet& n = fa.net[0];
   const t2o_layout& L = fa.L;
   const t2o_layout& G = args.G;
+  const int na = RT ? fa.na : A, nq = na + 3, lk = 2 * na + 3;
   const int w = wave_id();
   float* X0 = smem + args.lds_w + w * Bd::PERW;
   float* WORK = X0 + Dm::X0F;
@@ -481,12 +546,12 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   __syncthreads();
   const int b = blockIdx.x * args.waves + w;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
-  const size_t ntiles = (size_t)fa.B * n.T * Dm::QT;
   using Rec = TapeRec<E, H, FF>;
-  // multi-tile mixers: 16-record tiles over each block's compact record stream
-  // (mixer_tape_tiles); the last tile's records past the stream's end are zeros
-  const size_t nrec = (size_t)fa.B * n.T * Dm::Q, ctiles = (nrec + 15) / 16;
-  if (Dm::QT > 1 && blockIdx.x == 0 && w == 0) {
+  // each block's records form one compact stream, (step, episode, query row) in
+  // order, read by the contraction as 16-record tiles (t2o_bwd_tape_tiles); the
+  // last tile's records past the stream's end are zeros
+  const size_t nrec = (size_t)fa.B * n.T * nq, ctiles = (nrec + 15) / 16;
+  if (blockIdx.x == 0 && w == 0) {
     const int tail = (int)(ctiles * 16 - nrec) * Rec::SIZE;  // elements
     for (int d = 0; d < D; ++d) {
       WT* z = static_cast<WT*>(args.tape) + ((size_t)d * ctiles * 16 + nrec) * Rec::SIZE;
@@ -516,63 +581,33 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
     // the 16-AGV kernel spilled ~100 registers to scratch.
     constexpr bool LEAN = Dm::QT > 1;
     MixBwdIn<E, A, D> cur, nxt;
-    if constexpr (!LEAN) mixb_load<E, A, D>(args, n, b, n.T - 1, cur);
+    if constexpr (!LEAN) mixb_load<E, A, D>(args, n, b, n.T - 1, cur, na);
     for (int t = n.T - 1; t >= 0; --t) {
       const Wts<WT> P = step_view(P0);
       const size_t bt = (size_t)b * n.T + t;
-      if constexpr (LEAN) mixb_load<E, A, D, false>(args, n, b, t, cur);  // (block inputs: per tile, below)
-      mix_keys<E, A>(P, L, cur.m, X0);
+      if constexpr (LEAN) mixb_load<E, A, D, false>(args, n, b, t, cur, na);  // (block inputs: per tile, below)
+      mix_keys<E, A>(P, L, cur.m, X0, na);
 #pragma unroll
       for (int k = 0; k < MixBwdIn<E, A, D>::HW; ++k) {
         const int i = lane + 64 * k;
-        if (i < 3 * E) X0[(Dm::NS + A + i / E) * Dm::LDX + i % E] = cur.hwp[k];
+        if (i < 3 * E) X0[(2 * na + i / E) * Dm::LDX + i % E] = cur.hwp[k];
       }
       float* OUT = stage;  // forward final query rows
 #pragma unroll
       for (int k = 0; k < MixBwdIn<E, A, D>::XO; ++k) {
         const int i = lane + 64 * k;
-        if (i < Dm::Q * E) OUT[i] = cur.xo[k];
+        if (i < nq * E) OUT[i] = cur.xo[k];
       }
       if constexpr (!LEAN) {
-        if (t > 0) mixb_load<E, A, D>(args, n, b, t - 1, nxt);  // prefetch step t-1
+        if (t > 0) mixb_load<E, A, D>(args, n, b, t - 1, nxt, na);  // prefetch step t-1
       }
       __builtin_amdgcn_wave_barrier();
       // ---- mixing head backward (lanes = features)
-      float qv[A];
-      bcast_agents<A>(cur.m.qs[0], qv);
-      float pre_h, pre2;
-      (void)mixer_head<E, A>(P, L, OUT, qv, pre_h, pre2);
-      const float gyv = cur.gy;
-      const float hidden = elu1(pre_h);
-      const float xw2 = OUT[(A + 1) * E + f];
-      const float sgn_w2 = (xw2 > 0.f) - (xw2 < 0.f);
-      const float gpre = gyv * fabsf(xw2) * (pre_h > 0.f ? 1.f : expf(pre_h));
-      const float gpre2 = pre2 > 0.f ? gyv : 0.f;
-      float gout[A + 3];
-      float gqm = 0.f;  // lane a < A: dL/dqvals[a]
-#pragma unroll
-      for (int ag = 0; ag < A; ++ag) {
-        const float xa = OUT[ag * E + f];
-        gout[ag] = qv[ag] * gpre * ((xa > 0.f) - (xa < 0.f));
-        const float gq = feat_sum<E>(fv ? gpre * fabsf(xa) : 0.f);
-        gqm = lane == ag ? gq : gqm;
-      }
-      if (lane < A) args.gqv[bt * A + lane] = gqm;
 #pragma unroll
       for (int k = 0; k < 3; ++k) ghw[k] += cur.ghx[k];
-      gout[A] = gpre + ghw[0];
-      gout[A + 1] = gyv * hidden * sgn_w2 + ghw[1];
-      const float x2 = OUT[(A + 2) * E + f];
-      gout[A + 2] = gpre2 * P.s(L.Wo + f) + ghw[2];
-      gWo += gpre2 * x2;
-      gbo += gpre2;
-      __builtin_amdgcn_wave_barrier();
       float* GOUT = Bd::GOUT ? GOUTB : stage;
-      if (fv) {
-#pragma unroll
-        for (int q = 0; q < A + 3; ++q) GOUT[q * E + f] = gout[q];
-      }
-      for (int i = Dm::Q * E + lane; i < Dm::OUTF; i += 64) GOUT[i] = 0.f;
+      mixer_head_bwd<E, A>(P, L, OUT, GOUT, cur.m.qs[0], cur.gy, ghw, args.gqv + bt * na + lane, gWo, gbo, na);
+      for (int i = nq * E + lane; i < Dm::OUTF; i += 64) GOUT[i] = 0.f;
       __builtin_amdgcn_wave_barrier();
       // ---- blocks backward per query tile; gX0 accumulates in registers
       KeyFrags<E, KT, sizeof(WT) == 2> K;
@@ -586,8 +621,9 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
       if constexpr (LEAN) {
         // one query tile at a time, not unrolled: its grads come from and go back
         // to GOUT (LDS), its block inputs straight from HBM
+        const int nqt = (nq + 15) / 16;
 #pragma unroll 1
-        for (int qt = 0; qt < Dm::QT; ++qt) {
+        for (int qt = 0; qt < nqt; ++qt) {
           const int q = 16 * qt + c;
           f4 gx[ET];
 #pragma unroll
@@ -596,59 +632,55 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
           for (int d = D - 1; d >= 0; --d) {
             f4 x[ET];
 #pragma unroll
-            for (int ft = 0; ft < ET; ++ft) x[ft] = q < Dm::Q ? ld4(X0 + (Dm::NS + q) * Dm::LDX + 16 * ft + 4 * g) : zero4();
+            for (int ft = 0; ft < ET; ++ft) x[ft] = q < nq ? ld4(X0 + (na + q) * Dm::LDX + 16 * ft + 4 * g) : zero4();
             if (d > 0) {
               if (args.xmid) {
 #pragma unroll
                 for (int ft = 0; ft < ET; ++ft)
-                  x[ft] = q < Dm::Q ? ld4(args.xmid + ((bt * (D - 1) + d - 1) * Dm::Q + q) * E + 16 * ft + 4 * g)
-                                    : zero4();
+                  x[ft] = q < nq ? ld4(args.xmid + ((bt * (D - 1) + d - 1) * nq + q) * E + 16 * ft + 4 * g)
+                                 : zero4();
               } else {
-                for (int dd = 0; dd < d; ++dd) mixer_block_fwd<E, H, KT, FF, false>(P, L, dd, K, Dm::LK, x, nullptr);
+                for (int dd = 0; dd < d; ++dd) mixer_block_fwd<E, H, KT, FF, false>(P, L, dd, K, lk, x, nullptr);
               }
             }
-            // one compact record stream per block, (t, b, query row) in order: a
-            // tile's 16 records, or the Q - 16·qt real ones of the last (no
-            // padding records in HBM; the stream's tail is zeroed below)
+            // a tile's 16 records, or the nq - 16·qt real ones of the last
             WT* tile = static_cast<WT*>(args.tape) +
-                       ((size_t)d * ctiles * 16 + ((size_t)t * fa.B + b) * Dm::Q + 16 * qt) * Rec::SIZE;
+                       ((size_t)d * ctiles * 16 + ((size_t)t * fa.B + b) * nq + 16 * qt) * Rec::SIZE;
             MixerCacheLean<E, H, KT, FF> cache;
-            const MaskedRec<WT> rec(tile, min(16, Dm::Q - 16 * qt), Rec::SIZE);
-            mixer_block_fwd_lean<E, H, KT, FF>(P, L, d, K, Dm::LK, x, cache, rec);
-            mixer_block_bwd_lean<E, H, KT, FF>(P, L, gs, rec, stage, d, K, Dm::LK, gX0, cache, gx, ln2[d]);
+            const MaskedRec<WT> rec(tile, min(16, nq - 16 * qt), Rec::SIZE);
+            mixer_block_fwd_lean<E, H, KT, FF>(P, L, d, K, lk, x, cache, rec);
+            mixer_block_bwd_lean<E, H, KT, FF>(P, L, gs, rec, stage, d, K, lk, gX0, cache, gx, ln2[d]);
           }
           __builtin_amdgcn_wave_barrier();
 #pragma unroll
-          for (int ft = 0; ft < ET; ++ft) st4(GOUT + (16 * qt + c) * E + 16 * ft + 4 * g, q < Dm::Q ? gx[ft] : zero4());
+          for (int ft = 0; ft < ET; ++ft) st4(GOUT + (16 * qt + c) * E + 16 * ft + 4 * g, q < nq ? gx[ft] : zero4());
         }
       } else {
+      static_assert(LEAN || Dm::QT == 1, "the unrolled path runs one query tile");
 #pragma unroll
-      for (int qt = 0; qt < Dm::QT; ++qt)
-#pragma unroll
-        for (int ft = 0; ft < ET; ++ft) gq0[qt][ft] = ld4(GOUT + (16 * qt + c) * E + 16 * ft + 4 * g);
+      for (int ft = 0; ft < ET; ++ft) gq0[0][ft] = ld4(GOUT + c * E + 16 * ft + 4 * g);
       __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int qt = 0; qt < Dm::QT; ++qt) {
-        const int q = 16 * qt + c;
+      {
+        const int q = c;
         f4 gx[ET];
         f4 xs[D][ET];
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft) {
-          gx[ft] = gq0[qt][ft];
-          xs[0][ft] = q < Dm::Q ? ld4(X0 + (Dm::NS + q) * Dm::LDX + 16 * ft + 4 * g) : zero4();
+          gx[ft] = gq0[0][ft];
+          xs[0][ft] = q < nq ? ld4(X0 + (na + q) * Dm::LDX + 16 * ft + 4 * g) : zero4();
         }
         if (args.xmid) {  // stored block inputs of blocks 1..D-1 (no plain recompute)
 #pragma unroll
           for (int d = 1; d < D; ++d)
 #pragma unroll
-            for (int ft = 0; ft < ET; ++ft) xs[d][ft] = cur.xm[qt][d - 1][ft];
+            for (int ft = 0; ft < ET; ++ft) xs[d][ft] = cur.xm[0][d - 1][ft];
         } else {
 #pragma unroll
           for (int d = 0; d + 1 < D; ++d) {
             f4 x[ET];
 #pragma unroll
             for (int ft = 0; ft < ET; ++ft) x[ft] = xs[d][ft];
-            mixer_block_fwd<E, H, KT, FF, false>(P, L, d, K, Dm::LK, x, nullptr);
+            mixer_block_fwd<E, H, KT, FF, false>(P, L, d, K, lk, x, nullptr);
 #pragma unroll
             for (int ft = 0; ft < ET; ++ft) xs[d + 1][ft] = x[ft];
           }
@@ -658,18 +690,14 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
           f4 x[ET];
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft) x[ft] = xs[d][ft];
-          // one tile per (episode, step, query tile); padding rows carry zero gradients
-          // tiles are step-major (t, b, qt): at any step the grid writes one contiguous window
-          // (a one-tile mixer's tiles hold just its Q rows: mixer_tape_records)
-          constexpr int RT = mixer_tape_records(A);
-          WT* tile = static_cast<WT*>(args.tape) +
-                     ((size_t)d * ntiles + ((size_t)t * fa.B + b) * Dm::QT + qt) * Rec::SIZE * RT;
+          // the (episode, step)'s nq records of the block's compact stream
+          WT* tile = static_cast<WT*>(args.tape) + ((size_t)d * ctiles * 16 + ((size_t)t * fa.B + b) * nq) * Rec::SIZE;
           MixerCache<E, H, KT, FF> cache;
-          mixer_block_fwd<E, H, KT, FF, true>(P, L, d, K, Dm::LK, x, &cache);
-          mixer_block_bwd<E, H, KT, FF>(P, L, G, gs, c < RT ? tile : nullptr, stage, d, K, gX0, cache, gx, ln2[d]);
+          mixer_block_fwd<E, H, KT, FF, true>(P, L, d, K, lk, x, &cache);
+          mixer_block_bwd<E, H, KT, FF>(P, L, G, gs, c < nq ? tile : nullptr, stage, d, K, gX0, cache, gx, ln2[d]);
         }
 #pragma unroll
-        for (int ft = 0; ft < ET; ++ft) gq0[qt][ft] = q < Dm::Q ? gx[ft] : zero4();
+        for (int ft = 0; ft < ET; ++ft) gq0[0][ft] = q < nq ? gx[ft] : zero4();
       }
       }
       // ---- state embedding grads straight from the key-grad registers:
@@ -680,7 +708,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
         for (int ft = 0; ft < ET; ++ft) {
           f4 am;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) am[r] = 16 * s + 4 * g + r < Dm::NS ? gX0[s][ft][r] : 0.f;
+          for (int r = 0; r < 4; ++r) am[r] = 16 * s + 4 * g + r < na ? gX0[s][ft][r] : 0.f;
           if constexpr (sizeof(WT) == 2) {
             gWe[ft] = mfma_b16(to_bf4(am), to_bf4(cur.stT[s]), gWe[ft]);
           } else {
@@ -701,20 +729,20 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
       for (int qt = 0; qt < Dm::QT; ++qt) {
         const int q = 16 * qt + c;
-        if (q < Dm::Q) {
+        if (q < nq) {
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft) {
-            float* dst = GX0 + (Dm::NS + q) * E + 16 * ft + 4 * g;
-            const f4 gq = LEAN ? ld4(GOUT + q * E + 16 * ft + 4 * g) : gq0[LEAN ? 0 : qt][ft];
+            float* dst = GX0 + (na + q) * E + 16 * ft + 4 * g;
+            const f4 gq = LEAN ? ld4(GOUT + q * E + 16 * ft + 4 * g) : gq0[0][ft];
             st4(dst, ld4(dst) + gq);
           }
         }
       }
       __builtin_amdgcn_wave_barrier();
       // ---- key-token grads: agent hidden tokens out, hyper tokens carried
-      for (int i = lane; i < A * E / 4; i += 64) st4(args.ghid + bt * A * E + 4 * i, ld4(GX0 + Dm::NS * E + 4 * i));
+      for (int i = lane; i < na * E / 4; i += 64) st4(args.ghid + bt * na * E + 4 * i, ld4(GX0 + na * E + 4 * i));
 #pragma unroll
-      for (int k = 0; k < 3; ++k) ghw[k] = fv ? GX0[(Dm::NS + A + k) * E + f] : 0.f;
+      for (int k = 0; k < 3; ++k) ghw[k] = fv ? GX0[(2 * na + k) * E + f] : 0.f;
       __builtin_amdgcn_wave_barrier();
       if constexpr (!LEAN) cur = nxt;
     }
@@ -759,10 +787,12 @@ template <int E, int A>
 struct MixPipeDims {
   using Dm = MixDims<E, A>;
   using Bd = MixBwdDims<E, A>;
-  static constexpr int XCH = Dm::LK * E;  // offset of the query-row grads in R
-  static constexpr int REGION = Bd::W0 > Dm::GX0F ? Bd::W0 : Dm::GX0F;
+  static constexpr int XCH = Dm::LKCAP * E;  // offset of the query-row grads in R
+  static constexpr int R0 = Bd::W0 > Dm::GX0F ? Bd::W0 : Dm::GX0F;
+  // (the hand-over needs R to hold the key grads and, past them, the query-row grads)
+  static constexpr int REGION = R0 > XCH + Dm::QCAP * E ? R0 : XCH + Dm::QCAP * E;
   static constexpr int PAIRF = Dm::X0F + REGION;
-  static constexpr bool OK = Dm::QT == 1 && XCH + Dm::Q * E <= REGION;
+  static constexpr bool OK = Dm::QT == 1;
 };
 
 // T2O_MIXER_BWD=single selects the one-wave kernel (A/B timing, parity cross-check)
@@ -794,12 +824,13 @@ struct MixPIn {
 };
 
 template <int E, int A>
-T2O_DEV void mixp_load(const MixerBwdArgs& args, int b, int t, MixPIn<E, A>& in) {
+T2O_DEV void mixp_load(const MixerBwdArgs& args, int b, int t, MixPIn<E, A>& in, int na) {
   using Dm = MixDims<E, A>;
   using In = MixPIn<E, A>;
   const MixerFwdArgs& fa = args.f;
   const MixerNet& n = fa.net[0];
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
+  const int nq = na + 3;
   const float* st = fa.states + b * fa.st_sb + t * fa.st_st;
 #pragma unroll
   for (int s = 0; s < Dm::ST; ++s) {
@@ -807,17 +838,17 @@ T2O_DEV void mixp_load(const MixerBwdArgs& args, int b, int t, MixPIn<E, A>& in)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int f = 4 * g + r;
-      in.st[s][r] = ld_or0(st, j * fa.Fs + f, j < Dm::NS && f < fa.Fs);
+      in.st[s][r] = ld_or0(st, j * fa.Fs + f, j < na && f < fa.Fs);
     }
   }
   const float* hd = n.hid + b * n.hid_sb + t * n.hid_st;
 #pragma unroll
   for (int k = 0; k < In::HV; ++k) {
     const int i = lane + 64 * k;
-    in.hid[k] = i < A * E / 4 ? ld4(hd + 4 * i) : zero4();
+    in.hid[k] = i < na * E / 4 ? ld4(hd + 4 * i) : zero4();
   }
   const size_t bt = (size_t)b * n.T + t;
-  in.qv = n.qv_in[bt * A + (lane < A ? lane : A - 1)];
+  in.qv = n.qv_in[bt * na + (lane < na ? lane : na - 1)];
 #pragma unroll
   for (int k = 0; k < In::HW; ++k) {
     const int i = lane + 64 * k;
@@ -828,18 +859,18 @@ T2O_DEV void mixp_load(const MixerBwdArgs& args, int b, int t, MixPIn<E, A>& in)
 #pragma unroll
   for (int k = 0; k < In::XO; ++k) {
     const int i = lane + 64 * k;
-    in.xo[k] = i < Dm::Q * E ? args.xout[bt * Dm::Q * E + i] : 0.f;
+    in.xo[k] = i < nq * E ? args.xout[bt * nq * E + i] : 0.f;
   }
 #pragma unroll
   for (int k = 0; k < 3; ++k) in.ghx[k] = (args.ghw_ext && lane < E) ? args.ghw_ext[(bt * 3 + k) * E + lane] : 0.f;
   in.gy = args.gy[bt];
 #pragma unroll
   for (int ft = 0; ft < In::ET; ++ft)
-    in.xm[ft] = c < Dm::Q ? ld4(args.xmid + (bt * Dm::Q + c) * E + 16 * ft + 4 * g) : zero4();
+    in.xm[ft] = c < nq ? ld4(args.xmid + (bt * nq + c) * E + 16 * ft + 4 * g) : zero4();
 }
 
 template <int E, int A>
-T2O_DEV void mixp_load_stT(const MixerFwdArgs& fa, int b, int t, f4 (&stT)[MixDims<E, A>::ST]) {
+T2O_DEV void mixp_load_stT(const MixerFwdArgs& fa, int b, int t, f4 (&stT)[MixDims<E, A>::ST], int na) {
   using Dm = MixDims<E, A>;
   const int c = lane_c(), g = lane_g();
   const float* st = fa.states + b * fa.st_sb + t * fa.st_st;
@@ -848,8 +879,8 @@ T2O_DEV void mixp_load_stT(const MixerFwdArgs& fa, int b, int t, f4 (&stT)[MixDi
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int j = 16 * s + 4 * g + r;
-      float v = ld_or0(st, j * fa.Fs + c, j < Dm::NS && c < fa.Fs);
-      if (j < Dm::NS && c == fa.Fs) v = 1.f;
+      float v = ld_or0(st, j * fa.Fs + c, j < na && c < fa.Fs);
+      if (j < na && c == fa.Fs) v = 1.f;
       stT[s][r] = v;
     }
 }
@@ -857,7 +888,8 @@ T2O_DEV void mixp_load_stT(const MixerFwdArgs& fa, int b, int t, f4 (&stT)[MixDi
 // block-1 wave: key block + block-1 recompute, then head + block-1 backward
 template <int E, int H, int A, int FF, typename WT>
 T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_layout& L, const t2o_layout& Lb,
-                         const t2o_layout& Gb, float* __restrict__ gs, float* X0, float* R, int b, PairBarrier& pb) {
+                         const t2o_layout& Gb, float* __restrict__ gs, float* X0, float* R, int b, PairBarrier& pb,
+                         int na) {
   using Dm = MixDims<E, A>;
   using Pd = MixPipeDims<E, A>;
   using In = MixPIn<E, A>;
@@ -867,10 +899,12 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
   const MixerFwdArgs& fa = args.f;
   const MixerNet& n = fa.net[0];
   const int T = n.T;
+  const int nq = na + 3, lk = 2 * na + 3;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
   const int f = lane < E ? lane : 0;
   const bool fv = lane < E;
-  const size_t ntiles = (size_t)fa.B * T;
+  // block 1's compact record stream (mixer_bwd_kernel)
+  const size_t ctiles = ((size_t)fa.B * T * nq + 15) / 16;
   constexpr size_t RECD = 1;  // tape block
   f4 ln2[2 * ET];
 #pragma unroll
@@ -879,86 +913,56 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
   In cur;
   for (int t = T - 1; t >= 0; --t) {
     const size_t bt = (size_t)b * T + t;
-    // tape tiles of exactly the Q query rows (mixer_tape_records)
-    const MaskedRec<WT> rec(static_cast<WT*>(args.tape) + (RECD * ntiles + (size_t)t * fa.B + b) * Rec::SIZE * Dm::Q,
-                            Dm::Q, Rec::SIZE);
+    // the (episode, step)'s nq records
+    const MaskedRec<WT> rec(static_cast<WT*>(args.tape) + (RECD * ctiles * 16 + ((size_t)t * fa.B + b) * nq) * Rec::SIZE,
+                            nq, Rec::SIZE);
     MixerCacheLean<E, H, KT, FF> cache;
     KeyFrags<E, KT, BF> K;
     {  // ---- recompute: key block of step t, block-1 forward with cache
       // (this phase has slack under the block-0 backward: the step's inputs load here)
-      mixp_load<E, A>(args, b, t, cur);
+      mixp_load<E, A>(args, b, t, cur, na);
       const Wts<WT> P = step_view(P0);
-      mix_keys<E, A>(P, L, cur, X0);
+      mix_keys<E, A>(P, L, cur, X0, na);
 #pragma unroll
       for (int k = 0; k < In::HW; ++k) {
         const int i = lane + 64 * k;
-        if (i < 3 * E) X0[(Dm::NS + A + i / E) * Dm::LDX + i % E] = cur.hwp[k];
+        if (i < 3 * E) X0[(2 * na + i / E) * Dm::LDX + i % E] = cur.hwp[k];
       }
       __builtin_amdgcn_wave_barrier();
       K.template load<Dm::LDX>(X0);
       f4 x[ET];
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) x[ft] = cur.xm[ft];
-      mixer_block_fwd_lean<E, H, KT, FF>(P, Lb, 0, K, Dm::LK, x, cache, rec);
+      mixer_block_fwd_lean<E, H, KT, FF>(P, Lb, 0, K, lk, x, cache, rec);
     }
     pb.sync();
     {  // ---- backward: mixing head, block 1
       const Wts<WT> P = step_view(P0);
       float ghw[3];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) ghw[k] = (t < T - 1 && fv) ? R[(Dm::NS + A + k) * E + f] : 0.f;
+      for (int k = 0; k < 3; ++k) ghw[k] = (t < T - 1 && fv) ? R[(2 * na + k) * E + f] : 0.f;
       __builtin_amdgcn_wave_barrier();
       float* OUT = R;  // forward final query rows, then their grads in place
 #pragma unroll
       for (int k = 0; k < In::XO; ++k) {
         const int i = lane + 64 * k;
-        if (i < Dm::Q * E) OUT[i] = cur.xo[k];
+        if (i < nq * E) OUT[i] = cur.xo[k];
       }
       __builtin_amdgcn_wave_barrier();
-      float qv[A];
-      bcast_agents<A>(cur.qv, qv);
-      float pre_h, pre2;
-      (void)mixer_head<E, A>(P, L, OUT, qv, pre_h, pre2);
-      const float gyv = cur.gy;
-      const float hidden = elu1(pre_h);
-      const float xw2 = OUT[(A + 1) * E + f];
-      const float sgn_w2 = (xw2 > 0.f) - (xw2 < 0.f);
-      const float gpre = gyv * fabsf(xw2) * (pre_h > 0.f ? 1.f : expf(pre_h));
-      const float gpre2 = pre2 > 0.f ? gyv : 0.f;
-      float gout[A + 3];
-      float gqm = 0.f;
-#pragma unroll
-      for (int ag = 0; ag < A; ++ag) {
-        const float xa = OUT[ag * E + f];
-        gout[ag] = qv[ag] * gpre * ((xa > 0.f) - (xa < 0.f));
-        const float gq = feat_sum<E>(fv ? gpre * fabsf(xa) : 0.f);
-        gqm = lane == ag ? gq : gqm;
-      }
-      if (lane < A) args.gqv[bt * A + lane] = gqm;
 #pragma unroll
       for (int k = 0; k < 3; ++k) ghw[k] += cur.ghx[k];
-      gout[A] = gpre + ghw[0];
-      gout[A + 1] = gyv * hidden * sgn_w2 + ghw[1];
-      const float x2 = OUT[(A + 2) * E + f];
-      gout[A + 2] = gpre2 * P.s(L.Wo + f) + ghw[2];
-      gWo += gpre2 * x2;
-      gbo += gpre2;
-      __builtin_amdgcn_wave_barrier();
-      if (fv) {
-#pragma unroll
-        for (int q = 0; q < A + 3; ++q) OUT[q * E + f] = gout[q];
-      }
+      mixer_head_bwd<E, A>(P, L, OUT, OUT, cur.qv, cur.gy, ghw, args.gqv + bt * na + lane, gWo, gbo, na);
       __builtin_amdgcn_wave_barrier();
       f4 gx[ET];
 #pragma unroll
-      for (int ft = 0; ft < ET; ++ft) gx[ft] = c < Dm::Q ? ld4(OUT + c * E + 16 * ft + 4 * g) : zero4();
+      for (int ft = 0; ft < ET; ++ft) gx[ft] = c < nq ? ld4(OUT + c * E + 16 * ft + 4 * g) : zero4();
       __builtin_amdgcn_wave_barrier();
       f4 gX0[KT][ET];
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft) gX0[kt][ft] = zero4();
-      mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, Dm::LK, gX0, cache, gx, ln2);
+      mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, lk, gX0, cache, gx, ln2);
       __builtin_amdgcn_wave_barrier();
       // hand-over to the block-0 wave
 #pragma unroll
@@ -968,9 +972,9 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = 16 * kt + 4 * g + r;
-            if (row < Dm::LK) R[row * E + 16 * ft + c] = gX0[kt][ft][r];
+            if (row < lk) R[row * E + 16 * ft + c] = gX0[kt][ft][r];
           }
-      if (c < Dm::Q) {
+      if (c < nq) {
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft) st4(R + Pd::XCH + c * E + 16 * ft + 4 * g, gx[ft]);
       }
@@ -987,7 +991,7 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
 // block-0 wave: block-0 recompute, then block-0 backward and the step's key grads
 template <int E, int H, int A, int FF, typename WT>
 T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_layout& Lb, const t2o_layout& Gb,
-                         float* __restrict__ gs, const float* X0, float* R, int b, PairBarrier& pb) {
+                         float* __restrict__ gs, const float* X0, float* R, int b, PairBarrier& pb, int na) {
   using Dm = MixDims<E, A>;
   using Pd = MixPipeDims<E, A>;
   using Rec = TapeRec<E, H, FF>;
@@ -995,7 +999,8 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
   constexpr bool BF = sizeof(WT) == 2;
   const MixerFwdArgs& fa = args.f;
   const int T = fa.net[0].T;
-  const size_t ntiles = (size_t)fa.B * T;
+  const int nq = na + 3, lk = 2 * na + 3;
+  const size_t ctiles = ((size_t)fa.B * T * nq + 15) / 16;
   constexpr size_t RECD = 0;  // tape block
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
   const int f = lane < E ? lane : 0;
@@ -1007,19 +1012,19 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
   pb.sync();  // one phase behind the block-1 wave
   for (int t = T - 1; t >= 0; --t) {
     const size_t bt = (size_t)b * T + t;
-    // tape tiles of exactly the Q query rows (mixer_tape_records)
-    const MaskedRec<WT> rec(static_cast<WT*>(args.tape) + (RECD * ntiles + (size_t)t * fa.B + b) * Rec::SIZE * Dm::Q,
-                            Dm::Q, Rec::SIZE);
+    // the (episode, step)'s nq records
+    const MaskedRec<WT> rec(static_cast<WT*>(args.tape) + (RECD * ctiles * 16 + ((size_t)t * fa.B + b) * nq) * Rec::SIZE,
+                            nq, Rec::SIZE);
     MixerCacheLean<E, H, KT, FF> cache;
     KeyFrags<E, KT, BF> K;
-    {  // ---- recompute: block-0 forward with cache (queries = X0's last A+3 rows)
-      mixp_load_stT<E, A>(fa, b, t, stT);  // for this step's state-embedding grads
+    {  // ---- recompute: block-0 forward with cache (queries = X0's last na+3 rows)
+      mixp_load_stT<E, A>(fa, b, t, stT, na);  // for this step's state-embedding grads
       const Wts<WT> P = step_view(P0);
       K.template load<Dm::LDX>(X0);
       f4 x[ET];
 #pragma unroll
-      for (int ft = 0; ft < ET; ++ft) x[ft] = c < Dm::Q ? ld4(X0 + (Dm::NS + c) * Dm::LDX + 16 * ft + 4 * g) : zero4();
-      mixer_block_fwd_lean<E, H, KT, FF>(P, Lb, 0, K, Dm::LK, x, cache, rec);
+      for (int ft = 0; ft < ET; ++ft) x[ft] = c < nq ? ld4(X0 + (na + c) * Dm::LDX + 16 * ft + 4 * g) : zero4();
+      mixer_block_fwd_lean<E, H, KT, FF>(P, Lb, 0, K, lk, x, cache, rec);
     }
     pb.sync();
     {  // ---- backward: block 0, then the step's key-token grads
@@ -1032,12 +1037,12 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = 16 * kt + 4 * g + r;
-            gX0[kt][ft][r] = row < Dm::LK ? R[row * E + 16 * ft + c] : 0.f;
+            gX0[kt][ft][r] = row < lk ? R[row * E + 16 * ft + c] : 0.f;
           }
 #pragma unroll
-      for (int ft = 0; ft < ET; ++ft) gx[ft] = c < Dm::Q ? ld4(R + Pd::XCH + c * E + 16 * ft + 4 * g) : zero4();
+      for (int ft = 0; ft < ET; ++ft) gx[ft] = c < nq ? ld4(R + Pd::XCH + c * E + 16 * ft + 4 * g) : zero4();
       __builtin_amdgcn_wave_barrier();
-      mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, Dm::LK, gX0, cache, gx, ln2);
+      mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, lk, gX0, cache, gx, ln2);
       // state embedding grads from the key-grad registers (as mixer_bwd_kernel)
 #pragma unroll
       for (int s = 0; s < Dm::ST; ++s)
@@ -1045,7 +1050,7 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
         for (int ft = 0; ft < ET; ++ft) {
           f4 am;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) am[r] = 16 * s + 4 * g + r < Dm::NS ? gX0[s][ft][r] : 0.f;
+          for (int r = 0; r < 4; ++r) am[r] = 16 * s + 4 * g + r < na ? gX0[s][ft][r] : 0.f;
           if constexpr (BF) {
             gWe[ft] = mfma_b16(to_bf4(am), to_bf4(stT[s]), gWe[ft]);
           } else {
@@ -1061,18 +1066,18 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
 #pragma unroll
           for (int r = 0; r < 4; ++r) R[(16 * kt + 4 * g + r) * E + 16 * ft + c] = gX0[kt][ft][r];
       __builtin_amdgcn_wave_barrier();
-      if (c < Dm::Q) {  // the query path: block-0 input rows are X0's last A+3 rows
+      if (c < nq) {  // the query path: block-0 input rows are X0's last na+3 rows
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft) {
-          float* dst = R + (Dm::NS + c) * E + 16 * ft + 4 * g;
+          float* dst = R + (na + c) * E + 16 * ft + 4 * g;
           st4(dst, ld4(dst) + gx[ft]);
         }
       }
       __builtin_amdgcn_wave_barrier();
-      for (int i = lane; i < A * E / 4; i += 64) st4(args.ghid + bt * A * E + 4 * i, ld4(R + Dm::NS * E + 4 * i));
+      for (int i = lane; i < na * E / 4; i += 64) st4(args.ghid + bt * na * E + 4 * i, ld4(R + na * E + 4 * i));
       if (t == 0 && args.ghw0 && fv) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) args.ghw0[((size_t)b * 3 + k) * E + f] = R[(Dm::NS + A + k) * E + f];
+        for (int k = 0; k < 3; ++k) args.ghw0[((size_t)b * 3 + k) * E + f] = R[(2 * na + k) * E + f];
       }
     }
     pb.sync();
@@ -1095,14 +1100,14 @@ inline __host__ __device__ int64_t mixp_weight_elems(const t2o_layout& L) {
   return sizeof(WT) == 4 ? L.fwd_total : L.total;
 }
 
-template <int E, int H, int D, int A, int FF, typename WT>
+template <int E, int H, int D, int A, int FF, bool RT, typename WT>
 __global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) {
   static_assert(D == 2 && MixPipeDims<E, A>::OK, "one wave per block of a depth-2 stack, one query tile");
-  static_assert(mixer_tape_records(A) == MixDims<E, A>::Q, "tape tiles hold exactly the query rows");
   using Dm = MixDims<E, A>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const t2o_layout& L = args.f.L;
   const t2o_layout& G = args.G;
+  const int na = RT ? args.f.na : A;
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
   // the block this wave owns.  Waves w and w + 4 share a SIMD: with four pairs,
   // pairs 2-3 swap their block roles so every SIMD holds one block-0 and one
@@ -1124,6 +1129,15 @@ __global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) 
     for (int i = threadIdx.x & 63; i < Dm::X0F; i += 64) X0[i] = 0.f;
   int* const flags = reinterpret_cast<int*>(smem + args.lds_w + args.waves * MixPipeDims<E, A>::PAIRF);
   if (threadIdx.x < PAIR_FLAG_FLOATS) flags[threadIdx.x] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < 64) {  // zero each block's compact stream past its last record
+    using Rec = TapeRec<E, H, FF>;
+    const size_t nrec = (size_t)args.f.B * args.f.net[0].T * (na + 3), ctiles = (nrec + 15) / 16;
+    const int tail = (int)(ctiles * 16 - nrec) * Rec::SIZE;
+    for (int dd = 0; dd < D; ++dd) {
+      WT* z = static_cast<WT*>(args.tape) + ((size_t)dd * ctiles * 16 + nrec) * Rec::SIZE;
+      for (int i = threadIdx.x; i < tail; i += 64) z[i] = WT(0.f);
+    }
+  }
   __syncthreads();
   PairBarrier pb = PairBarrier::make(flags, w);  // partner: the pair's other wave
   const int b = blockIdx.x * args.waves + pr;  // the launcher makes every pair valid
@@ -1137,11 +1151,11 @@ __global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) 
 #define T2O_MIXP_PRIO_BLOCK 1
 #endif
   if (T2O_MIXP_PRIO_BLOCK >= 0 && d == T2O_MIXP_PRIO_BLOCK) __builtin_amdgcn_s_setprio(1);
-  if (d == 1) mixp_block1<E, H, A, FF, WT>(args, P0, L, Lb, Gb, gs, X0, R, b, pb);
-  else mixp_block0<E, H, A, FF, WT>(args, P0, Lb, Gb, gs, X0, R, b, pb);
+  if (d == 1) mixp_block1<E, H, A, FF, WT>(args, P0, L, Lb, Gb, gs, X0, R, b, pb, na);
+  else mixp_block0<E, H, A, FF, WT>(args, P0, Lb, Gb, gs, X0, R, b, pb, na);
 }
 
-template <int E, int H, int D, int A, int FF, typename WT>
+template <int E, int H, int D, int A, int FF, bool RT, typename WT>
 int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
   constexpr int PERW = MixBwdDims<E, A>::PERW;
   const t2o_layout& L = args.f.L;
@@ -1157,7 +1171,7 @@ int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t 
         args.lds_w = lds_w;
         const int grid = args.f.B / pairs;
         if (grid > max_slabs) return T2O_EINVAL;
-        auto kern = mixer_bwd_pipe_kernel<E, H, D, A, FF, WT>;
+        auto kern = mixer_bwd_pipe_kernel<E, H, D, A, FF, RT, WT>;
         (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipLaunchKernelGGL(kern, dim3(grid), dim3(128 * pairs), lds, stream, args);
         *nslab = grid;
@@ -1182,7 +1196,7 @@ int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t 
   }
   const int grid = (args.f.B + args.waves - 1) / args.waves;
   if (grid > max_slabs) return T2O_EINVAL;
-  auto kern = wlds ? mixer_bwd_kernel<E, H, D, A, FF, true, WT> : mixer_bwd_kernel<E, H, D, A, FF, false, WT>;
+  auto kern = wlds ? mixer_bwd_kernel<E, H, D, A, FF, RT, true, WT> : mixer_bwd_kernel<E, H, D, A, FF, RT, false, WT>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(grid), dim3(64 * args.waves), lds, stream, args);
   *nslab = grid;
@@ -1234,6 +1248,7 @@ extern "C" int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, c
   a.av_st = av_st;
   a.B = B;
   a.Fs = L->F;
+  a.na = L->n_ent;
   auto check_mode = [&](int mode, const float* qv, const float* qsel) {
     if (mode == 0) return qv != nullptr;
     if (mode == 1) return qsel && actions;
@@ -1253,9 +1268,9 @@ extern "C" int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, c
     nnet = 2;
   }
   int rc = T2O_EUNSUPPORTED;
-  T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
-               rc = (L->prec ? launch_mixer_fwd<E_, H_, D_, NE_, FF_, __bf16>(a, nnet, (hipStream_t)stream)
-                             : launch_mixer_fwd<E_, H_, D_, NE_, FF_, float>(a, nnet, (hipStream_t)stream)));
+  T2O_DISPATCH_MIXER(L->E, L->H, L->D, L->n_ent, L->FF,
+                     rc = (L->prec ? launch_mixer_fwd<E_, H_, D_, NE_, FF_, RT_, __bf16>(a, nnet, (hipStream_t)stream)
+                                   : launch_mixer_fwd<E_, H_, D_, NE_, FF_, RT_, float>(a, nnet, (hipStream_t)stream)));
   return rc;
 }
 
@@ -1280,6 +1295,7 @@ extern "C" int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, cons
   a.f.st_st = st_st;
   a.f.B = B;
   a.f.Fs = L->F;
+  a.f.na = L->n_ent;
   a.f.net[0] = MixerNet{pack, hw0, hid, hid_sb, hid_st, nullptr, qv, 0, T, nullptr, nullptr, nullptr, nullptr,
                         nullptr};
   a.xmid = xmid;
@@ -1294,8 +1310,8 @@ extern "C" int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, cons
   a.slabs = gslabs;
   a.tape = tape;
   int rc = T2O_EUNSUPPORTED;
-  T2O_DISPATCH(L->E, L->H, L->D, L->n_ent, L->FF,
-               rc = (L->prec ? launch_mixer_bwd<E_, H_, D_, NE_, FF_, __bf16>(a, max_slabs, nslab, (hipStream_t)stream)
-                             : launch_mixer_bwd<E_, H_, D_, NE_, FF_, float>(a, max_slabs, nslab, (hipStream_t)stream)));
+  T2O_DISPATCH_MIXER(L->E, L->H, L->D, L->n_ent, L->FF,
+                     rc = (L->prec ? launch_mixer_bwd<E_, H_, D_, NE_, FF_, RT_, __bf16>(a, max_slabs, nslab, (hipStream_t)stream)
+                                   : launch_mixer_bwd<E_, H_, D_, NE_, FF_, RT_, float>(a, max_slabs, nslab, (hipStream_t)stream)));
   return rc;
 }

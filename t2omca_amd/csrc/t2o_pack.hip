@@ -220,6 +220,12 @@ struct Builder {
 };
 }  // namespace
 
+extern "C" int t2o_layout_instance(const t2o_layout* L) {
+  if (!L) return T2O_EINVAL;
+  if (L->generic) return T2O_INSTANCE_GENERIC;
+  return t2o_exact_shape(L->E, L->H, L->D, L->n_ent, L->FF) ? T2O_INSTANCE_EXACT : T2O_INSTANCE_RUNTIME;
+}
+
 extern "C" int t2o_layout_init(t2o_layout* L, int kind, int E, int H, int D, int F, int NA, int FF, int n_ent,
                                int prec) {
   return t2o_layout_init_ex(L, kind, E, H, D, F, NA, FF, n_ent, prec, 0, T2O_POS_ABS, 1.0f, 0);

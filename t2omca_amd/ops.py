@@ -49,6 +49,13 @@ class NetShape:
         return bool(self.layout().generic)
 
     @property
+    def instance(self):
+        """Which kernels run this network: "exact" (MFMA instance compiled for its entity
+        count), "runtime" (MFMA instance of a capacity class, entity count read at run
+        time) or "generic" (runtime-shaped fp32 kernels) — include/t2omca.h."""
+        return ("exact", "runtime", "generic")[int(lib().t2o_layout_instance(ctypes.byref(self.layout())))]
+
+    @property
     def agents(self):
         return self.n_agents or self.n_ent
 

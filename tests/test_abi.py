@@ -99,12 +99,16 @@ def test_dropin_modules_state_dict_matches_reference_keys():
         assert list(mine) == list(ref) and mine == ref
 
 
-@pytest.mark.parametrize("E,H,D,FF,n,generic", [(32, 3, 2, 128, 8, 0), (32, 3, 2, 128, 5, 1), (30, 3, 2, 120, 8, 1),
-                                                 (64, 4, 2, 256, 8, 1), (16, 1, 3, 32, 6, 1), (16, 2, 1, 64, 3, 0)])
+@pytest.mark.parametrize("E,H,D,FF,n,generic", [(32, 3, 2, 128, 8, 0), (32, 3, 2, 128, 5, 0), (32, 3, 2, 128, 12, 0),
+                                                 (32, 3, 2, 128, 33, 0), (32, 3, 2, 128, 64, 0), (30, 3, 2, 120, 8, 1),
+                                                 (64, 4, 2, 256, 8, 1), (16, 1, 3, 32, 6, 1), (16, 2, 1, 64, 3, 0),
+                                                 (16, 2, 1, 64, 4, 1)])
 def test_layout_tuned_or_generic(E, H, D, FF, n, generic):
-    """Shapes with a tuned MFMA instance get the folded pack; every other shape within
-    the runtime-shaped kernels' limits gets generic = 1 and a pack of the reference
-    parameters + transposed copies, with reference-order gradients."""
+    """Shapes with a tuned MFMA instance — the default network (emb 32, 3 heads,
+    depth 2, FF 128) at ANY entity count 1..64 (exact or runtime-entity instances,
+    t2o_dispatch.hpp), plus the emb-16 fixture shape — get the folded pack; every
+    other shape within the runtime-shaped kernels' limits gets generic = 1 and a pack
+    of the reference parameters + transposed copies, with reference-order gradients."""
     from t2omca_amd import _lib
     for kind in (0, 1):
         L = _lib.make_layout(kind, E, H, D, 9, 5, FF, n, flags=0)
@@ -128,14 +132,14 @@ def test_bwd_tape_tiles_host_logic():
     B, T = 5, 7
     La = _lib.make_layout(0, 32, 3, 2, 9, 5, 128, 8)
     assert lib.t2o_bwd_tape_tiles(C.byref(La), B, T, 8) == T * ((B * 8 + 15) // 16)
-    Lm8 = _lib.make_layout(1, 32, 3, 2, 8, 1, 128, 8)
-    assert lib.t2o_bwd_tape_tiles(C.byref(Lm8), B, T, 8) == B * T  # 11 query rows: one tile each
-    for A in (16, 64):
+    # tuned mixers (exact and runtime-agent instances): each block's query-row records
+    # form one compact stream cut into 16-record tiles
+    for A in (3, 8, 12, 16, 32, 64):
         Lm = _lib.make_layout(1, 32, 3, 2, 8, 1, 128, A)
         assert Lm.generic == 0
         assert lib.t2o_bwd_tape_tiles(C.byref(Lm), B, T, A) == (B * T * (A + 3) + 15) // 16
         assert lib.t2o_bwd_tape_tiles(C.byref(Lm), B, T, A - 1) == -1
-    Lg = _lib.make_layout(1, 32, 3, 2, 8, 1, 128, 32)  # generic: one tile-set per (episode, step)
+    Lg = _lib.make_layout(1, 32, 4, 2, 8, 1, 128, 32)  # generic: one tile-set per (episode, step)
     assert Lg.generic == 1
     assert lib.t2o_bwd_tape_tiles(C.byref(Lg), B, T, 32) == B * T * 3
     assert lib.t2o_bwd_tape_tiles(C.byref(Lg), 0, T, 32) == -1

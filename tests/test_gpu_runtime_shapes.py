@@ -1,0 +1,63 @@
+"""GPU: the runtime-entity MFMA instances (csrc/t2o_dispatch.hpp) — the default
+network of every BASELINE config (emb 32, 3 heads, depth 2, ff_hidden_mult 4) at an
+AGV count without an exact instance (environment_multi_mec.py:9-11 takes any
+agv_num; transf_agent.py:9-48 / n_transf_mixer.py:13-50 any n_agents).  Each
+instance is compiled for a capacity class and reads the real count at run time:
+
+  agent   8 / 16 entities in registers (padding entities score -inf), 64 streamed in
+          8-entity chunks (a partial last chunk masked);
+  mixer   8 and 13 agents: one 16-row query tile, the two-wave pipelined BPTT;
+          16 / 32 / 64: the multi-tile kernels (query tiles past A + 3 skipped,
+          padding keys -inf).
+
+The cases below put every class on both sides of its boundaries (A = 2 ... 63).
+Checked against the reference modules' goldens (5 and 32 AGVs, per-step forward +
+autograd through the drop-in modules) and against the fp64 oracle's full TD update
+(oracle/ref_learner; TD semantics parity-unpinned).
+
+Bars (normwise max|Δ| / max|ref|): fp32 forward quantities (Q_tot,
+targets, priorities) <= 1e-5, gradients <= 3e-5; bf16 <= 2e-2 / 6e-2 (bf16 MFMA
+operands, fp32 accumulation / LayerNorm / softmax / recurrent state), as the exact
+instances (tests/test_gpu_configs.py).
+"""
+import os
+
+import pytest
+
+from tests.gpu_util import require_gpu
+from tests.test_gpu_generic import GOLD, _cfg_of, _td, agent_module_check, mixer_module_check
+
+pytestmark = pytest.mark.gpu
+
+# (A, B, T): every capacity class, padded and full, of both networks
+FP32_CASES = [(2, 4, 6), (5, 4, 6), (12, 4, 6), (13, 3, 5), (14, 3, 5), (20, 2, 5), (32, 2, 4), (40, 2, 4),
+              (63, 2, 3)]
+BF16_CASES = [(5, 4, 6), (12, 4, 6), (20, 2, 5), (40, 2, 4)]
+
+
+@pytest.fixture(autouse=True)
+def _tuned(monkeypatch):
+    monkeypatch.setenv("T2O_GENERIC", "0")
+
+
+@pytest.mark.parametrize("A,B,T", FP32_CASES, ids=lambda v: str(v))
+def test_runtime_instance_td_update_fp32(A, B, T):
+    require_gpu()
+    learner, _ = _td(dict(_cfg_of(A), tag=f"A{A}"), B, T)
+    assert learner.sa.instance == "runtime" and learner.sm.instance == "runtime"
+
+
+@pytest.mark.parametrize("A,B,T", BF16_CASES, ids=lambda v: str(v))
+def test_runtime_instance_td_update_bf16(A, B, T):
+    require_gpu()
+    learner, _ = _td(dict(_cfg_of(A), tag=f"A{A}"), B, T, precision="bf16", tol=(2e-2, 6e-2))
+    assert learner.sa.instance == "runtime" and learner.sm.instance == "runtime"
+
+
+@pytest.mark.parametrize("name", ["a5_e32_h3_d2", "a32_e32_h3_d2"])
+def test_runtime_instance_modules_vs_reference_goldens(name):
+    """The drop-in modules (reference signatures, one step per call + autograd) on
+    the runtime instances, against the reference modules' own outputs."""
+    require_gpu()
+    assert agent_module_check(os.path.join(GOLD, f"agent_{name}.npz")) == "runtime"
+    assert mixer_module_check(os.path.join(GOLD, f"mixer_{name}.npz")) == "runtime"
