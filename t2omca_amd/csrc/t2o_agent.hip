@@ -228,22 +228,22 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
   const size_t tiles_per_step = (size_t)(R + 15) / 16;
   const size_t ntiles = (size_t)T * tiles_per_step;
 
-  if (rt * args.rpw < R) {
-    f4 gWe[ET][1], gWo[1][ET];
+  f4 gWe[ET][1], gWo[1][ET];
 #pragma unroll
-    for (int t = 0; t < ET; ++t) gWe[t][0] = gWo[0][t] = zero4();
+  for (int t = 0; t < ET; ++t) gWe[t][0] = gWo[0][t] = zero4();
+  // per-lane partial sums over the wave's steps, reduced once at the end:
+  // LN2 vectors of every block, embedding bias, head bias
+  f4 ln2[D][2 * ET], gbe[ET], gbo = zero4();
+#pragma unroll
+  for (int t = 0; t < ET; ++t) {
+    gbe[t] = zero4();
+#pragma unroll
+    for (int d = 0; d < D; ++d) ln2[d][t] = ln2[d][ET + t] = zero4();
+  }
+  if (rt * args.rpw < R) {
     f4 gh_rec[ET];
 #pragma unroll
     for (int t = 0; t < ET; ++t) gh_rec[t] = zero4();
-    // per-lane partial sums over the wave's steps, reduced once at the end:
-    // LN2 vectors of every block, embedding bias, head bias
-    f4 ln2[D][2 * ET], gbe[ET], gbo = zero4();
-#pragma unroll
-    for (int t = 0; t < ET; ++t) {
-      gbe[t] = zero4();
-#pragma unroll
-      for (int d = 0; d < D; ++d) ln2[d][t] = ln2[d][ET + t] = zero4();
-    }
     for (int step = T - 1; step >= 0; --step) {
       const Wts<WT> P = step_view(P0);
       f4 h[ET];
@@ -347,12 +347,16 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
 #pragma unroll
       for (int t = 0; t < ET; ++t) st4(args.gh0 + (size_t)row * E + 16 * t + 4 * g, gh_rec[t]);
     }
-    flush_tiles_g<ET, 1>(gs + G.We, 16, gWe);
-    flush_tiles_g<1, ET>(gs + G.Wo, E, gWo);
-    vec_accumulate_g<ET>(gs + G.be, gbe);
-    vec_accumulate_g<1>(gs + G.bo, &gbo);
-    ln2_flush<E, D>(gs, G, ln2);
   }
+  flush_in_wave_order([&] {
+    if (rt * args.rpw < R) {
+      flush_tiles_g<ET, 1>(gs + G.We, 16, gWe);
+      flush_tiles_g<1, ET>(gs + G.Wo, E, gWo);
+      vec_accumulate_g<ET>(gs + G.be, gbe);
+      vec_accumulate_g<1>(gs + G.bo, &gbo);
+      ln2_flush<E, D>(gs, G, ln2);
+    }
+  });
 }
 
 // ---------------------------------------------------------------------------
@@ -637,20 +641,22 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
   }
   if (d == 1) pb.sync();
   if constexpr (ACC) agent_dw_deferred<E, H>(stage, gM, gN, gWe);  // the last backward phase's
-  if (tile_ok) {
-    if constexpr (ACC) {
-      flush_tiles_g<HET, ET>(gs + Gb.M[0], E, gM);
-      flush_tiles_g<ET, HET>(gs + Gb.N[0], H * E, gN);
+  flush_in_wave_order([&] {
+    if (tile_ok) {
+      if constexpr (ACC) {
+        flush_tiles_g<HET, ET>(gs + Gb.M[0], E, gM);
+        flush_tiles_g<ET, HET>(gs + Gb.N[0], H * E, gN);
+      }
+      flush_tiles_g<ET, 1>(gs + G.We, 16, gWe);
+      vec_accumulate_g<ET>(gs + G.be, gbe);
+      vec_accumulate_g<ET>(gs + Gb.g2[0], &ln2[0]);
+      vec_accumulate_g<ET>(gs + Gb.n2[0], &ln2[ET]);
+      if (d == 1) {
+        flush_tiles_g<1, ET>(gs + G.Wo, E, gWo);
+        vec_accumulate_g<1>(gs + G.bo, &gbo);
+      }
     }
-    flush_tiles_g<ET, 1>(gs + G.We, 16, gWe);
-    vec_accumulate_g<ET>(gs + G.be, gbe);
-    vec_accumulate_g<ET>(gs + Gb.g2[0], &ln2[0]);
-    vec_accumulate_g<ET>(gs + Gb.n2[0], &ln2[ET]);
-    if (d == 1) {
-      flush_tiles_g<1, ET>(gs + G.Wo, E, gWo);
-      vec_accumulate_g<1>(gs + G.bo, &gbo);
-    }
-  }
+  });
 }
 
 template <int E, int H, int D, int NE, int FF, typename WT>

@@ -797,6 +797,26 @@ T2O_DEV void vec_accumulate_g(float* __restrict__ gv, const f4* v) {
   }
 }
 
+// Deterministic end-of-kernel slab flush: the workgroup's waves add their
+// partial sums into the workgroup's slab one wave at a time, in wave order —
+// wave w's float atomics are performed at L2 (s_waitcnt) before the barrier that
+// lets wave w + 1 issue — so every slab element receives its addends in the same
+// order on every run (concurrent waves' atomics would not, and the update would
+// not be bit-reproducible).  Within a wave each flush touches an element at most
+// once.  Every wave of the workgroup must call this exactly once.
+template <typename F>
+T2O_DEV void flush_in_wave_order(F&& flush) {
+  const int nw = (int)(blockDim.x >> 6);
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  for (int turn = 0; turn < nw; ++turn) {
+    if (turn == w) {
+      flush();
+      __builtin_amdgcn_s_waitcnt(0);
+    }
+    __syncthreads();
+  }
+}
+
 // Flush an MFMA-layout register block acc[o][i] (lane (g,c), reg r holds
 // dW[16o+4g+r][16i+c]) into a global row-major matrix with float atomics.
 template <int OT, int IT>

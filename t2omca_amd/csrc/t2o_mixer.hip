@@ -67,9 +67,14 @@ struct MixDims {
   static constexpr int QT = (QCAP + 15) / 16;
   static constexpr int ST = (A + 15) / 16;
   static constexpr int LDX = E + 4;
+  // row stride of the [row][feature] LDS blocks (final query rows, their grads, the
+  // key grads): E + 4 floats, so the T-layout accesses (lane c = row, 16-B chunk
+  // 4g of features) spread the 16 rows over distinct banks — at stride E = 32 a
+  // ds_write_b128 of 8 rows hit one 4-bank set (8-way) and a ds_read_b128 4-way
+  static constexpr int LDO = E + 4;
   static constexpr int X0F = KT * 16 * LDX;
-  static constexpr int OUTF = QT * 16 * E;
-  static constexpr int GX0F = KT * 16 * E;
+  static constexpr int OUTF = QT * 16 * LDO;
+  static constexpr int GX0F = KT * 16 * LDO;
   // forward: with one query tile the final query rows are complete only after
   // every key read of the step, so they can live in the key block itself
   static constexpr int FWD_PERW = X0F + (QT == 1 ? 0 : OUTF);
@@ -225,18 +230,19 @@ T2O_DEV void mix_keys(const Wts<WT>& P, const t2o_layout& L, const In& in, float
 template <int E, int A, typename WT>
 T2O_DEV float mixer_head(const Wts<WT>& P, const t2o_layout& L, const float* OUT,
                          const float (&qv)[A], float& pre_h, float& pre2, int na) {
+  constexpr int LDO = MixDims<E, A>::LDO;
   const int f = threadIdx.x & 63;
   const bool fv = f < E;
   const int fc = fv ? f : 0;
-  float ph = OUT[na * E + fc];
+  float ph = OUT[na * LDO + fc];
 #pragma unroll
   for (int ag = 0; ag < A; ++ag)
-    if (ag < na) ph += qv[ag] * fabsf(OUT[ag * E + fc]);
+    if (ag < na) ph += qv[ag] * fabsf(OUT[ag * LDO + fc]);
   pre_h = ph;
   const float hidden = elu1(ph);
-  const float w2 = fabsf(OUT[(na + 1) * E + fc]);
+  const float w2 = fabsf(OUT[(na + 1) * LDO + fc]);
   const float yv = feat_sum<E>(fv ? hidden * w2 : 0.f);
-  const float p2 = feat_sum<E>(fv ? P.s(L.Wo + fc) * OUT[(na + 2) * E + fc] : 0.f) + P.v[L.bo];
+  const float p2 = feat_sum<E>(fv ? P.s(L.Wo + fc) * OUT[(na + 2) * LDO + fc] : 0.f) + P.v[L.bo];
   pre2 = p2;
   return yv + fmaxf(p2, 0.f);
 }
@@ -303,7 +309,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
         if (qt == 0) T2O_MARK(2 + d);
       }
 #pragma unroll
-      for (int ft = 0; ft < ET; ++ft) st4(OUT + q * E + 16 * ft + 4 * g, x[ft]);
+      for (int ft = 0; ft < ET; ++ft) st4(OUT + q * Dm::LDO + 16 * ft + 4 * g, x[ft]);
     }
     __builtin_amdgcn_wave_barrier();
     float qv[A];
@@ -317,11 +323,11 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
 #pragma unroll
     for (int k = 0; k < (3 * E + 63) / 64; ++k) {
       const int i = lane + 64 * k;
-      hv[k] = i < 3 * E ? OUT[(na + i / E) * E + i % E] : 0.f;
+      hv[k] = i < 3 * E ? OUT[(na + i / E) * Dm::LDO + i % E] : 0.f;
       if (i < 3 * E) n.hw[bt * 3 * E + i] = hv[k];
     }
     if (n.xout) {
-      for (int i = lane; i < nq * E; i += 64) n.xout[bt * nq * E + i] = OUT[i];
+      for (int i = lane; i < nq * E; i += 64) n.xout[bt * nq * E + i] = OUT[(i / E) * Dm::LDO + i % E];
     }
     __builtin_amdgcn_wave_barrier();  // OUT (may alias X0) fully read before the hyper rows change
 #pragma unroll
@@ -479,6 +485,7 @@ struct MixBwdDims {
 template <int E, int A, typename WT>
 T2O_DEV void mixer_head_bwd(const Wts<WT>& P, const t2o_layout& L, const float* OUT, float* GOUT, float myq,
                             float gyv, const float (&ghw)[3], float* gqv, float& gWo, float& gbo, int na) {
+  constexpr int LDO = MixDims<E, A>::LDO;
   const int lane = threadIdx.x & 63;
   const int f = lane < E ? lane : 0;
   const bool fv = lane < E;
@@ -487,7 +494,7 @@ T2O_DEV void mixer_head_bwd(const Wts<WT>& P, const t2o_layout& L, const float* 
   float pre_h, pre2;
   (void)mixer_head<E, A>(P, L, OUT, qv, pre_h, pre2, na);
   const float hidden = elu1(pre_h);
-  const float xw2 = OUT[(na + 1) * E + f];
+  const float xw2 = OUT[(na + 1) * LDO + f];
   const float sgn_w2 = (xw2 > 0.f) - (xw2 < 0.f);
   const float gpre = gyv * fabsf(xw2) * (pre_h > 0.f ? 1.f : expf(pre_h));
   const float gpre2 = pre2 > 0.f ? gyv : 0.f;
@@ -497,7 +504,7 @@ T2O_DEV void mixer_head_bwd(const Wts<WT>& P, const t2o_layout& L, const float* 
 #pragma unroll
   for (int ag = 0; ag < A; ++ag) {
     if (ag < na) {
-      const float xa = OUT[ag * E + f];
+      const float xa = OUT[ag * LDO + f];
       gout[ag] = qv[ag] * gpre * ((xa > 0.f) - (xa < 0.f));
       const float gq = feat_sum<E>(fv ? gpre * fabsf(xa) : 0.f);
       gqm = lane == ag ? gq : gqm;
@@ -506,7 +513,7 @@ T2O_DEV void mixer_head_bwd(const Wts<WT>& P, const t2o_layout& L, const float* 
   if (lane < na) *gqv = gqm;
   gout[A] = gpre + ghw[0];
   gout[A + 1] = gyv * hidden * sgn_w2 + ghw[1];
-  const float x2 = OUT[(na + 2) * E + f];
+  const float x2 = OUT[(na + 2) * LDO + f];
   gout[A + 2] = gpre2 * P.s(L.Wo + f) + ghw[2];
   gWo += gpre2 * x2;
   gbo += gpre2;
@@ -514,8 +521,8 @@ T2O_DEV void mixer_head_bwd(const Wts<WT>& P, const t2o_layout& L, const float* 
   if (fv) {
 #pragma unroll
     for (int q = 0; q < A + 3; ++q) {
-      if (q < na) GOUT[q * E + f] = gout[q];
-      else if (q >= A) GOUT[(q - A + na) * E + f] = gout[q];
+      if (q < na) GOUT[q * LDO + f] = gout[q];
+      else if (q >= A) GOUT[(q - A + na) * LDO + f] = gout[q];
     }
   }
 }
@@ -558,22 +565,22 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
       for (int i = lane_c() + 16 * lane_g(); i < tail; i += 64) z[i] = WT(0.f);
     }
   }
+  const int f = lane < E ? lane : 0;
+  const bool fv = lane < E;
+  // state embedding grads as MFMA tiles: lane (g, c) reg r = dWe[16ft+4g+r][c]
+  // (column Fs = d be); hyper_b2 grads per lane (feature)
+  f4 gWe[ET];
+#pragma unroll
+  for (int ft = 0; ft < ET; ++ft) gWe[ft] = zero4();
+  f4 ln2[D][2 * ET];  // LN2 vector grads, per-lane partial sums over the episode's steps
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+#pragma unroll
+    for (int t = 0; t < 2 * ET; ++t) ln2[d][t] = zero4();
+  float gWo = 0.f, gbo = 0.f;
   if (b < fa.B) {
     for (int i = lane; i < Dm::X0F; i += 64) X0[i] = 0.f;
     float ghw[3] = {0.f, 0.f, 0.f};  // grad wrt this step's hyper outputs, lane = feature
-    const int f = lane < E ? lane : 0;
-    const bool fv = lane < E;
-    // state embedding grads as MFMA tiles: lane (g, c) reg r = dWe[16ft+4g+r][c]
-    // (column Fs = d be); hyper_b2 grads per lane (feature)
-    f4 gWe[ET];
-#pragma unroll
-    for (int ft = 0; ft < ET; ++ft) gWe[ft] = zero4();
-    f4 ln2[D][2 * ET];  // LN2 vector grads, per-lane partial sums over the episode's steps
-#pragma unroll
-    for (int d = 0; d < D; ++d)
-#pragma unroll
-      for (int t = 0; t < 2 * ET; ++t) ln2[d][t] = zero4();
-    float gWo = 0.f, gbo = 0.f;
     // Multi-tile mixers (A+3 > 16 query rows) hold a register file's worth of
     // state per step: they use the lean block cache (the forward recompute writes
     // the record's X / Z / Y fields itself) and load each step's inputs when the
@@ -596,7 +603,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
       for (int k = 0; k < MixBwdIn<E, A, D>::XO; ++k) {
         const int i = lane + 64 * k;
-        if (i < nq * E) OUT[i] = cur.xo[k];
+        if (i < nq * E) OUT[(i / E) * Dm::LDO + i % E] = cur.xo[k];
       }
       if constexpr (!LEAN) {
         if (t > 0) mixb_load<E, A, D>(args, n, b, t - 1, nxt, na);  // prefetch step t-1
@@ -607,7 +614,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
       for (int k = 0; k < 3; ++k) ghw[k] += cur.ghx[k];
       float* GOUT = Bd::GOUT ? GOUTB : stage;
       mixer_head_bwd<E, A>(P, L, OUT, GOUT, cur.m.qs[0], cur.gy, ghw, args.gqv + bt * na + lane, gWo, gbo, na);
-      for (int i = nq * E + lane; i < Dm::OUTF; i += 64) GOUT[i] = 0.f;
+      for (int i = nq * Dm::LDO + lane; i < Dm::OUTF; i += 64) GOUT[i] = 0.f;
       __builtin_amdgcn_wave_barrier();
       // ---- blocks backward per query tile; gX0 accumulates in registers
       KeyFrags<E, KT, sizeof(WT) == 2> K;
@@ -627,7 +634,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
           const int q = 16 * qt + c;
           f4 gx[ET];
 #pragma unroll
-          for (int ft = 0; ft < ET; ++ft) gx[ft] = ld4(GOUT + (16 * qt + c) * E + 16 * ft + 4 * g);
+          for (int ft = 0; ft < ET; ++ft) gx[ft] = ld4(GOUT + (16 * qt + c) * Dm::LDO + 16 * ft + 4 * g);
 #pragma unroll
           for (int d = D - 1; d >= 0; --d) {
             f4 x[ET];
@@ -653,12 +660,13 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
           }
           __builtin_amdgcn_wave_barrier();
 #pragma unroll
-          for (int ft = 0; ft < ET; ++ft) st4(GOUT + (16 * qt + c) * E + 16 * ft + 4 * g, q < nq ? gx[ft] : zero4());
+          for (int ft = 0; ft < ET; ++ft)
+            st4(GOUT + (16 * qt + c) * Dm::LDO + 16 * ft + 4 * g, q < nq ? gx[ft] : zero4());
         }
       } else {
       static_assert(LEAN || Dm::QT == 1, "the unrolled path runs one query tile");
 #pragma unroll
-      for (int ft = 0; ft < ET; ++ft) gq0[0][ft] = ld4(GOUT + c * E + 16 * ft + 4 * g);
+      for (int ft = 0; ft < ET; ++ft) gq0[0][ft] = ld4(GOUT + c * Dm::LDO + 16 * ft + 4 * g);
       __builtin_amdgcn_wave_barrier();
       {
         const int q = c;
@@ -724,7 +732,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) GX0[(16 * kt + 4 * g + r) * E + 16 * ft + c] = gX0[kt][ft][r];
+          for (int r = 0; r < 4; ++r) GX0[(16 * kt + 4 * g + r) * Dm::LDO + 16 * ft + c] = gX0[kt][ft][r];
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int qt = 0; qt < Dm::QT; ++qt) {
@@ -732,17 +740,18 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
         if (q < nq) {
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft) {
-            float* dst = GX0 + (na + q) * E + 16 * ft + 4 * g;
-            const f4 gq = LEAN ? ld4(GOUT + q * E + 16 * ft + 4 * g) : gq0[0][ft];
+            float* dst = GX0 + (na + q) * Dm::LDO + 16 * ft + 4 * g;
+            const f4 gq = LEAN ? ld4(GOUT + q * Dm::LDO + 16 * ft + 4 * g) : gq0[0][ft];
             st4(dst, ld4(dst) + gq);
           }
         }
       }
       __builtin_amdgcn_wave_barrier();
       // ---- key-token grads: agent hidden tokens out, hyper tokens carried
-      for (int i = lane; i < na * E / 4; i += 64) st4(args.ghid + bt * na * E + 4 * i, ld4(GX0 + na * E + 4 * i));
+      for (int i = lane; i < na * E / 4; i += 64)
+        st4(args.ghid + bt * na * E + 4 * i, ld4(GX0 + (na + 4 * i / E) * Dm::LDO + (4 * i) % E));
 #pragma unroll
-      for (int k = 0; k < 3; ++k) ghw[k] = fv ? GX0[(2 * na + k) * E + f] : 0.f;
+      for (int k = 0; k < 3; ++k) ghw[k] = fv ? GX0[(2 * na + k) * Dm::LDO + f] : 0.f;
       __builtin_amdgcn_wave_barrier();
       if constexpr (!LEAN) cur = nxt;
     }
@@ -750,18 +759,22 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) args.ghw0[((size_t)b * 3 + k) * E + f] = ghw[k];
     }
-#pragma unroll
-    for (int ft = 0; ft < ET; ++ft)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int fe = 16 * ft + 4 * g + r;
-        if (c < fa.Fs) unsafeAtomicAdd(gs + G.We + fe * 16 + c, gWe[ft][r]);
-        else if (c == fa.Fs) unsafeAtomicAdd(gs + G.be + fe, gWe[ft][r]);
-      }
-    if (fv) unsafeAtomicAdd(gs + G.Wo + f, gWo);
-    if (lane == 0) unsafeAtomicAdd(gs + G.bo, gbo);
-    ln2_flush<E, D>(gs, G, ln2);
   }
+  flush_in_wave_order([&] {
+    if (b < fa.B) {
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int fe = 16 * ft + 4 * g + r;
+          if (c < fa.Fs) unsafeAtomicAdd(gs + G.We + fe * 16 + c, gWe[ft][r]);
+          else if (c == fa.Fs) unsafeAtomicAdd(gs + G.be + fe, gWe[ft][r]);
+        }
+      if (fv) unsafeAtomicAdd(gs + G.Wo + f, gWo);
+      if (lane == 0) unsafeAtomicAdd(gs + G.bo, gbo);
+      ln2_flush<E, D>(gs, G, ln2);
+    }
+  });
 }
 
 // ---- two waves per episode (depth 2, one query tile) ------------------------
@@ -787,10 +800,10 @@ template <int E, int A>
 struct MixPipeDims {
   using Dm = MixDims<E, A>;
   using Bd = MixBwdDims<E, A>;
-  static constexpr int XCH = Dm::LKCAP * E;  // offset of the query-row grads in R
+  static constexpr int XCH = Dm::LKCAP * Dm::LDO;  // offset of the query-row grads in R
   static constexpr int R0 = Bd::W0 > Dm::GX0F ? Bd::W0 : Dm::GX0F;
   // (the hand-over needs R to hold the key grads and, past them, the query-row grads)
-  static constexpr int REGION = R0 > XCH + Dm::QCAP * E ? R0 : XCH + Dm::QCAP * E;
+  static constexpr int REGION = R0 > XCH + Dm::QCAP * Dm::LDO ? R0 : XCH + Dm::QCAP * Dm::LDO;
   static constexpr int PAIRF = Dm::X0F + REGION;
   static constexpr bool OK = Dm::QT == 1;
 };
@@ -940,13 +953,13 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
       const Wts<WT> P = step_view(P0);
       float ghw[3];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) ghw[k] = (t < T - 1 && fv) ? R[(2 * na + k) * E + f] : 0.f;
+      for (int k = 0; k < 3; ++k) ghw[k] = (t < T - 1 && fv) ? R[(2 * na + k) * Dm::LDO + f] : 0.f;
       __builtin_amdgcn_wave_barrier();
       float* OUT = R;  // forward final query rows, then their grads in place
 #pragma unroll
       for (int k = 0; k < In::XO; ++k) {
         const int i = lane + 64 * k;
-        if (i < nq * E) OUT[i] = cur.xo[k];
+        if (i < nq * E) OUT[(i / E) * Dm::LDO + i % E] = cur.xo[k];
       }
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -955,7 +968,7 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
       __builtin_amdgcn_wave_barrier();
       f4 gx[ET];
 #pragma unroll
-      for (int ft = 0; ft < ET; ++ft) gx[ft] = c < nq ? ld4(OUT + c * E + 16 * ft + 4 * g) : zero4();
+      for (int ft = 0; ft < ET; ++ft) gx[ft] = c < nq ? ld4(OUT + c * Dm::LDO + 16 * ft + 4 * g) : zero4();
       __builtin_amdgcn_wave_barrier();
       f4 gX0[KT][ET];
 #pragma unroll
@@ -972,20 +985,22 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = 16 * kt + 4 * g + r;
-            if (row < lk) R[row * E + 16 * ft + c] = gX0[kt][ft][r];
+            if (row < lk) R[row * Dm::LDO + 16 * ft + c] = gX0[kt][ft][r];
           }
       if (c < nq) {
 #pragma unroll
-        for (int ft = 0; ft < ET; ++ft) st4(R + Pd::XCH + c * E + 16 * ft + 4 * g, gx[ft]);
+        for (int ft = 0; ft < ET; ++ft) st4(R + Pd::XCH + c * Dm::LDO + 16 * ft + 4 * g, gx[ft]);
       }
     }
     pb.sync();
   }
   pb.sync();  // the block-0 wave's last backward phase
-  vec_accumulate_g<ET>(gs + Gb.g2[0], &ln2[0]);
-  vec_accumulate_g<ET>(gs + Gb.n2[0], &ln2[ET]);
-  if (fv) unsafeAtomicAdd(gs + Gb.Wo + f, gWo);
-  if (lane == 0) unsafeAtomicAdd(gs + Gb.bo, gbo);
+  flush_in_wave_order([&] {
+    vec_accumulate_g<ET>(gs + Gb.g2[0], &ln2[0]);
+    vec_accumulate_g<ET>(gs + Gb.n2[0], &ln2[ET]);
+    if (fv) unsafeAtomicAdd(gs + Gb.Wo + f, gWo);
+    if (lane == 0) unsafeAtomicAdd(gs + Gb.bo, gbo);
+  });
 }
 
 // block-0 wave: block-0 recompute, then block-0 backward and the step's key grads
@@ -1037,10 +1052,10 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = 16 * kt + 4 * g + r;
-            gX0[kt][ft][r] = row < lk ? R[row * E + 16 * ft + c] : 0.f;
+            gX0[kt][ft][r] = row < lk ? R[row * Dm::LDO + 16 * ft + c] : 0.f;
           }
 #pragma unroll
-      for (int ft = 0; ft < ET; ++ft) gx[ft] = c < nq ? ld4(R + Pd::XCH + c * E + 16 * ft + 4 * g) : zero4();
+      for (int ft = 0; ft < ET; ++ft) gx[ft] = c < nq ? ld4(R + Pd::XCH + c * Dm::LDO + 16 * ft + 4 * g) : zero4();
       __builtin_amdgcn_wave_barrier();
       mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, lk, gX0, cache, gx, ln2);
       // state embedding grads from the key-grad registers (as mixer_bwd_kernel)
@@ -1064,34 +1079,37 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) R[(16 * kt + 4 * g + r) * E + 16 * ft + c] = gX0[kt][ft][r];
+          for (int r = 0; r < 4; ++r) R[(16 * kt + 4 * g + r) * Dm::LDO + 16 * ft + c] = gX0[kt][ft][r];
       __builtin_amdgcn_wave_barrier();
       if (c < nq) {  // the query path: block-0 input rows are X0's last na+3 rows
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft) {
-          float* dst = R + (na + c) * E + 16 * ft + 4 * g;
+          float* dst = R + (na + c) * Dm::LDO + 16 * ft + 4 * g;
           st4(dst, ld4(dst) + gx[ft]);
         }
       }
       __builtin_amdgcn_wave_barrier();
-      for (int i = lane; i < na * E / 4; i += 64) st4(args.ghid + bt * na * E + 4 * i, ld4(R + na * E + 4 * i));
+      for (int i = lane; i < na * E / 4; i += 64)
+        st4(args.ghid + bt * na * E + 4 * i, ld4(R + (na + 4 * i / E) * Dm::LDO + (4 * i) % E));
       if (t == 0 && args.ghw0 && fv) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) args.ghw0[((size_t)b * 3 + k) * E + f] = R[(2 * na + k) * E + f];
+        for (int k = 0; k < 3; ++k) args.ghw0[((size_t)b * 3 + k) * E + f] = R[(2 * na + k) * Dm::LDO + f];
       }
     }
     pb.sync();
   }
+  flush_in_wave_order([&] {
 #pragma unroll
-  for (int ft = 0; ft < ET; ++ft)
+    for (int ft = 0; ft < ET; ++ft)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int fe = 16 * ft + 4 * g + r;
-      if (c < fa.Fs) unsafeAtomicAdd(gs + Gb.We + fe * 16 + c, gWe[ft][r]);
-      else if (c == fa.Fs) unsafeAtomicAdd(gs + Gb.be + fe, gWe[ft][r]);
-    }
-  vec_accumulate_g<ET>(gs + Gb.g2[0], &ln2[0]);
-  vec_accumulate_g<ET>(gs + Gb.n2[0], &ln2[ET]);
+      for (int r = 0; r < 4; ++r) {
+        const int fe = 16 * ft + 4 * g + r;
+        if (c < fa.Fs) unsafeAtomicAdd(gs + Gb.We + fe * 16 + c, gWe[ft][r]);
+        else if (c == fa.Fs) unsafeAtomicAdd(gs + Gb.be + fe, gWe[ft][r]);
+      }
+    vec_accumulate_g<ET>(gs + Gb.g2[0], &ln2[0]);
+    vec_accumulate_g<ET>(gs + Gb.n2[0], &ln2[ET]);
+  });
   (void)fv;
 }
 

@@ -143,3 +143,26 @@ def test_bwd_tape_tiles_host_logic():
     assert Lg.generic == 1
     assert lib.t2o_bwd_tape_tiles(C.byref(Lg), B, T, 32) == B * T * 3
     assert lib.t2o_bwd_tape_tiles(C.byref(Lg), 0, T, 32) == -1
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_layout_instance_classes(kind):
+    """t2o_layout_instance (host-only): exact MFMA instances at 3 / 8 / 16 / 64 entities,
+    runtime-entity instances at every other count 1..64 of the default network, the
+    generic kernels past 64, for other networks, and when forced (include/t2omca.h)."""
+    import ctypes as C
+
+    from t2omca_amd import _lib
+    lib = _lib.lib()
+    for n in range(1, 65):
+        L = _lib.make_layout(kind, 32, 3, 2, 9 if kind == 0 else 8, 5 if kind == 0 else 1, 128, n, flags=0)
+        want = 0 if n in (3, 8, 16, 64) else 1
+        assert lib.t2o_layout_instance(C.byref(L)) == want, n
+        Lf = _lib.make_layout(kind, 32, 3, 2, 9 if kind == 0 else 8, 5 if kind == 0 else 1, 128, n,
+                              flags=_lib.LAYOUT_FORCE_GENERIC)
+        assert lib.t2o_layout_instance(C.byref(Lf)) == 2
+    Lo = _lib.make_layout(kind, 64, 4, 2, 9, 5, 256, 8, flags=0)
+    assert lib.t2o_layout_instance(C.byref(Lo)) == 2
+    Lx = _lib.make_layout(kind, 16, 2, 1, 9, 5, 64, 3, flags=0)
+    assert lib.t2o_layout_instance(C.byref(Lx)) == 0
+    assert lib.t2o_layout_instance(None) < 0

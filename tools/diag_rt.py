@@ -40,7 +40,17 @@ def main():
     cpu = {k: (v.cpu().double() if v.is_floating_point() else v.cpu()) for k, v in batch.items()}
     pa_g = {k: v.clone().requires_grad_(True) for k, v in pa.items()}
     pm_g = {k: v.clone().requires_grad_(True) for k, v in pm.items()}
+    import torch.nn.functional as Fn
+    from oracle import ref_model
+    relu, mins = Fn.relu, []
+
+    def hook(x, *a, **k):  # |FFN pre-activation| of the kept token (agent: row 0)
+        mins.append(float((x.detach()[:, 0] if x.dim() == 3 else x.detach()).abs().min()))
+        return relu(x, *a, **k)
+    ref_model.F.relu = hook
     loss, prio, ex = ref_learner.td_forward(pa_g, pm_g, pa, pm, cpu, cfg, per_weight=w.cpu().double())
+    ref_model.F.relu = relu
+    print(f"   min |ReLU pre-activation| of kept rows: {min(mins):.2e}")
     loss.backward()
     learner.train(batch, 0, 0, per_weight=w)
     torch.cuda.synchronize()
