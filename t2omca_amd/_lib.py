@@ -105,8 +105,9 @@ EXPORTS = {
                                                                  ctypes.c_uint64, ctypes.c_int64, ctypes.c_void_p]),
 }
 
-# exports only tests / tools call (never on the product path)
-_DIAGNOSTIC = {"t2o_bf_swz", "t2o_probe_lane_ops"}
+# exports only tests / tools call (never on the product path), and the newest
+# reporting export: an older build loaded under A/B timing (T2O_LIB) may lack them
+_DIAGNOSTIC = {"t2o_bf_swz", "t2o_probe_lane_ops", "t2o_layout_instance"}
 
 _lib = None
 

@@ -806,6 +806,10 @@ T2O_DEV void vec_accumulate_g(float* __restrict__ gv, const f4* v) {
 // once.  Every wave of the workgroup must call this exactly once.
 template <typename F>
 T2O_DEV void flush_in_wave_order(F&& flush) {
+#ifdef T2O_NONDET_FLUSH  // A/B builds only: concurrent flushes (not bit-reproducible)
+  flush();
+  return;
+#endif
   const int nw = (int)(blockDim.x >> 6);
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   for (int turn = 0; turn < nw; ++turn) {

@@ -226,11 +226,10 @@ T2O_DEV void mix_keys(const Wts<WT>& P, const t2o_layout& L, const In& in, float
 // Mixing head (n_transf_mixer.py:75-89, pos_func abs: t2o_layout_init lays out
 // every other qmix_pos_func generic) on the final query rows OUT[q][f],
 // lanes = features.  Returns y; writes hyper tokens back into X0.
-// (qv: capacity-sized; entries ag >= na are not read)
-template <int E, int A, typename WT>
+// (qv: capacity-sized; entries ag >= na are not read; LDO: OUT's row stride)
+template <int E, int A, typename WT, int LDO = MixDims<E, A>::LDO>
 T2O_DEV float mixer_head(const Wts<WT>& P, const t2o_layout& L, const float* OUT,
                          const float (&qv)[A], float& pre_h, float& pre2, int na) {
-  constexpr int LDO = MixDims<E, A>::LDO;
   const int f = threadIdx.x & 63;
   const bool fv = f < E;
   const int fc = fv ? f : 0;
@@ -482,17 +481,16 @@ struct MixBwdDims {
 // [0, nq), stride E) and dL/dy, writes the grads wrt those rows to GOUT (may
 // alias OUT), lane a < na's dL/dqvals[a] to gqv, and accumulates the hyper_b2
 // grads.  ghw: grads wrt the step's hyper outputs (carried + external).
-template <int E, int A, typename WT>
+template <int E, int A, typename WT, int LDO = MixDims<E, A>::LDO>
 T2O_DEV void mixer_head_bwd(const Wts<WT>& P, const t2o_layout& L, const float* OUT, float* GOUT, float myq,
                             float gyv, const float (&ghw)[3], float* gqv, float& gWo, float& gbo, int na) {
-  constexpr int LDO = MixDims<E, A>::LDO;
   const int lane = threadIdx.x & 63;
   const int f = lane < E ? lane : 0;
   const bool fv = lane < E;
   float qv[A];
   bcast_agents<A>(myq, qv);
   float pre_h, pre2;
-  (void)mixer_head<E, A>(P, L, OUT, qv, pre_h, pre2, na);
+  (void)mixer_head<E, A, WT, LDO>(P, L, OUT, qv, pre_h, pre2, na);
   const float hidden = elu1(pre_h);
   const float xw2 = OUT[(na + 1) * LDO + f];
   const float sgn_w2 = (xw2 > 0.f) - (xw2 < 0.f);
@@ -800,10 +798,18 @@ template <int E, int A>
 struct MixPipeDims {
   using Dm = MixDims<E, A>;
   using Bd = MixBwdDims<E, A>;
-  static constexpr int XCH = Dm::LKCAP * Dm::LDO;  // offset of the query-row grads in R
-  static constexpr int R0 = Bd::W0 > Dm::GX0F ? Bd::W0 : Dm::GX0F;
+// Row stride of the pair region's [row][feature] blocks.  E + 4 (the other
+// kernels' LDO) removes their T-layout bank conflicts here too, but measured slower
+// in this register-bound kernel: interleaved A/B, overlapped, 3 rounds
+// (profiles/r3_ab2/): mixer_bwd 0.618 ms at E vs 0.630 at E + 4.
+#ifndef T2O_MIXP_LDR
+#define T2O_MIXP_LDR E
+#endif
+  static constexpr int LDR = T2O_MIXP_LDR;
+  static constexpr int XCH = Dm::LKCAP * LDR;  // offset of the query-row grads in R
+  static constexpr int R0 = Bd::W0 > Dm::KT * 16 * LDR ? Bd::W0 : Dm::KT * 16 * LDR;
   // (the hand-over needs R to hold the key grads and, past them, the query-row grads)
-  static constexpr int REGION = R0 > XCH + Dm::QCAP * Dm::LDO ? R0 : XCH + Dm::QCAP * Dm::LDO;
+  static constexpr int REGION = R0 > XCH + Dm::QCAP * LDR ? R0 : XCH + Dm::QCAP * LDR;
   static constexpr int PAIRF = Dm::X0F + REGION;
   static constexpr bool OK = Dm::QT == 1;
 };
@@ -953,22 +959,22 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
       const Wts<WT> P = step_view(P0);
       float ghw[3];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) ghw[k] = (t < T - 1 && fv) ? R[(2 * na + k) * Dm::LDO + f] : 0.f;
+      for (int k = 0; k < 3; ++k) ghw[k] = (t < T - 1 && fv) ? R[(2 * na + k) * Pd::LDR + f] : 0.f;
       __builtin_amdgcn_wave_barrier();
       float* OUT = R;  // forward final query rows, then their grads in place
 #pragma unroll
       for (int k = 0; k < In::XO; ++k) {
         const int i = lane + 64 * k;
-        if (i < nq * E) OUT[(i / E) * Dm::LDO + i % E] = cur.xo[k];
+        if (i < nq * E) OUT[(i / E) * Pd::LDR + i % E] = cur.xo[k];
       }
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int k = 0; k < 3; ++k) ghw[k] += cur.ghx[k];
-      mixer_head_bwd<E, A>(P, L, OUT, OUT, cur.qv, cur.gy, ghw, args.gqv + bt * na + lane, gWo, gbo, na);
+      mixer_head_bwd<E, A, WT, Pd::LDR>(P, L, OUT, OUT, cur.qv, cur.gy, ghw, args.gqv + bt * na + lane, gWo, gbo, na);
       __builtin_amdgcn_wave_barrier();
       f4 gx[ET];
 #pragma unroll
-      for (int ft = 0; ft < ET; ++ft) gx[ft] = c < nq ? ld4(OUT + c * Dm::LDO + 16 * ft + 4 * g) : zero4();
+      for (int ft = 0; ft < ET; ++ft) gx[ft] = c < nq ? ld4(OUT + c * Pd::LDR + 16 * ft + 4 * g) : zero4();
       __builtin_amdgcn_wave_barrier();
       f4 gX0[KT][ET];
 #pragma unroll
@@ -985,11 +991,11 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = 16 * kt + 4 * g + r;
-            if (row < lk) R[row * Dm::LDO + 16 * ft + c] = gX0[kt][ft][r];
+            if (row < lk) R[row * Pd::LDR + 16 * ft + c] = gX0[kt][ft][r];
           }
       if (c < nq) {
 #pragma unroll
-        for (int ft = 0; ft < ET; ++ft) st4(R + Pd::XCH + c * Dm::LDO + 16 * ft + 4 * g, gx[ft]);
+        for (int ft = 0; ft < ET; ++ft) st4(R + Pd::XCH + c * Pd::LDR + 16 * ft + 4 * g, gx[ft]);
       }
     }
     pb.sync();
@@ -1052,10 +1058,10 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int row = 16 * kt + 4 * g + r;
-            gX0[kt][ft][r] = row < lk ? R[row * Dm::LDO + 16 * ft + c] : 0.f;
+            gX0[kt][ft][r] = row < lk ? R[row * Pd::LDR + 16 * ft + c] : 0.f;
           }
 #pragma unroll
-      for (int ft = 0; ft < ET; ++ft) gx[ft] = c < nq ? ld4(R + Pd::XCH + c * Dm::LDO + 16 * ft + 4 * g) : zero4();
+      for (int ft = 0; ft < ET; ++ft) gx[ft] = c < nq ? ld4(R + Pd::XCH + c * Pd::LDR + 16 * ft + 4 * g) : zero4();
       __builtin_amdgcn_wave_barrier();
       mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, lk, gX0, cache, gx, ln2);
       // state embedding grads from the key-grad registers (as mixer_bwd_kernel)
@@ -1079,21 +1085,21 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) R[(16 * kt + 4 * g + r) * Dm::LDO + 16 * ft + c] = gX0[kt][ft][r];
+          for (int r = 0; r < 4; ++r) R[(16 * kt + 4 * g + r) * Pd::LDR + 16 * ft + c] = gX0[kt][ft][r];
       __builtin_amdgcn_wave_barrier();
       if (c < nq) {  // the query path: block-0 input rows are X0's last na+3 rows
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft) {
-          float* dst = R + (na + c) * Dm::LDO + 16 * ft + 4 * g;
+          float* dst = R + (na + c) * Pd::LDR + 16 * ft + 4 * g;
           st4(dst, ld4(dst) + gx[ft]);
         }
       }
       __builtin_amdgcn_wave_barrier();
       for (int i = lane; i < na * E / 4; i += 64)
-        st4(args.ghid + bt * na * E + 4 * i, ld4(R + (na + 4 * i / E) * Dm::LDO + (4 * i) % E));
+        st4(args.ghid + bt * na * E + 4 * i, ld4(R + (na + 4 * i / E) * Pd::LDR + (4 * i) % E));
       if (t == 0 && args.ghw0 && fv) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) args.ghw0[((size_t)b * 3 + k) * E + f] = R[(2 * na + k) * Dm::LDO + f];
+        for (int k = 0; k < 3; ++k) args.ghw0[((size_t)b * 3 + k) * E + f] = R[(2 * na + k) * Pd::LDR + f];
       }
     }
     pb.sync();

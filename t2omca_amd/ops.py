@@ -53,6 +53,8 @@ class NetShape:
         """Which kernels run this network: "exact" (MFMA instance compiled for its entity
         count), "runtime" (MFMA instance of a capacity class, entity count read at run
         time) or "generic" (runtime-shaped fp32 kernels) — include/t2omca.h."""
+        if not hasattr(lib(), "t2o_layout_instance"):  # an older build under A/B timing (T2O_LIB)
+            return "generic" if self.generic else "exact"
         return ("exact", "runtime", "generic")[int(lib().t2o_layout_instance(ctypes.byref(self.layout())))]
 
     @property

@@ -18,7 +18,13 @@ autograd through the drop-in modules) and against the fp64 oracle's full TD upda
 Bars (normwise max|Δ| / max|ref|): fp32 forward quantities (Q_tot,
 targets, priorities) <= 1e-5, gradients <= 3e-5; bf16 <= 2e-2 / 6e-2 (bf16 MFMA
 operands, fp32 accumulation / LayerNorm / softmax / recurrent state), as the exact
-instances (tests/test_gpu_configs.py).
+instances (tests/test_gpu_configs.py).  The fp32 cases draw a batch in which no
+kept FFN pre-activation lies within 1e-6 of 0 (tests/test_gpu_generic.py _td): such
+a value can take the other ReLU branch in fp32 than in fp64 whatever the summation
+order — seed 3 at 40 AGVs has one 1.8e-8 from 0, and its gradient error is 1e-3,
+while seeds 4 and 5 give 4e-7 (profiles/r3_rt2/).  Measured on the box
+(profiles/r3_rt2/pytest.log), fp32: Q_tot <= 1.1e-6, gradients <= 1.2e-6 (A = 63)
+and <= 3.6e-7 elsewhere; bf16: Q_tot <= 1.0e-2, gradients <= 1.4e-2.
 """
 import os
 
@@ -43,7 +49,7 @@ def _tuned(monkeypatch):
 @pytest.mark.parametrize("A,B,T", FP32_CASES, ids=lambda v: str(v))
 def test_runtime_instance_td_update_fp32(A, B, T):
     require_gpu()
-    learner, _ = _td(dict(_cfg_of(A), tag=f"A{A}"), B, T)
+    learner, _ = _td(dict(_cfg_of(A), tag=f"A{A}"), B, T, avoid_relu_ties=True)
     assert learner.sa.instance == "runtime" and learner.sm.instance == "runtime"
 
 
