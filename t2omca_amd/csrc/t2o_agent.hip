@@ -213,7 +213,7 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
   float* stage = smem + lds_w + wave_id() * STAGE;
   float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
   const Wts<WT> P0 = stage_weights(smem, args.pack, L, nw, WT{});
-  for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) gs[i] = 0.f;
+  zero_flushed_regions(gs, G, false);  // (full record: the contraction writes M / N)
   __syncthreads();
 
   const int A = args.A, F = args.F, T = args.T;
@@ -436,7 +436,7 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
   const int lane = threadIdx.x & 63;
   float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
   const Wts<WT> P0 = stage_weights(smem, args.pack, L, nw, WT{});
-  for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) gs[i] = 0.f;
+  zero_flushed_regions(gs, G, ACC);  // (lean record: dM / dN flushed from registers)
   int* const flags = reinterpret_cast<int*>(smem + lds_w + 2 * AGP_TILES * STAGE + AGP_TILES * agp_xch_floats<E>());
   if (threadIdx.x < PAIR_FLAG_FLOATS) flags[threadIdx.x] = 0;
   __syncthreads();

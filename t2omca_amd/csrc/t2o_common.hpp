@@ -797,6 +797,24 @@ T2O_DEV void vec_accumulate_g(float* __restrict__ gv, const f4* v) {
   }
 }
 
+// Zero the parts of a workgroup's gradient slab (compact layout, grad_layout)
+// that its BPTT kernel flushes into: the head region (We, be, Wo, bo), every
+// block's LN2 vectors and, when the tape does not carry their operands (lean
+// agent record), every block's M and N.  The tape contraction (t2o_dwgemm.hip)
+// overwrites every other region of every slab it owns with plain stores, so
+// zeroing the whole slab (grad_total floats per workgroup: 86 MB per agent BPTT
+// at configs[2]) only added HBM writes.  All threads of the workgroup take part;
+// the caller's barrier follows.
+T2O_DEV void zero_flushed_regions(float* __restrict__ gs, const t2o_layout& G, bool mn) {
+  const int nt = (int)blockDim.x;
+  for (int i = threadIdx.x; i < (int)G.M[0]; i += nt) gs[i] = 0.f;  // We, be, Wo, bo
+  for (int d = 0; d < G.D; ++d) {
+    for (int i = threadIdx.x; i < 2 * G.E; i += nt) gs[G.g2[d] + i] = 0.f;  // g2, n2 (adjacent)
+    if (mn)
+      for (int i = threadIdx.x; i < 2 * G.H * G.E * G.E; i += nt) gs[G.M[d] + i] = 0.f;  // M, N (adjacent)
+  }
+}
+
 // Deterministic end-of-kernel slab flush: the workgroup's waves add their
 // partial sums into the workgroup's slab one wave at a time, in wave order —
 // wave w's float atomics are performed at L2 (s_waitcnt) before the barrier that

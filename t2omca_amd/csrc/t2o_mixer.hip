@@ -547,7 +547,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   // beside the per-wave buffers, else read through L2 (large mixers)
   const Wts<WT> P0 = WLDS ? stage_weights(smem, n.pack, L, L.fwd_total, WT{})
                           : global_weights(n.pack, L, WT{});
-  for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) gs[i] = 0.f;
+  zero_flushed_regions(gs, G, false);
   __syncthreads();
   const int b = blockIdx.x * args.waves + w;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
@@ -1148,7 +1148,7 @@ __global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) 
   // bf16: with the transposed copies (the pipelined kernel is register-bound at two
   // waves per SIMD; transposed reads of the forward image cost it spills)
   const Wts<WT> P0 = stage_weights(smem, args.f.net[0].pack, L, mixp_weight_elems<WT>(L), WT{}, false);
-  for (int i = threadIdx.x; i < G.grad_total; i += blockDim.x) gs[i] = 0.f;
+  zero_flushed_regions(gs, G, false);
   if (d == 1)
     for (int i = threadIdx.x & 63; i < Dm::X0F; i += 64) X0[i] = 0.f;
   int* const flags = reinterpret_cast<int*>(smem + args.lds_w + args.waves * MixPipeDims<E, A>::PAIRF);
