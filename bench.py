@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--no-cpu-configs0", action="store_true",
                     help="skip the configs[0]-shape (16 AGVs, T=150) CPU-baseline figure")
     ap.add_argument("--mecs", type=int, default=2, help="rollout mode: MEC servers")
+    ap.add_argument("--qmix-pos-func", choices=("abs", "softplus", "quadratic", "identity"), default="abs",
+                    help="the mixer head's positivity function (n_transf_mixer.py:95-103); the tuned mixer "
+                         "head is abs-only, the others run the runtime-shaped mixer kernels")
     ap.add_argument("--priorities", choices=("device", "cpu"), default="device",
                     help="where each update's |TD errors| go: device (consumed by the device-resident "
                          "PrioritizedReplayBuffer, t2omca_amd/replay.py) or cpu (the reference driver's "
@@ -500,7 +503,7 @@ def main():
         return expand_bench(args, world, rank, dev)
     def make_learner(precision):
         torch.manual_seed(0)
-        margs = make_args(A, device=str(dev))
+        margs = make_args(A, device=str(dev), qmix_pos_func=args.qmix_pos_func)
         agent = TransformerAgent(None, margs).to(dev)
         mixer = TransformerMixer(margs).to(dev)
         return TDLearner(agent, mixer, target_update_interval=10 ** 9, precision=precision,
@@ -614,7 +617,8 @@ def main():
         "config": {"workload": f"{train_config_name(A, B, T)}: full TD update fwd+bwd+Adam, {A} AGVs, "
                                f"batch {B} episodes/GPU x T={T}",
                    "global_batch": B * world, "seq_len": T, "agents": A, "emb": 32, "heads": 3, "depth": 2,
-                   "parallelism": f"dp{world}", "priorities": args.priorities, "kernels": kernels},
+                   "parallelism": f"dp{world}", "priorities": args.priorities, "kernels": kernels,
+                   "mixer_head": args.qmix_pos_func},
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": peak_tf,
                      "unit": "TFLOP/s", "frac": achieved / peak_tf, "traffic": traffic_for(dom, workload_tag(args)),
                      "basis": "SURVEY.md §8(d) reference-order necessary FLOPs of the kernel's share "

@@ -63,12 +63,14 @@ inline int t2o_mixer_cap(int a) { return a <= 8 ? 8 : a <= 13 ? 13 : a <= 16 ? 1
     }                                                                                           \
   } while (0)
 
-// mixer kernels: exact instance, else the runtime instance of the agent count's class
-#define T2O_DISPATCH_MIXER(EV, HV, DV, NEV, FFV, STMT)                                          \
+// mixer kernels: exact instance (abs head only), else the runtime instance of the
+// agent count's class (which also computes the other qmix_pos_funcs)
+#define T2O_DISPATCH_MIXER(EV, HV, DV, NEV, FFV, ABS, STMT)                                     \
   do {                                                                                          \
     const int e_ = (EV), h_ = (HV), d_ = (DV), ne_ = (NEV), ff_ = (FFV);                        \
-    T2O_DISPATCH_EXACT(STMT)                                                                    \
-    else if (t2o_default_net(e_, h_, d_, ff_) && ne_ >= 1 && ne_ <= 64) {                       \
+    if ((ABS) && t2o_exact_shape(e_, h_, d_, ne_, ff_)) {                                       \
+      T2O_DISPATCH_EXACT(STMT)                                                                  \
+    } else if (t2o_default_net(e_, h_, d_, ff_) && ne_ >= 1 && ne_ <= 64) {                     \
       const int cap_ = t2o_mixer_cap(ne_);                                                      \
       if (cap_ == 8) T2O_CASE_X(32, 3, 2, 8, 128, true, STMT)                                   \
       else if (cap_ == 13) T2O_CASE_X(32, 3, 2, 13, 128, true, STMT)                            \

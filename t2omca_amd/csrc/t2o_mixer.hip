@@ -226,20 +226,22 @@ T2O_DEV void mix_keys(const Wts<WT>& P, const t2o_layout& L, const In& in, float
 // Mixing head (n_transf_mixer.py:75-89, pos_func abs: t2o_layout_init lays out
 // every other qmix_pos_func generic) on the final query rows OUT[q][f],
 // lanes = features.  Returns y; writes hyper tokens back into X0.
-// (qv: capacity-sized; entries ag >= na are not read; LDO: OUT's row stride)
+// (qv: capacity-sized; entries ag >= na are not read; LDO: OUT's row stride;
+// pf / pb: qmix_pos_func and its softplus beta, n_transf_mixer.py:95-103 — the
+// exact instances pass the constant abs, the runtime-entity ones the layout's)
 template <int E, int A, typename WT, int LDO = MixDims<E, A>::LDO>
 T2O_DEV float mixer_head(const Wts<WT>& P, const t2o_layout& L, const float* OUT,
-                         const float (&qv)[A], float& pre_h, float& pre2, int na) {
+                         const float (&qv)[A], float& pre_h, float& pre2, int na, int pf, float pb) {
   const int f = threadIdx.x & 63;
   const bool fv = f < E;
   const int fc = fv ? f : 0;
   float ph = OUT[na * LDO + fc];
 #pragma unroll
   for (int ag = 0; ag < A; ++ag)
-    if (ag < na) ph += qv[ag] * fabsf(OUT[ag * LDO + fc]);
+    if (ag < na) ph += qv[ag] * posf(OUT[ag * LDO + fc], pf, pb);
   pre_h = ph;
   const float hidden = elu1(ph);
-  const float w2 = fabsf(OUT[(na + 1) * LDO + fc]);
+  const float w2 = posf(OUT[(na + 1) * LDO + fc], pf, pb);
   const float yv = feat_sum<E>(fv ? hidden * w2 : 0.f);
   const float p2 = feat_sum<E>(fv ? P.s(L.Wo + fc) * OUT[(na + 2) * LDO + fc] : 0.f) + P.v[L.bo];
   pre2 = p2;
@@ -256,6 +258,8 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
   const MixerNet n = args.net[blockIdx.y];
   const t2o_layout& L = args.L;
   const int na = RT ? args.na : A, nq = na + 3, lk = 2 * na + 3;
+  const int pf = RT ? L.pos_func : T2O_POS_ABS;  // the mixer head's positivity function
+  const float pb = RT ? L.pos_beta : 1.f;
   // forward weights in LDS for the unroll when they fit beside the per-wave buffers
   const int lds_w = WLDS ? (int)((lds_weight_floats<WT>(L, L.fwd_total) + 15) / 16 * 16) : 0;
   Wts<WT> P0;
@@ -314,7 +318,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
     float qv[A];
     bcast_agents<A>(myq, qv);
     float pre_h, pre2;
-    const float y = mixer_head<E, A>(P, L, OUT, qv, pre_h, pre2, na);
+    const float y = mixer_head<E, A>(P, L, OUT, qv, pre_h, pre2, na, pf, pb);
     const size_t bt = (size_t)b * n.T + t;
     if (lane == 0) n.y[bt] = y;
     if (n.qv && lane < na) n.qv[bt * na + lane] = myq;
@@ -470,9 +474,15 @@ struct MixBwdDims {
   // dW staging area (blocks), and the key-token grad block gX0 [KT*16][E].
   // With one query tile the grads are in registers before staging starts, so
   // the three uses can alias; otherwise the grads keep their own region.
-  static constexpr int GOUT = Dm::QT == 1 ? 0 : Dm::OUTF;
-  static constexpr int W0 = Dm::OUTF > STAGE ? Dm::OUTF : STAGE;
-  static constexpr int WORK = GOUT + (W0 > Dm::GX0F ? W0 : Dm::GX0F);
+  // row stride of the [row][feature] blocks: padded (Dm::LDO) with one query tile;
+  // the multi-tile kernels keep stride E — padded, the 64-AGV kernel's per-wave
+  // buffers no longer fit two waves per workgroup beside the weights
+  static constexpr int LDB = Dm::QT == 1 ? Dm::LDO : E;
+  static constexpr int OUTB = Dm::QT * 16 * LDB;
+  static constexpr int GX0B = KT * 16 * LDB;
+  static constexpr int GOUT = Dm::QT == 1 ? 0 : OUTB;
+  static constexpr int W0 = OUTB > STAGE ? OUTB : STAGE;
+  static constexpr int WORK = GOUT + (W0 > GX0B ? W0 : GX0B);
   static constexpr int PERW = Dm::X0F + WORK;
 };
 
@@ -483,18 +493,19 @@ struct MixBwdDims {
 // grads.  ghw: grads wrt the step's hyper outputs (carried + external).
 template <int E, int A, typename WT, int LDO = MixDims<E, A>::LDO>
 T2O_DEV void mixer_head_bwd(const Wts<WT>& P, const t2o_layout& L, const float* OUT, float* GOUT, float myq,
-                            float gyv, const float (&ghw)[3], float* gqv, float& gWo, float& gbo, int na) {
+                            float gyv, const float (&ghw)[3], float* gqv, float& gWo, float& gbo, int na, int pf,
+                            float pb) {
   const int lane = threadIdx.x & 63;
   const int f = lane < E ? lane : 0;
   const bool fv = lane < E;
   float qv[A];
   bcast_agents<A>(myq, qv);
   float pre_h, pre2;
-  (void)mixer_head<E, A, WT, LDO>(P, L, OUT, qv, pre_h, pre2, na);
+  (void)mixer_head<E, A, WT, LDO>(P, L, OUT, qv, pre_h, pre2, na, pf, pb);
   const float hidden = elu1(pre_h);
   const float xw2 = OUT[(na + 1) * LDO + f];
-  const float sgn_w2 = (xw2 > 0.f) - (xw2 < 0.f);
-  const float gpre = gyv * fabsf(xw2) * (pre_h > 0.f ? 1.f : expf(pre_h));
+  const float sgn_w2 = dposf(xw2, pf, pb);
+  const float gpre = gyv * posf(xw2, pf, pb) * (pre_h > 0.f ? 1.f : expf(pre_h));
   const float gpre2 = pre2 > 0.f ? gyv : 0.f;
   // gout[0, A): the agents' weight rows (entries >= na unused); gout[A + k]: hyper row na + k
   float gout[A + 3];
@@ -503,8 +514,8 @@ T2O_DEV void mixer_head_bwd(const Wts<WT>& P, const t2o_layout& L, const float* 
   for (int ag = 0; ag < A; ++ag) {
     if (ag < na) {
       const float xa = OUT[ag * LDO + f];
-      gout[ag] = qv[ag] * gpre * ((xa > 0.f) - (xa < 0.f));
-      const float gq = feat_sum<E>(fv ? gpre * fabsf(xa) : 0.f);
+      gout[ag] = qv[ag] * gpre * dposf(xa, pf, pb);
+      const float gq = feat_sum<E>(fv ? gpre * posf(xa, pf, pb) : 0.f);
       gqm = lane == ag ? gq : gqm;
     }
   }
@@ -601,7 +612,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
       for (int k = 0; k < MixBwdIn<E, A, D>::XO; ++k) {
         const int i = lane + 64 * k;
-        if (i < nq * E) OUT[(i / E) * Dm::LDO + i % E] = cur.xo[k];
+        if (i < nq * E) OUT[(i / E) * Bd::LDB + i % E] = cur.xo[k];
       }
       if constexpr (!LEAN) {
         if (t > 0) mixb_load<E, A, D>(args, n, b, t - 1, nxt, na);  // prefetch step t-1
@@ -611,8 +622,9 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
       for (int k = 0; k < 3; ++k) ghw[k] += cur.ghx[k];
       float* GOUT = Bd::GOUT ? GOUTB : stage;
-      mixer_head_bwd<E, A>(P, L, OUT, GOUT, cur.m.qs[0], cur.gy, ghw, args.gqv + bt * na + lane, gWo, gbo, na);
-      for (int i = nq * Dm::LDO + lane; i < Dm::OUTF; i += 64) GOUT[i] = 0.f;
+      mixer_head_bwd<E, A, WT, Bd::LDB>(P, L, OUT, GOUT, cur.m.qs[0], cur.gy, ghw, args.gqv + bt * na + lane, gWo, gbo, na,
+                           RT ? L.pos_func : T2O_POS_ABS, RT ? L.pos_beta : 1.f);
+      for (int i = nq * Bd::LDB + lane; i < Bd::OUTB; i += 64) GOUT[i] = 0.f;
       __builtin_amdgcn_wave_barrier();
       // ---- blocks backward per query tile; gX0 accumulates in registers
       KeyFrags<E, KT, sizeof(WT) == 2> K;
@@ -632,7 +644,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
           const int q = 16 * qt + c;
           f4 gx[ET];
 #pragma unroll
-          for (int ft = 0; ft < ET; ++ft) gx[ft] = ld4(GOUT + (16 * qt + c) * Dm::LDO + 16 * ft + 4 * g);
+          for (int ft = 0; ft < ET; ++ft) gx[ft] = ld4(GOUT + (16 * qt + c) * Bd::LDB + 16 * ft + 4 * g);
 #pragma unroll
           for (int d = D - 1; d >= 0; --d) {
             f4 x[ET];
@@ -659,12 +671,12 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
           __builtin_amdgcn_wave_barrier();
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft)
-            st4(GOUT + (16 * qt + c) * Dm::LDO + 16 * ft + 4 * g, q < nq ? gx[ft] : zero4());
+            st4(GOUT + (16 * qt + c) * Bd::LDB + 16 * ft + 4 * g, q < nq ? gx[ft] : zero4());
         }
       } else {
       static_assert(LEAN || Dm::QT == 1, "the unrolled path runs one query tile");
 #pragma unroll
-      for (int ft = 0; ft < ET; ++ft) gq0[0][ft] = ld4(GOUT + c * Dm::LDO + 16 * ft + 4 * g);
+      for (int ft = 0; ft < ET; ++ft) gq0[0][ft] = ld4(GOUT + c * Bd::LDB + 16 * ft + 4 * g);
       __builtin_amdgcn_wave_barrier();
       {
         const int q = c;
@@ -730,7 +742,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) GX0[(16 * kt + 4 * g + r) * Dm::LDO + 16 * ft + c] = gX0[kt][ft][r];
+          for (int r = 0; r < 4; ++r) GX0[(16 * kt + 4 * g + r) * Bd::LDB + 16 * ft + c] = gX0[kt][ft][r];
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int qt = 0; qt < Dm::QT; ++qt) {
@@ -738,8 +750,8 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
         if (q < nq) {
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft) {
-            float* dst = GX0 + (na + q) * Dm::LDO + 16 * ft + 4 * g;
-            const f4 gq = LEAN ? ld4(GOUT + q * Dm::LDO + 16 * ft + 4 * g) : gq0[0][ft];
+            float* dst = GX0 + (na + q) * Bd::LDB + 16 * ft + 4 * g;
+            const f4 gq = LEAN ? ld4(GOUT + q * Bd::LDB + 16 * ft + 4 * g) : gq0[0][ft];
             st4(dst, ld4(dst) + gq);
           }
         }
@@ -747,9 +759,9 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
       __builtin_amdgcn_wave_barrier();
       // ---- key-token grads: agent hidden tokens out, hyper tokens carried
       for (int i = lane; i < na * E / 4; i += 64)
-        st4(args.ghid + bt * na * E + 4 * i, ld4(GX0 + (na + 4 * i / E) * Dm::LDO + (4 * i) % E));
+        st4(args.ghid + bt * na * E + 4 * i, ld4(GX0 + (na + 4 * i / E) * Bd::LDB + (4 * i) % E));
 #pragma unroll
-      for (int k = 0; k < 3; ++k) ghw[k] = fv ? GX0[(2 * na + k) * Dm::LDO + f] : 0.f;
+      for (int k = 0; k < 3; ++k) ghw[k] = fv ? GX0[(2 * na + k) * Bd::LDB + f] : 0.f;
       __builtin_amdgcn_wave_barrier();
       if constexpr (!LEAN) cur = nxt;
     }
@@ -907,8 +919,8 @@ T2O_DEV void mixp_load_stT(const MixerFwdArgs& fa, int b, int t, f4 (&stT)[MixDi
 // block-1 wave: key block + block-1 recompute, then head + block-1 backward
 template <int E, int H, int A, int FF, typename WT>
 T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_layout& L, const t2o_layout& Lb,
-                         const t2o_layout& Gb, float* __restrict__ gs, float* X0, float* R, int b, PairBarrier& pb,
-                         int na) {
+                         const t2o_layout& Gb, float* __restrict__ gs, float* X0, float* R, int b, PairBarrier& pbar,
+                         int na, int pf, float pb) {
   using Dm = MixDims<E, A>;
   using Pd = MixPipeDims<E, A>;
   using In = MixPIn<E, A>;
@@ -954,7 +966,7 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
       for (int ft = 0; ft < ET; ++ft) x[ft] = cur.xm[ft];
       mixer_block_fwd_lean<E, H, KT, FF>(P, Lb, 0, K, lk, x, cache, rec);
     }
-    pb.sync();
+    pbar.sync();
     {  // ---- backward: mixing head, block 1
       const Wts<WT> P = step_view(P0);
       float ghw[3];
@@ -970,7 +982,8 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int k = 0; k < 3; ++k) ghw[k] += cur.ghx[k];
-      mixer_head_bwd<E, A, WT, Pd::LDR>(P, L, OUT, OUT, cur.qv, cur.gy, ghw, args.gqv + bt * na + lane, gWo, gbo, na);
+      mixer_head_bwd<E, A, WT, Pd::LDR>(P, L, OUT, OUT, cur.qv, cur.gy, ghw, args.gqv + bt * na + lane, gWo, gbo, na,
+                                        pf, pb);
       __builtin_amdgcn_wave_barrier();
       f4 gx[ET];
 #pragma unroll
@@ -998,9 +1011,9 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
         for (int ft = 0; ft < ET; ++ft) st4(R + Pd::XCH + c * Pd::LDR + 16 * ft + 4 * g, gx[ft]);
       }
     }
-    pb.sync();
+    pbar.sync();
   }
-  pb.sync();  // the block-0 wave's last backward phase
+  pbar.sync();  // the block-0 wave's last backward phase
   flush_in_wave_order([&] {
     vec_accumulate_g<ET>(gs + Gb.g2[0], &ln2[0]);
     vec_accumulate_g<ET>(gs + Gb.n2[0], &ln2[ET]);
@@ -1175,7 +1188,9 @@ __global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) 
 #define T2O_MIXP_PRIO_BLOCK 1
 #endif
   if (T2O_MIXP_PRIO_BLOCK >= 0 && d == T2O_MIXP_PRIO_BLOCK) __builtin_amdgcn_s_setprio(1);
-  if (d == 1) mixp_block1<E, H, A, FF, WT>(args, P0, L, Lb, Gb, gs, X0, R, b, pb, na);
+  if (d == 1)
+    mixp_block1<E, H, A, FF, WT>(args, P0, L, Lb, Gb, gs, X0, R, b, pb, na, RT ? L.pos_func : T2O_POS_ABS,
+                                 RT ? L.pos_beta : 1.f);
   else mixp_block0<E, H, A, FF, WT>(args, P0, Lb, Gb, gs, X0, R, b, pb, na);
 }
 
@@ -1292,7 +1307,7 @@ extern "C" int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, c
     nnet = 2;
   }
   int rc = T2O_EUNSUPPORTED;
-  T2O_DISPATCH_MIXER(L->E, L->H, L->D, L->n_ent, L->FF,
+  T2O_DISPATCH_MIXER(L->E, L->H, L->D, L->n_ent, L->FF, L->pos_func == T2O_POS_ABS,
                      rc = (L->prec ? launch_mixer_fwd<E_, H_, D_, NE_, FF_, RT_, __bf16>(a, nnet, (hipStream_t)stream)
                                    : launch_mixer_fwd<E_, H_, D_, NE_, FF_, RT_, float>(a, nnet, (hipStream_t)stream)));
   return rc;
@@ -1334,7 +1349,7 @@ extern "C" int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, cons
   a.slabs = gslabs;
   a.tape = tape;
   int rc = T2O_EUNSUPPORTED;
-  T2O_DISPATCH_MIXER(L->E, L->H, L->D, L->n_ent, L->FF,
+  T2O_DISPATCH_MIXER(L->E, L->H, L->D, L->n_ent, L->FF, L->pos_func == T2O_POS_ABS,
                      rc = (L->prec ? launch_mixer_bwd<E_, H_, D_, NE_, FF_, RT_, __bf16>(a, max_slabs, nslab, (hipStream_t)stream)
                                    : launch_mixer_bwd<E_, H_, D_, NE_, FF_, RT_, float>(a, max_slabs, nslab, (hipStream_t)stream)));
   return rc;

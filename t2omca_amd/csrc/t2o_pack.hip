@@ -223,7 +223,8 @@ struct Builder {
 extern "C" int t2o_layout_instance(const t2o_layout* L) {
   if (!L) return T2O_EINVAL;
   if (L->generic) return T2O_INSTANCE_GENERIC;
-  return t2o_exact_shape(L->E, L->H, L->D, L->n_ent, L->FF) ? T2O_INSTANCE_EXACT : T2O_INSTANCE_RUNTIME;
+  const bool abs_head = L->kind == 0 || L->pos_func == T2O_POS_ABS;  // (exact mixer instances: abs head only)
+  return abs_head && t2o_exact_shape(L->E, L->H, L->D, L->n_ent, L->FF) ? T2O_INSTANCE_EXACT : T2O_INSTANCE_RUNTIME;
 }
 
 extern "C" int t2o_layout_init(t2o_layout* L, int kind, int E, int H, int D, int F, int NA, int FF, int n_ent,
@@ -249,11 +250,12 @@ extern "C" int t2o_layout_init_ex(t2o_layout* L, int kind, int E, int H, int D, 
   for (int d = 0; d < T2O_MAX_DEPTH; ++d)
     L->M[d] = L->MT[d] = L->N[d] = L->NT[d] = L->bu[d] = L->g1[d] = L->n1[d] = L->W1[d] = L->W1T[d] = L->c1[d] =
         L->W2[d] = L->W2T[d] = L->c2[d] = L->g2[d] = L->n2[d] = -1;
-  // the tuned mixer head computes pos_func abs only (the reference default): a
-  // runtime switch there measured slower and, at 64 agents, fell over a compiler
-  // limit; the other functions run the generic kernels
+  // the exact mixer instances compute pos_func abs only (the reference default);
+  // the runtime-entity instances take it as a parameter, so the default network
+  // runs every qmix_pos_func on MFMA kernels (t2o_dispatch.hpp), other networks
+  // with a non-abs head run the generic kernels
   if ((flags & T2O_LAYOUT_FORCE_GENERIC) || n_agents != n_ent || !t2o_tuned_shape(E, H, D, n_ent, FF) ||
-      (kind == 1 && pos_func != T2O_POS_ABS)) {
+      (kind == 1 && pos_func != T2O_POS_ABS && !t2o_default_net(E, H, D, FF))) {
     // runtime-shaped kernels (t2o_generic.hip): pack = reference-order params +
     // transposed copies; compact grads = reference order
     const bool ok = E <= 64 && H <= 8 && H * E <= 512 && FF <= 512 &&

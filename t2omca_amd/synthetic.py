@@ -26,12 +26,13 @@ def make_batch(B, T, A, n_actions=5, obs_feats=9, state_feats=8, seed=1, device=
     return batch, weights
 
 
-def make_args(A, *, emb=32, heads=3, depth=2, n_actions=5, device="cuda"):
+def make_args(A, *, emb=32, heads=3, depth=2, n_actions=5, device="cuda", qmix_pos_func="abs", qmix_pos_func_beta=1.0):
     """SimpleNamespace with every field the agent/mixer constructors read
     (transf_agent.py:9-48, n_transf_mixer.py:13-53)."""
     import types
     return types.SimpleNamespace(
         n_agents=A, n_entities=A, obs_entity_feats=9, state_entity_feats=8, emb=emb, heads=heads,
         depth=depth, mixer_emb=emb, mixer_heads=heads, mixer_depth=depth, ff_hidden_mult=4, dropout=0.0,
-        action_selector="epsilon_greedy", n_actions=n_actions, device=device, qmix_pos_func="abs",
+        action_selector="epsilon_greedy", n_actions=n_actions, device=device, qmix_pos_func=qmix_pos_func,
+        qmix_pos_func_beta=qmix_pos_func_beta,
         env_args={"state_entity_mode": True})

@@ -11,6 +11,9 @@ instance is compiled for a capacity class and reads the real count at run time:
           padding keys -inf).
 
 The cases below put every class on both sides of its boundaries (A = 2 ... 63).
+The runtime mixer instances also compute every qmix_pos_func (softplus with beta,
+quadratic, identity; n_transf_mixer.py:95-103) — the exact ones are abs-only — so
+those heads run on MFMA kernels at every AGV count, including the exact ones.
 Checked against the reference modules' goldens (5 and 32 AGVs, per-step forward +
 autograd through the drop-in modules) and against the fp64 oracle's full TD update
 (oracle/ref_learner; TD semantics parity-unpinned).
@@ -67,3 +70,23 @@ def test_runtime_instance_modules_vs_reference_goldens(name):
     require_gpu()
     assert agent_module_check(os.path.join(GOLD, f"agent_{name}.npz")) == "runtime"
     assert mixer_module_check(os.path.join(GOLD, f"mixer_{name}.npz")) == "runtime"
+
+
+@pytest.mark.parametrize("name", ["a8_softplus", "a8_quadratic", "a8_identity"])
+def test_runtime_mixer_heads_vs_reference_goldens(name):
+    """Every non-abs qmix_pos_func on the runtime mixer instance, against the
+    reference module's own outputs and autograd (n_transf_mixer.py:95-103)."""
+    require_gpu()
+    assert mixer_module_check(os.path.join(GOLD, f"mixer_{name}.npz")) == "runtime"
+
+
+@pytest.mark.parametrize("A,B,T,head,beta,precision", [(8, 4, 6, "softplus", 0.5, "fp32"),
+                                                       (12, 3, 5, "quadratic", 1.0, "fp32"),
+                                                       (5, 4, 6, "identity", 1.0, "fp32"),
+                                                       (8, 4, 6, "softplus", 2.0, "bf16")])
+def test_runtime_mixer_heads_td_update(A, B, T, head, beta, precision):
+    require_gpu()
+    cfg = dict(_cfg_of(A, qmix_pos_func=head, qmix_pos_func_beta=beta), tag=f"A{A}-{head}")
+    tol = (2e-2, 6e-2) if precision == "bf16" else None
+    learner, _ = _td(cfg, B, T, precision=precision, tol=tol, avoid_relu_ties=precision == "fp32")
+    assert learner.sm.instance == "runtime"
