@@ -150,6 +150,7 @@ void agent_fwd_kernel(AgentFwdArgs args) {
 
 template <int E, int H, int D, int NE, int FF, bool RT, typename WT>
 int launch_fwd(const AgentFwdArgs& args, int nnet, hipStream_t stream) {
+  if (!kernel_layout_matches<E, H, D, FF, WT>(args.L)) return T2O_EINVAL;  // (kernels use the compile-time offsets)
   const int R = args.B * args.A;
   AgentFwdArgs a = args;
   a.rpw = rows_per_wave(R);
@@ -682,6 +683,7 @@ int bwd_tape_format(const t2o_layout& L, bool has_hmid) {
 
 template <int E, int H, int D, int NE, int FF, bool RT, typename WT>
 int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
+  if (!kernel_layout_matches<E, H, D, FF, WT>(args.L)) return T2O_EINVAL;  // (kernels use the compile-time offsets)
   const int R = args.B * args.A;
   args.rpw = rows_per_wave(R);
   const int tiles = (R + args.rpw - 1) / args.rpw;

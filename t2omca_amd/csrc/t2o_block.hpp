@@ -202,22 +202,30 @@ T2O_DEV void post_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restr
 // Layout whose block-0 slots hold block d's offsets: the block code is then
 // called with the constant d = 0, and every offset it reads is a scalar.
 T2O_DEV t2o_layout block_view(const t2o_layout& L, int d) {
+  // (selects between the constant-indexed fields, not a run-time index: a local
+  // layout indexed at run time would be spilled whole to scratch to be addressed)
+  const auto pick = [d](const int64_t (&f)[T2O_MAX_DEPTH]) {
+    int64_t v = f[0];
+#pragma unroll
+    for (int k = 1; k < T2O_MAX_DEPTH; ++k) v = d == k ? f[k] : v;
+    return v;
+  };
   t2o_layout V = L;
-  V.M[0] = L.M[d];
-  V.MT[0] = L.MT[d];
-  V.N[0] = L.N[d];
-  V.NT[0] = L.NT[d];
-  V.bu[0] = L.bu[d];
-  V.g1[0] = L.g1[d];
-  V.n1[0] = L.n1[d];
-  V.W1[0] = L.W1[d];
-  V.W1T[0] = L.W1T[d];
-  V.c1[0] = L.c1[d];
-  V.W2[0] = L.W2[d];
-  V.W2T[0] = L.W2T[d];
-  V.c2[0] = L.c2[d];
-  V.g2[0] = L.g2[d];
-  V.n2[0] = L.n2[d];
+  V.M[0] = pick(L.M);
+  V.MT[0] = pick(L.MT);
+  V.N[0] = pick(L.N);
+  V.NT[0] = pick(L.NT);
+  V.bu[0] = pick(L.bu);
+  V.g1[0] = pick(L.g1);
+  V.n1[0] = pick(L.n1);
+  V.W1[0] = pick(L.W1);
+  V.W1T[0] = pick(L.W1T);
+  V.c1[0] = pick(L.c1);
+  V.W2[0] = pick(L.W2);
+  V.W2T[0] = pick(L.W2T);
+  V.c2[0] = pick(L.c2);
+  V.g2[0] = pick(L.g2);
+  V.n2[0] = pick(L.n2);
   return V;
 }
 

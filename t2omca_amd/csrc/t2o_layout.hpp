@@ -115,7 +115,7 @@ inline int tape_tile_records(const t2o_layout&) { return 16; }
 
 // Compact gradient layout (what the backward kernels accumulate in LDS and
 // write per workgroup): the pack layout without transposed copies.
-inline void grad_layout(const t2o_layout& L, t2o_layout& G) {
+__host__ __device__ constexpr void grad_layout(const t2o_layout& L, t2o_layout& G) {
   G = L;
   int64_t o = 0;
   const int64_t E = L.E, HE = (int64_t)L.H * L.E, FF = L.FF;
@@ -140,6 +140,102 @@ inline void grad_layout(const t2o_layout& L, t2o_layout& G) {
     G.n2[d] = o; o += E;
   }
   G.total = G.grad_total = G.fwd_total = o;
+}
+
+// Offsets of the folded MFMA pack of a tuned network — forward matrices, then
+// forward vectors (one contiguous LDS copy; in bf16 mode the vectors stay fp32),
+// then the backward's transposed copies; every size a multiple of 16 elements, so
+// every section stays 64-B aligned.  They depend on (E, H, D, FF, prec) only.
+// ONE definition: t2o_layout_init_ex fills a caller's layout with it, and the
+// tuned kernels instantiate it as a compile-time constant (kernel_layout), so
+// every offset is an immediate there instead of a 64-bit kernel argument held in
+// SGPRs (the BPTT kernels spilled 70-170 SGPRs to VGPR lanes holding them).
+__host__ __device__ constexpr void tuned_pack_offsets(t2o_layout& L, int E, int H, int D, int FF, int prec) {
+  int64_t o = 0;
+  const int64_t HE = (int64_t)H * E;
+  L.WeT = o; o += 16 * (int64_t)E;
+  L.We = o; o += (int64_t)E * 16;
+  L.Wo = o; o += 16 * (int64_t)E;
+  for (int d = 0; d < D; ++d) {
+    L.M[d] = o; o += HE * E;
+    L.N[d] = o; o += E * HE;
+    L.W1[d] = o; o += (int64_t)FF * E;
+    L.W2[d] = o; o += (int64_t)E * FF;
+  }
+  L.vec_lo = o;
+  L.be = o; o += E;
+  L.bo = o; o += 16;
+  for (int d = 0; d < D; ++d) {
+    L.bu[d] = o; o += E;
+    L.g1[d] = o; o += E;
+    L.n1[d] = o; o += E;
+    L.c1[d] = o; o += FF;
+    L.c2[d] = o; o += E;
+    L.g2[d] = o; o += E;
+    L.n2[d] = o; o += E;
+  }
+  L.fwd_total = o;
+  L.WoT = o; o += (int64_t)E * 16;
+  for (int d = 0; d < D; ++d) {
+    L.MT[d] = o; o += E * HE;
+    L.NT[d] = o; o += HE * E;
+    L.W1T[d] = o; o += (int64_t)E * FF;
+    L.W2T[d] = o; o += (int64_t)FF * E;
+  }
+  L.total = o;
+  L.pack_floats = prec ? o + ((o + 1) / 2 + 3) / 4 * 4 : o;
+  t2o_layout G{};
+  grad_layout(L, G);
+  L.grad_total = G.grad_total;
+}
+
+template <int E, int H, int D, int FF, int PREC>
+__host__ __device__ constexpr t2o_layout tuned_layout_const() {
+  t2o_layout L{};
+  L.E = E; L.H = H; L.D = D; L.FF = FF; L.prec = PREC;
+  for (int d = 0; d < T2O_MAX_DEPTH; ++d)
+    L.M[d] = L.MT[d] = L.N[d] = L.NT[d] = L.bu[d] = L.g1[d] = L.n1[d] = L.W1[d] = L.W1T[d] = L.c1[d] =
+        L.W2[d] = L.W2T[d] = L.c2[d] = L.g2[d] = L.n2[d] = -1;
+  tuned_pack_offsets(L, E, H, D, FF, PREC);
+  return L;
+}
+
+// A tuned kernel's layout: the compile-time pack offsets of its instance with
+// the caller's run-time scalars (kind, feature / action / entity counts, mixer
+// head).  The launchers check the caller's offsets equal the constant ones
+// (kernel_layout_matches), so the two can never disagree silently.
+template <int E, int H, int D, int FF, typename WT>
+__host__ __device__ inline t2o_layout kernel_layout(const t2o_layout& rt) {
+  constexpr t2o_layout C = tuned_layout_const<E, H, D, FF, sizeof(WT) == 2>();
+  t2o_layout L = C;
+  L.kind = rt.kind; L.F = rt.F; L.NA = rt.NA; L.n_ent = rt.n_ent; L.n_agents = rt.n_agents;
+  L.pos_func = rt.pos_func; L.pos_beta = rt.pos_beta;
+  return L;
+}
+template <int E, int H, int D, int FF, int PREC>
+__host__ __device__ constexpr t2o_layout tuned_grad_layout_const() {
+  const t2o_layout C = tuned_layout_const<E, H, D, FF, PREC>();
+  t2o_layout G{};
+  grad_layout(C, G);
+  return G;
+}
+template <int E, int H, int D, int FF, typename WT>
+__host__ __device__ inline t2o_layout kernel_grad_layout() {
+  constexpr t2o_layout G = tuned_grad_layout_const<E, H, D, FF, sizeof(WT) == 2>();
+  return G;
+}
+template <int E, int H, int D, int FF, typename WT>
+inline bool kernel_layout_matches(const t2o_layout& rt) {
+  constexpr t2o_layout C = tuned_layout_const<E, H, D, FF, sizeof(WT) == 2>();
+  bool ok = rt.WeT == C.WeT && rt.We == C.We && rt.be == C.be && rt.Wo == C.Wo && rt.bo == C.bo &&
+            rt.WoT == C.WoT && rt.fwd_total == C.fwd_total && rt.total == C.total &&
+            rt.grad_total == C.grad_total && rt.vec_lo == C.vec_lo && rt.pack_floats == C.pack_floats && !rt.generic;
+  for (int d = 0; d < D; ++d)
+    ok = ok && rt.M[d] == C.M[d] && rt.MT[d] == C.MT[d] && rt.N[d] == C.N[d] && rt.NT[d] == C.NT[d] &&
+         rt.bu[d] == C.bu[d] && rt.g1[d] == C.g1[d] && rt.n1[d] == C.n1[d] && rt.W1[d] == C.W1[d] &&
+         rt.W1T[d] == C.W1T[d] && rt.c1[d] == C.c1[d] && rt.W2[d] == C.W2[d] && rt.W2T[d] == C.W2T[d] &&
+         rt.c2[d] == C.c2[d] && rt.g2[d] == C.g2[d] && rt.n2[d] == C.n2[d];
+  return ok;
 }
 
 }  // namespace t2o

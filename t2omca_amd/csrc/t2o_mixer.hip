@@ -346,6 +346,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
 
 template <int E, int H, int D, int A, int FF, bool RT, typename WT>
 int launch_mixer_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
+  if (!kernel_layout_matches<E, H, D, FF, WT>(args.L)) return T2O_EINVAL;  // (kernels use the compile-time offsets)
   using Dm = MixDims<E, A>;
   MixerFwdArgs a = args;
   const size_t wfl = (lds_weight_floats<WT>(args.L, args.L.fwd_total) + 15) / 16 * 16, perw = Dm::FWD_PERW;
@@ -918,9 +919,10 @@ T2O_DEV void mixp_load_stT(const MixerFwdArgs& fa, int b, int t, f4 (&stT)[MixDi
 
 // block-1 wave: key block + block-1 recompute, then head + block-1 backward
 template <int E, int H, int A, int FF, typename WT>
-T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_layout& L, const t2o_layout& Lb,
-                         const t2o_layout& Gb, float* __restrict__ gs, float* X0, float* R, int b, PairBarrier& pbar,
-                         int na, int pf, float pb) {
+T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_layout& L, const t2o_layout& G,
+                         float* __restrict__ gs, float* X0, float* R, int b, PairBarrier& pbar, int na, int pf,
+                         float pb) {
+  const t2o_layout Lb = block_view(L, 1), Gb = block_view(G, 1);  // (constant block: immediate offsets)
   using Dm = MixDims<E, A>;
   using Pd = MixPipeDims<E, A>;
   using In = MixPIn<E, A>;
@@ -1024,8 +1026,9 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
 
 // block-0 wave: block-0 recompute, then block-0 backward and the step's key grads
 template <int E, int H, int A, int FF, typename WT>
-T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_layout& Lb, const t2o_layout& Gb,
+T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_layout& L, const t2o_layout& G,
                          float* __restrict__ gs, const float* X0, float* R, int b, PairBarrier& pb, int na) {
+  const t2o_layout Lb = block_view(L, 0), Gb = block_view(G, 0);
   using Dm = MixDims<E, A>;
   using Pd = MixPipeDims<E, A>;
   using Rec = TapeRec<E, H, FF>;
@@ -1138,12 +1141,10 @@ inline __host__ __device__ int64_t mixp_weight_elems(const t2o_layout& L) {
 }
 
 template <int E, int H, int D, int A, int FF, bool RT, typename WT>
-__global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) {
+T2O_DEV void mixer_bwd_pipe_body(const MixerBwdArgs& args, const t2o_layout& L, const t2o_layout& G) {
   static_assert(D == 2 && MixPipeDims<E, A>::OK, "one wave per block of a depth-2 stack, one query tile");
   using Dm = MixDims<E, A>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const t2o_layout& L = args.f.L;
-  const t2o_layout& G = args.G;
   const int na = RT ? args.f.na : A;
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
   // the block this wave owns.  Waves w and w + 4 share a SIMD: with four pairs,
@@ -1178,7 +1179,6 @@ __global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) 
   __syncthreads();
   PairBarrier pb = PairBarrier::make(flags, w);  // partner: the pair's other wave
   const int b = blockIdx.x * args.waves + pr;  // the launcher makes every pair valid
-  const t2o_layout Lb = block_view(L, d), Gb = block_view(G, d);
   // the block-1 wave issues first on its SIMD.  With pair barriers (each pair
   // waits only for itself) that is the head + bwd1 end of the dependent chain:
   // A/B, overlapped, 3 rounds: block 1 mixer_bwd 0.596 ms / update 2.556 ms,
@@ -1189,13 +1189,30 @@ __global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) 
 #endif
   if (T2O_MIXP_PRIO_BLOCK >= 0 && d == T2O_MIXP_PRIO_BLOCK) __builtin_amdgcn_s_setprio(1);
   if (d == 1)
-    mixp_block1<E, H, A, FF, WT>(args, P0, L, Lb, Gb, gs, X0, R, b, pb, na, RT ? L.pos_func : T2O_POS_ABS,
+    mixp_block1<E, H, A, FF, WT>(args, P0, L, G, gs, X0, R, b, pb, na, RT ? L.pos_func : T2O_POS_ABS,
                                  RT ? L.pos_beta : 1.f);
-  else mixp_block0<E, H, A, FF, WT>(args, P0, Lb, Gb, gs, X0, R, b, pb, na);
+  else mixp_block0<E, H, A, FF, WT>(args, P0, L, G, gs, X0, R, b, pb, na);
+}
+
+// bf16: the pack / gradient offsets as compile-time constants (t2o_layout.hpp
+// kernel_layout): SGPR spills (to VGPR lanes, a v_readlane per reload in the
+// step loop) 169 -> 113, mixer_bwd 0.598 -> 0.582 ms, update 2.490 -> 2.483 ms
+// (interleaved A/B, overlapped, 3 rounds, profiles/r3_ab5/).  fp32 keeps the
+// kernel-argument layout: with constants its VGPR spills rose 5 -> 88 and the
+// kernel 1.74 -> 2.14 ms (profiles/r3_ab4f/); the other kernels measured no
+// gain with them (agent_fwd +2 %, profiles/r3_ab4/).
+template <int E, int H, int D, int A, int FF, bool RT, typename WT>
+__global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) {
+  if constexpr (sizeof(WT) == 2)
+    mixer_bwd_pipe_body<E, H, D, A, FF, RT, WT>(args, kernel_layout<E, H, D, FF, WT>(args.f.L),
+                                                kernel_grad_layout<E, H, D, FF, WT>());
+  else
+    mixer_bwd_pipe_body<E, H, D, A, FF, RT, WT>(args, args.f.L, args.G);
 }
 
 template <int E, int H, int D, int A, int FF, bool RT, typename WT>
 int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
+  if (!kernel_layout_matches<E, H, D, FF, WT>(args.f.L)) return T2O_EINVAL;  // (compile-time offsets)
   constexpr int PERW = MixBwdDims<E, A>::PERW;
   const t2o_layout& L = args.f.L;
   args.lds_w = (int)((lds_weight_floats<WT>(L, L.fwd_total) + 15) / 16 * 16);

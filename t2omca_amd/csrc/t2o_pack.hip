@@ -269,45 +269,7 @@ extern "C" int t2o_layout_init_ex(t2o_layout* L, int kind, int E, int H, int D, 
     L->grad_total = g.P.total;
     return 0;
   }
-  int64_t o = 0;
-  const int64_t HE = (int64_t)H * E;
-  // forward matrices, then forward vectors (one contiguous LDS copy; in bf16
-  // mode the vectors stay fp32), then the backward's transposed copies.  Every
-  // size is a multiple of 16 elements, so every section stays 64-B aligned.
-  L->WeT = o; o += 16 * (int64_t)E;
-  L->We = o; o += (int64_t)E * 16;
-  L->Wo = o; o += 16 * (int64_t)E;
-  for (int d = 0; d < D; ++d) {
-    L->M[d] = o; o += HE * E;
-    L->N[d] = o; o += E * HE;
-    L->W1[d] = o; o += (int64_t)FF * E;
-    L->W2[d] = o; o += (int64_t)E * FF;
-  }
-  L->vec_lo = o;
-  L->be = o; o += E;
-  L->bo = o; o += 16;
-  for (int d = 0; d < D; ++d) {
-    L->bu[d] = o; o += E;
-    L->g1[d] = o; o += E;
-    L->n1[d] = o; o += E;
-    L->c1[d] = o; o += FF;
-    L->c2[d] = o; o += E;
-    L->g2[d] = o; o += E;
-    L->n2[d] = o; o += E;
-  }
-  L->fwd_total = o;
-  L->WoT = o; o += (int64_t)E * 16;
-  for (int d = 0; d < D; ++d) {
-    L->MT[d] = o; o += E * HE;
-    L->NT[d] = o; o += HE * E;
-    L->W1T[d] = o; o += (int64_t)E * FF;
-    L->W2T[d] = o; o += (int64_t)FF * E;
-  }
-  L->total = o;
-  L->pack_floats = prec ? o + ((o + 1) / 2 + 3) / 4 * 4 : o;
-  t2o_layout G;
-  grad_layout(*L, G);
-  L->grad_total = G.grad_total;
+  tuned_pack_offsets(*L, E, H, D, FF, prec);  // (t2o_layout.hpp: also the kernels' compile-time copy)
   return 0;
 }
 
