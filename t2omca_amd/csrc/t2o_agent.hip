@@ -401,7 +401,7 @@ constexpr int agp_stage_floats() {
 }
 
 template <int E, int H, int D, int NE, int FF, bool RT, typename WT>
-__global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(AgentBwdArgs args) {
+T2O_DEV void agent_bwd_pipe_body(const AgentBwdArgs& args, const t2o_layout& L, const t2o_layout& G) {
   static_assert(D == 2, "one wave per block of a depth-2 stack");
   constexpr int ET = E / 16, HET = H * ET;
   constexpr bool BF = sizeof(WT) == 2;
@@ -415,8 +415,6 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
   // written by the recompute phase) unless the entities are streamed in chunks
   using Cache = typename std::conditional<CHUNK, AgentCacheCh<E, H, NE, FF>, AgentCacheLean<E, H, NE, FF>>::type;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const t2o_layout& L = args.L;
-  const t2o_layout& G = args.G;
   const int64_t nw = L.fwd_total;
   const int lds_w = (int)((lds_weight_floats<WT>(L, nw) + 15) / 16 * 16);
   // wave-uniform by construction; readfirstlane tells the compiler, so the block's
@@ -658,6 +656,22 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
       }
     }
   });
+}
+
+// The kernel-argument layout.  Compile-time pack offsets (t2o_layout.hpp
+// kernel_layout, as the bf16 mixer BPTT reads them) cut this kernel's SGPR spills
+// 71 -> 62 but cost 9 more AGPRs and 5 spilled VGPRs: agent_bwd 0.623 -> 0.643 ms
+// (interleaved A/B, profiles/r3_ab6/).  -DT2O_AGP_CONST_LAYOUT=1 builds that variant.
+#ifndef T2O_AGP_CONST_LAYOUT
+#define T2O_AGP_CONST_LAYOUT 0
+#endif
+template <int E, int H, int D, int NE, int FF, bool RT, typename WT>
+__global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(AgentBwdArgs args) {
+  if constexpr (sizeof(WT) == 2 && T2O_AGP_CONST_LAYOUT)
+    agent_bwd_pipe_body<E, H, D, NE, FF, RT, WT>(args, kernel_layout<E, H, D, FF, WT>(args.L),
+                                                 kernel_grad_layout<E, H, D, FF, WT>());
+  else
+    agent_bwd_pipe_body<E, H, D, NE, FF, RT, WT>(args, args.L, args.G);
 }
 
 template <int E, int H, int D, int NE, int FF, typename WT>
