@@ -54,10 +54,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=16, help="episodes in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--mode", choices=("train", "forward", "rollout", "expand"), default="train",
+    ap.add_argument("--mode", choices=("train", "forward", "rollout", "expand", "dropin"), default="train",
                     help="train: the TD update (the BASELINE metric); forward: online agent + mixer "
                          "unroll only (configs[1], inference over a replay batch); rollout: closed-loop "
-                         "env step + agent step + ε-greedy over --envs envs per GPU (configs[4])")
+                         "env step + agent step + ε-greedy over --envs envs per GPU (configs[4]); dropin: "
+                         "per-call cost of the drop-in modules' per-step forward")
     ap.add_argument("--envs", type=int, default=8192, help="rollout mode: envs per GPU")
     ap.add_argument("--compact-obs", action="store_true",
                     help="rollout mode: store obs in the compact wire format (SURVEY.md §8 f3)")
@@ -83,7 +84,7 @@ def parse():
                     help="print the tag that keys profiles/hbm_traffic.json for these args and exit")
     a = ap.parse_args()
     # per-mode defaults: each mode's BASELINE config (SURVEY.md §8 scenario mapping)
-    scen = a.mode in ("forward", "rollout")
+    scen = a.mode in ("forward", "rollout", "dropin")
     if a.agents is None:
         a.agents = 16 if scen else 8
     if a.T is None:
@@ -428,6 +429,66 @@ def expand_bench(args, world, rank, dev):
         dist.destroy_process_group()
 
 
+def dropin_bench(args, world, rank, dev):
+    """The drop-in modules called as the reference calls them: one
+    TransformerAgent.forward per env step for every env of the runner
+    (parallel_runner.py:121 -> transf_agent.py:54-76) and one
+    TransformerMixer.forward per step (n_transf_mixer.py:55-91), under no_grad.
+    Times the cached path (the pack is rebuilt only when the weights change,
+    modules._PackCache) against re-packing on every call (the round-2 behaviour:
+    concatenate + pack per call), and the bare kernel launch, at the runner's
+    small batch and at --envs."""
+    from t2omca_amd import ops
+    from t2omca_amd.modules import TransformerAgent, TransformerMixer
+    from t2omca_amd.synthetic import make_args
+    A, E = args.agents, 32
+    torch.manual_seed(0)
+    margs = make_args(A, device=str(dev))
+    agent, mixer = TransformerAgent(None, margs).to(dev), TransformerMixer(margs).to(dev)
+    calls = max(args.steps, 1) * 20
+
+    def per_call_ms(fn):
+        for _ in range(max(args.warmup, 1) * 5):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(calls):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / calls * 1e3
+
+    sizes = {}
+    for n in sorted({8, args.envs}):
+        g = torch.Generator(device=dev).manual_seed(n)
+        obs = torch.randn(n, A, 9 * A, device=dev, generator=g)
+        hid = torch.zeros(n, A, E, device=dev)
+        qv = torch.randn(n, 1, A, device=dev, generator=g)
+        st = torch.randn(n, 8 * A, device=dev, generator=g)
+        hw = torch.zeros(n, 3, E, device=dev)
+        res = {}
+        with torch.no_grad():
+            res["agent_cached_ms"] = per_call_ms(lambda: agent(obs, hid))
+            res["agent_repack_ms"] = per_call_ms(lambda: (agent._pack_cache.invalidate(), agent(obs, hid)))
+            _, _, pack = agent._pack_cache.get(agent, agent.shape)
+            o4, h0 = obs.view(n, 1, A, 9 * A), hid.reshape(n * A, E)
+            res["agent_kernel_only_ms"] = per_call_ms(lambda: ops.agent_unroll_fwd(agent.shape, pack, o4, h0_on=h0))
+            res["mixer_cached_ms"] = per_call_ms(lambda: mixer(qv, hid, hw, st, None))
+            res["mixer_repack_ms"] = per_call_ms(lambda: (mixer._pack_cache.invalidate(), mixer(qv, hid, hw, st, None)))
+        sizes[str(n)] = {k: round(v, 5) for k, v in res.items()}
+    big = sizes[str(args.envs)]
+    out = {"metric": "agent forward calls/sec through the drop-in module (one env step of every env)",
+           "value": 1e3 / big["agent_cached_ms"], "unit": "calls/s", "n_gpus": 1, "steps": calls,
+           "warmup": max(args.warmup, 1) * 5, "ms_per_step": big["agent_cached_ms"], "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "fp32", "data": "synthetic (N(0,1) obs, zero hidden)",
+           "config": {"workload": f"TransformerAgent.forward / TransformerMixer.forward per env step, {A} AGVs, "
+                                  f"batch = envs (8: a runner's parallel envs; {args.envs}: configs[4]'s envs)",
+                      "agents": A, "envs": sorted(int(k) for k in sizes)},
+           "per_call_ms": sizes,
+           "pack_rebuilds": {"agent": agent._pack_cache.rebuilds, "mixer": mixer._pack_cache.rebuilds}}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
 def free_port():
     import socket
     with socket.socket() as s:
@@ -501,6 +562,8 @@ def main():
         return rollout_bench(args, world, rank, dev)
     if args.mode == "expand":
         return expand_bench(args, world, rank, dev)
+    if args.mode == "dropin":
+        return dropin_bench(args, world, rank, dev)
     def make_learner(precision):
         torch.manual_seed(0)
         margs = make_args(A, device=str(dev), qmix_pos_func=args.qmix_pos_func)

@@ -204,16 +204,34 @@ __device__ void write_wire(const EnvArgs& a, int e, const EnvLds& L) {
 
 // get_obs (:184-186) = A sequential normaliser updates; writes outputs if out != 0.
 // The update count n is kept in a register by every lane (the caller loads and
-// stores it once), so no lane ever reads another lane's global store.
+// stores it once), so no lane ever reads another lane's global store.  Lane l owns
+// features l, l + 64, ... : their running (mean, S) live in registers over the A
+// updates and reach HBM once at the end, with the last std (the only one read
+// later); the IEEE operations and their order are the reference's.
+constexpr int OBS_SLOTS = (9 * MAXA + 63) / 64;
+
 __device__ void get_obs(const EnvArgs& a, int e, EnvLds& L, bool out, int64_t& n) {
   // normaliser rows keep their [9A] stride in both modes (state[14..16])
   const int A = a.A, n9 = 9 * A, no = obs_len(a.sp.obs_entity, A), lane = threadIdx.x & 63;
   double* mean = a.s.nrm_mean + (size_t)e * n9;
   double* S = a.s.nrm_S + (size_t)e * n9;
   double* sd = a.s.nrm_std + (size_t)e * n9;
+  double mr[OBS_SLOTS], sr[OBS_SLOTS], dr[OBS_SLOTS];
+#pragma unroll
+  for (int k = 0; k < OBS_SLOTS; ++k) {
+    const int p = lane + 64 * k;
+    mr[k] = sr[k] = dr[k] = 0.0;
+    if (p < no) {
+      mr[k] = mean[p];
+      sr[k] = S[p];
+    }
+  }
   for (int i = 0; i < A; ++i) {
     ++n;
-    for (int p = lane; p < no; p += 64) {
+#pragma unroll
+    for (int k = 0; k < OBS_SLOTS; ++k) {
+      const int p = lane + 64 * k;
+      if (p >= no) break;
       double x = 0.0;
       if (!a.sp.obs_entity) {
         x = p == 0 ? (double)L.ack[i] : L.inf[i][p - 1];  // [last_ack (raw -1/0/1), get_agent_inf]
@@ -228,23 +246,32 @@ __device__ void get_obs(const EnvArgs& a, int e, EnvLds& L, bool out, int64_t& n
       double m, s, d;
       if (n == 1) {
         m = x;
-        s = S[p];
+        s = sr[k];
         d = x;
       } else {
-        const double old = mean[p];
+        const double old = mr[k];
         m = old + (x - old) / (double)n;
-        s = S[p] + (x - old) * (x - m);
+        s = sr[k] + (x - old) * (x - m);
         d = sqrt(s / (double)n);
       }
-      mean[p] = m;
-      S[p] = s;
-      sd[p] = d;
+      mr[k] = m;
+      sr[k] = s;
+      dr[k] = d;
       if (out) {
         const double v = (x - m) / (d + 1e-8);
         const size_t o = ((size_t)e * A + i) * no + p;
         if (a.o.obs) a.o.obs[o] = (float)v;
         if (a.o.obs64) a.o.obs64[o] = v;
       }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < OBS_SLOTS; ++k) {
+    const int p = lane + 64 * k;
+    if (p < no && A > 0) {
+      mean[p] = mr[k];
+      S[p] = sr[k];
+      sd[p] = dr[k];
     }
   }
 }

@@ -80,6 +80,7 @@ class TDLearner:
         # data parallel: every replica starts from rank 0's parameters (ranks that
         # initialised with different seeds would otherwise drift apart silently)
         broadcast_state([self.params, self.target_params], self.pg)
+        self._params_written()
         self.adam_ws = torch.empty(int(ops.lib().t2o_adam_workspace_floats()), device=dev)
         self.grad_norm = torch.zeros(1, device=dev)
         self.lr, self.betas, self.eps, self.wd = lr, optim_betas, optim_eps, weight_decay
@@ -99,6 +100,16 @@ class TDLearner:
         self._slabs = {}
 
     # -- parameters --------------------------------------------------------
+    def _params_written(self):
+        """The Adam kernel and the replica broadcasts write the modules' parameters
+        through raw pointers, which autograd's version counters do not see: drop the
+        modules' cached kernel packs (modules._PackCache) so their next per-step
+        forward re-packs."""
+        for m in (self.agent, self.mixer):
+            cache = getattr(m, "_pack_cache", None)
+            if cache is not None:
+                cache.invalidate()
+
     def agent_params(self, target=False):
         src = self.target_params if target else self.params
         return src[:self.na]
@@ -206,6 +217,7 @@ class TDLearner:
             step = torch.tensor([float(self.step_count)], device=self.device)
             broadcast_state([self.params, self.target_params, self.exp_avg, self.exp_avg_sq, step], self.pg)
             self.step_count = int(step.item())
+        self._params_written()
         self._pack_targets()
 
     # -- the TD update -------------------------------------------------------
@@ -296,6 +308,7 @@ class TDLearner:
         ops.adam_step(self.params, self.grad[:-1], self.exp_avg, self.exp_avg_sq, self.step_count, lr=self.lr,
                       betas=self.betas, eps=self.eps, weight_decay=self.wd, max_grad_norm=self.clip,
                       workspace=self.adam_ws, grad_div=self.grad[-1:], grad_norm_out=self.grad_norm)
+        self._params_written()
         if (episode_num - self.last_target_update_episode) / self.target_update_interval >= 1.0:
             self.update_targets()
             self.last_target_update_episode = episode_num

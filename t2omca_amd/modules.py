@@ -56,8 +56,50 @@ class Transformer(nn.Module):
                                        for _ in range(depth)])
 
 
-def _flat(module):
-    return torch.cat([p.reshape(-1) for p in module.parameters()])
+class _PackCache:
+    """The flat parameters and folded kernel pack of a module, rebuilt only when a
+    parameter changes.
+
+    The reference MAC calls the agent once per env step (parallel_runner.py:121 ->
+    transf_agent.py:54-76) with the same weights until the learner's next update.
+    Concatenating and re-packing them on every call (forward and again in the
+    backward) cost two extra launches per step.  The key is every parameter's
+    storage pointer and autograd version counter: optimiser steps,
+    ``load_state_dict`` and ``copy_`` bump the version, re-binding a parameter
+    changes its pointer, so a stale pack is never used.  A rebuild allocates new
+    tensors, so a pack saved for an earlier backward is never overwritten."""
+
+    def __init__(self):
+        self.key = None
+        self.flat = None
+        self.pack = None
+        self.rebuilds = 0
+
+    def get(self, module, shape):
+        params = tuple(module.parameters())
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        if key != self.key:
+            with torch.no_grad():
+                flat = torch.cat([p.detach().reshape(-1) for p in params])
+            self.flat, self.pack = flat, ops.pack_params(shape, flat)
+            self.key = key
+            self.rebuilds += 1
+        return params, self.flat, self.pack
+
+    def invalidate(self):
+        """For writers that bypass autograd's version counters (the learner's Adam
+        kernel and broadcasts write the parameters through raw device pointers)."""
+        self.key = None
+
+
+def _split_like(gflat, shapes):
+    """The flat gradient (reference parameter order) as one view per parameter."""
+    out, o = [], 0
+    for sh in shapes:
+        n = sh.numel()
+        out.append(gflat[o:o + n].view(sh))
+        o += n
+    return tuple(out)
 
 
 def orthogonal_init_(m, gain=1.0):
@@ -72,29 +114,31 @@ def orthogonal_init_(m, gain=1.0):
 
 
 class _AgentStep(torch.autograd.Function):
+    """One agent step on the HIP kernels.  The parameters enter as separate inputs
+    (their gradients leave as views of one flat buffer), and the cached flat copy
+    and pack serve both directions."""
+
     @staticmethod
-    def forward(ctx, flat, inputs, hidden, shape):
+    def forward(ctx, shape, flat, pack, inputs, hidden, *params):
         b, a, nf = inputs.shape
-        pack = ops.pack_params(shape, flat.detach().contiguous())
         obs = inputs.detach().contiguous().view(b, 1, a, nf)
         h0 = hidden.detach().reshape(b * a, shape.E).contiguous()
         q, h = ops.agent_unroll_fwd(shape, pack, obs, h0_on=h0)
-        ctx.save_for_backward(flat, obs, h0, h)
-        ctx.shape = shape
+        ctx.save_for_backward(flat, pack, obs, h0, h)
+        ctx.shape, ctx.param_shapes = shape, [p.shape for p in params]
         return q[:, 0], h[:, 0]
 
     @staticmethod
     def backward(ctx, gq, gh):
-        flat, obs, h0, h = ctx.saved_tensors
+        flat, pack, obs, h0, h = ctx.saved_tensors
         shape = ctx.shape
-        pack = ops.pack_params(shape, flat.detach().contiguous())
         b, _, a, _ = obs.shape
         gq = (gq if gq is not None else torch.zeros_like(h[:, 0, :, :0])).contiguous().view(b, 1, a, -1)
         gh = (gh if gh is not None else torch.zeros_like(h[:, 0])).contiguous().view(b, 1, a, shape.E)
         gpack, gh0 = ops.agent_unroll_bwd(shape, pack, obs, h, h0=h0, gq=gq, gh=gh, want_gh0=True)
         gflat = torch.zeros_like(flat)
-        ops.unpack_grads(shape, flat.detach().contiguous(), gpack, gflat)
-        return gflat, None, gh0.view(b, a, shape.E), None
+        ops.unpack_grads(shape, flat, gpack, gflat)
+        return (None, None, None, None, gh0.view(b, a, shape.E)) + _split_like(gflat, ctx.param_shapes)
 
 
 class TransformerAgent(nn.Module):
@@ -115,6 +159,7 @@ class TransformerAgent(nn.Module):
         self.q_basic = nn.Linear(args.emb, args.n_actions)
         self.shape = ops.NetShape(ops.AGENT, args.emb, args.heads, args.depth, self.feat_dim, args.n_actions,
                                   args.ff_hidden_mult * args.emb, self.n_entities)
+        self._pack_cache = _PackCache()
 
     def init_hidden(self):
         return torch.zeros(1, self.args.emb, device=self.args.device)
@@ -123,40 +168,42 @@ class TransformerAgent(nn.Module):
         b, a, _ = inputs.size()
         if b * a * self.emb_dim != hidden_state.numel():
             hidden_state = hidden_state.expand(b, a, self.emb_dim)
-        q, h = _AgentStep.apply(_flat(self), inputs, hidden_state, self.shape)
+        params, flat, pack = self._pack_cache.get(self, self.shape)
+        q, h = _AgentStep.apply(self.shape, flat, pack, inputs, hidden_state, *params)
         return q.view(b, a, -1), h.view(b, a, -1)
 
 
 class _MixerStep(torch.autograd.Function):
+    """One mixer step on the HIP kernels (parameters as separate inputs, as _AgentStep)."""
+
     @staticmethod
-    def forward(ctx, flat, qvals, hidden_states, hyper_weights, states, shape):
+    def forward(ctx, shape, flat, pack, qvals, hidden_states, hyper_weights, states, *params):
         b = qvals.shape[0]
         A, E = shape.agents, shape.E
-        pack = ops.pack_params(shape, flat.detach().contiguous())
         qv = qvals.detach().reshape(b, 1, A).contiguous()
         hid = hidden_states.detach().reshape(b, 1, A, E).contiguous()
         hw0 = hyper_weights.detach().reshape(b, 3, E).contiguous()
         st = states.detach().reshape(b, 1, -1).contiguous()
         out = ops.mixer_unroll_fwd(shape, pack, st, hid, qmode_on=0, qv_on=qv, hw0_on=hw0)
-        ctx.save_for_backward(flat, qv, hid, hw0, st, out["y"], out["hw"], out["qv"], out["xout"])
+        ctx.save_for_backward(flat, pack, qv, hid, hw0, st, out["y"], out["hw"], out["qv"], out["xout"])
         ctx.xmid = out["xmid"]
-        ctx.shape = shape
+        ctx.shape, ctx.param_shapes = shape, [p.shape for p in params]
         return out["y"].view(b, 1, 1), out["hw"][:, 0]
 
     @staticmethod
     def backward(ctx, gy, ghw):
-        flat, qv, hid, hw0, st, y, hw, qvo, xout = ctx.saved_tensors
+        flat, pack, qv, hid, hw0, st, y, hw, qvo, xout = ctx.saved_tensors
         shape = ctx.shape
         b = qv.shape[0]
-        pack = ops.pack_params(shape, flat.detach().contiguous())
         gy = (gy if gy is not None else torch.zeros_like(y)).reshape(b, 1).contiguous()
         ghw = ghw.reshape(b, 1, 3, shape.E).contiguous() if ghw is not None else None
         fwd = dict(y=y, hw=hw, qv=qvo, xout=xout, xmid=ctx.xmid)
         gpack, gqv, ghid, ghw0 = ops.mixer_unroll_bwd(shape, pack, st, hid, fwd, gy, hw0=hw0, ghw_ext=ghw,
                                                       want_ghw0=True)
         gflat = torch.zeros_like(flat)
-        ops.unpack_grads(shape, flat.detach().contiguous(), gpack, gflat)
-        return gflat, gqv.view(b, 1, -1), ghid.view(b, -1, shape.E), ghw0, None, None
+        ops.unpack_grads(shape, flat, gpack, gflat)
+        return ((None, None, None, gqv.view(b, 1, -1), ghid.view(b, -1, shape.E), ghw0, None)
+                + _split_like(gflat, ctx.param_shapes))
 
 
 class TransformerMixer(nn.Module):
@@ -192,6 +239,7 @@ class TransformerMixer(nn.Module):
         self.shape = ops.NetShape(ops.MIXER, args.mixer_emb, args.mixer_heads, args.mixer_depth, self.feat_dim, 1,
                                   args.ff_hidden_mult * args.mixer_emb, n_tok, n_agents=self.n_agents,
                                   pos_func=pos, pos_beta=beta)
+        self._pack_cache = _PackCache()
 
     def init_hidden(self):
         # n_transf_mixer.py:52-53 (shape [1, A, E] as in the reference)
@@ -201,4 +249,5 @@ class TransformerMixer(nn.Module):
         b = qvals.size(0)
         hyper_weights = hyper_weights.expand(b, 3, self.emb_dim)
         tokens = states if self.custom_space else obs  # n_transf_mixer.py:60-63
-        return _MixerStep.apply(_flat(self), qvals, hidden_states, hyper_weights, tokens, self.shape)
+        params, flat, pack = self._pack_cache.get(self, self.shape)
+        return _MixerStep.apply(self.shape, flat, pack, qvals, hidden_states, hyper_weights, tokens, *params)
