@@ -230,14 +230,16 @@ int t2o_mixer_bwd_max_slabs(int B);
 int64_t t2o_bwd_tape_tiles(const t2o_layout* L, int B, int T, int A);
 
 /* Floats of backward tape workspace for `tiles` tiles of 16 records:
- * D * tiles * 16 * (6E + 2HE) elements of 4 (fp32) or 2 (bf16) bytes. */
+ * D * tiles * 16 * (4E + 2HE) elements of 4 (fp32) or 2 (bf16) bytes. */
 int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t tiles);
 
-/* Contract a backward tape (dM, dN, dW1, dW2 = Σ_records dYᵀ X, split-K over
+/* Contract a backward tape (dM, dN, dW2, P = Σ_records dYᵀ X, split-K over
  * the nslab slabs the backward call returned) into the M/N/W1/W2 regions of
- * those slabs.  pack = the same kernel pack the backward used (W1, W2ᵀ, c1
- * recompute the FFN operands the tape does not store).  Must follow the
- * t2o_*_unroll_bwd call that wrote the tape. */
+ * those slabs.  pack = the same kernel pack the backward used (g1, n1, W1, W2ᵀ,
+ * c1 recompute the FFN operands the tape does not store).  The W1 / g1 regions
+ * then hold P = Σ gf1 ⊗ x̂1 and Q = Σ gr2 ⊙ x̂1, which t2o_unpack_grads turns
+ * into the W1 / norm1 grads (the LN1 output and its grad are not on the tape).
+ * Must follow the t2o_*_unroll_bwd call that wrote the tape. */
 int t2o_bwd_tape_contract(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
                           float* gslabs, int nslab, void* stream);
 /* t2o_bwd_tape_contract for a tape in record format rec_format

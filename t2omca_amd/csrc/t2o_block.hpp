@@ -18,7 +18,6 @@ struct PostCache {
   f4 z[HET];   // per-head attention outputs
   f4 xh1[ET];
   float rs1;
-  f4 y[ET];
   f4 f1r[FT];  // relu(W1 y + c1); the ReLU mask is f1r > 0
   f4 xh2[ET];
   float rs2;
@@ -52,7 +51,6 @@ T2O_DEV void post_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* z,
     for (int t = 0; t < ET; ++t) {
       c->x[t] = x[t];
       c->xh1[t] = xh1[t];
-      c->y[t] = y[t];
     }
 #pragma unroll
     for (int t = 0; t < HET; ++t) c->z[t] = z[t];
@@ -99,16 +97,13 @@ T2O_DEV void post_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G
   for (int t = 0; t < FT; ++t)
 #pragma unroll
     for (int r = 0; r < 4; ++r) gf1[t][r] = c.f1r[t][r] > 0.f ? gf1[t][r] : 0.f;
-  if (rec) rec_store<R::SIZE, ET>(rec, R::Y, c.y);  // f1, gf1 (and d c1) are recomputed from (y, gr2)
   f4 gy[ET];
   matvec_tr<ET, FT>(P, L.W1[d], E, L.W1T[d], FF, gf1, gy);
 #pragma unroll
   for (int t = 0; t < ET; ++t) gy[t] += gr2[t];
-  // LN1: y = xh1*g1 + n1 (d g1, d n1 from the tape's (x̂1, gy))
-  if (rec) {
-    rec_store<R::SIZE, ET>(rec, R::XH1, c.xh1);
-    rec_store<R::SIZE, ET>(rec, R::GY, gy);
-  }
+  // LN1: y = xh1*g1 + n1 (y, f1, gf1 and the g1 / n1 grads come from the tape's
+  // (x̂1, gr2): TapeRec)
+  if (rec) rec_store<R::SIZE, ET>(rec, R::XH1, c.xh1);
   layernorm_bwd<ET>(gy, c.xh1, c.rs1, P.v + L.g1[d], gres);
   // r1 = N z + b_U + x
   if (rec) {
@@ -119,8 +114,8 @@ T2O_DEV void post_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G
 }
 
 // Lean variant for the two-wave pipelined kernels, whose cache must live in
-// half a register file: the tape operands already known in the forward (x, z,
-// y) are written to the record by the recompute itself, and the FFN's ReLU is
+// half a register file: the tape operands already known in the forward (x, z)
+// are written to the record by the recompute itself, and the FFN's ReLU is
 // kept as a bit mask (its only use in the backward).  Same records, same math.
 template <int E, int H, int FF>
 struct PostCacheLean {
@@ -147,7 +142,6 @@ T2O_DEV void post_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d, const f
   for (int t = 0; t < ET; ++t) r1[t] += vec_t(P.v + L.bu[d], t) + x[t];
   f4 y[ET];
   layernorm_fwd<ET>(r1, P.v + L.g1[d], P.v + L.n1[d], y, c->xh1, c->rs1);
-  rec.template store<ET>(R::Y, y);
   f4 f1[FT], f1r[FT];
   matvec<FT, ET>(P.w + L.W1[d], E, y, f1);
   uint32_t m = 0;
@@ -168,7 +162,7 @@ T2O_DEV void post_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d, const f
   layernorm_fwd<ET>(r2, P.v + L.g2[d], P.v + L.n2[d], x, c->xh2, c->rs2);
 }
 
-// post_bwd for the lean cache (the X, Z, Y record fields were written forward)
+// post_bwd for the lean cache (the X, Z record fields were written forward)
 template <int E, int H, int FF, typename WT, typename R = TapeRec<E, H, FF>>
 T2O_DEV void post_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restrict__ gs, const MaskedRec<WT>& rec,
                            int d, const PostCacheLean<E, H, FF>& c, const f4* gx, f4* gz, f4* gres, f4* ln2) {
@@ -192,7 +186,6 @@ T2O_DEV void post_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restr
 #pragma unroll
   for (int t = 0; t < ET; ++t) gy[t] += gr2[t];
   rec.template store<ET>(R::XH1, c.xh1);
-  rec.template store<ET>(R::GY, gy);
   layernorm_bwd<ET>(gy, c.xh1, c.rs1, P.v + L.g1[d], gres);
   rec.template store<ET>(R::GRES, gres);
   matvec_tr<HET, ET>(P, L.N[d], H * E, L.NT[d], E, gres, gz);

@@ -857,11 +857,16 @@ T2O_DEV void flush_tiles_g(float* __restrict__ W, int ldw, const f4 (&acc)[OT][I
 // (M, N, W1, W2), nor the FFN / LN1 / unify vectors, themselves: per (row,
 // step, block) they stream a record to an HBM tape, and t2o_dwgemm.hip
 // contracts the tape over all records with MFMA:
-//   dM = Σ gu ⊗ x,  dN = Σ gres ⊗ z,  dW2 = Σ gr2 ⊗ relu(f1),  dW1 = Σ gf1 ⊗ y,
-//   d bu = Σ gres,  d c2 = Σ gr2,  d c1 = Σ gf1,  d n1 = Σ gy,  d g1 = Σ gy ⊙ x̂1
-// with f1 = W1 y + c1 and gf1 = [f1 > 0] ⊙ W2ᵀ gr2 RECOMPUTED from (y, gr2) by
-// the contraction (two FF-wide operands are 44 % of a full record; recomputing
-// them is a few MFMAs per 16 records in a kernel that is HBM-bound anyway).
+//   dM = Σ gu ⊗ x,  dN = Σ gres ⊗ z,  dW2 = Σ gr2 ⊗ relu(f1),  P = Σ gf1 ⊗ x̂1,
+//   d bu = Σ gres,  d c2 = Σ gr2,  d c1 = Σ gf1,  Q = Σ gr2 ⊙ x̂1
+// with y = x̂1 ⊙ g1 + n1, f1 = W1 y + c1 and gf1 = [f1 > 0] ⊙ W2ᵀ gr2
+// RECOMPUTED by the contraction from (x̂1, gr2).  The LN1 output y and its grad
+// gy = gr2 + W1ᵀ gf1 are not stored: every quantity they fed is linear in them,
+// so t2o_unpack_grads completes the three affected grads from the summed slab
+// (T_UNFOLD_LN1, t2o_pack.hip):
+//   dW1 = Σ gf1 ⊗ y = P ⊙ g1 + d c1 ⊗ n1
+//   d g1 = Σ gy ⊙ x̂1 = Q + Σ_J W1[J] ⊙ P[J]
+//   d n1 = Σ gy = d c2 + W1ᵀ d c1
 // Only the LN2 vectors (g2, n2) and the small embedding / head grads are still
 // summed inside the backward kernels.  Feature offsets of one record:
 template <int E, int H, int FF>
@@ -870,11 +875,9 @@ struct TapeRec {
   static constexpr int GU = X + E;            // dL/du              (HE)  M:  dY
   static constexpr int Z = GU + H * E;        // head outputs z     (HE)  N:  X
   static constexpr int GRES = Z + H * E;      // dL/d(N z + bu)     (E)   N:  dY, bu
-  static constexpr int Y = GRES + E;          // LN1 output y       (E)   W1: X, and f1
-  static constexpr int GR2 = Y + E;           // dL/d(W2 f + c2 + y)(E)   W2: dY, gf1, c2
-  static constexpr int XH1 = GR2 + E;         // LN1 x̂             (E)   g1
-  static constexpr int GY = XH1 + E;          // dL/dy              (E)   g1, n1
-  static constexpr int SIZE = GY + E;
+  static constexpr int GR2 = GRES + E;        // dL/d(W2 f + c2 + y)(E)   W2: dY, gf1, c2, Q
+  static constexpr int XH1 = GR2 + E;         // LN1 x̂             (E)   y, P, Q
+  static constexpr int SIZE = XH1 + E;
 };
 
 // The agent's pipelined bf16 BPTT accumulates dM and dN in registers
@@ -884,11 +887,9 @@ template <int E, int H, int FF>
 struct TapeRecA {
   static constexpr int X = -1, GU = -1, Z = -1;
   static constexpr int GRES = 0;
-  static constexpr int Y = GRES + E;
-  static constexpr int GR2 = Y + E;
+  static constexpr int GR2 = GRES + E;
   static constexpr int XH1 = GR2 + E;
-  static constexpr int GY = XH1 + E;
-  static constexpr int SIZE = GY + E;
+  static constexpr int SIZE = XH1 + E;
 };
 
 // Layout: tiles of 16 records (one wave's rows at one step), RECORD-major

@@ -3,10 +3,12 @@
 // Per block d, over every record n (row x step of the agent, query row x step
 // of the mixer):
 //   dM  = Σ_n gu_n ⊗ x_n          dN  = Σ_n gres_n ⊗ z_n
-//   dW2 = Σ_n gr2_n ⊗ relu(f1_n)  dW1 = Σ_n gf1_n ⊗ y_n
-//   d bu = Σ gres,  d c2 = Σ gr2,  d c1 = Σ gf1,  d n1 = Σ gy,  d g1 = Σ gy ⊙ x̂1
-// where f1 = W1 y + c1 and gf1 = [f1 > 0] ⊙ (W2ᵀ gr2) are recomputed here from
-// the record's (y, gr2) — the backward kernels do not store them.
+//   dW2 = Σ_n gr2_n ⊗ relu(f1_n)  P   = Σ_n gf1_n ⊗ x̂1_n
+//   d bu = Σ gres,  d c2 = Σ gr2,  d c1 = Σ gf1,  Q = Σ gr2 ⊙ x̂1
+// where y = x̂1 ⊙ g1 + n1, f1 = W1 y + c1 and gf1 = [f1 > 0] ⊙ (W2ᵀ gr2) are
+// recomputed here from the record's (x̂1, gr2) — the backward kernels store
+// neither y nor its grad.  P and Q go to the slab's W1 and g1 slots;
+// t2o_unpack_grads turns them into dW1, d g1 and d n1 (TapeRec's comment).
 //
 // This is a tall-skinny GEMM with K = records (≈1M per block at config 3) and
 // HBM-bound: every tape byte is read once.  Structure:
@@ -19,9 +21,9 @@
 //     loads by all its threads (records padded in LDS so both read kinds below
 //     are bank-conflict-free), double-buffered in LDS with a two-deep register
 //     ring (prefetch distance two groups), one barrier per group;
-//   * 4 waves per block read the staged tiles: wave 0 dM (+ g1, n1), wave 1
+//   * 4 waves per block read the staged tiles: wave 0 dM (+ Q), wave 1
 //     dN (+ bu), waves 2 and 3 one half of the FF features each (recompute
-//     f1 / gf1 with MFMA, then dW1 / dW2 and c1; wave 2 also c2).  All
+//     y, f1 / gf1 with MFMA, then P / dW2 and c1; wave 2 also c2).  All
 //     accumulators stay in registers for the whole launch.
 // MFMA shapes: bf16 tape -> v_mfma_f32_16x16x16_bf16 with K = the 16 records
 // of a tile.  The tape is record-major, so the feature-major K-slices (records
@@ -168,7 +170,7 @@ T2O_DEV f4 kmma(f4 a, f4 b, f4 acc) {
   return acc;
 }
 
-// Role state: the accumulators of one wave.  ROLE 0 dM (+ g1, n1), 1 dN (+ bu),
+// Role state: the accumulators of one wave.  ROLE 0 dM (+ Q), 1 dN (+ bu),
 // 2/3 FFN half 0/1 (+ c1 of the half; role 2 also c2).
 template <int ROLE, int E, int H, int FF, int D, typename TT, int FMT>
 struct DwRole;
@@ -179,14 +181,14 @@ struct DwRole<0, E, H, FF, D, TT, FMT> {
   using R = typename Dm::R;
   using Frag = typename std::conditional<Dm::BF, bf4, f4>::type;
   f4 acc[Dm::HET][Dm::ET];  // dM[gu feature][x feature]
-  float vn1[Dm::ET], vg1[Dm::ET];
+  float vq[Dm::ET];         // Q = Σ gr2 ⊙ x̂1
   T2O_DEV void init(const DwGemmArgs&, int, const TT*) {
 #pragma unroll
     for (int o = 0; o < Dm::HET; ++o)
 #pragma unroll
       for (int i = 0; i < Dm::ET; ++i) acc[o][i] = zero4();
 #pragma unroll
-    for (int i = 0; i < Dm::ET; ++i) vn1[i] = vg1[i] = 0.f;
+    for (int i = 0; i < Dm::ET; ++i) vq[i] = 0.f;
   }
   T2O_DEV void tile(const TT* t) {
     constexpr int S = Dm::RSTR;
@@ -202,16 +204,16 @@ struct DwRole<0, E, H, FF, D, TT, FMT> {
       }
     }
 #pragma unroll
-    for (int i = 0; i < Dm::ET; ++i) {
-      const Frag gy = kslice<S>(t, R::GY + 16 * i), xh = kslice<S>(t, R::XH1 + 16 * i);
-      vn1[i] += bsum4(gy);
-      vg1[i] += bdot4(gy, xh);
-    }
+    for (int i = 0; i < Dm::ET; ++i) vq[i] += bdot4(kslice<S>(t, R::GR2 + 16 * i), kslice<S>(t, R::XH1 + 16 * i));
   }
   T2O_DEV void finish(const DwGemmArgs& a, float* slab, int d) {
     if constexpr (Dm::MN) dw_tiles_store<Dm::HET, Dm::ET>(slab + a.G.M[d], E, acc);
-    dw_vec_store<Dm::ET>(slab + a.G.n1[d], vn1);
-    dw_vec_store<Dm::ET>(slab + a.G.g1[d], vg1);
+    dw_vec_store<Dm::ET>(slab + a.G.g1[d], vq);
+    // (the n1 slot is unused: t2o_unpack_grads derives d n1 from d c1, d c2)
+    if (lane_g() == 0) {
+#pragma unroll
+      for (int i = 0; i < Dm::ET; ++i) slab[a.G.n1[d] + 16 * i + lane_c()] = 0.f;
+    }
   }
 };
 
@@ -253,10 +255,11 @@ struct DwRole<1, E, H, FF, D, TT, FMT> {
   }
 };
 
-// FFN half HALF: recompute f1 = W1 y + c1 and gf1 = [f1 > 0] ⊙ W2ᵀ gr2 for the
-// half's FH feature tiles as [records x features] MFMA tiles (lane (g, c) =
-// records 4g..4g+3 of feature 16J + c — already the K-slice layout of the
-// contraction), then dW2[e][J] += gr2 ⊗ relu(f1), dW1[J][e] += gf1 ⊗ y.
+// FFN half HALF: recompute y = x̂1 ⊙ g1 + n1, f1 = W1 y + c1 and gf1 = [f1 > 0] ⊙
+// W2ᵀ gr2 for the half's FH feature tiles as [records x features] MFMA tiles
+// (lane (g, c) = records 4g..4g+3 of feature 16J + c — already the K-slice
+// layout of the contraction), then dW2[e][J] += gr2 ⊗ relu(f1) and
+// P[J][e] += gf1 ⊗ x̂1 (t2o_unpack_grads makes dW1 of P).
 // Weight fragments: bf16 from the workgroup's LDS copy of the pack's
 // (swizzled) bf16 image; fp32 straight from the pack (L2-resident).
 template <int HALF, int E, int H, int FF, int D, typename TT, int FMT>
@@ -265,10 +268,11 @@ struct DwFfn {
   using R = typename Dm::R;
   static constexpr int ET = Dm::ET, FH = Dm::FH;
   using Frag = typename std::conditional<Dm::BF, bf4, f4>::type;
-  f4 acc1[FH][ET];  // dW1 rows of this half
+  f4 acc1[FH][ET];  // P rows of this half
   f4 acc2[ET][FH];  // dW2 columns of this half
   float vc1[FH], vc2[ET];
   float c1v[FH];
+  f4 g1r[ET], n1r[ET];  // LN1 affine of this lane's record-major features 16s + 4g .. +3
   const TT* wl;     // bf16: LDS W1 [FF][E] then W2ᵀ [FF][E] of this block
   const float* wsrc;
   int64_t o1, o2;
@@ -288,6 +292,13 @@ struct DwFfn {
     o2 = a.L.W2T[d];
 #pragma unroll
     for (int jt = 0; jt < FH; ++jt) c1v[jt] = a.pack[a.L.c1[d] + 16 * (HALF * FH + jt) + c];
+#pragma unroll
+    for (int s = 0; s < ET; ++s)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        g1r[s][r] = a.pack[a.L.g1[d] + 16 * s + 4 * lane_g() + r];
+        n1r[s][r] = a.pack[a.L.n1[d] + 16 * s + 4 * lane_g() + r];
+      }
   }
   // fragment of W (0: W1, 1: W2ᵀ): row 16J + c, features 16s + 4g .. +3
   T2O_DEV Frag wfrag(int m, int jt, int s) const {
@@ -299,14 +310,22 @@ struct DwFfn {
       return ld4(wsrc + (m ? o2 : o1) + (int64_t)row * E + 16 * s + 4 * lane_g());
     }
   }
+  // y = x̂1 ⊙ g1 + n1 of a record-major slice (the LN1 affine, layernorm_fwd)
+  T2O_DEV Frag affine(Frag xh, int s) const {
+    f4 y;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) y[r] = (float)xh[r] * g1r[s][r] + n1r[s][r];
+    if constexpr (Dm::BF) return to_bf4(y);
+    else return y;
+  }
   T2O_DEV void tile(const TT* t) {
     constexpr int S = Dm::RSTR;
-    Frag yr[ET], gr[ET], yk[ET], gk[ET];
+    Frag yr[ET], gr[ET], xk[ET], gk[ET];
 #pragma unroll
     for (int s = 0; s < ET; ++s) {
-      yr[s] = rslice<S>(t, R::Y + 16 * s);
+      yr[s] = affine(rslice<S>(t, R::XH1 + 16 * s), s);
       gr[s] = rslice<S>(t, R::GR2 + 16 * s);
-      yk[s] = kslice<S>(t, R::Y + 16 * s);
+      xk[s] = kslice<S>(t, R::XH1 + 16 * s);
       gk[s] = kslice<S>(t, R::GR2 + 16 * s);
       if (HALF == 0) vc2[s] += bsum4(gk[s]);
     }
@@ -338,7 +357,7 @@ struct DwFfn {
 #pragma unroll
       for (int e = 0; e < ET; ++e) {
         acc2[e][jt] = kmma(gk[e], frb, acc2[e][jt]);  // dW2[e][J] += gr2 ⊗ relu(f1)
-        acc1[jt][e] = kmma(gfb, yk[e], acc1[jt][e]);  // dW1[J][e] += gf1 ⊗ y
+        acc1[jt][e] = kmma(gfb, xk[e], acc1[jt][e]);  // P[J][e] += gf1 ⊗ x̂1
       }
     }
   }
@@ -465,7 +484,7 @@ using namespace t2o;
 extern "C" int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t tiles) {
   if (!L || tiles < 0) return -1;
   if (L->generic) return gen_tape_floats(L, tiles);
-  const int64_t elems = (int64_t)L->D * tiles * tape_tile_records(*L) * (6 * L->E + 2 * L->H * L->E);
+  const int64_t elems = (int64_t)L->D * tiles * tape_tile_records(*L) * (4 * L->E + 2 * L->H * L->E);
   return L->prec ? (elems + 1) / 2 : elems;
 }
 

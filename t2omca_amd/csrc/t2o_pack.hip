@@ -32,6 +32,7 @@ enum TaskKind : int {
   T_FOLD_N,       // head h: N[o][hE+k] = NT[hE+k][o] = Σ_m U[o][hE+m] Wv[hE+m][k]
   T_UNFOLD_QK,    // head h: gWq[hE+m][k] += s Σ_i Wk[hE+m][i] gM[hE+i][k]; gWk[hE+m][i] += s Σ_k Wq[hE+m][k] gM[hE+i][k]
   T_UNFOLD_VU,    // head h: gWv[hE+m][k] += Σ_o U[o][hE+m] gN[o][hE+k];  gU[o][hE+m] += Σ_k gN[o][hE+k] Wv[hE+m][k]
+  T_UNFOLD_LN1,   // block: the LN1 / W1 grads from the contraction's P, Q (TapeRec, t2o_common.hpp)
 };
 
 struct Task {
@@ -167,6 +168,47 @@ __global__ __launch_bounds__(256) void pack_kernel(TaskTable tab, const float* _
       }
       break;
     }
+    case T_UNFOLD_LN1: {
+      // a / b / c = W1 [R=FF][C=E], g1, n1 (params; the grads sit at the same offsets);
+      // gpack: dst = P [FF][E], dst2 = Q [E], sr = d c1 [FF], sc = d c2 [E].
+      //   dW1 = P ⊙ g1 + d c1 ⊗ n1,  d g1 = Q + Σ_J W1[J] ⊙ P[J],  d n1 = d c2 + W1ᵀ d c1
+      const int FFn = tk.R, En = tk.C;
+      const float* W1 = src + tk.a;
+      const float* g1 = src + tk.b;
+      const float* n1 = src + tk.c;
+      const float* Pm = src2 + tk.dst;
+      const float* dc1 = src2 + tk.sr;
+      for (int i = threadIdx.x; i < FFn * En; i += blockDim.x) {
+        const int J = i / En, e = i % En;
+        dst[tk.a + i] += Pm[i] * g1[e] + dc1[J] * n1[e];
+      }
+      // column sums over J: thread (q, e) takes J = q, q + NQ, ... ; partials in LDS
+      const int NQ = (int)blockDim.x / En;
+      float* part = sm;  // [2][NQ][E]
+      if ((int)threadIdx.x < NQ * En) {
+        const int e = threadIdx.x % En, q = threadIdx.x / En;
+        float sg = 0.f, sn = 0.f;
+        for (int J = q; J < FFn; J += NQ) {
+          const float w = W1[(int64_t)J * En + e];
+          sg = fmaf(w, Pm[(int64_t)J * En + e], sg);
+          sn = fmaf(w, dc1[J], sn);
+        }
+        part[q * En + e] = sg;
+        part[(NQ + q) * En + e] = sn;
+      }
+      __syncthreads();
+      if ((int)threadIdx.x < En) {
+        const int e = threadIdx.x;
+        float sg = 0.f, sn = 0.f;
+        for (int q = 0; q < NQ; ++q) {
+          sg += part[q * En + e];
+          sn += part[(NQ + q) * En + e];
+        }
+        dst[tk.b + e] += src2[tk.dst2 + e] + sg;
+        dst[tk.c + e] += src2[tk.sc + e] + sn;
+      }
+      break;
+    }
     default: break;
   }
 }
@@ -203,6 +245,12 @@ struct Builder {
   void head(int kind, int h, int64_t dst_off, int64_t dst2_off, int64_t a, int64_t b, int64_t c = 0, int bf = 0) {
     Task& t = next(1);
     t.kind = kind; t.h = h; t.bf = bf; t.dst = dst_off; t.dst2 = dst2_off; t.a = a; t.b = b; t.c = c;
+  }
+  // T_UNFOLD_LN1: one workgroup per block
+  void ln1(int64_t w1, int64_t g1, int64_t n1, int64_t gP, int64_t gQ, int64_t gc1, int64_t gc2, int FF, int E) {
+    Task& t = next(1);
+    t.kind = T_UNFOLD_LN1; t.R = FF; t.C = E; t.a = w1; t.b = g1; t.c = n1; t.dst = gP; t.dst2 = gQ;
+    t.sr = (int)gc1; t.sc = (int)gc2;
   }
   void flush() {
     if (nb > 0 && rc == 0) {
@@ -358,9 +406,7 @@ extern "C" int t2o_unpack_grads(const t2o_layout* L, const float* params, const 
       b.head(T_UNFOLD_VU, h, P.Wv[d], P.U[d], P.U[d], P.Wv[d], G.N[d]);
     }
     b.ew(T_ADD, 1, E, P.bu[d], G.bu[d]);
-    b.ew(T_ADD, 1, E, P.g1[d], G.g1[d]);
-    b.ew(T_ADD, 1, E, P.n1[d], G.n1[d]);
-    b.ew(T_ADD, FF, E, P.W1[d], G.W1[d]);
+    b.ln1(P.W1[d], P.g1[d], P.n1[d], G.W1[d], G.g1[d], G.c1[d], G.c2[d], FF, E);
     b.ew(T_ADD, 1, FF, P.c1[d], G.c1[d]);
     b.ew(T_ADD, E, FF, P.W2[d], G.W2[d]);
     b.ew(T_ADD, 1, E, P.c2[d], G.c2[d]);

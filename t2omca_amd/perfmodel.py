@@ -50,7 +50,7 @@ def dw_record_bytes(E=32, H=3, D=2, FF=None, elem=4):
     """Tape bytes per record (all D blocks): written once by the backward, read once
     by the contraction; elem = 4 (fp32 mode) or 2 (bf16 mode)."""
     FF = FF or 4 * E
-    return D * elem * (6 * E + 2 * H * E)
+    return D * elem * (4 * E + 2 * H * E)
 
 
 def td_update_flops(B, T, A, E=32, H=3, D=2, F=9, Fs=8, NA=5):
@@ -92,10 +92,11 @@ def td_update_bytes(B, T, A, E=32, F=9, Fs=8, NA=5, elem=4):
 def td_tape_bytes(B, T, A, E=32, elem=4):
     """Weight-gradient tape bytes per update (valid records only, in the MFMA operand
     type): written by the BPTT kernel, read back by its contraction (agent_dw /
-    mixer_dw).  The mixer's record is always the full one; the agent's pipelined
-    bf16 kernel writes the lean record (160 of 384 features) at up to 8 entities."""
+    mixer_dw).  The mixer's record is always the full one (x, gu, z, gres, gr2, x̂1:
+    320 features at E 32 / H 3); the agent's pipelined bf16 kernel writes the lean
+    record (gres, gr2, x̂1: 96 of 320) at up to 8 entities."""
     full = dw_record_bytes(E, elem=elem)
-    agent_rec = full * 160 // 384 if (elem == 2 and A <= 8) else full
+    agent_rec = full * 3 * E // (4 * E + 2 * 3 * E) if (elem == 2 and A <= 8) else full
     return {"agent": B * T * A * agent_rec, "mixer": B * T * (A + 3) * full}
 
 

@@ -62,6 +62,14 @@ def test_pack_and_unpack(kind):
         gb["N"] = gb["N"].view(E, H * E)
         gb["W1"] = gb["W1"].view(FF, E)
         gb["W2"] = gb["W2"].view(E, FF)
+        # the tuned contraction leaves P = Σ gf1 ⊗ x̂1 in W1's slot and Q = Σ gr2 ⊙ x̂1
+        # in g1's (n1's is unused); unpack completes them (TapeRec, t2o_common.hpp)
+        pre = f"transformer.tblocks.{d}."
+        W1, g1, n1 = pd[pre + "ff.0.weight"], pd[pre + "norm1.weight"], pd[pre + "norm1.bias"]
+        P, Q = gb["W1"], gb["g1"]
+        gb["W1"] = P * g1[None, :] + gb["c1"][:, None] * n1[None, :]
+        gb["g1"] = Q + (W1 * P).sum(0)
+        gb["n1"] = gb["c2"] + W1.T @ gb["c1"]
         gblocks.append(gb)
     assert o == Gtot
     exp = am.fold_grads(pd, "transformer.", E, H, D, gblocks)
