@@ -21,8 +21,12 @@ timeout -k 10 400 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { t
 cut -c1-300 "$OUT/bench.json"
 step profile
 bash tools/profile_box.sh "$TAG/prof" > "$OUT/prof.log" 2>&1 || { tail -5 "$OUT/prof.log"; exit 1; }
+python3 tools/timeline_trace.py $(find "$OUT/prof/trace" -name "*kernel_trace.csv" | head -1) > "$OUT/prof/timeline.txt"
+tail -1 "$OUT/prof/timeline.txt"
 step rollout
 timeout -k 10 300 python bench.py --mode rollout > "$OUT/rollout.json" 2> "$OUT/rollout.err" || { tail -5 "$OUT/rollout.err"; exit 1; }
+step dropin
+timeout -k 10 300 python bench.py --mode dropin > "$OUT/dropin.json" 2> "$OUT/dropin.err" || { tail -5 "$OUT/dropin.err"; exit 1; }
 step configs
 bash tools/configs_box.sh "$TAG/configs" > "$OUT/configs.log" 2>&1 || { tail -5 "$OUT/configs.log"; exit 1; }
 cat "$OUT/configs.log"
