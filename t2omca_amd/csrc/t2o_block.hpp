@@ -130,9 +130,9 @@ struct PostCacheLean {
 
 // R: the tape record (TapeRec; TapeRecA has no X / Z fields — its writer keeps
 // dN's operands itself).
-template <int E, int H, int FF, typename WT, typename R = TapeRec<E, H, FF>>
+template <int E, int H, int FF, typename WT, typename R = TapeRec<E, H, FF>, int CP = 0>
 T2O_DEV void post_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d, const f4* z, f4* x,
-                           PostCacheLean<E, H, FF>* c, const MaskedRec<WT>& rec) {
+                           PostCacheLean<E, H, FF>* c, const MaskedRec<WT, CP>& rec) {
   constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
   if constexpr (R::X >= 0) rec.template store<ET>(R::X, x);
   if constexpr (R::Z >= 0) rec.template store<HET>(R::Z, z);
@@ -163,8 +163,8 @@ T2O_DEV void post_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d, const f
 }
 
 // post_bwd for the lean cache (the X, Z record fields were written forward)
-template <int E, int H, int FF, typename WT, typename R = TapeRec<E, H, FF>>
-T2O_DEV void post_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restrict__ gs, const MaskedRec<WT>& rec,
+template <int E, int H, int FF, typename WT, typename R = TapeRec<E, H, FF>, int CP = 0>
+T2O_DEV void post_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restrict__ gs, const MaskedRec<WT, CP>& rec,
                            int d, const PostCacheLean<E, H, FF>& c, const f4* gx, f4* gz, f4* gres, f4* ln2) {
   constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
 #pragma unroll

@@ -922,10 +922,13 @@ T2O_DEV void rec_store(TT* __restrict__ tile, int off, const f4* v) {
 // stores, so a tile of fewer than 16 records needs no per-lane branch (exec-mask
 // control flow around every store costs registers in the two-wave kernels).
 // The tile base must be wave-uniform.
-#ifndef T2O_TAPE_CPOL  // cache policy of the tape stores: nt (A/B, profiles/r3_cpol: update 2.506 -> 2.491 ms; sc1 2.598)
-#define T2O_TAPE_CPOL 2
-#endif
-template <typename TT>
+// CPOL: cache policy of the tape stores (the buffer instructions' aux bits; 2 =
+// non-temporal).  Interleaved A/B (profiles/r3_cpol/, r3_shp/): nt cut the
+// multi-tile mixer BPTT at 32 AGVs 8.16 -> 7.32 ms and left the one-tile
+// pipelined mixer and the agent kernels unchanged in time while their PMC write
+// bytes rose 18-39 % (partial-line nt writes), so only the multi-tile mixer uses
+// it; write-through (sc1) was slower everywhere (update 2.506 -> 2.598 ms).
+template <typename TT, int CPOL = 0>
 struct MaskedRec {
   __amdgpu_buffer_rsrc_t rsrc;
   int voff;  // bytes: this lane's record, features 4g.. ; or out of range
@@ -948,9 +951,9 @@ struct MaskedRec {
     for (int t = 0; t < NT; ++t) {
       const int o = voff + (off + 16 * t) * (int)sizeof(TT);
       if constexpr (sizeof(TT) == 2) {
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i, to_bf4(v[t])), rsrc, o, 0, T2O_TAPE_CPOL);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i, to_bf4(v[t])), rsrc, o, 0, CPOL);
       } else {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v[t]), rsrc, o, 0, T2O_TAPE_CPOL);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4i, v[t]), rsrc, o, 0, CPOL);
       }
     }
   }

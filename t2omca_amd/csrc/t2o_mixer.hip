@@ -665,7 +665,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
             WT* tile = static_cast<WT*>(args.tape) +
                        ((size_t)d * ctiles * 16 + ((size_t)t * fa.B + b) * nq + 16 * qt) * Rec::SIZE;
             MixerCacheLean<E, H, KT, FF> cache;
-            const MaskedRec<WT> rec(tile, min(16, nq - 16 * qt), Rec::SIZE);
+            const MaskedRec<WT, 2> rec(tile, min(16, nq - 16 * qt), Rec::SIZE);  // non-temporal (MaskedRec)
             mixer_block_fwd_lean<E, H, KT, FF>(P, L, d, K, lk, x, cache, rec);
             mixer_block_bwd_lean<E, H, KT, FF>(P, L, gs, rec, stage, d, K, lk, gX0, cache, gx, ln2[d]);
           }

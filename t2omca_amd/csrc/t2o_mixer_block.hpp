@@ -230,10 +230,10 @@ T2O_DEV void attn_probs(const KeyFrags<E, KT, BF>& K, const f4* u, int Lk, f4* s
   for (int kt = 0; kt < KT; ++kt) s[kt] *= il;
 }
 
-template <int E, int H, int KT, int FF, typename WT>
+template <int E, int H, int KT, int FF, typename WT, int CP>
 T2O_DEV void mixer_block_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d,
                                   const KeyFrags<E, KT, sizeof(WT) == 2>& K, int Lk, f4* x,
-                                  MixerCacheLean<E, H, KT, FF>& cache, const MaskedRec<WT>& rec) {
+                                  MixerCacheLean<E, H, KT, FF>& cache, const MaskedRec<WT, CP>& rec) {
   constexpr int ET = E / 16, HET = H * ET;
   constexpr bool BF = sizeof(WT) == 2;
   matvec<HET, ET>(P.w + L.M[d], E, x, cache.u);
@@ -251,9 +251,9 @@ T2O_DEV void mixer_block_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d,
   post_fwd_lean<E, H, FF>(P, L, d, z, x, &cache.post, rec);
 }
 
-template <int E, int H, int KT, int FF, typename WT>
+template <int E, int H, int KT, int FF, typename WT, int CP>
 T2O_DEV void mixer_block_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restrict__ gs,
-                                  const MaskedRec<WT>& rec, float* __restrict__ stage, int d,
+                                  const MaskedRec<WT, CP>& rec, float* __restrict__ stage, int d,
                                   const KeyFrags<E, KT, sizeof(WT) == 2>& K, int Lk, f4 (&gX0)[KT][E / 16],
                                   const MixerCacheLean<E, H, KT, FF>& c, f4* gx, f4* ln2) {
   constexpr int ET = E / 16, HET = H * ET;
