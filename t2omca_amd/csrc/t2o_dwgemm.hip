@@ -272,7 +272,7 @@ struct DwFfn {
   f4 acc2[ET][FH];  // dW2 columns of this half
   float vc1[FH], vc2[ET];
   float c1v[FH];
-  f4 g1r[ET], n1r[ET];  // LN1 affine of this lane's record-major features 16s + 4g .. +3
+  f4 g1r[ET], n1r[ET];  // fp32: LN1 affine of this lane's record-major features 16s + 4g .. +3
   const TT* wl;     // bf16: LDS W1 [FF][E] then W2ᵀ [FF][E] of this block
   const float* wsrc;
   int64_t o1, o2;
@@ -292,13 +292,23 @@ struct DwFfn {
     o2 = a.L.W2T[d];
 #pragma unroll
     for (int jt = 0; jt < FH; ++jt) c1v[jt] = a.pack[a.L.c1[d] + 16 * (HALF * FH + jt) + c];
+    if constexpr (Dm::BF) {  // the LDS W1 image carries g1; fold n1 into the bias
 #pragma unroll
-    for (int s = 0; s < ET; ++s)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        g1r[s][r] = a.pack[a.L.g1[d] + 16 * s + 4 * lane_g() + r];
-        n1r[s][r] = a.pack[a.L.n1[d] + 16 * s + 4 * lane_g() + r];
+      for (int jt = 0; jt < FH; ++jt) {
+        const float* w = a.pack + a.L.W1[d] + (int64_t)(16 * (HALF * FH + jt) + c) * E;
+        float acc = 0.f;
+        for (int e = 0; e < E; ++e) acc = fmaf(w[e], a.pack[a.L.n1[d] + e], acc);
+        c1v[jt] += acc;
       }
+    } else {
+#pragma unroll
+      for (int s = 0; s < ET; ++s)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          g1r[s][r] = a.pack[a.L.g1[d] + 16 * s + 4 * lane_g() + r];
+          n1r[s][r] = a.pack[a.L.n1[d] + 16 * s + 4 * lane_g() + r];
+        }
+    }
   }
   // fragment of W (0: W1, 1: W2ᵀ): row 16J + c, features 16s + 4g .. +3
   T2O_DEV Frag wfrag(int m, int jt, int s) const {
@@ -310,13 +320,18 @@ struct DwFfn {
       return ld4(wsrc + (m ? o2 : o1) + (int64_t)row * E + 16 * s + 4 * lane_g());
     }
   }
-  // y = x̂1 ⊙ g1 + n1 of a record-major slice (the LN1 affine, layernorm_fwd)
+  // the recompute's record-major operand: bf16, x̂1 itself (g1 / n1 are folded
+  // into the staged W1 and c1); fp32, y = x̂1 ⊙ g1 + n1 (the LN1 affine, layernorm_fwd)
   T2O_DEV Frag affine(Frag xh, int s) const {
-    f4 y;
+    if constexpr (Dm::BF) {
+      (void)s;
+      return xh;
+    } else {
+      f4 y;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) y[r] = (float)xh[r] * g1r[s][r] + n1r[s][r];
-    if constexpr (Dm::BF) return to_bf4(y);
-    else return y;
+      for (int r = 0; r < 4; ++r) y[r] = xh[r] * g1r[s][r] + n1r[s][r];
+      return y;
+    }
   }
   T2O_DEV void tile(const TT* t) {
     constexpr int S = Dm::RSTR;
@@ -420,12 +435,22 @@ __global__ __launch_bounds__(256 * D) void dw_gemm_kernel(DwGemmArgs a) {
   TT* const buf1 = buf0 + Dm::GELEM;
   TT* const wlds = buf1 + Dm::GELEM;  // bf16: [D][W1, W2ᵀ][FF][E] (the pack's swizzled image)
   if constexpr (Dm::BF) {  // made visible by dw_run's first barrier
+    // W2ᵀ: the pack's swizzled bf16 image; W1: folded with the LN1 gain,
+    // W1[J][e]·g1[e], rounded to bf16 in the same swizzled placement, so the
+    // recompute f1 = (W1 ⊙ g1) x̂1 + (c1 + W1 n1) reads the tape's x̂1 directly
     const TT* img = reinterpret_cast<const TT*>(a.pack + a.L.total);
     constexpr int MAT = FF * E;
     for (int q = threadIdx.x; q < D * 2 * MAT / Dm::PER; q += Dm::NT) {
       const int e = q * Dm::PER, dd = e / (2 * MAT), m = (e / MAT) & 1, k = e % MAT;
-      const int64_t src = (m ? a.L.W2T[dd] : a.L.W1[dd]) + k;
-      *reinterpret_cast<u4v*>(wlds + e) = *reinterpret_cast<const u4v*>(img + src);
+      if (m) {
+        *reinterpret_cast<u4v*>(wlds + e) = *reinterpret_cast<const u4v*>(img + a.L.W2T[dd] + k);
+      } else {
+        const int row = k / E, c0 = (k % E) ^ bf_swz(row, E);  // 8 consecutive image slots = 8 columns
+        const float* w = a.pack + a.L.W1[dd] + (int64_t)row * E + c0;
+        const float* g = a.pack + a.L.g1[dd] + c0;
+#pragma unroll
+        for (int i = 0; i < Dm::PER; ++i) wlds[e + i] = (TT)(w[i] * g[i]);
+      }
     }
   }
   if constexpr (RT < 16) {  // compact tiles: LDS records RT..15 stay zero (they add nothing)
