@@ -74,10 +74,11 @@ def parse():
                          "host-side buffer contract: one device->host copy and sync per update)")
     ap.add_argument("--serial", action="store_true",
                     help="no side-stream overlap: every kernel's HIP-event time is its isolated cost")
-    ap.add_argument("--kernel-timer-every", type=int, default=2,
+    ap.add_argument("--kernel-timer-every", type=int, default=5,
                     help="bracket the kernels with HIP events on every k-th timed step (the per-kernel "
                          "times and the roofline come from those steps; the events cost ~40 us per "
-                         "instrumented update, so every step would inflate ms_per_step ~1.5%%; 0: never)")
+                         "instrumented update, so every step would inflate ms_per_step ~1.5%%, every 5th "
+                         "~0.3%%; 0: never)")
     ap.add_argument("--no-fp32-companion", dest="fp32_companion", action="store_false",
                     help="skip the fp32-precision companion timing of the same workload (bf16 runs)")
     ap.add_argument("--print-workload-tag", action="store_true",
