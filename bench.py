@@ -40,8 +40,10 @@ PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E spec peak
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    # untimed; the GPU's clocks ramp over the first ~10 updates (per-update period
+    # 2.74 -> 2.43 ms at configs[2], profiles/r3_f3/NOTE.txt)
+    ap.add_argument("--warmup", type=int, default=12)
     ap.add_argument("--batch", type=int, default=None,
                     help="episodes per GPU (default: 1024 train = configs[2]; 128 forward = configs[1])")
     ap.add_argument("--T", type=int, default=None,
