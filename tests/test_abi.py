@@ -145,6 +145,30 @@ def test_bwd_tape_tiles_host_logic():
     assert lib.t2o_bwd_tape_tiles(C.byref(Lg), 0, T, 32) == -1
 
 
+def test_bwd_tape_floats_record_size():
+    """t2o_bwd_tape_floats (host-only): D blocks x 16 records per tile x the record
+    [x, gu, z, gres, gr2, x̂1] = 4E + 2HE features (t2o_common.hpp TapeRec; the LN1
+    output and its grad are not stored), in fp32 floats or packed bf16; the perf
+    model's tape bytes (the bench line's tape_bytes_per_update) agree."""
+    import ctypes as C
+
+    from t2omca_amd import _lib, perfmodel
+    lib = _lib.lib()
+    lib.t2o_bwd_tape_floats.restype = C.c_int64
+    E, H, D, tiles = 32, 3, 2, 11
+    rec = 4 * E + 2 * H * E
+    assert rec == 320
+    for prec in (0, 1):
+        L = _lib.make_layout(1, E, H, D, 8, 1, 4 * E, 8, prec)
+        n = lib.t2o_bwd_tape_floats(C.byref(L), C.c_int64(tiles))
+        elems = D * tiles * 16 * rec
+        assert n == (elems if prec == 0 else (elems + 1) // 2)
+    assert perfmodel.dw_record_bytes(E, H, D, elem=2) == D * 2 * rec
+    tb = perfmodel.td_tape_bytes(1024, 60, 8, E, elem=2)
+    assert tb["mixer"] == 1024 * 60 * 11 * D * 2 * rec
+    assert tb["agent"] == 1024 * 60 * 8 * D * 2 * 3 * E  # the lean agent record: gres, gr2, x̂1
+
+
 @pytest.mark.parametrize("kind", [0, 1])
 def test_layout_instance_classes(kind):
     """t2o_layout_instance (host-only): exact MFMA instances at 3 / 8 / 16 / 64 entities,
