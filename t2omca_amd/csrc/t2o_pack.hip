@@ -172,15 +172,21 @@ __global__ __launch_bounds__(256) void pack_kernel(TaskTable tab, const float* _
       // a / b / c = W1 [R=FF][C=E], g1, n1 (params; the grads sit at the same offsets);
       // gpack: dst = P [FF][E], dst2 = Q [E], sr = d c1 [FF], sc = d c2 [E].
       //   dW1 = P ⊙ g1 + d c1 ⊗ n1,  d g1 = Q + Σ_J W1[J] ⊙ P[J],  d n1 = d c2 + W1ᵀ d c1
+      // workgroup 0: the two column sums; workgroups 1..: dW1, EW_PER_BLOCK entries each
       const int FFn = tk.R, En = tk.C;
       const float* W1 = src + tk.a;
       const float* g1 = src + tk.b;
       const float* n1 = src + tk.c;
       const float* Pm = src2 + tk.dst;
       const float* dc1 = src2 + tk.sr;
-      for (int i = threadIdx.x; i < FFn * En; i += blockDim.x) {
-        const int J = i / En, e = i % En;
-        dst[tk.a + i] += Pm[i] * g1[e] + dc1[J] * n1[e];
+      if (lb > 0) {
+        const int64_t n = (int64_t)FFn * En, i0 = (int64_t)(lb - 1) * EW_PER_BLOCK;
+#pragma unroll 4
+        for (int64_t i = i0 + threadIdx.x; i < n && i < i0 + EW_PER_BLOCK; i += blockDim.x) {
+          const int J = (int)(i / En), e = (int)(i % En);
+          dst[tk.a + i] += Pm[i] * g1[e] + dc1[J] * n1[e];
+        }
+        break;
       }
       // column sums over J: thread (q, e) takes J = q, q + NQ, ... ; partials in LDS
       const int NQ = (int)blockDim.x / En;
@@ -188,6 +194,7 @@ __global__ __launch_bounds__(256) void pack_kernel(TaskTable tab, const float* _
       if ((int)threadIdx.x < NQ * En) {
         const int e = threadIdx.x % En, q = threadIdx.x / En;
         float sg = 0.f, sn = 0.f;
+#pragma unroll 4
         for (int J = q; J < FFn; J += NQ) {
           const float w = W1[(int64_t)J * En + e];
           sg = fmaf(w, Pm[(int64_t)J * En + e], sg);
@@ -246,9 +253,9 @@ struct Builder {
     Task& t = next(1);
     t.kind = kind; t.h = h; t.bf = bf; t.dst = dst_off; t.dst2 = dst2_off; t.a = a; t.b = b; t.c = c;
   }
-  // T_UNFOLD_LN1: one workgroup per block
+  // T_UNFOLD_LN1: per block, one workgroup for the column sums plus the dW1 workgroups
   void ln1(int64_t w1, int64_t g1, int64_t n1, int64_t gP, int64_t gQ, int64_t gc1, int64_t gc2, int FF, int E) {
-    Task& t = next(1);
+    Task& t = next(1 + (int)(((int64_t)FF * E + EW_PER_BLOCK - 1) / EW_PER_BLOCK));
     t.kind = T_UNFOLD_LN1; t.R = FF; t.C = E; t.a = w1; t.b = g1; t.c = n1; t.dst = gP; t.dst2 = gQ;
     t.sr = (int)gc1; t.sc = (int)gc2;
   }
