@@ -12,6 +12,7 @@
 // and torch.nn.utils.clip_grad_norm_ + torch.optim.Adam (non-amsgrad, L2
 // weight decay) on the flat parameter buffer.
 #include <math.h>
+#include <stdlib.h>
 
 #include "t2o_common.hpp"
 
@@ -126,6 +127,92 @@ __global__ __launch_bounds__(256) void td_loss_kernel(TDArgs a, int EP) {
   }
 }
 
+// The same targets / loss / priorities with one WAVE per episode: the TD(λ)
+// recursion ret_t = λγ·ret_{t+1} + B_t (B_t = m_t (r_t + (1-λ)γ Q'_{t+1}(1-term_t)),
+// B_T = Q'_T (1 - Σ term)) is linear with a constant multiplier, so lane l takes
+// the chunk [lC, lC + C) of t = 0..T (C = ⌈(T+1)/64⌉), folds it from its end
+// (G_l, P_l = λγ^len), a Hillis–Steele suffix scan of (G, P) pairs across the
+// wave gives each chunk its incoming ret, and a second pass over the chunk
+// re-runs the recursion from it.  Reassociated (fp32 rounding differs from the
+// sequential order by ~1e-7 relative), deterministic, and the T-step serial
+// chain becomes C + 6 steps.
+constexpr int TDW_WAVES = 4;
+
+__global__ __launch_bounds__(64 * TDW_WAVES) void td_loss_wave_kernel(TDArgs a) {
+  __shared__ float red[2][TDW_WAVES];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b = blockIdx.x * TDW_WAVES + w;
+  const int T = a.T;
+  const float A = a.lambda_ * a.gamma, G1 = (1.f - a.lambda_) * a.gamma;
+  const float denom = a.mask_sum > 0.f ? a.mask_sum : 1.f;
+  float lsum = 0.f, msum = 0.f;
+  if (b < a.B) {
+    const int C = (T + 1 + 63) / 64;
+    const int t0 = min(lane * C, T + 1), t1 = min(t0 + C, T + 1);
+    auto tm = [&](int t) { return a.term ? mask_at(a.term, (int64_t)b * a.tm_sb + (int64_t)t * a.tm_st, a.tm_dt) : 0.f; };
+    auto fl = [&](int t) { return a.filled ? mask_at(a.filled, (int64_t)b * a.fl_sb + (int64_t)t * a.fl_st, a.fl_dt) : 1.f; };
+    const float* qt = a.qtot_tgt + (size_t)b * (T + 1);
+    float ts = 0.f;
+    for (int t = t0; t < t1 && t < T; ++t) ts += tm(t);
+    for (int o = 32; o > 0; o >>= 1) ts += __shfl_xor(ts, o);
+    auto mask = [&](int t) { return fl(t) * (t > 0 ? 1.f - tm(t - 1) : 1.f); };
+    auto Bt = [&](int t) {
+      if (t == T) return qt[T] * (1.f - ts);
+      return mask(t) * (a.reward[(int64_t)b * a.rw_sb + (int64_t)t * a.rw_st] + G1 * qt[t + 1] * (1.f - tm(t)));
+    };
+    float g = 0.f, p = 1.f;
+    for (int t = t1 - 1; t >= t0; --t) {
+      g = Bt(t) + A * g;
+      p *= A;
+    }
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const float gd = __shfl_down(g, d), pd = __shfl_down(p, d);
+      if (lane + d < 64) {
+        g = g + p * gd;
+        p = p * pd;
+      }
+    }
+    float ret = __shfl_down(g, 1);
+    if (lane == 63) ret = 0.f;
+    const float wb = a.weight ? a.weight[b] : 1.f;
+    float absum = 0.f, mb = 0.f, lb = 0.f;
+    for (int t = t1 - 1; t >= t0; --t) {
+      ret = Bt(t) + A * ret;
+      if (t == T) continue;
+      const float m = mask(t);
+      const float td = a.qtot[(size_t)b * T + t] - ret;
+      a.gq[(size_t)b * T + t] = wb * m * td / denom;
+      if (a.targets) a.targets[(size_t)b * T + t] = ret;
+      absum += fabsf(td) * m;
+      mb += m;
+      lb += 0.5f * td * td * m;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      absum += __shfl_xor(absum, o);
+      mb += __shfl_xor(mb, o);
+      lb += __shfl_xor(lb, o);
+    }
+    if (lane == 0) a.prio[b] = mb > 0.f ? absum / sqrtf(mb) : 0.f;  // an all-masked episode: 0, not 0/0
+    lsum = lb * wb;
+    msum = mb;
+  }
+  if (lane == 0) {
+    red[0][w] = lsum;
+    red[1][w] = msum;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float l = 0.f, m = 0.f;
+    for (int i = 0; i < TDW_WAVES; ++i) {
+      l += red[0][i];
+      m += red[1][i];
+    }
+    unsafeAtomicAdd(a.loss, l / denom);
+    unsafeAtomicAdd(a.loss + 1, m);
+  }
+}
+
 // mask_sum <= 0: normalise by the local Σ mask once it is complete.
 __global__ __launch_bounds__(256) void td_normalise_kernel(float* __restrict__ gq, int64_t n, float* loss) {
   const float inv = 1.0f / loss[1];  // (PyMARL2: / mask.sum())
@@ -188,6 +275,16 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
 
 }  // namespace
 
+// T2O_TD_WAVE=1 selects the one-wave-per-episode scan kernel (A/B), else the
+// sequential per-episode kernel
+static bool td_wave_scan() {
+  static const bool wave = [] {
+    const char* e = getenv("T2O_TD_WAVE");
+    return e && e[0] == '1';
+  }();
+  return wave;
+}
+
 extern "C" int t2o_td_loss_ex(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
                               int64_t rw_st, const void* term, int term_dtype, int64_t tm_sb, int64_t tm_st,
                               const void* filled, int filled_dtype, int64_t fl_sb, int64_t fl_st,
@@ -208,9 +305,13 @@ extern "C" int t2o_td_loss_ex(const float* qtot, const float* qtot_tgt, const fl
   if (ep > ep_fill) ep = ep_fill;
   if (ep < 1) return T2O_EUNSUPPORTED;
   if (hipMemsetAsync(loss, 0, 2 * sizeof(float), s) != hipSuccess) return (int)hipGetLastError();
-  (void)hipFuncSetAttribute((const void*)td_loss_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)(ep * per_ep));
-  hipLaunchKernelGGL(td_loss_kernel, dim3((B + ep - 1) / ep), dim3(256), ep * per_ep, s, a, ep);
+  if (td_wave_scan()) {
+    hipLaunchKernelGGL(td_loss_wave_kernel, dim3((B + TDW_WAVES - 1) / TDW_WAVES), dim3(64 * TDW_WAVES), 0, s, a);
+  } else {
+    (void)hipFuncSetAttribute((const void*)td_loss_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)(ep * per_ep));
+    hipLaunchKernelGGL(td_loss_kernel, dim3((B + ep - 1) / ep), dim3(256), ep * per_ep, s, a, ep);
+  }
   if (mask_sum <= 0.f)
     hipLaunchKernelGGL(td_normalise_kernel, dim3(1), dim3(256), 0, s, gq, (int64_t)B * T, loss);
   return (int)hipGetLastError();
