@@ -68,8 +68,13 @@ def parse():
                     help="skip the configs[0]-shape (16 AGVs, T=150) CPU-baseline figure")
     ap.add_argument("--mecs", type=int, default=2, help="rollout mode: MEC servers")
     ap.add_argument("--qmix-pos-func", choices=("abs", "softplus", "quadratic", "identity"), default="abs",
-                    help="the mixer head's positivity function (n_transf_mixer.py:95-103); the tuned mixer "
-                         "head is abs-only, the others run the runtime-shaped mixer kernels")
+                    help="the mixer head's positivity function (n_transf_mixer.py:95-103); the exact mixer "
+                         "instances compute abs only, so softplus / quadratic / identity run the runtime-entity "
+                         "MFMA mixer instance of the AGV count's capacity class (ops.NetShape.instance; the "
+                         "bench line's config.kernels says which)")
+    ap.add_argument("--td-algo", choices=("auto", "sequential", "wave"), default="auto",
+                    help="TD(lambda) target kernel (t2o_td_loss_ex2): the sequential per-episode recursion "
+                         "or the one-wave-per-episode suffix scan; auto = the library default")
     ap.add_argument("--priorities", choices=("device", "cpu"), default="device",
                     help="where each update's |TD errors| go: device (consumed by the device-resident "
                          "PrioritizedReplayBuffer, t2omca_amd/replay.py) or cpu (the reference driver's "
@@ -573,7 +578,8 @@ def main():
         agent = TransformerAgent(None, margs).to(dev)
         mixer = TransformerMixer(margs).to(dev)
         return TDLearner(agent, mixer, target_update_interval=10 ** 9, precision=precision,
-                         overlap=not args.serial, priorities_to_cpu=args.priorities == "cpu")
+                         overlap=not args.serial, priorities_to_cpu=args.priorities == "cpu",
+                         td_algo=args.td_algo)
 
     learner = make_learner(args.dtype)
     batch, w = make_batch(B, T, A, seed=1 + rank, device=dev)

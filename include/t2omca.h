@@ -40,6 +40,15 @@ extern "C" {
 
 #define T2O_MAX_DEPTH 4
 
+/* Bumped whenever an entry point's signature, t2o_layout, or a workspace / tape
+ * size or layout formula changes, so a binding built against one header can
+ * refuse a library built from another (t2o_abi_version).  History: 3 = round-3
+ * library (tuned one-tile mixers write one compact tape stream per block,
+ * ceil(B*T*(A+3)/16) tiles; records of 4E + 2HE features); 4 = t2o_td_loss_ex2,
+ * t2o_bwd_tape_contract_pair, t2o_abi_version. */
+#define T2O_ABI_VERSION 4
+int t2o_abi_version(void);
+
 enum {
   T2O_OK = 0,
   T2O_EINVAL = -1,      /* unsupported size / null pointer */
@@ -275,6 +284,23 @@ int t2o_td_loss_ex(const float* qtot, const float* qtot_tgt, const float* reward
                    const void* filled, int filled_dtype, int64_t fl_sb, int64_t fl_st,
                    const float* per_weight, float gamma, float td_lambda, float mask_sum, float* gq,
                    float* targets, float* prio, float* loss, int B, int T, void* stream);
+
+/* t2o_td_loss_ex2 algorithms */
+#define T2O_TD_AUTO 0        /* the library's default (currently T2O_TD_SEQUENTIAL) */
+#define T2O_TD_SEQUENTIAL 1  /* one thread per episode, the reference's backward order (T <= ~4900) */
+#define T2O_TD_WAVE_SCAN 2   /* one wave per episode: suffix scan of the linear TD(λ) recursion
+                                (reassociated: fp32 rounding differs by ~1e-7 relative; any T) */
+
+/* t2o_td_loss_ex with the algorithm chosen explicitly and, when mask_sum_acc is
+ * non-NULL, the local Σ mask also added (atomically) into *mask_sum_acc — the
+ * learner's flat gradient buffer keeps Σ mask in its last slot, so the data-parallel
+ * all-reduce sums it with the grads and Adam divides by the global value. */
+int t2o_td_loss_ex2(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
+                    int64_t rw_st, const void* term, int term_dtype, int64_t tm_sb, int64_t tm_st,
+                    const void* filled, int filled_dtype, int64_t fl_sb, int64_t fl_st,
+                    const float* per_weight, float gamma, float td_lambda, float mask_sum, float* gq,
+                    float* targets, float* prio, float* loss, float* mask_sum_acc, int algo, int B, int T,
+                    void* stream);
 
 /* clip_grad_norm_(max_grad_norm) + Adam (torch.optim.Adam semantics, L2
  * weight decay) over n floats.  workspace: t2o_adam_workspace_floats() floats

@@ -36,8 +36,17 @@ def build_td_lambda_targets(rewards, terminated, mask, target_qs, gamma, td_lamb
 
 
 def td_forward(p_agent, p_mixer, p_agent_tgt, p_mixer_tgt, batch, cfg, *, gamma=0.99, td_lambda=0.6,
-               per_weight=None, detach_mixer_hidden=False):
-    """Returns (loss, td_errors_abs [B], extras)."""
+               per_weight=None, detach_mixer_hidden=False, relu=None):
+    """Returns (loss, td_errors_abs [B], extras).  relu: an optional
+    ref_model.TieAwareRelu used for every FFN ReLU of this call (its recorded ties'
+    backward branches can then be chosen before loss.backward)."""
+    if relu is not None:
+        prev, ref_model._ffn_relu = ref_model._ffn_relu, relu
+        try:
+            return td_forward(p_agent, p_mixer, p_agent_tgt, p_mixer_tgt, batch, cfg, gamma=gamma,
+                              td_lambda=td_lambda, per_weight=per_weight, detach_mixer_hidden=detach_mixer_hidden)
+        finally:
+            ref_model._ffn_relu = prev
     obs, state = batch["obs"], batch["state"]
     actions, avail = batch["actions"], batch["avail_actions"]
     B, T1, A, _ = obs.shape

@@ -48,23 +48,31 @@ def mha(p, pre, q, k, heads):
     return F.linear(out, p[pre + "unifyheads.weight"], p[pre + "unifyheads.bias"])
 
 
-def block(p, pre, q, k, heads):
-    """transformer.py:120-140 (dropout p=0 is the identity)."""
+# The FFN's ReLU (transformer.py:113).  Tests may install a TieAwareRelu here
+# (oracle/ref_learner.py td_forward(relu=...)) to choose the backward branch of
+# pre-activations that lie within rounding of 0; None = F.relu.
+_ffn_relu = None
+
+
+def block(p, pre, q, k, heads, keep=None):
+    """transformer.py:120-140 (dropout p=0 is the identity).  keep: the token rows
+    whose block output is consumed downstream (token pruning; only a tie-aware
+    ReLU hook reads it)."""
     e = q.shape[-1]
     attended = mha(p, pre + "attention.", q, k, heads)
     x = F.layer_norm(attended + q, (e,), p[pre + "norm1.weight"], p[pre + "norm1.bias"])
     ff = F.linear(x, p[pre + "ff.0.weight"], p[pre + "ff.0.bias"])
-    ff = F.relu(ff)
+    ff = F.relu(ff) if _ffn_relu is None else _ffn_relu(ff, keep)
     ff = F.linear(ff, p[pre + "ff.2.weight"], p[pre + "ff.2.bias"])
     x = F.layer_norm(ff + x, (e,), p[pre + "norm2.weight"], p[pre + "norm2.bias"])
     return x
 
 
-def transformer(p, pre, q, k, heads, depth):
+def transformer(p, pre, q, k, heads, depth, keep=None):
     """transformer.py:169-178: keys are never updated across blocks."""
     x = q
     for d in range(depth):
-        x = block(p, f"{pre}tblocks.{d}.", x, k, heads)
+        x = block(p, f"{pre}tblocks.{d}.", x, k, heads, keep)
     return x
 
 
@@ -75,7 +83,7 @@ def agent_forward(p, inputs, hidden_state, *, n_entities, feat_dim, emb, heads, 
     hidden_state = hidden_state.reshape(-1, 1, emb)
     embs = _lin(inputs, p, "feat_embedding")
     x = torch.cat((hidden_state, embs), 1)
-    embs = transformer(p, "transformer.", x, x, heads, depth)
+    embs = transformer(p, "transformer.", x, x, heads, depth, keep=slice(0, 1))
     h = embs[:, 0:1, :]
     q = _lin(h, p, "q_basic")
     return q.view(b, a, -1), h.view(b, a, -1)
@@ -92,7 +100,7 @@ def mixer_forward(p, qvals, hidden_states, hyper_weights, states, *, n_agents, n
         inputs = obs.reshape(b, n_agents * n_entities, feat_dim)
     embs = _lin(inputs, p, "feat_embedding")
     x = torch.cat((embs, hidden_states, hyper_weights), 1)
-    embs = transformer(p, "transformer.", x, x, heads, depth)
+    embs = transformer(p, "transformer.", x, x, heads, depth, keep=slice(x.shape[1] - n_agents - 3, None))
     w1 = embs[:, -3 - n_agents:-3, :]
     b1 = embs[:, -3, :].view(-1, 1, emb)
     w2 = embs[:, -2, :].view(-1, emb, 1)
@@ -179,3 +187,50 @@ def init_params(kind, cfg, seed, dtype=torch.float32):
         if bias:
             p[name + ".bias"] = ((torch.rand(shp[0], generator=g) * 2 - 1) * bound).to(dtype)
     return p
+
+
+class _MaskedRelu(torch.autograd.Function):
+    """relu(x) = x * mask with mask = [x > 0]; the backward multiplies by the mask
+    as it is WHEN THE BACKWARD RUNS, so a caller may flip entries between
+    backward passes of one graph (TieAwareRelu)."""
+
+    @staticmethod
+    def forward(ctx, x, mask):
+        ctx.mask = mask  # not save_for_backward: it is meant to be edited in place
+        return x * mask
+
+    @staticmethod
+    def backward(ctx, g):
+        return g * ctx.mask, None
+
+
+class TieAwareRelu:
+    """FFN ReLU that records every pre-activation of a consumed token row lying
+    within `margin` of 0 (a "tie": fp32 arithmetic in any summation order may put
+    it on the other side of 0 than fp64 does) and lets the caller choose each tie's
+    backward branch.  The forward value at a tie differs between the branches by
+    less than `margin`, so only the backward is overridden; ties are recorded in
+    execution order, for tensors that require grad (the online networks)."""
+
+    def __init__(self, margin):
+        self.margin = margin
+        self.ties = []  # (mask tensor, flat index, fp64 pre-activation)
+
+    def __call__(self, x, keep):
+        mask = (x.detach() > 0).to(x.dtype)
+        if x.requires_grad:
+            near = x.detach().abs() < self.margin
+            if keep is not None:
+                kept = torch.zeros_like(near)
+                kept[:, keep] = True
+                near &= kept
+            for i in near.reshape(-1).nonzero().reshape(-1).tolist():
+                self.ties.append((mask, i, float(x.detach().reshape(-1)[i])))
+        return _MaskedRelu.apply(x, mask)
+
+    def branches(self):
+        return [bool(m.reshape(-1)[i] > 0) for m, i, _ in self.ties]
+
+    def set_branches(self, on):
+        for (m, i, _), b in zip(self.ties, on):
+            m.reshape(-1)[i] = 1.0 if b else 0.0

@@ -11,6 +11,7 @@ import torch
 from .build import LIB
 
 MAX_DEPTH = 4
+ABI_VERSION = 4  # include/t2omca.h T2O_ABI_VERSION this binding mirrors
 _I64x = ctypes.c_int64 * MAX_DEPTH
 
 
@@ -81,6 +82,12 @@ EXPORTS = {
                        [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_int64] * 2 +
                        [ctypes.c_void_p] + [ctypes.c_float] * 3 + [ctypes.c_void_p] * 4 +
                        [ctypes.c_int] * 2 + [ctypes.c_void_p]),
+    "t2o_td_loss_ex2": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_int64] * 2 +
+                        [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_int64] * 2 +
+                        [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_int64] * 2 +
+                        [ctypes.c_void_p] + [ctypes.c_float] * 3 + [ctypes.c_void_p] * 5 +
+                        [ctypes.c_int] * 3 + [ctypes.c_void_p]),
+    "t2o_abi_version": (ctypes.c_int, []),
     "t2o_adam_step": (ctypes.c_int, [ctypes.c_void_p] * 5 + [ctypes.c_int64] + [ctypes.c_double] * 3 +
                       [ctypes.c_float] * 3 + [ctypes.c_int64] + [ctypes.c_void_p] * 3),
     "t2o_adam_workspace_floats": (ctypes.c_int, []),
@@ -107,7 +114,7 @@ EXPORTS = {
 
 # exports only tests / tools call (never on the product path), and the newest
 # reporting export: an older build loaded under A/B timing (T2O_LIB) may lack them
-_DIAGNOSTIC = {"t2o_bf_swz", "t2o_probe_lane_ops", "t2o_layout_instance"}
+_DIAGNOSTIC = {"t2o_bf_swz", "t2o_probe_lane_ops", "t2o_layout_instance", "t2o_abi_version", "t2o_td_loss_ex2"}
 
 _lib = None
 
@@ -128,6 +135,9 @@ def lib():
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args
+        if hasattr(h, "t2o_abi_version") and h.t2o_abi_version() != ABI_VERSION and path == LIB:
+            raise RuntimeError(f"t2omca_amd: {path} has C-ABI version {h.t2o_abi_version()}, this binding "
+                               f"mirrors include/t2omca.h version {ABI_VERSION}; rebuild the library")
         _lib = h
     return _lib
 

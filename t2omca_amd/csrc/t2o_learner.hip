@@ -12,7 +12,6 @@
 // and torch.nn.utils.clip_grad_norm_ + torch.optim.Adam (non-amsgrad, L2
 // weight decay) on the flat parameter buffer.
 #include <math.h>
-#include <stdlib.h>
 
 #include "t2o_common.hpp"
 
@@ -32,6 +31,7 @@ struct TDArgs {
   float* targets;         // [B][T]  (may be null)
   float* prio;            // [B]
   float* loss;            // [2]: loss, Σ mask
+  float* mask_acc;        // optional: += Σ mask (the learner's grad[-1] slot)
   int B, T;
   int tm_dt, fl_dt;       // T2O_DT_* (t2omca.h): the EpisodeBatch's own dtypes, read in place
 };
@@ -124,6 +124,7 @@ __global__ __launch_bounds__(256) void td_loss_kernel(TDArgs a, int EP) {
   if (threadIdx.x == 0) {
     unsafeAtomicAdd(a.loss, lsum / denom);
     unsafeAtomicAdd(a.loss + 1, msum);
+    if (a.mask_acc) unsafeAtomicAdd(a.mask_acc, msum);
   }
 }
 
@@ -210,6 +211,7 @@ __global__ __launch_bounds__(64 * TDW_WAVES) void td_loss_wave_kernel(TDArgs a) 
     }
     unsafeAtomicAdd(a.loss, l / denom);
     unsafeAtomicAdd(a.loss + 1, m);
+    if (a.mask_acc) unsafeAtomicAdd(a.mask_acc, m);
   }
 }
 
@@ -275,39 +277,32 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
 
 }  // namespace
 
-// T2O_TD_WAVE=1 selects the one-wave-per-episode scan kernel (A/B), else the
-// sequential per-episode kernel
-static bool td_wave_scan() {
-  static const bool wave = [] {
-    const char* e = getenv("T2O_TD_WAVE");
-    return e && e[0] == '1';
-  }();
-  return wave;
-}
-
-extern "C" int t2o_td_loss_ex(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
-                              int64_t rw_st, const void* term, int term_dtype, int64_t tm_sb, int64_t tm_st,
-                              const void* filled, int filled_dtype, int64_t fl_sb, int64_t fl_st,
-                              const float* per_weight, float gamma, float td_lambda, float mask_sum, float* gq,
-                              float* targets, float* prio, float* loss, int B, int T, void* stream) {
+extern "C" int t2o_td_loss_ex2(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
+                               int64_t rw_st, const void* term, int term_dtype, int64_t tm_sb, int64_t tm_st,
+                               const void* filled, int filled_dtype, int64_t fl_sb, int64_t fl_st,
+                               const float* per_weight, float gamma, float td_lambda, float mask_sum, float* gq,
+                               float* targets, float* prio, float* loss, float* mask_sum_acc, int algo, int B,
+                               int T, void* stream) {
   if (!qtot || !qtot_tgt || !reward || !gq || !prio || !loss || B < 1 || T < 1) return T2O_EINVAL;
   auto dt_ok = [](int dt) { return dt == T2O_DT_F32 || dt == T2O_DT_U8 || dt == T2O_DT_I32 || dt == T2O_DT_I64; };
   if (!dt_ok(term_dtype) || !dt_ok(filled_dtype)) return T2O_EINVAL;
+  if (algo < T2O_TD_AUTO || algo > T2O_TD_WAVE_SCAN) return T2O_EINVAL;
   TDArgs a{qtot, qtot_tgt, reward, term, filled, per_weight, rw_sb, rw_st, tm_sb, tm_st, fl_sb, fl_st,
-           gamma, td_lambda, mask_sum, gq, targets, prio, loss, B, T, term_dtype, filled_dtype};
+           gamma, td_lambda, mask_sum, gq, targets, prio, loss, mask_sum_acc, B, T, term_dtype, filled_dtype};
   hipStream_t s = (hipStream_t)stream;
-  const size_t per_ep = sizeof(float) * (5 * (size_t)T + 1);
-  // episodes per workgroup: few enough that the grid covers the CUs (the
-  // staging loads, not the per-episode scan, dominate a fat workgroup)
-  int ep = (int)((96 * 1024) / per_ep);
-  if (ep > 64) ep = 64;
-  const int ep_fill = (B + 255) / 256;
-  if (ep > ep_fill) ep = ep_fill;
-  if (ep < 1) return T2O_EUNSUPPORTED;
+  const bool wave = algo == T2O_TD_WAVE_SCAN;  // (AUTO = the sequential kernel: the reference's order)
   if (hipMemsetAsync(loss, 0, 2 * sizeof(float), s) != hipSuccess) return (int)hipGetLastError();
-  if (td_wave_scan()) {
+  if (wave) {
     hipLaunchKernelGGL(td_loss_wave_kernel, dim3((B + TDW_WAVES - 1) / TDW_WAVES), dim3(64 * TDW_WAVES), 0, s, a);
   } else {
+    const size_t per_ep = sizeof(float) * (5 * (size_t)T + 1);
+    // episodes per workgroup: few enough that the grid covers the CUs (the
+    // staging loads, not the per-episode scan, dominate a fat workgroup)
+    int ep = (int)((96 * 1024) / per_ep);
+    if (ep > 64) ep = 64;
+    const int ep_fill = (B + 255) / 256;
+    if (ep > ep_fill) ep = ep_fill;
+    if (ep < 1) return T2O_EUNSUPPORTED;  // T beyond the LDS staging (> ~4900 steps): use the wave scan
     (void)hipFuncSetAttribute((const void*)td_loss_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)(ep * per_ep));
     hipLaunchKernelGGL(td_loss_kernel, dim3((B + ep - 1) / ep), dim3(256), ep * per_ep, s, a, ep);
@@ -315,6 +310,16 @@ extern "C" int t2o_td_loss_ex(const float* qtot, const float* qtot_tgt, const fl
   if (mask_sum <= 0.f)
     hipLaunchKernelGGL(td_normalise_kernel, dim3(1), dim3(256), 0, s, gq, (int64_t)B * T, loss);
   return (int)hipGetLastError();
+}
+
+extern "C" int t2o_td_loss_ex(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
+                              int64_t rw_st, const void* term, int term_dtype, int64_t tm_sb, int64_t tm_st,
+                              const void* filled, int filled_dtype, int64_t fl_sb, int64_t fl_st,
+                              const float* per_weight, float gamma, float td_lambda, float mask_sum, float* gq,
+                              float* targets, float* prio, float* loss, int B, int T, void* stream) {
+  return t2o_td_loss_ex2(qtot, qtot_tgt, reward, rw_sb, rw_st, term, term_dtype, tm_sb, tm_st, filled,
+                         filled_dtype, fl_sb, fl_st, per_weight, gamma, td_lambda, mask_sum, gq, targets, prio,
+                         loss, nullptr, T2O_TD_AUTO, B, T, stream);
 }
 
 extern "C" int t2o_td_loss(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,

@@ -332,6 +332,8 @@ extern "C" int t2o_layout_init_ex(t2o_layout* L, int kind, int E, int H, int D, 
 
 extern "C" int t2o_layout_sizeof(void) { return (int)sizeof(t2o_layout); }
 
+extern "C" int t2o_abi_version(void) { return T2O_ABI_VERSION; }
+
 extern "C" int64_t t2o_param_count(int kind, int E, int H, int D, int F, int NA, int FF) {
   return param_offsets(kind, E, H, D, F, NA, FF).total;
 }

@@ -53,7 +53,7 @@ class TDLearner:
     def __init__(self, agent, mixer, *, lr=1e-3, gamma=0.99, td_lambda=0.6, grad_norm_clip=10.0,
                  target_update_interval=200, optim_betas=(0.9, 0.999), optim_eps=1e-8, weight_decay=0.0,
                  detach_mixer_hidden=False, process_group=None, priorities_to_cpu=True, precision="fp32",
-                 overlap=True):
+                 overlap=True, td_algo="auto"):
         dev = next(agent.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("TDLearner needs the modules on a HIP device (no CPU fallback)")
@@ -89,6 +89,7 @@ class TDLearner:
         self.detach_mixer_hidden = detach_mixer_hidden
         self.priorities_to_cpu = priorities_to_cpu
         self.overlap = overlap  # mixer tape contraction on a side stream beside the agent BPTT
+        self.td_algo = td_algo  # ops.TD_ALGOS
         self.step_count = 0
         self.last_target_update_episode = 0
         self.timer = None   # optional callable(tag) recording HIP events around the big kernels
@@ -274,8 +275,10 @@ class TDLearner:
                                           timer=self.timer)
         # 3. TD(λ) targets / loss (un-normalised: Σ mask is applied in Adam so the
         #    data-parallel sum over ranks divides by the GLOBAL Σ mask)
+        #    (Σ mask also lands in grad[-1] straight from the kernel: grad was cleared
+        #    on the side stream before the mixer forward, which waited for it)
         td = ops.td_loss(o_on["y"], o_tg["y"], reward, term, filled, w, gamma=self.gamma,
-                         td_lambda=self.td_lambda, mask_sum=1.0)
+                         td_lambda=self.td_lambda, mask_sum=1.0, algo=self.td_algo, mask_sum_acc=self.grad[-1:])
         # 4. mixer BPTT.  Its weight-grad tape contraction (HBM-bound) runs on a
         #    side stream, overlapping the agent BPTT (latency-bound, half the SIMDs)
         tape_m = self._slab("tape_m", ops.tape_floats(self.sm, ops.mixer_tape_tiles(B, T, A, self.sm)))
@@ -286,7 +289,6 @@ class TDLearner:
                                                         defer_contract=True)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            self.grad[-1:].copy_(td["loss"][1:2])
             gm = contract_m()
             # mixer grads in reference parameter order, still off the critical path
             ops.unpack_grads(self.sm, self.params[self.na:], gm, self.grad[self.na:self.na + self.nm])

@@ -67,7 +67,10 @@ class _PackCache:
     storage pointer and autograd version counter: optimiser steps,
     ``load_state_dict`` and ``copy_`` bump the version, re-binding a parameter
     changes its pointer, so a stale pack is never used.  A rebuild allocates new
-    tensors, so a pack saved for an earlier backward is never overwritten."""
+    tensors, so a pack saved for an earlier backward is never overwritten.
+    Writes the version counter cannot see — through ``p.data`` (``p.data.copy_``
+    shares the storage, not the counter) or through raw device pointers (the
+    learner's Adam kernel) — must be followed by ``invalidate()``."""
 
     def __init__(self):
         self.key = None

@@ -330,13 +330,19 @@ def _mask_dtype(t):
     return _MASK_DT[t.dtype]
 
 
+TD_ALGOS = {"auto": 0, "sequential": 1, "wave": 2}  # include/t2omca.h T2O_TD_*
+
+
 def td_loss(qtot, qtot_tgt, reward, terminated=None, filled=None, per_weight=None, gamma=0.99,
-            td_lambda=0.6, mask_sum=0.0):
+            td_lambda=0.6, mask_sum=0.0, algo="auto", mask_sum_acc=None):
     """TD(λ) targets / loss / grads / priorities (PyMARL2 NQLearner contract).
     qtot [B,T], qtot_tgt [B,T+1]; reward [B, >=T] float view; terminated / filled
     [B, >=T] views in float32, uint8/bool, int32 or int64 (read in place).
+    algo: "sequential" (the reference's backward order, one thread per episode),
+    "wave" (one wave per episode, suffix scan) or "auto" (the library default).
+    mask_sum_acc: optional 1-float device tensor that receives += Σ mask.
     Returns dict(gq [B,T], targets [B,T], prio [B], loss [2])."""
-    _dev(qtot, qtot_tgt, reward, per_weight)
+    _dev(qtot, qtot_tgt, reward, per_weight, mask_sum_acc)
     for m in (terminated, filled):  # any mask dtype of _MASK_DT, device-resident
         if m is not None and not m.is_cuda:
             raise RuntimeError("t2omca_amd ops need HIP-device tensors (no CPU fallback)")
@@ -347,11 +353,16 @@ def td_loss(qtot, qtot_tgt, reward, terminated=None, filled=None, per_weight=Non
     out = dict(gq=torch.empty(B, T, device=dev), targets=torch.empty(B, T, device=dev),
                prio=torch.empty(B, device=dev), loss=torch.empty(2, device=dev))
     rs, ts, fs = _mstrides(reward), _mstrides(terminated), _mstrides(filled)
-    check(lib().t2o_td_loss_ex(ptr(qtot), ptr(qtot_tgt), ptr(reward), rs[0], rs[1], ptr(terminated),
-                               _mask_dtype(terminated), ts[0], ts[1], ptr(filled), _mask_dtype(filled), fs[0],
-                               fs[1], ptr(per_weight), float(gamma), float(td_lambda), float(mask_sum),
-                               ptr(out["gq"]), ptr(out["targets"]), ptr(out["prio"]), ptr(out["loss"]), B, T,
-                               stream_ptr()), "td_loss")
+    args = (ptr(qtot), ptr(qtot_tgt), ptr(reward), rs[0], rs[1], ptr(terminated), _mask_dtype(terminated), ts[0],
+            ts[1], ptr(filled), _mask_dtype(filled), fs[0], fs[1], ptr(per_weight), float(gamma), float(td_lambda),
+            float(mask_sum), ptr(out["gq"]), ptr(out["targets"]), ptr(out["prio"]), ptr(out["loss"]))
+    if hasattr(lib(), "t2o_td_loss_ex2"):
+        check(lib().t2o_td_loss_ex2(*args, ptr(mask_sum_acc), TD_ALGOS[algo], B, T, stream_ptr()), "td_loss")
+    else:  # an older build under A/B timing (T2O_LIB)
+        assert algo == "auto"
+        check(lib().t2o_td_loss_ex(*args, B, T, stream_ptr()), "td_loss")
+        if mask_sum_acc is not None:
+            mask_sum_acc.add_(out["loss"][1:2])
     return out
 
 

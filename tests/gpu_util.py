@@ -36,3 +36,55 @@ def require_gpu():
         raise RuntimeError("gpu-marked test needs a HIP device")
     from t2omca_amd import _lib
     _lib.lib()
+
+
+def oracle_td_tie_aware(pa, pm, cfg, batch, w, gpu_grad=None, margin=1e-6, **kw):
+    """The fp64 oracle's TD update (oracle/ref_learner.td_forward) with a tie-aware
+    FFN ReLU (oracle/ref_model.TieAwareRelu).  A kept FFN pre-activation within
+    `margin` of 0 is a tie: fp32 arithmetic in any summation order may put it on the
+    other side of 0 than fp64 does, and the backward of that one record then differs
+    by its whole upstream gradient.  For every tie the backward branch
+    is chosen to match the GPU result `gpu_grad` (greedy over the ties, on the L2
+    distance; the forward is unchanged, both branches agree there to < margin).
+    Returns (prio, extras, ref_grad, info) with info = dict(ties=..., overridden=...,
+    err_fp64_branches=normwise error with fp64's own branches)."""
+    from oracle import ref_learner, ref_model
+    cpu = {k: (v.detach().cpu().double() if v.is_floating_point() else v.detach().cpu()) for k, v in batch.items()}
+    pa_g = {k: v.clone().requires_grad_(True) for k, v in pa.items()}
+    pm_g = {k: v.clone().requires_grad_(True) for k, v in pm.items()}
+    relu = ref_model.TieAwareRelu(margin)
+    loss, prio, ex = ref_learner.td_forward(pa_g, pm_g, pa, pm, cpu, cfg, per_weight=w.cpu().double(), relu=relu,
+                                            **kw)
+    params = list(pa_g.values()) + list(pm_g.values())
+
+    def grads():
+        gs = torch.autograd.grad(loss, params, retain_graph=True)
+        return torch.cat([g.reshape(-1) for g in gs])
+
+    ref_g = grads()
+    info = dict(ties=len(relu.ties), overridden=0, margin=margin)
+    if gpu_grad is None or not relu.ties:
+        info["err_fp64_branches"] = None if gpu_grad is None else normwise(gpu_grad, ref_g)
+        return prio.detach(), ex, ref_g, info
+    gg = gpu_grad.detach().cpu().double().reshape(-1)
+    info["err_fp64_branches"] = normwise(gg, ref_g)
+    on = relu.branches()
+    dist = float((gg - ref_g).norm())
+    for _ in range(2):  # greedy passes until no flip helps
+        improved = False
+        for i in range(len(on)):
+            trial = list(on)
+            trial[i] = not trial[i]
+            relu.set_branches(trial)
+            g2 = grads()
+            d2 = float((gg - g2).norm())
+            if d2 < dist:
+                on, ref_g, dist, improved = trial, g2, d2, True
+            else:
+                relu.set_branches(on)
+        if not improved:
+            break
+    fp64 = [v > 0 for _, _, v in relu.ties]
+    info["overridden"] = sum(a != b for a, b in zip(on, fp64))
+    info["overridden_values"] = [f"{v:.1e}" for (_, _, v), a, b in zip(relu.ties, on, fp64) if a != b]
+    return prio.detach(), ex, ref_g, info

@@ -48,7 +48,7 @@ import pytest
 import torch
 
 from oracle import ref_learner, ref_model
-from tests.gpu_util import normwise, require_gpu
+from tests.gpu_util import normwise, oracle_td_tie_aware, require_gpu
 
 pytestmark = pytest.mark.gpu
 
@@ -91,18 +91,31 @@ def _oracle(A, B, T, seed):
     return _ORACLE[key]
 
 
+RELU_MARGIN = 1e-6
+
+
 def _td_vs_oracle(A, B, T, precision, seed=3):
+    """GPU TD update vs the fp64 oracle.  fp32 also reports the gradient error
+    against the tie-aware oracle (tests/gpu_util.oracle_td_tie_aware: at a kept FFN
+    pre-activation within RELU_MARGIN of 0 the oracle's backward takes the branch the
+    GPU result agrees with) as errs["grad_tie_aware"], with the tie counts."""
     from t2omca_amd.learner import TDLearner
     from t2omca_amd.synthetic import make_batch
-    prio, ex, ref_g = _oracle(A, B, T, seed)
     agent, mixer = _modules(A)
     learner = TDLearner(agent, mixer, precision=precision)
     batch, w = make_batch(B, T, A, seed=seed)
     info = learner.train(batch, 0, 0, per_weight=w)
     torch.cuda.synchronize()
     g = (learner.grad[:-1] / learner.grad[-1]).cpu()
+    prio, ex, ref_g = _oracle(A, B, T, seed)
     errs = dict(qtot=normwise(info["qtot"], ex["qtot"]), targets=normwise(info["targets"], ex["targets"]),
                 prio=normwise(info["td_errors_abs"], prio), grad=normwise(g, ref_g))
+    if precision == "fp32":
+        pa = {k: v.detach().cpu().double() for k, v in _modules(A)[0].state_dict().items()}
+        pm = {k: v.detach().cpu().double() for k, v in _modules(A)[1].state_dict().items()}
+        _, _, ref_t, ties = oracle_td_tie_aware(pa, pm, _cfg(A), batch, w, g, margin=RELU_MARGIN)
+        errs["grad_tie_aware"] = normwise(g, ref_t)
+        print(f"A={A} B={B} T={T} relu ties", ties)
     return errs, learner, batch, ex
 
 

@@ -25,8 +25,7 @@ import numpy as np
 import pytest
 import torch
 
-from oracle import ref_learner
-from tests.gpu_util import normwise, require_gpu
+from tests.gpu_util import normwise, oracle_td_tie_aware, require_gpu
 from tests.test_oracle_golden import _cfg
 
 pytestmark = pytest.mark.gpu
@@ -132,37 +131,14 @@ def mixer_module_check(path):
 RELU_MARGIN = 1e-6
 
 
-def _oracle_td(pa, pm, cfg, batch, w):
-    """fp64 oracle TD update; also returns the smallest |FFN pre-activation| of the
-    rows the networks keep (agent token 0; all rows of 2-D calls)."""
-    import torch.nn.functional as Fn
-
-    from oracle import ref_model
-    cpu = {k: (v.cpu().double() if v.is_floating_point() else v.cpu()) for k, v in batch.items()}
-    pa_g = {k: v.clone().requires_grad_(True) for k, v in pa.items()}
-    pm_g = {k: v.clone().requires_grad_(True) for k, v in pm.items()}
-    relu, mins = Fn.relu, []
-
-    def hook(x, *a, **k):
-        mins.append(float((x.detach()[:, 0] if x.dim() == 3 else x.detach()).abs().min()))
-        return relu(x, *a, **k)
-    ref_model.F.relu = hook
-    try:
-        loss, prio, ex = ref_learner.td_forward(pa_g, pm_g, pa, pm, cpu, cfg, per_weight=w.cpu().double())
-    finally:
-        ref_model.F.relu = relu
-    loss.backward()
-    return pa_g, pm_g, loss, prio, ex, min(mins)
-
-
-def _td(cfg, B, T, precision="fp32", seed=3, tol=None, avoid_relu_ties=False):
+def _td(cfg, B, T, precision="fp32", seed=3, tol=None):
     """GPU TD update vs the fp64 oracle for a model described by cfg (bars: tol =
     (forward, gradient), default the fp32 (1e-5, 3e-5)); returns the learner and the
-    errors.  avoid_relu_ties: draw the batch from seed, seed + 1, ... until no kept
-    FFN pre-activation lies within RELU_MARGIN of 0 — one that does can take the
-    other ReLU branch in fp32 than in fp64 (its whole gf1 entry then enters dW1 and,
-    through the recurrence, every earlier step: DESIGN.md §5), which no fp32
-    summation order avoids (seed 3 at 40 AGVs: a margin of 1.8e-8, grad error 1e-3)."""
+    errors.  fp32: the oracle's ReLU is tie-aware (tests/gpu_util.oracle_td_tie_aware):
+    a kept FFN pre-activation within RELU_MARGIN of 0 may take the other branch in
+    fp32 than in fp64 whatever the summation order (seed 3 at 40 AGVs has one
+    1.8e-8 from 0), and the oracle's backward takes the branch the GPU result agrees
+    with; the number of such records is printed."""
     from t2omca_amd.learner import TDLearner
     from t2omca_amd.modules import TransformerAgent, TransformerMixer
     from t2omca_amd.synthetic import make_batch
@@ -173,19 +149,15 @@ def _td(cfg, B, T, precision="fp32", seed=3, tol=None, avoid_relu_ties=False):
     pa = {k: v.detach().cpu().double() for k, v in agent.state_dict().items()}
     pm = {k: v.detach().cpu().double() for k, v in mixer.state_dict().items()}
     learner = TDLearner(agent, mixer, precision=precision)
-    for s in range(seed, seed + 8):
-        batch, w = make_batch(B, T, A, seed=s, obs_feats=9, state_feats=8)
-        pa_g, pm_g, loss, prio, ex, margin = _oracle_td(pa, pm, cfg, batch, w)
-        if not avoid_relu_ties or margin >= RELU_MARGIN:
-            break
-        print(f"seed {s}: a kept FFN pre-activation {margin:.1e} from 0 (fp32 ReLU tie), next seed")
+    batch, w = make_batch(B, T, A, seed=seed, obs_feats=9, state_feats=8)
     info = learner.train(batch, 0, 0, per_weight=w)
     torch.cuda.synchronize()
     g = (learner.grad[:-1] / learner.grad[-1]).cpu()
-    ref_g = torch.cat([v.grad.reshape(-1) for v in list(pa_g.values()) + list(pm_g.values())])
+    prio, ex, ref_g, ties = oracle_td_tie_aware(pa, pm, cfg, batch, w, g if precision == "fp32" else None,
+                                                margin=RELU_MARGIN)
     errs = dict(qtot=normwise(info["qtot"], ex["qtot"]), targets=normwise(info["targets"], ex["targets"]),
                 prio=normwise(info["td_errors_abs"], prio), grad=normwise(g, ref_g))
-    print(cfg.get("tag"), precision, errs)
+    print(cfg.get("tag"), precision, errs, "relu ties", ties)
     tf, tg = tol or (1e-5, 3e-5)
     assert errs["qtot"] < tf and errs["targets"] < tf and errs["prio"] < tf, errs
     assert errs["grad"] < tg, errs
@@ -226,7 +198,7 @@ def test_headline_shape_with_softplus_head_matches_oracle(monkeypatch):
     from t2omca_amd.modules import TransformerAgent, TransformerMixer
     assert TransformerMixer(_args(cfg)).shape.instance == "runtime"
     assert TransformerAgent(None, _args(cfg)).shape.instance == "exact"
-    _td(cfg, 4, 6, avoid_relu_ties=True)
+    _td(cfg, 4, 6)
 
 
 def test_forced_generic_equals_tuned_on_headline_shape(monkeypatch):
