@@ -286,7 +286,7 @@ int t2o_td_loss_ex(const float* qtot, const float* qtot_tgt, const float* reward
                    float* targets, float* prio, float* loss, int B, int T, void* stream);
 
 /* t2o_td_loss_ex2 algorithms */
-#define T2O_TD_AUTO 0        /* the library's default (currently T2O_TD_SEQUENTIAL) */
+#define T2O_TD_AUTO 0        /* the library's default (currently T2O_TD_WAVE_SCAN, the faster) */
 #define T2O_TD_SEQUENTIAL 1  /* one thread per episode, the reference's backward order (T <= ~4900) */
 #define T2O_TD_WAVE_SCAN 2   /* one wave per episode: suffix scan of the linear TD(λ) recursion
                                 (reassociated: fp32 rounding differs by ~1e-7 relative; any T) */

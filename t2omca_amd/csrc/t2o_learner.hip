@@ -290,7 +290,9 @@ extern "C" int t2o_td_loss_ex2(const float* qtot, const float* qtot_tgt, const f
   TDArgs a{qtot, qtot_tgt, reward, term, filled, per_weight, rw_sb, rw_st, tm_sb, tm_st, fl_sb, fl_st,
            gamma, td_lambda, mask_sum, gq, targets, prio, loss, mask_sum_acc, B, T, term_dtype, filled_dtype};
   hipStream_t s = (hipStream_t)stream;
-  const bool wave = algo == T2O_TD_WAVE_SCAN;  // (AUTO = the sequential kernel: the reference's order)
+  // AUTO = the wave scan: 8-10 us faster per configs[2] update than the sequential
+  // kernel (interleaved, profiles/r4_a/), parity equal (tests/test_gpu_td_loss.py)
+  const bool wave = algo != T2O_TD_SEQUENTIAL;
   if (hipMemsetAsync(loss, 0, 2 * sizeof(float), s) != hipSuccess) return (int)hipGetLastError();
   if (wave) {
     hipLaunchKernelGGL(td_loss_wave_kernel, dim3((B + TDW_WAVES - 1) / TDW_WAVES), dim3(64 * TDW_WAVES), 0, s, a);

@@ -17,8 +17,8 @@ in seconds:
 Oracle: oracle/ref_learner.td_forward in fp64 (pinned to the reference modules'
 goldens by tests/test_oracle_golden.py; TD semantics parity-unpinned).
 Bars (normwise max|Δ| / max|ref|):
-  fp32   Q_tot, targets, priorities <= 1e-5; parameter gradients <= 2e-4 at these
-         horizons (3e-5 at the short-horizon tests, tests/test_gpu_learner.py);
+  fp32   Q_tot, targets, priorities <= 1e-5; parameter gradients <= 3e-5 against the
+         tie-aware oracle (below);
   bf16   Q_tot, targets, priorities <= 2e-2; gradients <= 6e-2; agent Q at every
          t <= 4e-2 (bf16 MFMA operands, fp32 accumulation / LayerNorm / softmax /
          recurrent state).  Measured on the box (profiles/r3_a/pytest.log), bf16:
@@ -32,15 +32,18 @@ Bars (normwise max|Δ| / max|ref|):
                                   1.8e-2 at t=59, 2.0e-2 max.
          (the rounding of the recurrent input to bf16 operands compounds over the
          unroll and then saturates; SURVEY §8c's all-bf16 probe: 4.5e-2).
-Why the fp32 gradient bar is wider over 60-150-step BPTT: an FFN pre-activation
-within fp32 rounding of 0 takes the other ReLU branch than in fp64, and that one
-record's whole gf1 entry (not a rounding-sized amount) enters dW1 and, through the
-recurrence, every earlier step's gradient.  With ~2M ReLU evaluations per update at
-configs[2]'s slice such a flip happens about once per run, in the CPU fp32 path too:
-the reference-order CPU restatement in fp32 vs fp64 gives 1.7e-7 - 3.0e-7 on seeds
-3-9 and 2.9e-5 on seed 10 (same shapes); the GPU path measured 8.6e-7, 2.2e-5 and
-6.0e-5 on seeds 4, 5 and 3.  Q_tot, targets and priorities (forward quantities) stay
-at 2e-7 - 5e-7.
+The fp32 gradient check and ReLU ties: an FFN pre-activation within fp32 rounding
+of 0 can take the other ReLU branch than in fp64 whatever the summation order, and
+that one record's whole upstream gradient (not a rounding-sized amount) then enters
+dW1 and, through the recurrence, every earlier step.  With ~2M ReLU evaluations per
+update at configs[2]'s slice that happens about once per run.  The oracle's FFN ReLU
+is therefore tie-aware (tests/gpu_util.oracle_td_tie_aware): at every kept
+pre-activation within 1e-6 of 0 its backward takes the branch the GPU result agrees
+with, and the test prints how many there were.  Measured (profiles/r4_a/pytest.log):
+configs[2] 7 ties, 1 overridden (a pre-activation of -9.7e-9): gradient error
+5.97e-5 with fp64's branches, 6.3e-7 tie-aware; configs[0] 15 ties / 3 overridden,
+4.7e-6 -> 3.6e-6; configs[3] 8 / 2, 7.3e-7 -> 7.2e-7.  Q_tot, targets and
+priorities (forward quantities) are not affected (2e-7 - 6e-7).
 """
 import dataclasses
 
@@ -52,7 +55,7 @@ from tests.gpu_util import normwise, oracle_td_tie_aware, require_gpu
 
 pytestmark = pytest.mark.gpu
 
-TOL = {"fp32": dict(q=1e-5, g=2e-4, qt=1e-5), "bf16": dict(q=2e-2, g=6e-2, qt=4e-2)}
+TOL = {"fp32": dict(q=1e-5, g=3e-5, qt=1e-5), "bf16": dict(q=2e-2, g=6e-2, qt=4e-2)}
 
 
 def _cfg(A):
@@ -138,7 +141,8 @@ def _check(errs, precision):
     tol = TOL[precision]
     print(precision, {k: f"{v:.2e}" for k, v in errs.items()})
     assert errs["qtot"] < tol["q"] and errs["targets"] < tol["q"] and errs["prio"] < tol["q"], errs
-    assert errs["grad"] < tol["g"], errs
+    # fp32: against the tie-aware oracle (_td_vs_oracle); bf16: plain
+    assert errs.get("grad_tie_aware", errs["grad"]) < tol["g"], errs
 
 
 @pytest.mark.parametrize("precision", ["fp32", "bf16"])
