@@ -56,11 +56,16 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=16, help="episodes in the CPU-baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
-    ap.add_argument("--mode", choices=("train", "forward", "rollout", "expand", "dropin"), default="train",
+    ap.add_argument("--mode", choices=("train", "forward", "rollout", "expand", "dropin", "loop"), default="train",
                     help="train: the TD update (the BASELINE metric); forward: online agent + mixer "
                          "unroll only (configs[1], inference over a replay batch); rollout: closed-loop "
                          "env step + agent step + ε-greedy over --envs envs per GPU (configs[4]); dropin: "
-                         "per-call cost of the drop-in modules' per-step forward")
+                         "per-call cost of the drop-in modules' per-step forward; loop: the driver's whole "
+                         "cycle (per_run.py:212-238): rollout of --envs envs -> insert -> PER sample -> "
+                         "TD update -> update_priorities, --updates-per-rollout updates of --batch episodes")
+    ap.add_argument("--updates-per-rollout", type=int, default=8,
+                    help="loop mode: learner updates per rollout (default 8 x 1024 episodes = the 8192 "
+                         "episodes each rollout collects)")
     ap.add_argument("--envs", type=int, default=8192, help="rollout mode: envs per GPU")
     ap.add_argument("--compact-obs", action="store_true",
                     help="rollout mode: store obs in the compact wire format (SURVEY.md §8 f3)")
@@ -72,6 +77,9 @@ def parse():
                          "instances compute abs only, so softplus / quadratic / identity run the runtime-entity "
                          "MFMA mixer instance of the AGV count's capacity class (ops.NetShape.instance; the "
                          "bench line's config.kernels says which)")
+    ap.add_argument("--contract", choices=("pair", "side"), default="pair",
+                    help="weight-gradient tape contractions: pair = both in one launch after the agent BPTT "
+                         "(default); side = the mixer's on a side stream issued before the agent BPTT")
     ap.add_argument("--td-algo", choices=("auto", "sequential", "wave"), default="auto",
                     help="TD(lambda) target kernel (t2o_td_loss_ex2): the sequential per-episode recursion "
                          "or the one-wave-per-episode suffix scan; auto = the library default")
@@ -92,7 +100,7 @@ def parse():
                     help="print the tag that keys profiles/hbm_traffic.json for these args and exit")
     a = ap.parse_args()
     # per-mode defaults: each mode's BASELINE config (SURVEY.md §8 scenario mapping)
-    scen = a.mode in ("forward", "rollout", "dropin")
+    scen = a.mode in ("forward", "rollout", "dropin", "loop")
     if a.agents is None:
         a.agents = 16 if scen else 8
     if a.T is None:
@@ -371,6 +379,172 @@ def rollout_bench(args, world, rank, dev):
         dist.destroy_process_group()
 
 
+def _cpu_loop_rate(A, M, T, ne, threads):
+    """The CPU path of the driver's cycle on a sample (per_run.py:212-238 with
+    parallel_runner.py:102-221): one rollout of `ne` envs (torch-CPU agent forward,
+    ε-greedy, the numpy env's worker step; as _cpu_rollout_rate), the episodes as an
+    EpisodeBatch-shaped dict, then one TD update (oracle/ref_learner, fp32, Adam) on
+    those same `ne` episodes — so, as in the GPU loop's default, every collected
+    episode is learned from once.  Returns (learned agent-transitions/s, env
+    steps/s, rollout s, train s)."""
+    import numpy as np
+    from oracle import ref_learner, ref_mac, ref_model
+    from oracle.ref_env import RefEnv
+    cfg = dict(n_agents=A, n_entities=A, obs_entity_feats=9, emb=32, heads=3, depth=2, ff_hidden_mult=4,
+               n_actions=5, state_entity_feats=8, mixer_emb=32, mixer_heads=3, mixer_depth=2)
+    pa, pm = ref_model.init_params("agent", cfg, 0), ref_model.init_params("mixer", cfg, 1)
+    learner = ref_learner.RefLearner(pa, pm, cfg)
+    envs = [RefEnv(M, A, T, 1, e) for e in range(ne)]
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        t0 = time.perf_counter()
+        st, av, ob = zip(*[e.worker_reset() for e in envs])
+        obs = [np.stack(ob)]
+        state = [np.stack(st)]
+        avail = [np.stack([np.asarray(a) for a in av])]
+        acts, rews = [], []
+        h = torch.zeros(ne, A, 32)
+        for t in range(T + 1):
+            with torch.no_grad():
+                q, h = ref_model.agent_forward(learner.pa, torch.as_tensor(obs[-1], dtype=torch.float32), h,
+                                               n_entities=A, feat_dim=9, emb=32, heads=3, depth=2)
+            act = ref_mac.select_actions(q.reshape(-1, 5).numpy(), avail[-1].reshape(-1, 5), 0.05, 3, t)
+            acts.append(act.reshape(ne, A))
+            if t == T:
+                break
+            res = [e.worker_step(acts[-1][i]) for i, e in enumerate(envs)]
+            rews.append([r[0] for r in res])
+            state.append(np.stack([r[3] for r in res]))
+            avail.append(np.stack([np.asarray(r[4]) for r in res]))
+            obs.append(np.stack([r[5] for r in res]))
+        t1 = time.perf_counter()
+        tm = lambda xs, dt: torch.as_tensor(np.stack(xs, 1), dtype=dt)  # noqa: E731
+        batch = {"obs": tm(obs, torch.float32), "state": tm(state, torch.float32),
+                 "avail_actions": tm(avail, torch.int64), "actions": tm(acts, torch.int64)[..., None],
+                 "reward": torch.cat([tm(rews, torch.float32), torch.zeros(ne, 1)], 1)[..., None],
+                 "terminated": torch.zeros(ne, T + 1, 1), "filled": torch.ones(ne, T + 1, 1)}
+        learner.train(batch, ne * T, 0, per_weight=torch.ones(ne))
+        t2 = time.perf_counter()
+    finally:
+        torch.set_num_threads(prev)
+    return ne * T * A / (t2 - t0), ne * T / (t2 - t0), t1 - t0, t2 - t1
+
+
+def loop_bench(args, world, rank, dev):
+    """The driver's cycle, per_run.py:212-238, on the device, each rank on its own
+    shard (no collective except the learner's gradient all-reduce):
+        episode_batch = runner.run()                          (RolloutRunner, --envs envs)
+        buffer.insert_episode_batch(episode_batch)
+        repeat --updates-per-rollout times:
+            sample, idx, w = buffer.sample(--batch, t_env); sample = sample[:, :sample.max_t_filled()]
+            info = learner.train(sample, t_env, episode, w)
+            buffer.update_priorities(idx, info["td_errors_abs"] + 1e-6)
+    A step = one such iteration.  Phase times from HIP events on the main stream
+    (every step); value = learned agent-transitions/s over all ranks."""
+    from t2omca_amd.env import VecEnv
+    from t2omca_amd.learner import TDLearner
+    from t2omca_amd.modules import TransformerAgent, TransformerMixer
+    from t2omca_amd.replay import PrioritizedReplayBuffer
+    from t2omca_amd.runner import RolloutRunner
+    from t2omca_amd.synthetic import make_args
+    A, T, n, B, U = args.agents, args.T, args.envs, args.batch, args.updates_per_rollout
+    torch.manual_seed(0)
+    margs = make_args(A, device=str(dev))
+    agent, mixer = TransformerAgent(None, margs).to(dev), TransformerMixer(margs).to(dev)
+    learner = TDLearner(agent, mixer, precision=args.dtype, priorities_to_cpu=False, td_algo=args.td_algo)
+    env = VecEnv(n, mec_num=args.mecs, agv_num=A, episode_limit=T, seed=1, device=dev, wire=args.compact_obs)
+    env.get_env_info()
+    runner = RolloutRunner(agent, env, seed=0, compact_obs=args.compact_obs)
+    buf = None
+    episode = 0
+    marks = []
+
+    def mark(tag):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        marks.append((tag, ev))
+
+    def iteration(timed):
+        nonlocal buf, episode
+        if timed:
+            mark("rollout")
+        eb = runner.run()
+        if buf is None:  # capacity: two rollouts of episodes (PyMARL2 keeps buffer_size >= the runner's batch)
+            buf = PrioritizedReplayBuffer(eb, 2 * n, T + 1, 0.6, 0.4, 10 ** 7, device=dev, seed=rank)
+        if timed:
+            mark("insert")
+        buf.insert_episode_batch(eb)
+        episode += n
+        for _ in range(U):
+            if timed:
+                mark("sample")
+            sample, idx, w = buf.sample(B, runner.t_env)
+            sample = sample[:, :sample.max_t_filled()]
+            if timed:
+                mark("train")
+            info = learner.train(sample, runner.t_env, episode, per_weight=w)
+            if timed:
+                mark("update_priorities")
+            buf.update_priorities(idx, info["td_errors_abs"].flatten() + 1e-6)
+        if timed:
+            mark("end")
+
+    for _ in range(args.warmup):
+        iteration(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        iteration(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    phases = {}
+    for (tag, e0), (_, e1) in zip(marks, marks[1:]):
+        if tag != "end":
+            phases[tag] = phases.get(tag, 0.0) + e0.elapsed_time(e1)
+    phases = {k: round(v / args.steps, 3) for k, v in phases.items()}  # ms per iteration
+    learned = world * args.steps * U * B * T * A
+    out = {"metric": "learned agent-transitions/sec of the closed driver loop (rollout -> insert -> PER sample -> "
+                     "TD update -> update_priorities)",
+           "value": learned / elapsed, "unit": "agent-transitions/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": f"{args.dtype} learner, fp32 rollout agent, fp64 env",
+           "data": "simulated (VecEnv, env_spec stand-ins) + device PER replay",
+           "config": {"workload": f"configs[4] feeding the learner: {n} envs/GPU x {A} AGVs x {args.mecs} MEC, "
+                                  f"episode {T} steps; per rollout {U} TD updates of {B} PER-sampled episodes "
+                                  f"(replay capacity {2 * n})" + (", compact obs" if args.compact_obs else ""),
+                      "global_envs": n * world, "agents": A, "learner_batch": B, "updates_per_rollout": U,
+                      "parallelism": f"dp{world}"},
+           "env_steps_per_s": world * args.steps * n * T / elapsed,
+           "collected_agent_transitions_per_s": world * args.steps * n * T * A / elapsed,
+           "phase_ms_per_step": phases}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        hc = host_cpus()
+        ne = 4
+        r, es, t_roll, t_train = _cpu_loop_rate(A, args.mecs, T, ne, hc["usable"])
+        out["cpu_baseline"] = {"value": r, "unit": "agent-transitions/s", "cores": hc["usable"], "kind": "port",
+                               "env_steps_per_s": es,
+                               "sample": f"one cycle on {ne} envs x {A} AGVs x {args.mecs} MEC x T={T}: rollout "
+                                         f"(torch-CPU agent, eps-greedy, numpy env; {t_roll:.2f} s) then one TD "
+                                         f"update on those {ne} episodes (oracle/ref_learner fp32 + Adam; "
+                                         f"{t_train:.2f} s), {hc['usable']} threads (host_cpus)",
+                               "host_cpus": hc}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def rollout_tag(args):
     return f"rollout_n{args.envs}_t{args.T}_a{args.agents}_m{args.mecs}" + ("_wire" if args.compact_obs else "")
 
@@ -572,6 +746,8 @@ def main():
         return expand_bench(args, world, rank, dev)
     if args.mode == "dropin":
         return dropin_bench(args, world, rank, dev)
+    if args.mode == "loop":
+        return loop_bench(args, world, rank, dev)
     def make_learner(precision):
         torch.manual_seed(0)
         margs = make_args(A, device=str(dev), qmix_pos_func=args.qmix_pos_func)
@@ -579,7 +755,7 @@ def main():
         mixer = TransformerMixer(margs).to(dev)
         return TDLearner(agent, mixer, target_update_interval=10 ** 9, precision=precision,
                          overlap=not args.serial, priorities_to_cpu=args.priorities == "cpu",
-                         td_algo=args.td_algo)
+                         td_algo=args.td_algo, contract=args.contract)
 
     learner = make_learner(args.dtype)
     batch, w = make_batch(B, T, A, seed=1 + rank, device=dev)
@@ -672,7 +848,7 @@ def main():
     achieved = ref_flops[dom] / (dom_ms * 1e-3) / 1e12
     ms_step = elapsed / args.steps * 1e3
     upd_flops = ref_order_flops_per_transition(A) * B * T * A
-    dw = {"agent_bwd": "agent_dw", "mixer_bwd": "mixer_dw"}.get(dom)
+    dw = "dw_pair" if "dw_pair" in kern else {"agent_bwd": "agent_dw", "mixer_bwd": "mixer_dw"}.get(dom)
     out = {
         "metric": "agent-transitions/sec for TD update fwd+bwd (whole node)",
         "value": value,
@@ -699,7 +875,7 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_.get(dom),
                      "tape_bytes_per_update": tape_,
                      "avg_launch_ms": dom_ms,
-                     "incl_tape_contraction": None if dw is None or dw not in kern else {
+                     "incl_tape_contraction": None if dw is None or dw not in kern else {"contraction": dw,
                          "ms": dom_ms + kern[dw],
                          "frac": ref_flops[dom] / ((dom_ms + kern[dw]) * 1e-3) / 1e12 / peak_tf},
                      "executed_algorithm": {"flops_per_launch": flops[dom],

@@ -258,6 +258,18 @@ int t2o_bwd_tape_contract(const t2o_layout* L, const float* pack, const void* ta
 int t2o_bwd_tape_contract_ex(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
                              float* gslabs, int nslab, int rec_format, void* stream);
 
+/* Both backwards' tape contractions in one launch: the mixer's (record format 0)
+ * and the agent's (rec_format_a, t2o_agent_bwd_tape_format), each exactly as
+ * t2o_bwd_tape_contract_ex would, with one grid of nslab_m + nslab_a workgroups
+ * (the two then share the chip from the start instead of the second waiting on
+ * the first).  Both layouts must be tuned instances of the same network shape
+ * and precision for the one-grid path; otherwise the two contractions run as two
+ * launches.  Must follow both t2o_*_unroll_bwd calls on the same stream. */
+int t2o_bwd_tape_contract_pair(const t2o_layout* Lm, const float* pack_m, const void* tape_m, int64_t tiles_m,
+                               float* slabs_m, int nslab_m, const t2o_layout* La, const float* pack_a,
+                               const void* tape_a, int64_t tiles_a, float* slabs_a, int nslab_a, int rec_format_a,
+                               void* stream);
+
 /* TD(λ) targets, masked PER-weighted loss, dL/dQtot and priorities
  * (PyMARL2 NQLearner semantics; see t2o_learner.hip).  qtot [B][T] (online
  * mixer), qtot_tgt [B][T+1] (target mixer), reward/term/filled [b][t] with

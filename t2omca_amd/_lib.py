@@ -72,6 +72,11 @@ EXPORTS = {
     "t2o_bwd_tape_contract_ex": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_void_p, ctypes.c_void_p,
                                                 ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                                 ctypes.c_void_p]),
+    "t2o_bwd_tape_contract_pair": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_int64, ctypes.c_void_p, ctypes.c_int,
+                                                  ctypes.POINTER(Layout), ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                  ctypes.c_void_p]),
     "t2o_agent_bwd_tape_format": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_int]),
     "t2o_td_loss": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_int64] * 2 + [ctypes.c_void_p] +
                     [ctypes.c_int64] * 2 + [ctypes.c_void_p] + [ctypes.c_int64] * 2 +
@@ -114,7 +119,8 @@ EXPORTS = {
 
 # exports only tests / tools call (never on the product path), and the newest
 # reporting export: an older build loaded under A/B timing (T2O_LIB) may lack them
-_DIAGNOSTIC = {"t2o_bf_swz", "t2o_probe_lane_ops", "t2o_layout_instance", "t2o_abi_version", "t2o_td_loss_ex2"}
+_DIAGNOSTIC = {"t2o_bf_swz", "t2o_probe_lane_ops", "t2o_layout_instance", "t2o_abi_version", "t2o_td_loss_ex2",
+               "t2o_bwd_tape_contract_pair"}
 
 _lib = None
 

@@ -100,9 +100,9 @@ struct DwDims {
 
 // group j of this workgroup: tape -> registers (tiles past the end read as zeros)
 template <typename Dm, typename TT>
-T2O_DEV void dw_load(const DwGemmArgs& a, int64_t j, u4v (&rg)[Dm::NLD]) {
+T2O_DEV void dw_load(const DwGemmArgs& a, int wg, int nwg, int64_t j, u4v (&rg)[Dm::NLD]) {
   const TT* __restrict__ tape = static_cast<const TT*>(a.tape);
-  const int64_t grp = blockIdx.x + j * gridDim.x;
+  const int64_t grp = wg + j * nwg;
 #pragma unroll
   for (int i = 0; i < Dm::NLD; ++i) {
     const int q = threadIdx.x + i * Dm::NT;
@@ -392,10 +392,10 @@ struct DwRole<3, E, H, FF, D, TT, FMT> : DwFfn<1, E, H, FF, D, TT, FMT> {};
 // the same barrier sequence; the roles only differ in what they read).
 // Pipeline: LDS double buffer, register ring of two, prefetch distance 2.
 template <int ROLE, int E, int H, int FF, int D, typename TT, int RT, int FMT>
-T2O_DEV void dw_run(const DwGemmArgs& a, TT* buf0, TT* buf1, const TT* wlds, int d) {
+T2O_DEV void dw_run(const DwGemmArgs& a, int wg, int nwg, TT* buf0, TT* buf1, const TT* wlds, int d) {
   using Dm = DwDims<E, H, FF, D, TT, RT, FMT>;
   const int64_t ngroups = (a.ntiles + Dm::TG - 1) / Dm::TG;
-  const int64_t nj = (int64_t)blockIdx.x < ngroups ? (ngroups - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  const int64_t nj = (int64_t)wg < ngroups ? (ngroups - 1 - wg) / nwg + 1 : 0;
   DwRole<ROLE, E, H, FF, D, TT, FMT> st;
   st.init(a, d, wlds);
   auto compute = [&](const TT* buf) {
@@ -406,31 +406,38 @@ T2O_DEV void dw_run(const DwGemmArgs& a, TT* buf0, TT* buf1, const TT* wlds, int
     }
   };
   u4v r0[Dm::NLD], r1[Dm::NLD];
-  if (nj > 0) dw_load<Dm, TT>(a, 0, r0);
-  if (nj > 1) dw_load<Dm, TT>(a, 1, r1);
+  if (nj > 0) dw_load<Dm, TT>(a, wg, nwg, 0, r0);
+  if (nj > 1) dw_load<Dm, TT>(a, wg, nwg, 1, r1);
   if (nj > 0) dw_store<Dm, TT>(buf0, r0);
   if (nj > 1) dw_store<Dm, TT>(buf1, r1);
-  if (nj > 2) dw_load<Dm, TT>(a, 2, r0);
-  if (nj > 3) dw_load<Dm, TT>(a, 3, r1);
+  if (nj > 2) dw_load<Dm, TT>(a, wg, nwg, 2, r0);
+  if (nj > 3) dw_load<Dm, TT>(a, wg, nwg, 3, r1);
   __syncthreads();
   for (int64_t j = 0; j < nj; j += 2) {
     compute(buf0);
     __syncthreads();
     if (j + 2 < nj) dw_store<Dm, TT>(buf0, r0);
-    if (j + 4 < nj) dw_load<Dm, TT>(a, j + 4, r0);
+    if (j + 4 < nj) dw_load<Dm, TT>(a, wg, nwg, j + 4, r0);
     if (j + 1 >= nj) break;
     compute(buf1);
     __syncthreads();
     if (j + 3 < nj) dw_store<Dm, TT>(buf1, r1);
-    if (j + 5 < nj) dw_load<Dm, TT>(a, j + 5, r1);
+    if (j + 5 < nj) dw_load<Dm, TT>(a, wg, nwg, j + 5, r1);
   }
-  st.finish(a, a.slabs + (size_t)blockIdx.x * a.slab_stride, d);
+  st.finish(a, a.slabs + (size_t)wg * a.slab_stride, d);
 }
 
-template <int E, int H, int FF, int D, int KIND, typename TT, int RT, int FMT>
-__global__ __launch_bounds__(256 * D) void dw_gemm_kernel(DwGemmArgs a) {
+// LDS elements (of TT) one workgroup of a contraction instance takes
+template <int E, int H, int FF, int D, typename TT, int FMT>
+constexpr size_t dw_lds_elems() {
+  using Dm = DwDims<E, H, FF, D, TT, 16, FMT>;
+  return (size_t)2 * Dm::GELEM + (Dm::BF ? (size_t)D * 2 * FF * E : 0);
+}
+
+// One workgroup's contraction: workgroup wg of nwg over the tape of `a`.
+template <int E, int H, int FF, int D, typename TT, int RT, int FMT>
+T2O_DEV void dw_gemm_wg(const DwGemmArgs& a, int wg, int nwg, float* smem) {
   using Dm = DwDims<E, H, FF, D, TT, RT, FMT>;
-  extern __shared__ __attribute__((aligned(16))) float smem[];
   TT* const buf0 = reinterpret_cast<TT*>(smem);
   TT* const buf1 = buf0 + Dm::GELEM;
   TT* const wlds = buf1 + Dm::GELEM;  // bf16: [D][W1, W2ᵀ][FF][E] (the pack's swizzled image)
@@ -464,19 +471,36 @@ __global__ __launch_bounds__(256 * D) void dw_gemm_kernel(DwGemmArgs a) {
   // Waves w and w + 4 share a SIMD.  Roles 2/3 (FFN halves: 32 MFMAs per tile
   // plus the W1/W2ᵀ reads) weigh about 2.7x roles 0/1 (12 MFMAs), so block 1
   // rotates its roles by two: every SIMD holds one light and one heavy role.
-#ifndef T2O_DW_NO_ROLE_ROTATE
   const int d = w >> 2, role = (w + 2 * d) & 3;
-#else
-  const int d = w >> 2, role = w & 3;
-#endif
   // the heavy (FFN-half) wave issues first on its SIMD, the light one fills its
   // gaps (A/B: mixer_dw 0.256 -> 0.249 ms; prioritising the light roles: no gain)
   if (role >= 2) __builtin_amdgcn_s_setprio(1);
   switch (role) {  // wave-uniform; the four paths issue the same barriers
-    case 0: dw_run<0, E, H, FF, D, TT, RT, FMT>(a, buf0, buf1, wlds, d); break;
-    case 1: dw_run<1, E, H, FF, D, TT, RT, FMT>(a, buf0, buf1, wlds, d); break;
-    case 2: dw_run<2, E, H, FF, D, TT, RT, FMT>(a, buf0, buf1, wlds, d); break;
-    default: dw_run<3, E, H, FF, D, TT, RT, FMT>(a, buf0, buf1, wlds, d); break;
+    case 0: dw_run<0, E, H, FF, D, TT, RT, FMT>(a, wg, nwg, buf0, buf1, wlds, d); break;
+    case 1: dw_run<1, E, H, FF, D, TT, RT, FMT>(a, wg, nwg, buf0, buf1, wlds, d); break;
+    case 2: dw_run<2, E, H, FF, D, TT, RT, FMT>(a, wg, nwg, buf0, buf1, wlds, d); break;
+    default: dw_run<3, E, H, FF, D, TT, RT, FMT>(a, wg, nwg, buf0, buf1, wlds, d); break;
+  }
+}
+
+template <int E, int H, int FF, int D, int KIND, typename TT, int RT, int FMT>
+__global__ __launch_bounds__(256 * D) void dw_gemm_kernel(DwGemmArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  dw_gemm_wg<E, H, FF, D, TT, RT, FMT>(a, blockIdx.x, gridDim.x, smem);
+}
+
+// Both backwards' tapes in ONE grid (t2o_bwd_tape_contract_pair): workgroups
+// [0, n0) contract tape 0 (record format 0: the mixer's), the rest tape 1
+// (format FMT1: the agent's).  After the agent BPTT the two contractions are the
+// update's tail; as one launch their workgroups share the chip from the first
+// wave on and the second launch's ramp and gap disappear.
+template <int E, int H, int FF, int D, typename TT, int FMT1>
+__global__ __launch_bounds__(256 * D) void dw_gemm_pair_kernel(DwGemmArgs a0, DwGemmArgs a1, int n0) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  if ((int)blockIdx.x < n0) {
+    dw_gemm_wg<E, H, FF, D, TT, 16, 0>(a0, blockIdx.x, n0, smem);
+  } else {
+    dw_gemm_wg<E, H, FF, D, TT, 16, FMT1>(a1, blockIdx.x - n0, gridDim.x - n0, smem);
   }
 }
 
@@ -493,12 +517,36 @@ int launch_dw_gemm(int kind, const void* tape, int64_t ntiles, const float* pack
   a.pack = pack;
   a.L = L;
   a.G = G;
-  const size_t lds = sizeof(TT) * ((size_t)2 * Dm::GELEM + (Dm::BF ? (size_t)D * 2 * FF * E : 0));
+  (void)sizeof(Dm);
+  const size_t lds = sizeof(TT) * dw_lds_elems<E, H, FF, D, TT, FMT>();
   // (every tuned mixer writes its records as one compact stream of 16-record tiles)
   auto kern = kind == 0 ? dw_gemm_kernel<E, H, FF, D, 0, TT, 16, FMT> : dw_gemm_kernel<E, H, FF, D, 1, TT, 16, 0>;
   if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(kern, dim3(nslab), dim3(256 * D), lds, stream, a);
+  return (int)hipGetLastError();
+}
+
+static DwGemmArgs dw_args(const void* tape, int64_t ntiles, const float* pack, float* slabs, const t2o_layout& L) {
+  DwGemmArgs a{};
+  a.tape = tape;
+  a.ntiles = ntiles;
+  a.slabs = slabs;
+  a.pack = pack;
+  a.L = L;
+  grad_layout(L, a.G);
+  a.slab_stride = a.G.grad_total;
+  return a;
+}
+
+template <int E, int H, int FF, int D, typename TT, int FMT1>
+int launch_dw_gemm_pair(const DwGemmArgs& a0, int n0, const DwGemmArgs& a1, int n1, hipStream_t stream) {
+  constexpr size_t l0 = dw_lds_elems<E, H, FF, D, TT, 0>(), l1 = dw_lds_elems<E, H, FF, D, TT, FMT1>();
+  const size_t lds = sizeof(TT) * (l0 > l1 ? l0 : l1);
+  if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
+  auto kern = dw_gemm_pair_kernel<E, H, FF, D, TT, FMT1>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(kern, dim3(n0 + n1), dim3(256 * D), lds, stream, a0, a1, n0);
   return (int)hipGetLastError();
 }
 
@@ -551,4 +599,31 @@ extern "C" int t2o_bwd_tape_contract_ex(const t2o_layout* L, const float* pack, 
 extern "C" int t2o_bwd_tape_contract(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
                                      float* gslabs, int nslab, void* stream) {
   return t2o_bwd_tape_contract_ex(L, pack, tape, tiles, gslabs, nslab, 0, stream);
+}
+
+extern "C" int t2o_bwd_tape_contract_pair(const t2o_layout* Lm, const float* pack_m, const void* tape_m,
+                                          int64_t tiles_m, float* slabs_m, int nslab_m, const t2o_layout* La,
+                                          const float* pack_a, const void* tape_a, int64_t tiles_a,
+                                          float* slabs_a, int nslab_a, int rec_format_a, void* stream) {
+  if (!Lm || !La || Lm->kind != 1 || La->kind != 0) return T2O_EINVAL;
+  if (!pack_m || !tape_m || !slabs_m || tiles_m < 0 || nslab_m < 1 || !pack_a || !tape_a || !slabs_a ||
+      tiles_a < 0 || nslab_a < 1 || rec_format_a < 0 || rec_format_a > 1 || (rec_format_a == 1 && !La->prec))
+    return T2O_EINVAL;
+  // one grid needs one kernel instance: both networks tuned, same (E, H, D, FF) and precision
+  const bool same = !Lm->generic && !La->generic && Lm->E == La->E && Lm->H == La->H && Lm->D == La->D &&
+                    Lm->FF == La->FF && Lm->prec == La->prec;
+  hipStream_t s = (hipStream_t)stream;
+  if (!same) {
+    int rc = t2o_bwd_tape_contract_ex(Lm, pack_m, tape_m, tiles_m, slabs_m, nslab_m, 0, stream);
+    return rc ? rc : t2o_bwd_tape_contract_ex(La, pack_a, tape_a, tiles_a, slabs_a, nslab_a, rec_format_a, stream);
+  }
+  const DwGemmArgs am = dw_args(tape_m, tiles_m, pack_m, slabs_m, *Lm);
+  const DwGemmArgs aa = dw_args(tape_a, tiles_a, pack_a, slabs_a, *La);
+  int rc = T2O_EUNSUPPORTED;
+  T2O_DISPATCH_NET(La->E, La->H, La->D, La->FF,
+                   rc = (La->prec ? (rec_format_a == 1
+                                         ? launch_dw_gemm_pair<E_, H_, FF_, D_, __bf16, 1>(am, nslab_m, aa, nslab_a, s)
+                                         : launch_dw_gemm_pair<E_, H_, FF_, D_, __bf16, 0>(am, nslab_m, aa, nslab_a, s))
+                                  : launch_dw_gemm_pair<E_, H_, FF_, D_, float, 0>(am, nslab_m, aa, nslab_a, s)));
+  return rc;
 }

@@ -10,11 +10,14 @@ DP update equal to the full-batch update:
     loss = Σ_b w_b Σ_t ½ td² m / Σ_all m   ->   grad = Σ_r g_r / Σ_r M_r
 
 At E = 32 that buffer is 84,007 floats (336 KB): latency-bound over xGMI, so
-it is not bucketed further.  It is split in two at the agent / mixer boundary
-only because the mixer half is final a whole kernel (the agent BPTT) earlier:
-that half's all-reduce is issued from the side stream as soon as it is
-unfolded and runs under the agent BPTT (``allreduce_async``), so only the
-agent half's latency stays on the critical path.
+it is one all-reduce, issued after both unfolds (the default learner path).
+It cannot be hidden under the BPTT kernels: they hold every SIMD (the agent
+BPTT one 503-register wave per SIMD), and an RCCL kernel, like any kernel
+issued on another stream, needs a wave slot — the round-3 trace shows a side-
+stream copy issued at the agent BPTT's start waiting until its end
+(profiles/r3_f5/prof/timeline.txt).  The learner's ``contract="side"`` mode
+still issues the mixer half from the side stream before the agent BPTT; it
+runs when that BPTT drains, not under it.
 
 Replicas start identical and stay identical: the learner broadcasts its
 parameters, target parameters and Adam moments from rank 0 when it is built
@@ -46,9 +49,7 @@ def allreduce_grad_and_mask(buf, group=None):
 def allreduce_async(buf, group=None):
     """Start an in-place SUM all-reduce of `buf` ordered after the work already
     queued on the CURRENT stream; returns a handle for ``wait_all`` (None
-    without a process group).  The learner issues the mixer half of the
-    gradient (+ Σ mask) from the side stream as soon as it is unfolded, so it
-    runs under the agent BPTT, and the agent half after the agent's unfold."""
+    without a process group)."""
     if world_size(group) > 1:
         return dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=group, async_op=True)
     return None

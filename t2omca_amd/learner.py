@@ -16,12 +16,14 @@ priorities are copied out):
   mixer unroll fwd, online (chosen Q, t < T) +
         target (double-Q, t <= T)                  t2o_mixer_unroll_fwd (1 launch)
   TD(λ) targets, loss, dL/dQtot, priorities        t2o_td_loss
-  mixer BPTT -> dL/dq_chosen, dL/dhidden           t2o_mixer_unroll_bwd + slab reduce
-  agent BPTT                                       t2o_agent_unroll_bwd + slab reduce
+  mixer BPTT -> dL/dq_chosen, dL/dhidden           t2o_mixer_unroll_bwd
+  agent BPTT                                       t2o_agent_unroll_bwd
+  both weight-gradient tapes contracted            t2o_bwd_tape_contract_pair (one launch)
+                                                   + slab reduce x2
   unfold grads into the reference parameter order  t2o_unpack_grads x2
-  [data parallel: all_reduce of the flat grad + Σ mask over RCCL, in two
-   halves: the mixer's (+ Σ mask) from the side stream under the agent BPTT,
-   the agent's after its unfold]
+  [data parallel: one all_reduce of the flat grad + Σ mask over RCCL, after
+   the unfolds: the BPTT kernels fill every SIMD, so nothing issued beside them
+   runs before they drain]
   clip_grad_norm_ + Adam                           t2o_adam_step
 """
 import dataclasses
@@ -53,7 +55,7 @@ class TDLearner:
     def __init__(self, agent, mixer, *, lr=1e-3, gamma=0.99, td_lambda=0.6, grad_norm_clip=10.0,
                  target_update_interval=200, optim_betas=(0.9, 0.999), optim_eps=1e-8, weight_decay=0.0,
                  detach_mixer_hidden=False, process_group=None, priorities_to_cpu=True, precision="fp32",
-                 overlap=True, td_algo="auto"):
+                 overlap=True, td_algo="auto", contract="pair"):
         dev = next(agent.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("TDLearner needs the modules on a HIP device (no CPU fallback)")
@@ -90,6 +92,12 @@ class TDLearner:
         self.priorities_to_cpu = priorities_to_cpu
         self.overlap = overlap  # mixer tape contraction on a side stream beside the agent BPTT
         self.td_algo = td_algo  # ops.TD_ALGOS
+        # "pair": both tape contractions in one launch after the agent BPTT (the
+        # default); "side": the mixer's on the side stream, issued before the agent
+        # BPTT (it cannot start until the BPTT's waves free the SIMDs, §7 DESIGN)
+        if contract not in ("pair", "side"):
+            raise ValueError("contract must be 'pair' or 'side'")
+        self.contract = contract
         self.step_count = 0
         self.last_target_update_episode = 0
         self.timer = None   # optional callable(tag) recording HIP events around the big kernels
@@ -279,32 +287,39 @@ class TDLearner:
         #    on the side stream before the mixer forward, which waited for it)
         td = ops.td_loss(o_on["y"], o_tg["y"], reward, term, filled, w, gamma=self.gamma,
                          td_lambda=self.td_lambda, mask_sum=1.0, algo=self.td_algo, mask_sum_acc=self.grad[-1:])
-        # 4. mixer BPTT.  Its weight-grad tape contraction (HBM-bound) runs on a
-        #    side stream, overlapping the agent BPTT (latency-bound, half the SIMDs)
+        # 4. mixer BPTT (its weight-grad tape is contracted after the agent BPTT)
         tape_m = self._slab("tape_m", ops.tape_floats(self.sm, ops.mixer_tape_tiles(B, T, A, self.sm)))
         tape_a = self._slab("tape_a", ops.tape_floats(self.sa, ops.agent_tape_tiles(B, T, A)))
         slabs_m = self._slab("m", int(ops.lib().t2o_mixer_bwd_max_slabs(B)) * self.sm.layout().grad_total)
         contract_m, gqv, ghid, _ = ops.mixer_unroll_bwd(self.sm, self.pack_m, state, h_on, o_on, td["gq"],
                                                         slabs=slabs_m, timer=self.timer, tape=tape_m,
                                                         defer_contract=True)
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            gm = contract_m()
-            # mixer grads in reference parameter order, still off the critical path
-            ops.unpack_grads(self.sm, self.params[self.na:], gm, self.grad[self.na:self.na + self.nm])
-            # data parallel: the mixer half (+ Σ mask) is final now; its all-reduce
-            # runs under the agent BPTT
-            work_m = allreduce_async(self.grad[self.na:], self.pg)
-        # 5. agent BPTT (grads of the chosen Q and, unless detached, of the hidden states)
         slabs_a = self._slab("a", int(ops.lib().t2o_agent_bwd_max_slabs(B, A)) * self.sa.layout().grad_total)
-        ga, _ = ops.agent_unroll_bwd(self.sa, self.pack_a, obs, h_on, gchosen=gqv, actions=act,
-                                     gh=None if self.detach_mixer_hidden else ghid, slabs=slabs_a,
-                                     timer=self.timer, hmid=hmid, tape=tape_a)
-        # 6. agent grads in reference parameter order
-        ops.unpack_grads(self.sa, self.params[:self.na], ga, self.grad[:self.na])
-        work_a = allreduce_async(self.grad[:self.na], self.pg)
-        main.wait_stream(side)
-        wait_all((work_m, work_a))
+        gh = None if self.detach_mixer_hidden else ghid
+        if self.contract == "pair":
+            # 5. agent BPTT (grads of the chosen Q and, unless detached, of the hidden
+            #    states), then both tapes contracted in one launch
+            contract_a, _ = ops.agent_unroll_bwd(self.sa, self.pack_a, obs, h_on, gchosen=gqv, actions=act, gh=gh,
+                                                 slabs=slabs_a, timer=self.timer, hmid=hmid, tape=tape_a,
+                                                 defer_contract=True)
+            gm, ga = ops.tape_contract_pair(contract_m, contract_a, timer=self.timer)
+            # 6. grads in reference parameter order; data parallel: one all-reduce of
+            #    [agent grads, mixer grads, Σ mask] (336 KB at the default network)
+            ops.unpack_grads(self.sm, self.params[self.na:], gm, self.grad[self.na:self.na + self.nm])
+            ops.unpack_grads(self.sa, self.params[:self.na], ga, self.grad[:self.na])
+            wait_all((allreduce_async(self.grad, self.pg),))
+        else:
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                gm = contract_m()
+                ops.unpack_grads(self.sm, self.params[self.na:], gm, self.grad[self.na:self.na + self.nm])
+                work_m = allreduce_async(self.grad[self.na:], self.pg)
+            ga, _ = ops.agent_unroll_bwd(self.sa, self.pack_a, obs, h_on, gchosen=gqv, actions=act, gh=gh,
+                                         slabs=slabs_a, timer=self.timer, hmid=hmid, tape=tape_a)
+            ops.unpack_grads(self.sa, self.params[:self.na], ga, self.grad[:self.na])
+            work_a = allreduce_async(self.grad[:self.na], self.pg)
+            main.wait_stream(side)
+            wait_all((work_m, work_a))
         # 7. clip + Adam
         self.step_count += 1
         ops.adam_step(self.params, self.grad[:-1], self.exp_avg, self.exp_avg_sq, self.step_count, lr=self.lr,

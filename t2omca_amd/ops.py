@@ -172,13 +172,28 @@ def _tape(shape, tiles, tape, device):
     return tape
 
 
+class DeferredContraction:
+    """A backward call's weight-gradient tape, not yet contracted: call it (on the
+    stream that should run the contraction + slab sum) for the compact gradient
+    block, or hand two of them to tape_contract_pair."""
+
+    def __init__(self, shape, pack, tape, tiles, slabs, nslab, timer, tag, fmt):
+        self.shape, self.pack, self.tape, self.tiles = shape, pack, tape, tiles
+        self.slabs, self.nslab, self.timer, self.tag, self.fmt = slabs, nslab, timer, tag, fmt
+
+    def __call__(self):
+        return tape_contract(self.shape, self.pack, self.tape, self.tiles, self.slabs, self.nslab, self.timer,
+                             self.tag, self.fmt)
+
+
 def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchosen=None, actions=None,
-                     gh=None, want_gh0=False, slabs=None, timer=None, hmid=None, tape=None):
+                     gh=None, want_gh0=False, slabs=None, timer=None, hmid=None, tape=None, defer_contract=False):
     """BPTT of agent_unroll_fwd over the first T = len(grads) steps.
 
     obs [B, >=T, A, nF]; h_seq [B, Ts>=T, A, E] (forward output); gq [B,T,A,NA],
     gchosen [B,T,A] + actions (int64 [B, >=T, A], a-stride 1), gh [B,T,A,E].
-    Returns (gpack, gh0) with gpack the compact weight-gradient block."""
+    Returns (gpack, gh0) with gpack the compact weight-gradient block (with
+    defer_contract, a DeferredContraction instead)."""
     _dev(pack, obs, h_seq, h0, gq, gchosen, actions, gh)
     B, _, A, _ = obs.shape
     T = next(t.shape[1] for t in (gq, gchosen, gh) if t is not None)
@@ -205,7 +220,8 @@ def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchose
           "agent_unroll_bwd")
     _mark(timer, "end:agent_bwd")
     fmt = int(lib().t2o_agent_bwd_tape_format(ctypes.byref(L), int(hmid is not None)))
-    return tape_contract(shape, pack, tape, tiles, slabs, nslab.value, timer, "agent_dw", fmt), gh0
+    dc = DeferredContraction(shape, pack, tape, tiles, slabs, nslab.value, timer, "agent_dw", fmt)
+    return (dc if defer_contract else dc()), gh0
 
 
 def _mstrides(t):
@@ -283,6 +299,24 @@ def tape_contract(shape: NetShape, pack, tape, tiles, slabs, nslab, timer=None, 
     return gpack
 
 
+def tape_contract_pair(dm: DeferredContraction, da: DeferredContraction, timer=None):
+    """Both backwards' tape contractions in one launch (t2o_bwd_tape_contract_pair;
+    dm the mixer's, da the agent's), then each slab sum.  Returns (gpack_m, gpack_a)."""
+    Lm, La = dm.shape.layout(), da.shape.layout()
+    _mark(timer, "begin:dw_pair")
+    check(lib().t2o_bwd_tape_contract_pair(ctypes.byref(Lm), ptr(dm.pack), ptr(dm.tape), int(dm.tiles), ptr(dm.slabs),
+                                           int(dm.nslab), ctypes.byref(La), ptr(da.pack), ptr(da.tape), int(da.tiles),
+                                           ptr(da.slabs), int(da.nslab), int(da.fmt), stream_ptr()),
+          "bwd_tape_contract_pair")
+    _mark(timer, "end:dw_pair")
+    out = []
+    for d, L in ((dm, Lm), (da, La)):
+        g = torch.empty(L.grad_total, device=d.slabs.device)
+        reduce_slabs(d.slabs, d.nslab, g)
+        out.append(g)
+    return out[0], out[1]
+
+
 def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_ext=None,
                      want_ghw0=False, slabs=None, timer=None, tape=None, defer_contract=False):
     """BPTT of mixer_unroll_fwd (one network, `fwd` = its output dict).
@@ -314,7 +348,7 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
         ptr(fwd.get("xmid")), ptr(gy), ptr(ghw_ext), ptr(gqv), ptr(ghid), ptr(ghw0), ptr(slabs), nmax, ctypes.byref(nslab),
         ptr(tape), B, T, stream_ptr()), "mixer_unroll_bwd")
     _mark(timer, "end:mixer_bwd")
-    contract = lambda: tape_contract(shape, pack, tape, tiles, slabs, nslab.value, timer, "mixer_dw")  # noqa: E731
+    contract = DeferredContraction(shape, pack, tape, tiles, slabs, nslab.value, timer, "mixer_dw", 0)
     return (contract if defer_contract else contract()), gqv, ghid, ghw0
 
 

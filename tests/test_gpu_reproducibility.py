@@ -47,3 +47,24 @@ def test_td_update_bit_reproducible_across_runs(A, B, T, precision):
         ndiff = int((a != b).sum())
         print(f"A={A} B={B} T={T} {precision} {name}: {ndiff} differing elements of {a.numel()}")
         assert torch.equal(a, b), (name, ndiff)
+
+
+@pytest.mark.parametrize("A,B,T,precision", [(8, 64, 12, "bf16"), (8, 6, 7, "fp32"), (16, 4, 6, "bf16"),
+                                             (64, 2, 3, "bf16"), (5, 3, 4, "fp32")])
+def test_paired_contraction_equals_separate_launches(A, B, T, precision):
+    """t2o_bwd_tape_contract_pair (both tapes in one grid, the learner's default)
+    gives exactly the gradients of the two separate contractions (contract="side"):
+    every workgroup runs the same code on the same tiles into the same slab."""
+    require_gpu()
+    from t2omca_amd.learner import TDLearner
+    from t2omca_amd.synthetic import make_batch
+    batch, w = make_batch(B, T, A, seed=12)
+    out = {}
+    for mode in ("pair", "side"):
+        agent, mixer, _, _ = _setup(A, seed=6)
+        learner = TDLearner(agent, mixer, precision=precision, priorities_to_cpu=False, contract=mode)
+        info = learner.train(batch, 0, 0, per_weight=w)
+        torch.cuda.synchronize()
+        out[mode] = (learner.grad.clone(), info["td_errors_abs"].clone(), learner.params.clone())
+    for name, a, b in zip(("grad", "priorities", "params"), out["pair"], out["side"]):
+        assert torch.equal(a, b), (name, int((a != b).sum()))
