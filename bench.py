@@ -77,9 +77,9 @@ def parse():
                          "instances compute abs only, so softplus / quadratic / identity run the runtime-entity "
                          "MFMA mixer instance of the AGV count's capacity class (ops.NetShape.instance; the "
                          "bench line's config.kernels says which)")
-    ap.add_argument("--contract", choices=("pair", "side"), default="pair",
-                    help="weight-gradient tape contractions: pair = both in one launch after the agent BPTT "
-                         "(default); side = the mixer's on a side stream issued before the agent BPTT")
+    ap.add_argument("--contract", choices=("pair", "side"), default="side",
+                    help="weight-gradient tape contractions: side (default) = the mixer's on a side stream "
+                         "issued before the agent BPTT; pair = both in one launch after the agent BPTT")
     ap.add_argument("--td-algo", choices=("auto", "sequential", "wave"), default="auto",
                     help="TD(lambda) target kernel (t2o_td_loss_ex2): the sequential per-episode recursion "
                          "or the one-wave-per-episode suffix scan; auto = the library default")
