@@ -658,20 +658,11 @@ T2O_DEV void agent_bwd_pipe_body(const AgentBwdArgs& args, const t2o_layout& L, 
   });
 }
 
-// The kernel-argument layout.  Compile-time pack offsets (t2o_layout.hpp
-// kernel_layout, as the bf16 mixer BPTT reads them) cut this kernel's SGPR spills
-// 71 -> 62 but cost 9 more AGPRs and 5 spilled VGPRs: agent_bwd 0.623 -> 0.643 ms
-// (interleaved A/B, profiles/r3_ab6/).  -DT2O_AGP_CONST_LAYOUT=1 builds that variant.
-#ifndef T2O_AGP_CONST_LAYOUT
-#define T2O_AGP_CONST_LAYOUT 0
-#endif
+// The kernel-argument layout.  (Compile-time pack offsets, as the bf16 mixer BPTT
+// reads them, measured slower here: agent_bwd 0.623 -> 0.643 ms, profiles/r3_ab6/.)
 template <int E, int H, int D, int NE, int FF, bool RT, typename WT>
 __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(AgentBwdArgs args) {
-  if constexpr (sizeof(WT) == 2 && T2O_AGP_CONST_LAYOUT)
-    agent_bwd_pipe_body<E, H, D, NE, FF, RT, WT>(args, kernel_layout<E, H, D, FF, WT>(args.L),
-                                                 kernel_grad_layout<E, H, D, FF, WT>());
-  else
-    agent_bwd_pipe_body<E, H, D, NE, FF, RT, WT>(args, args.L, args.G);
+  agent_bwd_pipe_body<E, H, D, NE, FF, RT, WT>(args, args.L, args.G);
 }
 
 template <int E, int H, int D, int NE, int FF, typename WT>

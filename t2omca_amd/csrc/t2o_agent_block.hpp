@@ -237,7 +237,6 @@ T2O_DEV void agent_attn_bwd(const Wts<WT>& P, const t2o_layout& L, float* __rest
     }
     f4 goh;
     matvec_tr<1, ET>(P, L.We, 16, L.WeT, E, gzh, &goh);
-#ifndef T2O_ABL_NODW  // ablation builds only: wrong gradients
     if constexpr (DEFER) {
       const int b = Tl::WET + hh * Tl::WEH;
 #pragma unroll
@@ -249,7 +248,6 @@ T2O_DEV void agent_attn_bwd(const Wts<WT>& P, const t2o_layout& L, float* __rest
     } else {
       dw_accumulate_regs<ET, 1, BF>(gWe, gzh, &c.oh[hh], stage);
     }
-#endif
     // softmax backward over [token 0, entities]; [gP, gp_0, goh·o_j] reduced in one batch
     float red[NE + 2];
     red[0] = gPp;
@@ -284,10 +282,8 @@ T2O_DEV void agent_attn_bwd(const Wts<WT>& P, const t2o_layout& L, float* __rest
       gh_in[t] += gs0 * uh[t];
       gbe[t] += gc * uh[t];
     }
-#ifndef T2O_ABL_NODW
     if constexpr (DEFER) stage_tile_bf(sb, Tl::WET + hh * Tl::WEH + 2 * ET + 1, gw);
     else dw_accumulate_regs<ET, 1, BF>(gWe, uh, &gw, stage);
-#endif
   }
 }
 

@@ -24,18 +24,18 @@ struct PostCache {
 };
 
 // x: in = block input, out = block output.
-template <int E, int H, int FF, bool CACHE, typename WT>
+template <int E, int H, int FF, bool CACHE, typename WT, bool HOIST = T2O_SWZ_HOIST>
 T2O_DEV void post_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* z, f4* x, PostCache<E, H, FF>* c) {
   constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
   f4 r1[ET];
-  matvec<ET, HET>(P.w + L.N[d], H * E, z, r1);
+  matvec<ET, HET, HOIST>(P.w + L.N[d], H * E, z, r1);
 #pragma unroll
   for (int t = 0; t < ET; ++t) r1[t] += vec_t(P.v + L.bu[d], t) + x[t];
   f4 y[ET], xh1[ET];
   float rs1;
   layernorm_fwd<ET>(r1, P.v + L.g1[d], P.v + L.n1[d], y, xh1, rs1);
   f4 f1[FT], f1r[FT];
-  matvec<FT, ET>(P.w + L.W1[d], E, y, f1);
+  matvec<FT, ET, HOIST>(P.w + L.W1[d], E, y, f1);
 #pragma unroll
   for (int t = 0; t < FT; ++t) {
     f1[t] += vec_t(P.v + L.c1[d], t);
@@ -43,7 +43,7 @@ T2O_DEV void post_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* z,
     for (int r = 0; r < 4; ++r) f1r[t][r] = fmaxf(f1[t][r], 0.f);
   }
   f4 r2[ET];
-  matvec<ET, FT>(P.w + L.W2[d], FF, f1r, r2);
+  matvec<ET, FT, HOIST>(P.w + L.W2[d], FF, f1r, r2);
 #pragma unroll
   for (int t = 0; t < ET; ++t) r2[t] += vec_t(P.v + L.c2[d], t) + y[t];
   if constexpr (CACHE) {
@@ -193,32 +193,30 @@ T2O_DEV void post_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restr
 }
 
 // Layout whose block-0 slots hold block d's offsets: the block code is then
-// called with the constant d = 0, and every offset it reads is a scalar.
+// called with the constant d = 0, and every offset it reads is a scalar.  L is
+// the kernel-argument layout (or a compile-time one indexed by a constant d): a
+// run-time d indexes the kernel-argument fields directly, one scalar load each.
+// (Round 3 replaced the indexing by a select over the T2O_MAX_DEPTH entries of
+// every field, for a compile-time layout indexed at run time; on the kernel-
+// argument layout that kept 4x the offsets live in SGPRs and cost the agent
+// BPTT 0.543 -> 0.604 ms, bisected in profiles/r4_bisect/.)
 T2O_DEV t2o_layout block_view(const t2o_layout& L, int d) {
-  // (selects between the constant-indexed fields, not a run-time index: a local
-  // layout indexed at run time would be spilled whole to scratch to be addressed)
-  const auto pick = [d](const int64_t (&f)[T2O_MAX_DEPTH]) {
-    int64_t v = f[0];
-#pragma unroll
-    for (int k = 1; k < T2O_MAX_DEPTH; ++k) v = d == k ? f[k] : v;
-    return v;
-  };
   t2o_layout V = L;
-  V.M[0] = pick(L.M);
-  V.MT[0] = pick(L.MT);
-  V.N[0] = pick(L.N);
-  V.NT[0] = pick(L.NT);
-  V.bu[0] = pick(L.bu);
-  V.g1[0] = pick(L.g1);
-  V.n1[0] = pick(L.n1);
-  V.W1[0] = pick(L.W1);
-  V.W1T[0] = pick(L.W1T);
-  V.c1[0] = pick(L.c1);
-  V.W2[0] = pick(L.W2);
-  V.W2T[0] = pick(L.W2T);
-  V.c2[0] = pick(L.c2);
-  V.g2[0] = pick(L.g2);
-  V.n2[0] = pick(L.n2);
+  V.M[0] = L.M[d];
+  V.MT[0] = L.MT[d];
+  V.N[0] = L.N[d];
+  V.NT[0] = L.NT[d];
+  V.bu[0] = L.bu[d];
+  V.g1[0] = L.g1[d];
+  V.n1[0] = L.n1[d];
+  V.W1[0] = L.W1[d];
+  V.W1T[0] = L.W1T[d];
+  V.c1[0] = L.c1[d];
+  V.W2[0] = L.W2[d];
+  V.W2T[0] = L.W2T[d];
+  V.c2[0] = L.c2[d];
+  V.g2[0] = L.g2[d];
+  V.n2[0] = L.n2[d];
   return V;
 }
 

@@ -118,7 +118,8 @@ T2O_DEV f4 mma_tile(const float* __restrict__ W, int ldw, int o, int i, f4 x, f4
 }
 
 // y[0..OT) = W[16*OT x 16*IT] · x[0..IT)  (T-layout in, T-layout out)
-template <int OT, int IT>
+// (HOIST: see the bf16 overload; nothing to hoist in fp32)
+template <int OT, int IT, bool HOIST = true>
 T2O_DEV void matvec(const float* __restrict__ W, int ldw, const f4* x, f4* y) {
 #pragma unroll
   for (int o = 0; o < OT; ++o) {
@@ -160,6 +161,20 @@ typedef short s4v __attribute__((ext_vector_type(4)));
 
 T2O_DEV bf4 to_bf4(f4 x) { return __builtin_convertvector(x, bf4); }
 T2O_DEV bf4 ldb4(const __bf16* p) { return *reinterpret_cast<const bf4*>(p); }
+// A weight fragment (4 bf16 of one image row).  From LDS it is a volatile
+// ds_read_b64: the compiler then loads each half of a 16x16x32 operand straight
+// into its registers instead of fusing the fragments of two rows into one
+// ds_read2st64_b64 (8 LDS cycles, banked mod 32 — the image swizzle is laid out
+// for ds_read_b64's mod-64 banks) and assembling the operand with four v_mov.
+// Per step loop: mixer_fwd 2217 -> 2103 instructions, mixer BPTT block-1 wave
+// 2619 -> 2497, block-0 2033 -> 1926, agent_fwd 2403 -> 2298 (gfx950 ISA).  The
+// address-space test folds at compile time (the weights' pointer comes from
+// stage_weights or global_weights).
+T2O_DEV bf4 ldw4(const __bf16* p) {
+  typedef __attribute__((address_space(3))) const volatile bf4 lds_bf4;
+  if (__builtin_amdgcn_is_shared((const __attribute__((address_space(0))) void*)p)) return *(lds_bf4*)(p);
+  return *reinterpret_cast<const bf4*>(p);
+}
 T2O_DEV f4 mfma_b16(bf4 a, bf4 b, f4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s4v, a), __builtin_bit_cast(s4v, b), acc, 0, 0,
                                                     0);
@@ -205,20 +220,21 @@ __host__ __device__ inline int bf_swz(int row, int ld) {
 
 T2O_DEV f4 mma_tile(const __bf16* __restrict__ W, int ldw, int o, int i, f4 x, f4 acc) {
   const int c = lane_c();
-  return mfma_b16(ldb4(W + (size_t)(16 * o + c) * ldw + ((16 * i + 4 * lane_g()) ^ bf_swz(c, ldw))), to_bf4(x), acc);
+  return mfma_b16(ldw4(W + (size_t)(16 * o + c) * ldw + ((16 * i + 4 * lane_g()) ^ bf_swz(c, ldw))), to_bf4(x), acc);
 }
 
 // y[0..OT) = W · x[0..IT), bf16 weights and operands, fp32 accumulate
-template <int OT, int IT>
+template <int OT, int IT, bool HOIST = T2O_SWZ_HOIST>
 T2O_DEV void matvec(const __bf16* __restrict__ W, int ldw, const f4* x, f4* y) {
-  // T2O_SWZ_HOIST 0 (the mixer kernels, register-bound at two waves per SIMD):
-  // the lane's row swizzle is derived per product from an opaque lane id, since
-  // hoisted out of the step loop one register per distinct row length stays
-  // live (mixer BPTT spills 26 -> 4 VGPRs).  1 (default; the agent kernels,
-  // issue-bound at one wave per SIMD): computed once, hoisted — per product it
-  // costs them ~7 % (interleaved A/B, profiles/r3_ab_swz/).
+  // HOIST false (T2O_SWZ_HOIST 0: the mixer BPTT kernels, register-bound at two
+  // waves per SIMD): the lane's row swizzle is derived per product from an opaque
+  // lane id, since hoisted out of the step loop one register per distinct row
+  // length stays live (mixer BPTT spills 26 -> 4 VGPRs).  true (the agent
+  // kernels and the mixer forward, which have registers to spare): computed
+  // once, hoisted — per product it costs the agent ~7 % (interleaved A/B,
+  // profiles/r3_ab_swz/).
   int l = threadIdx.x;
-  if (!T2O_SWZ_HOIST) asm volatile("" : "+v"(l));
+  if (!HOIST) asm volatile("" : "+v"(l));
   const int c = l & 15, g = (l >> 4) & 3;
   bf4 xb[IT];
 #pragma unroll
@@ -230,9 +246,9 @@ T2O_DEV void matvec(const __bf16* __restrict__ W, int ldw, const f4* x, f4* y) {
     f4 acc = zero4();
 #pragma unroll
     for (int i = 0; i + 1 < IT; i += 2)
-      acc = mfma_b32(ldb4(row + ((16 * i + 4 * g) ^ xs)), ldb4(row + ((16 * i + 16 + 4 * g) ^ xs)), xb[i], xb[i + 1],
+      acc = mfma_b32(ldw4(row + ((16 * i + 4 * g) ^ xs)), ldw4(row + ((16 * i + 16 + 4 * g) ^ xs)), xb[i], xb[i + 1],
                      acc);
-    if constexpr (IT & 1) acc = mfma_b16(ldb4(row + ((16 * (IT - 1) + 4 * g) ^ xs)), xb[IT - 1], acc);
+    if constexpr (IT & 1) acc = mfma_b16(ldw4(row + ((16 * (IT - 1) + 4 * g) ^ xs)), xb[IT - 1], acc);
     y[o] = acc;
   }
 }
@@ -780,9 +796,6 @@ T2O_DEV void vec_accumulate(float* __restrict__ ldsv, const f4* v) {
 // atomics (no return value, fire-and-forget at L2).
 template <int NT>
 T2O_DEV void vec_accumulate_g(float* __restrict__ gv, const f4* v) {
-#ifdef T2O_ABL_NOVEC  // ablation builds only (tools/build_variant.sh): wrong gradients
-  return;
-#endif
   const int c = lane_c(), g = lane_g();
   float s[NT][4];
 #pragma unroll
@@ -903,9 +916,6 @@ struct TapeRecA {
 // store a T-layout vector (NT tiles, features off + 16t + 4g + r of record c)
 template <int SIZE, int NT, typename TT>
 T2O_DEV void rec_store(TT* __restrict__ tile, int off, const f4* v) {
-#ifdef T2O_ABL_NOTAPE  // ablation builds only: wrong gradients
-  return;
-#endif
   TT* p = tile + lane_c() * SIZE + off + 4 * lane_g();
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
@@ -942,9 +952,6 @@ struct MaskedRec {
   // a T-layout vector (NT tiles): features off + 16t + 4g + r of this lane's record
   template <int NT>
   T2O_DEV void store(int off, const f4* v) const {
-#ifdef T2O_ABL_NOTAPE  // ablation builds only: wrong gradients
-    return;
-#endif
     typedef int v2i __attribute__((ext_vector_type(2)));
     typedef int v4i __attribute__((ext_vector_type(4)));
 #pragma unroll

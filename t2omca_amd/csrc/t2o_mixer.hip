@@ -201,7 +201,7 @@ T2O_DEV void bcast_agents(float mine, float (&qv)[A]) {
 
 // Key block X0 rows for one step from the prefetched inputs: state-entity
 // embeddings and agent hidden tokens (the hyper-token rows are carried in X0).
-template <int E, int A, typename WT, typename In>
+template <int E, int A, typename WT, typename In, bool HOIST = T2O_SWZ_HOIST>
 T2O_DEV void mix_keys(const Wts<WT>& P, const t2o_layout& L, const In& in, float* X0, int na) {
   using Dm = MixDims<E, A>;
   constexpr int ET = E / 16;
@@ -210,7 +210,7 @@ T2O_DEV void mix_keys(const Wts<WT>& P, const t2o_layout& L, const In& in, float
   for (int s = 0; s < Dm::ST; ++s) {
     const int j = 16 * s + c;
     f4 emb[ET];
-    matvec<ET, 1>(P.w + L.We, 16, &in.st[s], emb);
+    matvec<ET, 1, HOIST>(P.w + L.We, 16, &in.st[s], emb);
     if (j < na) {
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) st4(X0 + j * Dm::LDX + 16 * ft + 4 * g, emb[ft] + vec_t(P.v + L.be, ft));
@@ -284,7 +284,8 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
   for (int t = 0; t < n.T; ++t) {
     T2O_MARK(0);
     const Wts<WT> P = step_view(P0);
-    mix_keys<E, A>(P, L, in, X0, na);
+    // (the forward has registers to spare at two waves per SIMD: swizzles hoisted)
+    mix_keys<E, A, WT, MixIn<E, A>, true>(P, L, in, X0, na);
     const float myq = mix_qv<E, A>(n, in, args.n_actions, args.avail != nullptr);
     __builtin_amdgcn_sched_barrier(0);  // every read of this step's inputs issued before they are reloaded
     if (t + 1 < n.T) mix_load<E, A>(args, n, b, t + 1, in, na);  // prefetch step t+1 (in is consumed)
@@ -308,7 +309,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft) st4(xm + 16 * ft + 4 * g, x[ft]);
         }
-        mixer_block_fwd<E, H, Dm::KT, FF, false>(P, L, d, K, lk, x, nullptr);
+        mixer_block_fwd<E, H, Dm::KT, FF, false, WT, true>(P, L, d, K, lk, x, nullptr);
         if (qt == 0) T2O_MARK(2 + d);
       }
 #pragma unroll

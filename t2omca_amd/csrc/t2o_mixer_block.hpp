@@ -100,7 +100,8 @@ T2O_DEV void keys_combine(const KeyFrags<E, KT, BF>& K, const f4* w, f4* out) {
   }
 }
 
-template <int E, int H, int KT, int FF, bool CACHE, typename WT>
+// HOIST: matvec's swizzle hoisting (t2o_common.hpp), true from the forward kernel
+template <int E, int H, int KT, int FF, bool CACHE, typename WT, bool HOIST = T2O_SWZ_HOIST>
 T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
                              const KeyFrags<E, KT, sizeof(WT) == 2>& K, int Lk, f4* x,
                              MixerCache<E, H, KT, FF>* cache) {
@@ -108,7 +109,7 @@ T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
   constexpr bool BF = sizeof(WT) == 2;
   const int g = lane_g();
   f4 u[HET];
-  matvec<HET, ET>(P.w + L.M[d], E, x, u);
+  matvec<HET, ET, HOIST>(P.w + L.M[d], E, x, u);
   f4 z[HET];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
@@ -144,7 +145,7 @@ T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
 #pragma unroll
     for (int t = 0; t < HET; ++t) cache->u[t] = u[t];
   }
-  post_fwd<E, H, FF, CACHE>(P, L, d, z, x, CACHE ? &cache->post : nullptr);
+  post_fwd<E, H, FF, CACHE, WT, HOIST>(P, L, d, z, x, CACHE ? &cache->post : nullptr);
 }
 
 // Backward of block d for one query tile.  gx: in = grad wrt block output,
