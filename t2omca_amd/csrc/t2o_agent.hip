@@ -401,7 +401,15 @@ constexpr int agp_stage_floats() {
 }
 
 template <int E, int H, int D, int NE, int FF, bool RT, typename WT>
-T2O_DEV void agent_bwd_pipe_body(const AgentBwdArgs& args, const t2o_layout& L, const t2o_layout& G) {
+// (The body lives in the kernel itself.  Round 3 moved it into a device function
+// taking the args and layouts by reference, to be callable with a compile-time
+// layout: the compiler then spilled 28 B per lane to scratch, one reload in the
+// step loop, and agent_bwd went 0.543 -> 0.604 ms — bisected, profiles/r4_bisect/.
+// Compile-time offsets had measured slower here anyway: 0.623 -> 0.643 ms,
+// profiles/r3_ab6/.)
+__global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(AgentBwdArgs args) {
+  const t2o_layout& L = args.L;
+  const t2o_layout& G = args.G;
   static_assert(D == 2, "one wave per block of a depth-2 stack");
   constexpr int ET = E / 16, HET = H * ET;
   constexpr bool BF = sizeof(WT) == 2;
@@ -656,13 +664,6 @@ T2O_DEV void agent_bwd_pipe_body(const AgentBwdArgs& args, const t2o_layout& L, 
       }
     }
   });
-}
-
-// The kernel-argument layout.  (Compile-time pack offsets, as the bf16 mixer BPTT
-// reads them, measured slower here: agent_bwd 0.623 -> 0.643 ms, profiles/r3_ab6/.)
-template <int E, int H, int D, int NE, int FF, bool RT, typename WT>
-__global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(AgentBwdArgs args) {
-  agent_bwd_pipe_body<E, H, D, NE, FF, RT, WT>(args, args.L, args.G);
 }
 
 template <int E, int H, int D, int NE, int FF, typename WT>

@@ -38,8 +38,9 @@ inline int t2o_mixer_cap(int a) { return a <= 8 ? 8 : a <= 13 ? 13 : a <= 16 ? 1
 #define T2O_CASE_X(E, H, D, NE, FF, RT, STMT)                               \
   {                                                                          \
     constexpr int E_ = E, H_ = H, D_ = D, NE_ = NE, FF_ = FF;                \
-    constexpr bool RT_ = RT;                                                 \
-    (void)E_; (void)H_; (void)D_; (void)NE_; (void)FF_; (void)RT_;           \
+    constexpr bool RT_ = (RT) != 0;                                          \
+    constexpr int RTM_ = RT;                                                 \
+    (void)E_; (void)H_; (void)D_; (void)NE_; (void)FF_; (void)RT_; (void)RTM_; \
     STMT;                                                                    \
   }
 
@@ -63,13 +64,19 @@ inline int t2o_mixer_cap(int a) { return a <= 8 ? 8 : a <= 13 ? 13 : a <= 16 ? 1
     }                                                                                           \
   } while (0)
 
-// mixer kernels: exact instance (abs head only), else the runtime instance of the
-// agent count's class (which also computes the other qmix_pos_funcs)
+// mixer kernels: exact instance (abs head), else the runtime instance of the agent
+// count's class (which also computes the other qmix_pos_funcs).  RTM_ (the
+// mixer's instance mode): 0 exact counts + abs head, 1 runtime counts + runtime
+// head, 2 exact counts + runtime head — the headline's 8 AGVs with a softplus /
+// quadratic / identity head (the runtime instance's register file holds the
+// counts too and spilled: 1.05 vs 0.57 ms mixer BPTT, profiles/r3_f5/softplus.json)
 #define T2O_DISPATCH_MIXER(EV, HV, DV, NEV, FFV, ABS, STMT)                                     \
   do {                                                                                          \
     const int e_ = (EV), h_ = (HV), d_ = (DV), ne_ = (NEV), ff_ = (FFV);                        \
     if ((ABS) && t2o_exact_shape(e_, h_, d_, ne_, ff_)) {                                       \
       T2O_DISPATCH_EXACT(STMT)                                                                  \
+    } else if (!(ABS) && t2o_default_net(e_, h_, d_, ff_) && ne_ == 8) {                        \
+      T2O_CASE_X(32, 3, 2, 8, 128, 2, STMT)                                                     \
     } else if (t2o_default_net(e_, h_, d_, ff_) && ne_ >= 1 && ne_ <= 64) {                     \
       const int cap_ = t2o_mixer_cap(ne_);                                                      \
       if (cap_ == 8) T2O_CASE_X(32, 3, 2, 8, 128, true, STMT)                                   \

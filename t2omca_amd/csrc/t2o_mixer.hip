@@ -248,8 +248,10 @@ T2O_DEV float mixer_head(const Wts<WT>& P, const t2o_layout& L, const float* OUT
   return yv + fmaxf(p2, 0.f);
 }
 
-// RT: runtime-agent instance (A is a capacity, args.na the agent count)
-template <int E, int H, int D, int A, int FF, bool RT, bool WLDS, typename WT>
+// RT (t2o_dispatch.hpp RTM_): 0 exact agent count A + abs head; 1 runtime-agent
+// instance (A a capacity, args.na the agent count) + runtime head; 2 exact A +
+// runtime head (L.pos_func)
+template <int E, int H, int D, int A, int FF, int RT, bool WLDS, typename WT>
 __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
   using Dm = MixDims<E, A>;
   constexpr int ET = E / 16;
@@ -257,7 +259,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
   const int w = wave_id();
   const MixerNet n = args.net[blockIdx.y];
   const t2o_layout& L = args.L;
-  const int na = RT ? args.na : A, nq = na + 3, lk = 2 * na + 3;
+  const int na = RT == 1 ? args.na : A, nq = na + 3, lk = 2 * na + 3;
   const int pf = RT ? L.pos_func : T2O_POS_ABS;  // the mixer head's positivity function
   const float pb = RT ? L.pos_beta : 1.f;
   // forward weights in LDS for the unroll when they fit beside the per-wave buffers
@@ -295,7 +297,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
     T2O_MARK(1);
 #pragma unroll
     for (int qt = 0; qt < Dm::QT; ++qt) {
-      if (RT && 16 * qt >= nq) break;  // (wave-uniform) query tiles past the real rows
+      if (RT == 1 && 16 * qt >= nq) break;  // (wave-uniform) query tiles past the real rows
       const int q = 16 * qt + c;
       f4 x[ET];
 #pragma unroll
@@ -345,7 +347,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
   }
 }
 
-template <int E, int H, int D, int A, int FF, bool RT, typename WT>
+template <int E, int H, int D, int A, int FF, int RT, typename WT>
 int launch_mixer_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
   if (!kernel_layout_matches<E, H, D, FF, WT>(args.L)) return T2O_EINVAL;  // (kernels use the compile-time offsets)
   using Dm = MixDims<E, A>;
@@ -538,8 +540,8 @@ T2O_DEV void mixer_head_bwd(const Wts<WT>& P, const t2o_layout& L, const float* 
   }
 }
 
-// RT: runtime-agent instance (A is a capacity, args.f.na the agent count)
-template <int E, int H, int D, int A, int FF, bool RT, bool WLDS, typename WT>
+// RT: as mixer_fwd_kernel's
+template <int E, int H, int D, int A, int FF, int RT, bool WLDS, typename WT>
 __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   using Dm = MixDims<E, A>;
   using Bd = MixBwdDims<E, A>;
@@ -549,7 +551,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   const MixerNet& n = fa.net[0];
   const t2o_layout& L = fa.L;
   const t2o_layout& G = args.G;
-  const int na = RT ? fa.na : A, nq = na + 3, lk = 2 * na + 3;
+  const int na = RT == 1 ? fa.na : A, nq = na + 3, lk = 2 * na + 3;
   const int w = wave_id();
   float* X0 = smem + args.lds_w + w * Bd::PERW;
   float* WORK = X0 + Dm::X0F;
@@ -1141,12 +1143,12 @@ inline __host__ __device__ int64_t mixp_weight_elems(const t2o_layout& L) {
   return sizeof(WT) == 4 ? L.fwd_total : L.total;
 }
 
-template <int E, int H, int D, int A, int FF, bool RT, typename WT>
+template <int E, int H, int D, int A, int FF, int RT, typename WT>
 T2O_DEV void mixer_bwd_pipe_body(const MixerBwdArgs& args, const t2o_layout& L, const t2o_layout& G) {
   static_assert(D == 2 && MixPipeDims<E, A>::OK, "one wave per block of a depth-2 stack, one query tile");
   using Dm = MixDims<E, A>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int na = RT ? args.f.na : A;
+  const int na = RT == 1 ? args.f.na : A;
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
   // the block this wave owns.  Waves w and w + 4 share a SIMD: with four pairs,
   // pairs 2-3 swap their block roles so every SIMD holds one block-0 and one
@@ -1202,7 +1204,7 @@ T2O_DEV void mixer_bwd_pipe_body(const MixerBwdArgs& args, const t2o_layout& L, 
 // kernel-argument layout: with constants its VGPR spills rose 5 -> 88 and the
 // kernel 1.74 -> 2.14 ms (profiles/r3_ab4f/); the other kernels measured no
 // gain with them (agent_fwd +2 %, profiles/r3_ab4/).
-template <int E, int H, int D, int A, int FF, bool RT, typename WT>
+template <int E, int H, int D, int A, int FF, int RT, typename WT>
 __global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) {
   if constexpr (sizeof(WT) == 2)
     mixer_bwd_pipe_body<E, H, D, A, FF, RT, WT>(args, kernel_layout<E, H, D, FF, WT>(args.f.L),
@@ -1211,7 +1213,7 @@ __global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) 
     mixer_bwd_pipe_body<E, H, D, A, FF, RT, WT>(args, args.f.L, args.G);
 }
 
-template <int E, int H, int D, int A, int FF, bool RT, typename WT>
+template <int E, int H, int D, int A, int FF, int RT, typename WT>
 int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
   if (!kernel_layout_matches<E, H, D, FF, WT>(args.f.L)) return T2O_EINVAL;  // (compile-time offsets)
   constexpr int PERW = MixBwdDims<E, A>::PERW;
@@ -1326,8 +1328,8 @@ extern "C" int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, c
   }
   int rc = T2O_EUNSUPPORTED;
   T2O_DISPATCH_MIXER(L->E, L->H, L->D, L->n_ent, L->FF, L->pos_func == T2O_POS_ABS,
-                     rc = (L->prec ? launch_mixer_fwd<E_, H_, D_, NE_, FF_, RT_, __bf16>(a, nnet, (hipStream_t)stream)
-                                   : launch_mixer_fwd<E_, H_, D_, NE_, FF_, RT_, float>(a, nnet, (hipStream_t)stream)));
+                     rc = (L->prec ? launch_mixer_fwd<E_, H_, D_, NE_, FF_, RTM_, __bf16>(a, nnet, (hipStream_t)stream)
+                                   : launch_mixer_fwd<E_, H_, D_, NE_, FF_, RTM_, float>(a, nnet, (hipStream_t)stream)));
   return rc;
 }
 
@@ -1368,7 +1370,7 @@ extern "C" int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, cons
   a.tape = tape;
   int rc = T2O_EUNSUPPORTED;
   T2O_DISPATCH_MIXER(L->E, L->H, L->D, L->n_ent, L->FF, L->pos_func == T2O_POS_ABS,
-                     rc = (L->prec ? launch_mixer_bwd<E_, H_, D_, NE_, FF_, RT_, __bf16>(a, max_slabs, nslab, (hipStream_t)stream)
-                                   : launch_mixer_bwd<E_, H_, D_, NE_, FF_, RT_, float>(a, max_slabs, nslab, (hipStream_t)stream)));
+                     rc = (L->prec ? launch_mixer_bwd<E_, H_, D_, NE_, FF_, RTM_, __bf16>(a, max_slabs, nslab, (hipStream_t)stream)
+                                   : launch_mixer_bwd<E_, H_, D_, NE_, FF_, RTM_, float>(a, max_slabs, nslab, (hipStream_t)stream)));
   return rc;
 }

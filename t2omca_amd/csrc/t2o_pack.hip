@@ -280,8 +280,11 @@ struct Builder {
 extern "C" int t2o_layout_instance(const t2o_layout* L) {
   if (!L) return T2O_EINVAL;
   if (L->generic) return T2O_INSTANCE_GENERIC;
-  const bool abs_head = L->kind == 0 || L->pos_func == T2O_POS_ABS;  // (exact mixer instances: abs head only)
-  return abs_head && t2o_exact_shape(L->E, L->H, L->D, L->n_ent, L->FF) ? T2O_INSTANCE_EXACT : T2O_INSTANCE_RUNTIME;
+  const bool abs_head = L->kind == 0 || L->pos_func == T2O_POS_ABS;  // (exact mixer instances: abs head,
+  // and at 8 AGVs every head: t2o_dispatch.hpp T2O_DISPATCH_MIXER)
+  const bool exact_8 = L->kind == 1 && L->n_ent == 8 && t2o_default_net(L->E, L->H, L->D, L->FF);
+  return (abs_head || exact_8) && t2o_exact_shape(L->E, L->H, L->D, L->n_ent, L->FF) ? T2O_INSTANCE_EXACT
+                                                                                      : T2O_INSTANCE_RUNTIME;
 }
 
 extern "C" int t2o_layout_init(t2o_layout* L, int kind, int E, int H, int D, int F, int NA, int FF, int n_ent,

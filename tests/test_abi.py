@@ -195,7 +195,8 @@ def test_layout_instance_classes(kind):
 def test_layout_mixer_heads_run_runtime_instances():
     """A non-abs qmix_pos_func keeps the default network on MFMA kernels (runtime-entity
     instances, which take the head as a parameter) at every AGV count, exact counts
-    included; any other network with such a head runs the generic kernels."""
+    included (8 AGVs: the exact instance with a run-time head); any other network
+    with such a head runs the generic kernels."""
     import ctypes as C
 
     from t2omca_amd import _lib
@@ -203,7 +204,9 @@ def test_layout_mixer_heads_run_runtime_instances():
     for pf in (1, 2, 3):
         for n in (3, 8, 12, 16, 64):
             L = _lib.make_layout(1, 32, 3, 2, 8, 1, 128, n, pos_func=pf, pos_beta=0.5, flags=0)
-            assert L.generic == 0 and lib.t2o_layout_instance(C.byref(L)) == 1, (pf, n)
+            # 8 AGVs (the headline): the exact instance, head as a run-time parameter
+            want = 0 if n == 8 else 1
+            assert L.generic == 0 and lib.t2o_layout_instance(C.byref(L)) == want, (pf, n)
         Lo = _lib.make_layout(1, 64, 4, 2, 8, 1, 256, 8, pos_func=pf, flags=0)
         assert Lo.generic == 1 and lib.t2o_layout_instance(C.byref(Lo)) == 2
         Lx = _lib.make_layout(1, 16, 2, 1, 8, 1, 64, 3, pos_func=pf, flags=0)

@@ -189,14 +189,14 @@ def test_generic_td_update_matches_oracle(tag, cfg, B, T):
 
 
 def test_headline_shape_with_softplus_head_matches_oracle(monkeypatch):
-    """configs[2]'s model with a softplus head: the agent runs its exact instance, the
-    mixer the runtime-entity instance of its class (the exact mixer instances compute
-    the abs head only; the runtime ones take qmix_pos_func as a parameter)."""
+    """configs[2]'s model with a softplus head: the agent and the mixer run their exact
+    8-AGV instances (the mixer's with the head as a run-time parameter, t2o_dispatch.hpp
+    T2O_DISPATCH_MIXER mode 2)."""
     require_gpu()
     monkeypatch.setenv("T2O_GENERIC", "0")
     cfg = _cfg_of(8, qmix_pos_func="softplus", qmix_pos_func_beta=2.0, tag="headline-softplus")
     from t2omca_amd.modules import TransformerAgent, TransformerMixer
-    assert TransformerMixer(_args(cfg)).shape.instance == "runtime"
+    assert TransformerMixer(_args(cfg)).shape.instance == "exact"
     assert TransformerAgent(None, _args(cfg)).shape.instance == "exact"
     _td(cfg, 4, 6)
 

@@ -12,8 +12,9 @@ instance is compiled for a capacity class and reads the real count at run time:
 
 The cases below put every class on both sides of its boundaries (A = 2 ... 63).
 The runtime mixer instances also compute every qmix_pos_func (softplus with beta,
-quadratic, identity; n_transf_mixer.py:95-103) — the exact ones are abs-only — so
-those heads run on MFMA kernels at every AGV count, including the exact ones.
+quadratic, identity; n_transf_mixer.py:95-103), so those heads run on MFMA kernels
+at every AGV count; at 8 AGVs (the headline) a non-abs head runs the exact instance
+with the head as a run-time parameter.
 Checked against the reference modules' goldens (5 and 32 AGVs, per-step forward +
 autograd through the drop-in modules) and against the fp64 oracle's full TD update
 (oracle/ref_learner; TD semantics parity-unpinned).
@@ -75,20 +76,26 @@ def test_runtime_instance_modules_vs_reference_goldens(name):
 
 
 @pytest.mark.parametrize("name", ["a8_softplus", "a8_quadratic", "a8_identity"])
-def test_runtime_mixer_heads_vs_reference_goldens(name):
-    """Every non-abs qmix_pos_func on the runtime mixer instance, against the
-    reference module's own outputs and autograd (n_transf_mixer.py:95-103)."""
+def test_mixer_heads_vs_reference_goldens(name):
+    """Every non-abs qmix_pos_func against the reference module's own outputs and
+    autograd (n_transf_mixer.py:95-103).  At 8 AGVs these run the exact 8-AGV mixer
+    instance with the head as a run-time parameter (t2o_dispatch.hpp mode 2)."""
     require_gpu()
-    assert mixer_module_check(os.path.join(GOLD, f"mixer_{name}.npz")) == "runtime"
+    assert mixer_module_check(os.path.join(GOLD, f"mixer_{name}.npz")) == "exact"
 
 
-@pytest.mark.parametrize("A,B,T,head,beta,precision", [(8, 4, 6, "softplus", 0.5, "fp32"),
-                                                       (12, 3, 5, "quadratic", 1.0, "fp32"),
-                                                       (5, 4, 6, "identity", 1.0, "fp32"),
-                                                       (8, 4, 6, "softplus", 2.0, "bf16")])
-def test_runtime_mixer_heads_td_update(A, B, T, head, beta, precision):
+# 8 AGVs: the exact instance with a run-time head; 7 / 12 / 5: the runtime-entity
+# instances of capacity 8 and 13 (counts and head both run-time)
+@pytest.mark.parametrize("A,B,T,head,beta,precision,inst", [(8, 4, 6, "softplus", 0.5, "fp32", "exact"),
+                                                            (7, 4, 6, "softplus", 0.5, "fp32", "runtime"),
+                                                            (12, 3, 5, "quadratic", 1.0, "fp32", "runtime"),
+                                                            (5, 4, 6, "identity", 1.0, "fp32", "runtime"),
+                                                            (8, 4, 6, "quadratic", 1.0, "fp32", "exact"),
+                                                            (8, 4, 6, "softplus", 2.0, "bf16", "exact"),
+                                                            (7, 4, 6, "softplus", 2.0, "bf16", "runtime")])
+def test_mixer_heads_td_update(A, B, T, head, beta, precision, inst):
     require_gpu()
     cfg = dict(_cfg_of(A, qmix_pos_func=head, qmix_pos_func_beta=beta), tag=f"A{A}-{head}")
     tol = (2e-2, 6e-2) if precision == "bf16" else None
     learner, _ = _td(cfg, B, T, precision=precision, tol=tol)
-    assert learner.sm.instance == "runtime"
+    assert learner.sm.instance == inst
