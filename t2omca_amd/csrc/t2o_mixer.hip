@@ -258,7 +258,9 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int w = wave_id();
   const MixerNet n = args.net[blockIdx.y];
-  const t2o_layout& L = args.L;
+  // bf16: the pack offsets as compile-time constants (t2o_layout.hpp kernel_layout,
+  // as the pipelined BPTT reads them; the launcher checks they match)
+  const t2o_layout L = kernel_layout<E, H, D, FF, WT>(args.L);
   const int na = RT == 1 ? args.na : A, nq = na + 3, lk = 2 * na + 3;
   const int pf = RT ? L.pos_func : T2O_POS_ABS;  // the mixer head's positivity function
   const float pb = RT ? L.pos_beta : 1.f;
