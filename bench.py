@@ -486,7 +486,7 @@ def loop_bench(args, world, rank, dev):
             info = learner.train(sample, runner.t_env, episode, per_weight=w)
             if timed:
                 mark("update_priorities")
-            buf.update_priorities(idx, info["td_errors_abs"].flatten() + 1e-6)
+            buf.update_priorities(idx, info["td_errors_abs"].flatten(), add=1e-6)
         if timed:
             mark("end")
 
@@ -788,7 +788,8 @@ def main():
         def make_step(lr):
             def step(i):
                 info = lr.train(batch, 0, i, per_weight=w)
-                buf.update_priorities(idx, info["td_errors_abs"].flatten() + 1e-6)
+                # per_run.py:237-238's `+ 1e-6`, applied inside the priority kernel
+                buf.update_priorities(idx, info["td_errors_abs"].flatten(), add=1e-6)
             return step
         step = make_step(learner)
 

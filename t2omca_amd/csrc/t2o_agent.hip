@@ -68,6 +68,7 @@ void agent_fwd_kernel(AgentFwdArgs args) {
   } else {
     P0 = global_weights(net.pack, L, WT{});
   }
+  P0.vol = NE <= 8;  // (Wts::vol: the 16+-entity instances run one wave per SIMD)
   const int A = args.A, F = args.F;
   const int ne = RT ? A : NE;
   const int R = args.B * A;
@@ -131,7 +132,7 @@ void agent_fwd_kernel(AgentFwdArgs args) {
     }
     f4 q = zero4();
 #pragma unroll
-    for (int i = 0; i < ET; ++i) q = mma_tile(P.w + L.Wo, E, 0, i, x[i], q);
+    for (int i = 0; i < ET; ++i) q = mma_tile(P.w + L.Wo, E, 0, i, x[i], q, P.vol);
     q += vec_t(P.v + L.bo, 0);
 #pragma unroll
     for (int t = 0; t < ET; ++t) h[t] = x[t];
@@ -213,7 +214,8 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
   const int lds_w = (int)((lds_weight_floats<WT>(L, nw) + 15) / 16 * 16);
   float* stage = smem + lds_w + wave_id() * STAGE;
   float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
-  const Wts<WT> P0 = stage_weights(smem, args.pack, L, nw, WT{});
+  Wts<WT> P0 = stage_weights(smem, args.pack, L, nw, WT{});
+  P0.vol = NE <= 8;  // (Wts::vol)
   zero_flushed_regions(gs, G, false);  // (full record: the contraction writes M / N)
   __syncthreads();
 
@@ -442,7 +444,8 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
   f4* xch = reinterpret_cast<f4*>(smem + lds_w + 2 * AGP_TILES * STAGE + tl * agp_xch_floats<E>());
   const int lane = threadIdx.x & 63;
   float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
-  const Wts<WT> P0 = stage_weights(smem, args.pack, L, nw, WT{});
+  Wts<WT> P0 = stage_weights(smem, args.pack, L, nw, WT{});
+  P0.vol = NE <= 8;  // (Wts::vol: 16+ entities measured slower with volatile reads)
   zero_flushed_regions(gs, G, ACC);  // (lean record: dM / dN flushed from registers)
   int* const flags = reinterpret_cast<int*>(smem + lds_w + 2 * AGP_TILES * STAGE + AGP_TILES * agp_xch_floats<E>());
   if (threadIdx.x < PAIR_FLAG_FLOATS) flags[threadIdx.x] = 0;

@@ -46,12 +46,12 @@ T2O_DEV void agent_attn_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const 
   constexpr int ET = E / 16, HET = H * ET;
   const float* be = P.v + L.be;
   f4 u[HET];
-  matvec<HET, ET>(P.w + L.M[d], E, x, u);
+  matvec<HET, ET>(P.w + L.M[d], E, x, u, P.vol);
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
     float p[NE + 1];
     f4 w;
-    matvec<1, ET>(P.w + L.WeT, E, &u[hh * ET], &w);
+    matvec<1, ET>(P.w + L.WeT, E, &u[hh * ET], &w, P.vol);
     float cpart = 0.f, s0part = 0.f;
 #pragma unroll
     for (int t = 0; t < ET; ++t) {
@@ -91,7 +91,7 @@ T2O_DEV void agent_attn_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const 
       Ps += p[j + 1];
     }
     f4 zz[ET];
-    matvec<ET, 1>(P.w + L.We, 16, &oh, zz);
+    matvec<ET, 1>(P.w + L.We, 16, &oh, zz, P.vol);
 #pragma unroll
     for (int t = 0; t < ET; ++t) z[hh * ET + t] = zz[t] + p[0] * h[t] + Ps * vec_t(be, t);
     if (cache) {
@@ -275,7 +275,7 @@ T2O_DEV void agent_attn_bwd(const Wts<WT>& P, const t2o_layout& L, float* __rest
     }
     // s_h0 = u_h·h ; s_hj = (WeT u_h)·o_j + u_h·be
     f4 t1[ET];
-    matvec<ET, 1>(P.w + L.We, 16, &gw, t1);
+    matvec<ET, 1>(P.w + L.We, 16, &gw, t1, P.vol);
 #pragma unroll
     for (int t = 0; t < ET; ++t) {
       gu[hh * ET + t] = t1[t] + gs0 * h[t] + gc * vec_t(be, t);

@@ -67,12 +67,12 @@ T2O_DEV void agent_block_fwd_ch(const Wts<WT>& P, const t2o_layout& L, int d, co
   constexpr int ET = E / 16, HET = H * ET, CH = AG_CHUNK;
   const float* be = P.v + L.be;
   f4 u[HET];
-  matvec<HET, ET>(P.w + L.M[d], E, x, u);
+  matvec<HET, ET>(P.w + L.M[d], E, x, u, P.vol);
   f4 w[H], oh[H];
   float cval[H], s0[H], m[H], l[H], e0[H], Ps[H];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
-    matvec<1, ET>(P.w + L.WeT, E, &u[hh * ET], &w[hh]);
+    matvec<1, ET>(P.w + L.WeT, E, &u[hh * ET], &w[hh], P.vol);
     float cpart = 0.f, s0part = 0.f;
 #pragma unroll
     for (int t = 0; t < ET; ++t) {
@@ -133,7 +133,7 @@ T2O_DEV void agent_block_fwd_ch(const Wts<WT>& P, const t2o_layout& L, int d, co
     oh[hh] *= il;
     Ps[hh] *= il;
     f4 zz[ET];
-    matvec<ET, 1>(P.w + L.We, 16, &oh[hh], zz);
+    matvec<ET, 1>(P.w + L.We, 16, &oh[hh], zz, P.vol);
 #pragma unroll
     for (int t = 0; t < ET; ++t) z[hh * ET + t] = zz[t] + p0 * h[t] + Ps[hh] * vec_t(be, t);
     if constexpr (CACHE) {
@@ -224,7 +224,7 @@ T2O_DEV void agent_block_bwd_ch(const Wts<WT>& P, const t2o_layout& L, const t2o
     const f4* uh = &c.u[hh * ET];
     // s_h0 = u_h·h ; s_hj = (WeT u_h)·o_j + u_h·be
     f4 t1[ET];
-    matvec<ET, 1>(P.w + L.We, 16, &gw[hh], t1);
+    matvec<ET, 1>(P.w + L.We, 16, &gw[hh], t1, P.vol);
 #pragma unroll
     for (int t = 0; t < ET; ++t) {
       gu[hh * ET + t] = t1[t] + gs0[hh] * h[t] + gc[hh] * vec_t(be, t);

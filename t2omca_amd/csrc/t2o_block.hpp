@@ -28,14 +28,14 @@ template <int E, int H, int FF, bool CACHE, typename WT, bool HOIST = T2O_SWZ_HO
 T2O_DEV void post_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* z, f4* x, PostCache<E, H, FF>* c) {
   constexpr int ET = E / 16, HET = H * ET, FT = FF / 16;
   f4 r1[ET];
-  matvec<ET, HET, HOIST>(P.w + L.N[d], H * E, z, r1);
+  matvec<ET, HET, HOIST>(P.w + L.N[d], H * E, z, r1, P.vol);
 #pragma unroll
   for (int t = 0; t < ET; ++t) r1[t] += vec_t(P.v + L.bu[d], t) + x[t];
   f4 y[ET], xh1[ET];
   float rs1;
   layernorm_fwd<ET>(r1, P.v + L.g1[d], P.v + L.n1[d], y, xh1, rs1);
   f4 f1[FT], f1r[FT];
-  matvec<FT, ET, HOIST>(P.w + L.W1[d], E, y, f1);
+  matvec<FT, ET, HOIST>(P.w + L.W1[d], E, y, f1, P.vol);
 #pragma unroll
   for (int t = 0; t < FT; ++t) {
     f1[t] += vec_t(P.v + L.c1[d], t);
@@ -43,7 +43,7 @@ T2O_DEV void post_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* z,
     for (int r = 0; r < 4; ++r) f1r[t][r] = fmaxf(f1[t][r], 0.f);
   }
   f4 r2[ET];
-  matvec<ET, FT, HOIST>(P.w + L.W2[d], FF, f1r, r2);
+  matvec<ET, FT, HOIST>(P.w + L.W2[d], FF, f1r, r2, P.vol);
 #pragma unroll
   for (int t = 0; t < ET; ++t) r2[t] += vec_t(P.v + L.c2[d], t) + y[t];
   if constexpr (CACHE) {
@@ -137,13 +137,13 @@ T2O_DEV void post_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d, const f
   if constexpr (R::X >= 0) rec.template store<ET>(R::X, x);
   if constexpr (R::Z >= 0) rec.template store<HET>(R::Z, z);
   f4 r1[ET];
-  matvec<ET, HET>(P.w + L.N[d], H * E, z, r1);
+  matvec<ET, HET>(P.w + L.N[d], H * E, z, r1, P.vol);
 #pragma unroll
   for (int t = 0; t < ET; ++t) r1[t] += vec_t(P.v + L.bu[d], t) + x[t];
   f4 y[ET];
   layernorm_fwd<ET>(r1, P.v + L.g1[d], P.v + L.n1[d], y, c->xh1, c->rs1);
   f4 f1[FT], f1r[FT];
-  matvec<FT, ET>(P.w + L.W1[d], E, y, f1);
+  matvec<FT, ET>(P.w + L.W1[d], E, y, f1, P.vol);
   uint32_t m = 0;
 #pragma unroll
   for (int t = 0; t < FT; ++t) {
@@ -156,7 +156,7 @@ T2O_DEV void post_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d, const f
   }
   c->relu = m;
   f4 r2[ET];
-  matvec<ET, FT>(P.w + L.W2[d], FF, f1r, r2);
+  matvec<ET, FT>(P.w + L.W2[d], FF, f1r, r2, P.vol);
 #pragma unroll
   for (int t = 0; t < ET; ++t) r2[t] += vec_t(P.v + L.c2[d], t) + y[t];
   layernorm_fwd<ET>(r2, P.v + L.g2[d], P.v + L.n2[d], x, c->xh2, c->rs2);

@@ -108,7 +108,7 @@ T2O_DEV float ld_or0(const float* __restrict__ p, int64_t i, bool ok) {
 T2O_DEV void st4(float* p, f4 v) { *reinterpret_cast<f4*>(p) = v; }
 
 // acc += W[16o.. , 16i..] (16x16 tile of row-major W, leading dim ldw) · x_tile
-T2O_DEV f4 mma_tile(const float* __restrict__ W, int ldw, int o, int i, f4 x, f4 acc) {
+T2O_DEV f4 mma_tile(const float* __restrict__ W, int ldw, int o, int i, f4 x, f4 acc, bool = true) {
   const f4 w = ld4(W + (size_t)(16 * o + lane_c()) * ldw + 16 * i + 4 * lane_g());
   acc = mfma4(w[0], x[0], acc);
   acc = mfma4(w[1], x[1], acc);
@@ -120,7 +120,7 @@ T2O_DEV f4 mma_tile(const float* __restrict__ W, int ldw, int o, int i, f4 x, f4
 // y[0..OT) = W[16*OT x 16*IT] · x[0..IT)  (T-layout in, T-layout out)
 // (HOIST: see the bf16 overload; nothing to hoist in fp32)
 template <int OT, int IT, bool HOIST = true>
-T2O_DEV void matvec(const float* __restrict__ W, int ldw, const f4* x, f4* y) {
+T2O_DEV void matvec(const float* __restrict__ W, int ldw, const f4* x, f4* y, bool = true) {
 #pragma unroll
   for (int o = 0; o < OT; ++o) {
     f4 acc = zero4();
@@ -218,14 +218,15 @@ __host__ __device__ inline int bf_swz(int row, int ld) {
   return 8 * ((row >> 3) & 1);
 }
 
-T2O_DEV f4 mma_tile(const __bf16* __restrict__ W, int ldw, int o, int i, f4 x, f4 acc) {
+T2O_DEV f4 mma_tile(const __bf16* __restrict__ W, int ldw, int o, int i, f4 x, f4 acc, bool vol = true) {
   const int c = lane_c();
-  return mfma_b16(ldw4(W + (size_t)(16 * o + c) * ldw + ((16 * i + 4 * lane_g()) ^ bf_swz(c, ldw))), to_bf4(x), acc);
+  const __bf16* p = W + (size_t)(16 * o + c) * ldw + ((16 * i + 4 * lane_g()) ^ bf_swz(c, ldw));
+  return mfma_b16(vol ? ldw4(p) : ldb4(p), to_bf4(x), acc);
 }
 
 // y[0..OT) = W · x[0..IT), bf16 weights and operands, fp32 accumulate
 template <int OT, int IT, bool HOIST = T2O_SWZ_HOIST>
-T2O_DEV void matvec(const __bf16* __restrict__ W, int ldw, const f4* x, f4* y) {
+T2O_DEV void matvec(const __bf16* __restrict__ W, int ldw, const f4* x, f4* y, bool vol = true) {
   // HOIST false (T2O_SWZ_HOIST 0: the mixer BPTT kernels, register-bound at two
   // waves per SIMD): the lane's row swizzle is derived per product from an opaque
   // lane id, since hoisted out of the step loop one register per distinct row
@@ -245,10 +246,15 @@ T2O_DEV void matvec(const __bf16* __restrict__ W, int ldw, const f4* x, f4* y) {
     const __bf16* row = W + (size_t)(16 * o + c) * ldw;
     f4 acc = zero4();
 #pragma unroll
-    for (int i = 0; i + 1 < IT; i += 2)
-      acc = mfma_b32(ldw4(row + ((16 * i + 4 * g) ^ xs)), ldw4(row + ((16 * i + 16 + 4 * g) ^ xs)), xb[i], xb[i + 1],
-                     acc);
-    if constexpr (IT & 1) acc = mfma_b16(ldw4(row + ((16 * (IT - 1) + 4 * g) ^ xs)), xb[IT - 1], acc);
+    for (int i = 0; i + 1 < IT; i += 2) {
+      const __bf16* p0 = row + ((16 * i + 4 * g) ^ xs);
+      const __bf16* p1 = row + ((16 * i + 16 + 4 * g) ^ xs);
+      acc = mfma_b32(vol ? ldw4(p0) : ldb4(p0), vol ? ldw4(p1) : ldb4(p1), xb[i], xb[i + 1], acc);
+    }
+    if constexpr (IT & 1) {
+      const __bf16* p = row + ((16 * (IT - 1) + 4 * g) ^ xs);
+      acc = mfma_b16(vol ? ldw4(p) : ldb4(p), xb[IT - 1], acc);
+    }
     y[o] = acc;
   }
 }
@@ -262,6 +268,13 @@ struct Wts {
   // (ds_read_b64_tr_b16) — else the pack's transposed copies (global memory, or
   // an LDS copy that includes them)
   bool tr;
+  // bf16 weight fragments from LDS as volatile reads (ldw4) or plain ones the
+  // compiler may fuse (ldb4); a compile-time constant of the kernel (it folds):
+  // volatile pays in the two-wave-per-SIMD kernels, which are issue-bound;
+  // the one-wave-per-SIMD kernels of 16+ entities and the one-wave multi-tile
+  // mixer BPTT, latency-bound, measured slower with it (configs[0]-shape A/B,
+  // profiles/r4_h16/: agent_bwd 1.67 -> 1.84 ms, mixer_bwd 3.62 -> 3.84 ms)
+  bool vol = true;
   T2O_DEV float s(int64_t off) const { return (float)w[off]; }  // row 0 of a matrix (unswizzled row)
 };
 
@@ -282,7 +295,7 @@ T2O_DEV bf4 ld_tr_b16(const __bf16* p) {
 template <int OT, int IT>
 T2O_DEV void matvec_tr(const Wts<__bf16>& P, int64_t off, int ld, int64_t offT, int ldT, const f4* x, f4* y) {
   if (!P.tr) {
-    matvec<OT, IT>(P.w + offT, ldT, x, y);
+    matvec<OT, IT>(P.w + offT, ldT, x, y, P.vol);
     return;
   }
   // the lane's row q = 4g + (c >> 2) within a 16-row K tile and its column
@@ -326,7 +339,7 @@ template <typename WT>
 T2O_DEV Wts<WT> step_view(const Wts<WT>& p) {
   int off = 0;
   asm volatile("" : "+s"(off));
-  return Wts<WT>{p.w + off, p.v + off, p.tr};
+  return Wts<WT>{p.w + off, p.v + off, p.tr, p.vol};
 }
 
 template <int OT, int IT>

@@ -210,7 +210,7 @@ T2O_DEV void mix_keys(const Wts<WT>& P, const t2o_layout& L, const In& in, float
   for (int s = 0; s < Dm::ST; ++s) {
     const int j = 16 * s + c;
     f4 emb[ET];
-    matvec<ET, 1, HOIST>(P.w + L.We, 16, &in.st[s], emb);
+    matvec<ET, 1, HOIST>(P.w + L.We, 16, &in.st[s], emb, P.vol);
     if (j < na) {
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) st4(X0 + j * Dm::LDX + 16 * ft + 4 * g, emb[ft] + vec_t(P.v + L.be, ft));
@@ -564,8 +564,9 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
   // the forward section of the pack in LDS when it fits
   // beside the per-wave buffers, else read through L2 (large mixers)
-  const Wts<WT> P0 = WLDS ? stage_weights(smem, n.pack, L, L.fwd_total, WT{})
-                          : global_weights(n.pack, L, WT{});
+  Wts<WT> P0 = WLDS ? stage_weights(smem, n.pack, L, L.fwd_total, WT{})
+                    : global_weights(n.pack, L, WT{});
+  P0.vol = false;  // (Wts::vol: the one-wave multi-tile BPTT measured slower with volatile reads)
   zero_flushed_regions(gs, G, false);
   __syncthreads();
   const int b = blockIdx.x * args.waves + w;

@@ -109,7 +109,7 @@ T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
   constexpr bool BF = sizeof(WT) == 2;
   const int g = lane_g();
   f4 u[HET];
-  matvec<HET, ET, HOIST>(P.w + L.M[d], E, x, u);
+  matvec<HET, ET, HOIST>(P.w + L.M[d], E, x, u, P.vol);
   f4 z[HET];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
@@ -237,7 +237,7 @@ T2O_DEV void mixer_block_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d,
                                   MixerCacheLean<E, H, KT, FF>& cache, const MaskedRec<WT, CP>& rec) {
   constexpr int ET = E / 16, HET = H * ET;
   constexpr bool BF = sizeof(WT) == 2;
-  matvec<HET, ET>(P.w + L.M[d], E, x, cache.u);
+  matvec<HET, ET>(P.w + L.M[d], E, x, cache.u, P.vol);
   f4 z[HET];
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {

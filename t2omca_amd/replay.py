@@ -108,14 +108,17 @@ class PrioritizedReplayBuffer:
         return DeviceEpisodeBatch(self.gather(idx)), idx, w
 
     # -- priorities -----------------------------------------------------------------
-    def update_priorities(self, idxes, priorities):
+    def update_priorities(self, idxes, priorities, add=0.0):
         """priority_i ** alpha for the given episodes; max_priority tracked.
-        idxes / priorities: device tensors, or host sequences (reference driver)."""
+        idxes / priorities: device tensors, or host sequences (reference driver).
+        add: a constant added to every priority inside the kernel — the driver's
+        `td_errors_abs + 1e-6` (per_run.py:237-238) without a separate launch
+        (the same fp32 addition, so the same priorities)."""
         idx = torch.as_tensor(np.asarray(idxes) if not torch.is_tensor(idxes) else idxes, dtype=torch.int64)
         pr = torch.as_tensor(np.asarray(priorities) if not torch.is_tensor(priorities) else priorities,
                              dtype=torch.float32)
         idx = idx.to(self.device).contiguous()
         pr = pr.to(self.device).contiguous()
         check(lib().t2o_per_update(ptr(self.p), ptr(idx), ptr(pr), idx.numel(), ctypes.c_float(self.alpha),
-                                   ctypes.c_float(0.0), ptr(self.max_priority), stream_ptr(self.device)),
+                                   ctypes.c_float(add), ptr(self.max_priority), stream_ptr(self.device)),
               "per_update")

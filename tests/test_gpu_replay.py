@@ -53,6 +53,24 @@ def test_update_priorities_and_max():
     assert np.allclose(buf.p[10:12].cpu().numpy(), 3.0 ** 0.6, rtol=1e-6)
 
 
+def test_update_priorities_add_equals_adding_first():
+    """update_priorities(idx, td, add=1e-6) (the driver's `+ 1e-6` inside the kernel)
+    writes exactly what update_priorities(idx, td + 1e-6) does."""
+    require_gpu()
+    out = []
+    for fused in (False, True):
+        buf, batch = _buffer()
+        buf.insert_episode_batch({k: v[:10] for k, v in batch.items()})
+        idx = torch.tensor([0, 3, 9], device="cuda")
+        td = torch.tensor([2.5e-7, 0.125, 7.0], device="cuda")
+        if fused:
+            buf.update_priorities(idx, td, add=1e-6)
+        else:
+            buf.update_priorities(idx, td + 1e-6)
+        out.append((buf.p.clone(), buf.max_priority.clone()))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+
+
 def test_ring_insert_and_gather():
     require_gpu()
     buf, batch = _buffer(cap=32)
