@@ -82,12 +82,13 @@ struct EnvArgs {
   int NE, A, M, C, QMAX, T;
   uint64_t seed;
   int mode;                // 0 init, 1 reset, 2 step, 3 env_info
+  int apad, G;             // lane map (lane_map): agent lanes per env, envs per wave
 };
 
 constexpr int MAXA = 64;
 
 // ---- counter-based uniforms (env_spec.uniforms) -----------------------------
-__device__ double uniform(uint64_t seed, int env, int64_t idx) {
+__device__ __forceinline__ double uniform(uint64_t seed, int env, int64_t idx) {
   uint64_t x = ((uint64_t)env << 40) | (uint64_t)idx;
   x ^= seed * 0xD1B54A32D192ED03ull;
   uint64_t z = x + 0x9E3779B97F4A7C15ull;
@@ -97,10 +98,10 @@ __device__ double uniform(uint64_t seed, int env, int64_t idx) {
   return (double)(z >> 11) * 0x1.0p-53;
 }
 
-__device__ double round2_numpy(double x) { return rint(x * 100.0) / 100.0; }
+__device__ __forceinline__ double round2_numpy(double x) { return rint(x * 100.0) / 100.0; }
 
 // CPython round(x, 2): round-half-even of the EXACT value x*100, then /100.
-__device__ double round2_python(double x) {
+__device__ __forceinline__ double round2_python(double x) {
   const double p = x * 100.0;
   const double e = fma(x, 100.0, -p);  // exact: x*100 = p + e
   double r = rint(p);
@@ -112,12 +113,12 @@ __device__ double round2_python(double x) {
   return r / 100.0;
 }
 
-__device__ void mec_pos(const EnvArgs& a, int m, double& mx, double& my) {
+__device__ __forceinline__ void mec_pos(const EnvArgs& a, int m, double& mx, double& my) {
   mx = (double)m * (a.sp.mec_radius * 2) + a.sp.mec_radius;
   my = a.sp.mec_radius;
 }
 
-__device__ void position(const EnvArgs& a, int m, double u1, double u2, double& x, double& y) {
+__device__ __forceinline__ void position(const EnvArgs& a, int m, double u1, double u2, double& x, double& y) {
   double mx, my;
   mec_pos(a, m, mx, my);
   const double aa = 2.0 * u1 - 1.0;
@@ -127,7 +128,7 @@ __device__ void position(const EnvArgs& a, int m, double u1, double u2, double& 
 }
 
 // calculate_offload_delay (:106-121)
-__device__ double offload_delay(const EnvArgs& a, int mec, double x, double y, int size) {
+__device__ __forceinline__ double offload_delay(const EnvArgs& a, int mec, double x, double y, int size) {
   double mx, my;
   mec_pos(a, mec, mx, my);
   const double dx = x - mx, dy = y - my;
@@ -145,7 +146,7 @@ struct AgentView {
   double x, y;
 };
 
-__device__ void load_agent(const EnvArgs& a, int e, int ag, AgentView& v) {
+__device__ __forceinline__ void load_agent(const EnvArgs& a, int e, int ag, AgentView& v) {
   const int i = e * a.A + ag;
   v.mec = a.s.mec_index[i];
   v.x = a.s.x[i];
@@ -158,7 +159,7 @@ __device__ void load_agent(const EnvArgs& a, int e, int ag, AgentView& v) {
 }
 
 // get_agent_inf (:123-146) -> inf[5]
-__device__ void agent_inf(const EnvArgs& a, const AgentView& v, double* inf) {
+__device__ __forceinline__ void agent_inf(const EnvArgs& a, const AgentView& v, double* inf) {
   if (v.len) {
     inf[0] = (double)v.size;
     inf[1] = rint(((double)(v.size * (int64_t)a.sp.comp_cycles) / a.sp.user_cap) * 1000.0);
@@ -170,16 +171,57 @@ __device__ void agent_inf(const EnvArgs& a, const AgentView& v, double* inf) {
   }
 }
 
-// LDS scratch of one env (one wave)
-struct EnvLds {
-  double inf[MAXA][5];
-  int mec[MAXA];
-  int ack[MAXA];
-  int freq[16][17];
-  double dr[MAXA];
-  double rd[MAXA];
-  int tn[MAXA], ts[MAXA];
+// ---- lane map: G envs per wave ---------------------------------------------
+// A one-wave workgroup steps G = 64 / apad envs (apad = A rounded up to a power
+// of two; fewer when the per-env collision counters would not fit the LDS):
+// lane = g * apad + ag runs agent ag of env blockIdx.x * G + g in every per-agent
+// phase, and the normaliser's G * len(obs) (env, feature) items are spread over
+// all 64 lanes.  One env per wave left 48 of 64 lanes idle at 16 AGVs and, at
+// 139 VGPRs (3 waves / SIMD), needed 8192 / 3072 -> three rounds of waves.
+constexpr int FREQ_CAP = 1088;  // int counters: G * M * (C + 1)
+
+struct LaneMap {
+  int apad, G;
 };
+
+__host__ inline LaneMap lane_map(int A, int M, int C) {
+  int apad = 1;
+  while (apad < A) apad *= 2;
+  int G = 64 / apad;
+  const int cap = FREQ_CAP / (M * (C + 1));
+  return LaneMap{apad, G < cap ? G : cap};
+}
+
+// LDS scratch of one wave: per-agent arrays indexed by lane (g * apad + ag)
+struct EnvLds {
+  double inf[64][5];
+  double dr[64];
+  double rd[64];
+  int mec[64];
+  int ack[64];
+  int tn[64], ts[64];
+  int freq[FREQ_CAP];  // [g][mec][channel]
+  int64_t n[64];       // [g] normaliser update count
+};
+
+struct Who {
+  int lane, g, ag, e, gb;  // gb = g * apad: the group's first lane
+  bool agent;              // lane runs an agent of a live env
+  bool lead;               // lane is its live env's agent 0
+};
+
+__device__ __forceinline__ Who who(const EnvArgs& a) {
+  Who w;
+  w.lane = threadIdx.x & 63;
+  w.g = w.lane / a.apad;
+  w.ag = w.lane - w.g * a.apad;
+  w.gb = w.g * a.apad;
+  w.e = blockIdx.x * a.G + w.g;
+  const bool live = w.g < a.G && w.e < a.NE;
+  w.agent = live && w.ag < a.A;
+  w.lead = live && w.ag == 0;
+  return w;
+}
 
 // ---- compact observation wire format ---------------------
 // Everything get_obs_agent (:148-182) reads about entity j, as 4 int32:
@@ -190,128 +232,265 @@ struct EnvLds {
 // All fields are 0 when the queue is empty (get_agent_inf returns zeros).
 // Together with the normaliser (n, mean, S) at the start of the episode, the
 // wire records of t = 0..T reproduce every returned obs exactly (t2o_obs_expand).
-__device__ void write_wire(const EnvArgs& a, int e, const EnvLds& L) {
-  const int lane = threadIdx.x & 63;
-  if (!a.o.wire || lane >= a.A) return;
-  const double* inf = L.inf[lane];
-  int4 w;
-  w.x = (int)inf[0];
-  w.y = (int)inf[1];
-  w.z = (int)rint(inf[2] * 100.0);
-  w.w = ((int)inf[3] & 0xFFFF) | ((int)inf[4] << 16) | ((L.ack[lane] + 1) << 24) | (L.mec[lane] << 26);
-  reinterpret_cast<int4*>(a.o.wire)[(size_t)e * a.A + lane] = w;
+__device__ __forceinline__ void write_wire(const EnvArgs& a, const Who& w, const EnvLds& L) {
+  if (!a.o.wire || !w.agent) return;
+  const double* inf = L.inf[w.lane];
+  int4 v;
+  v.x = (int)inf[0];
+  v.y = (int)inf[1];
+  v.z = (int)rint(inf[2] * 100.0);
+  v.w = ((int)inf[3] & 0xFFFF) | ((int)inf[4] << 16) | ((L.ack[w.lane] + 1) << 24) | (L.mec[w.lane] << 26);
+  reinterpret_cast<int4*>(a.o.wire)[(size_t)w.e * a.A + w.ag] = v;
 }
 
-// get_obs (:184-186) = A sequential normaliser updates; writes outputs if out != 0.
-// The update count n is kept in a register by every lane (the caller loads and
-// stores it once), so no lane ever reads another lane's global store.  Lane l owns
-// features l, l + 64, ... : their running (mean, S) live in registers over the A
+// get_obs (:184-186) = A sequential normaliser updates per env; writes the obs if
+// out, and the normaliser's (n, mean, S) at the end into the reset snapshot if
+// snap.  Item q = lane + 64 k (k < OBS_SLOTS) is feature p = q % len of env
+// g = q / len of the wave: its running (mean, S) live in registers over the A
 // updates and reach HBM once at the end, with the last std (the only one read
-// later); the IEEE operations and their order are the reference's.
-constexpr int OBS_SLOTS = (9 * MAXA + 63) / 64;
+// later).  Entity mode: feature p = 9 j + f of agent i's obs is entity j's field
+// f if i and j share a MEC (f = 8: is_self), else 0 — j's value is fetched once
+// per call, each update only compares i's MEC.  The IEEE operations and their
+// order are the reference's.
+constexpr int OBS_SLOTS = 9;  // ceil(G * 9A / 64) <= 9 for every A <= 64
 
-__device__ void get_obs(const EnvArgs& a, int e, EnvLds& L, bool out, int64_t& n) {
-  // normaliser rows keep their [9A] stride in both modes (state[14..16])
-  const int A = a.A, n9 = 9 * A, no = obs_len(a.sp.obs_entity, A), lane = threadIdx.x & 63;
-  double* mean = a.s.nrm_mean + (size_t)e * n9;
-  double* S = a.s.nrm_S + (size_t)e * n9;
-  double* sd = a.s.nrm_std + (size_t)e * n9;
-  double mr[OBS_SLOTS], sr[OBS_SLOTS], dr[OBS_SLOTS];
+// a / n correctly rounded from y = RN(1/n): q within 1.5 ulp, one correction
+// brings it within one ulp, and Markstein's theorem makes the second exact (the
+// remainders are exact fma results).  Preconditions, which the normaliser's
+// operands meet: finite, far from the subnormal range, and never -0 (a = +0
+// gives +0; x and the running mean are never -0, so neither is x - mean, and S
+// is a sum of non-negative products from +0).  Checked against IEEE division on
+// 5.9e7 random (a, n <= 3e5) pairs with gcc.
+__device__ __forceinline__ double div_by(double a, double n, double y) {
+  double q = a * y;
+  double r = fma(-q, n, a);
+  q = fma(r, y, q);
+  r = fma(-q, n, a);
+  return fma(r, y, q);
+}
+
+// sqrt(t) correctly rounded for t = +0 or t >= 2^-767: the f64 sqrt expansion the
+// compiler emits (v_rsq_f64, then Goldschmidt / Newton steps on fma) without its
+// range scaling, which only t < 2^-767 needs.  The normaliser's S / n is +0 or
+// far above that: x lies on a grid of hundredths, so a non-zero running mean is
+// >= 0.01 / n, every non-zero x - mean >= an ulp of that, and S is a sum of
+// products of two such differences (>= 1e-68) over n < 2^53 updates.
+__device__ __forceinline__ double sqrt_nn(double t) {
+  const double r = __builtin_amdgcn_rsq(t);  // rsq(+0) = +inf
+  double g = t * r, h = 0.5 * r;
+  const double e = fma(-h, g, 0.5);
+  g = fma(g, e, g);
+  h = fma(h, e, h);
+  double d = fma(-g, g, t);
+  g = fma(d, h, g);
+  d = fma(-g, g, t);
+  g = fma(d, h, g);
+  return t == 0.0 ? t : g;
+}
+
+// The fast normaliser loop of get_obs (every env of the wave at the same count
+// n0 >= 1, so each update divides by the wave-uniform n >= 2: one reciprocal per
+// update and Markstein's correction, div_by, instead of one IEEE division per
+// item).  Entity mode: x = xv if agent i's MEC equals key (j's MEC), or, for the
+// is_self feature (key = -1 - j), if i == j; else 0.  Flat mode: x is agent i's
+// own feature p.  The obs go through range-checked buffers over this wave's envs:
+// an item past the last env / feature has an out-of-range offset, so it is
+// computed (on lane data of group 0) and dropped.
+template <bool OUT, bool ENT>
+__device__ __attribute__((always_inline)) void norm_fast(const EnvArgs& a, const Who& w, const EnvLds& L, int64_t nref,
+                                                        double (&mr)[OBS_SLOTS], double (&sr)[OBS_SLOTS],
+                                                        const double (&xv)[OBS_SLOTS], const int (&key)[OBS_SLOTS],
+                                                        const int (&gq)[OBS_SLOTS]) {
+  const int A = a.A, no = obs_len(ENT, A);
+  const int e0 = blockIdx.x * a.G, ne = a.NE - e0 < a.G ? a.NE - e0 : a.G;
+  float* obase = a.o.obs ? a.o.obs + (size_t)e0 * A * no : nullptr;
+  double* obase64 = a.o.obs64 ? a.o.obs64 + (size_t)e0 * A * no : nullptr;
+  const __amdgpu_buffer_rsrc_t orsrc =
+      __builtin_amdgcn_make_buffer_rsrc(obase, (short)0, a.o.obs ? ne * A * no * (int)sizeof(float) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t orsrc64 = __builtin_amdgcn_make_buffer_rsrc(
+      obase64, (short)0, a.o.obs64 ? ne * A * no * (int)sizeof(double) : 0, 0x00020000);
+  int ooff[OBS_SLOTS];  // bytes into the float obs; 2 * ooff (unsigned) into the fp64 copy
+  int lb[OBS_SLOTS];    // LDS lane of agent 0 of the item's env
 #pragma unroll
   for (int k = 0; k < OBS_SLOTS; ++k) {
-    const int p = lane + 64 * k;
-    mr[k] = sr[k] = dr[k] = 0.0;
-    if (p < no) {
-      mr[k] = mean[p];
-      sr[k] = S[p];
-    }
+    const int q = w.lane + 64 * k;
+    const int g = q / no, p = q - g * no;
+    ooff[k] = gq[k] < 0 ? 0x40000000 : (g * A * no + p) * (int)sizeof(float);
+    lb[k] = gq[k] < 0 ? 0 : gq[k];
   }
+  const double n0 = (double)nref;
   for (int i = 0; i < A; ++i) {
-    ++n;
+    const double n = n0 + (double)(i + 1);
+    const double y = 1.0 / n;
+    const int self = -1 - i;
 #pragma unroll
     for (int k = 0; k < OBS_SLOTS; ++k) {
-      const int p = lane + 64 * k;
-      if (p >= no) break;
-      double x = 0.0;
-      if (!a.sp.obs_entity) {
-        x = p == 0 ? (double)L.ack[i] : L.inf[i][p - 1];  // [last_ack (raw -1/0/1), get_agent_inf]
+      double x;
+      if constexpr (ENT) {
+        const int mi = L.mec[lb[k] + i];
+        x = (mi == key[k] || self == key[k]) ? xv[k] : 0.0;
       } else {
-        const int j = p / 9, f = p % 9;
-        if (L.mec[i] == L.mec[j]) {
-          if (f < 3) x = (f == L.ack[j] + 1) ? 1.0 : 0.0;  // ack_mapping: -1 -> [1,0,0], 0 -> [0,1,0], 1 -> [0,0,1]
-          else if (f < 8) x = L.inf[j][f - 3];
-          else x = (i == j) ? 1.0 : 0.0;
+        const int q = w.lane + 64 * k;
+        const int p = q - (q / no) * no;
+        x = p == 0 ? (double)L.ack[lb[k] + i] : L.inf[lb[k] + i][p - 1];  // [last_ack (raw -1/0/1), get_agent_inf]
+      }
+      const double old = mr[k], dx = x - old;
+      const double m = old + div_by(dx, n, y);
+      const double sn = sr[k] + dx * (x - m);
+      mr[k] = m;
+      sr[k] = sn;
+      if constexpr (OUT) {
+        const double v = (x - m) / (sqrt_nn(div_by(sn, n, y)) + 1e-8);
+        if (a.o.obs)
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, (float)v), orsrc, ooff[k],
+                                                i * no * (int)sizeof(float), 0);
+        if (a.o.obs64) {
+          typedef int v2i __attribute__((ext_vector_type(2)));
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i, v), orsrc64, 2 * ooff[k],
+                                                i * no * (int)sizeof(double), 0);
         }
       }
-      double m, s, d;
-      if (n == 1) {
-        m = x;
-        s = sr[k];
-        d = x;
-      } else {
-        const double old = mr[k];
-        m = old + (x - old) / (double)n;
-        s = sr[k] + (x - old) * (x - m);
-        d = sqrt(s / (double)n);
+    }
+  }
+}
+
+template <bool OUT>
+__device__ __attribute__((always_inline)) void get_obs(const EnvArgs& a, const Who& w, EnvLds& L, bool snap) {
+  // normaliser rows keep their [9A] stride in both modes (state[14..16])
+  const int A = a.A, n9 = 9 * A, no = obs_len(a.sp.obs_entity, A);
+  const int items = a.G * no;
+  double mr[OBS_SLOTS], sr[OBS_SLOTS], xv[OBS_SLOTS];
+  int64_t n0[OBS_SLOTS];  // the env's update count before this call
+  int key[OBS_SLOTS];  // entity mode: j's MEC, or -1 - j for is_self
+  int gq[OBS_SLOTS];   // the item's group base lane (-1: no item)
+#pragma unroll
+  for (int k = 0; k < OBS_SLOTS; ++k) {
+    const int q = w.lane + 64 * k;
+    const int g = q / no, p = q - g * no;
+    const int e = blockIdx.x * a.G + g;
+    gq[k] = -1;
+    mr[k] = sr[k] = xv[k] = 0.0;
+    key[k] = n0[k] = 0;
+    if (q < items && e < a.NE) {
+      gq[k] = g * a.apad;
+      mr[k] = a.s.nrm_mean[(size_t)e * n9 + p];
+      sr[k] = a.s.nrm_S[(size_t)e * n9 + p];
+      n0[k] = L.n[g];
+      if (a.sp.obs_entity) {
+        const int j = p / 9, f = p - 9 * (p / 9), lj = gq[k] + j;
+        if (f < 3) xv[k] = (f == L.ack[lj] + 1) ? 1.0 : 0.0;  // ack_mapping: -1 -> [1,0,0], 0 -> [0,1,0], 1 -> [0,0,1]
+        else if (f < 8) xv[k] = L.inf[lj][f - 3];
+        else xv[k] = 1.0;
+        key[k] = f == 8 ? -1 - j : L.mec[lj];
       }
-      mr[k] = m;
-      sr[k] = s;
-      dr[k] = d;
-      if (out) {
-        const double v = (x - m) / (d + 1e-8);
-        const size_t o = ((size_t)e * A + i) * no + p;
-        if (a.o.obs) a.o.obs[o] = (float)v;
-        if (a.o.obs64) a.o.obs64[o] = v;
+    }
+  }
+  // every env of the wave at the same update count n0 >= 1: always, past the first
+  // reset's first call
+  const int64_t nref = L.n[0];
+  bool same = true;
+#pragma unroll
+  for (int k = 0; k < OBS_SLOTS; ++k) same = same && (gq[k] < 0 || n0[k] == nref);
+  if (__all(same) && nref >= 1) {
+    if (a.sp.obs_entity) norm_fast<OUT, true>(a, w, L, nref, mr, sr, xv, key, gq);
+    else norm_fast<OUT, false>(a, w, L, nref, mr, sr, xv, key, gq);
+  } else {
+    for (int i = 0; i < A; ++i) {
+  #pragma unroll
+      for (int k = 0; k < OBS_SLOTS; ++k) {
+        if (gq[k] < 0) continue;
+        const int q = w.lane + 64 * k;
+        const int g = q / no, p = q - g * no;
+        const int li = gq[k] + i;
+        double x;
+        if (a.sp.obs_entity) {
+          x = (L.mec[li] == key[k] || -1 - i == key[k]) ? xv[k] : 0.0;
+        } else {
+          x = p == 0 ? (double)L.ack[li] : L.inf[li][p - 1];  // [last_ack (raw -1/0/1), get_agent_inf]
+        }
+        const double n = (double)(n0[k] + i + 1);
+        double m, s;
+        if (n == 1.0) {
+          m = x;
+          s = sr[k];
+        } else {
+          const double old = mr[k];
+          m = old + (x - old) / n;
+          s = sr[k] + (x - old) * (x - m);
+        }
+        mr[k] = m;
+        sr[k] = s;
+        if (OUT) {
+          const double d = n == 1.0 ? x : sqrt(s / n);
+          const double v = (x - m) / (d + 1e-8);
+          const size_t o = ((size_t)(blockIdx.x * a.G + g) * A + i) * no + p;
+          if (a.o.obs) a.o.obs[o] = (float)v;
+          if (a.o.obs64) a.o.obs64[o] = v;
+        }
       }
     }
   }
 #pragma unroll
   for (int k = 0; k < OBS_SLOTS; ++k) {
-    const int p = lane + 64 * k;
-    if (p < no && A > 0) {
-      mean[p] = mr[k];
-      S[p] = sr[k];
-      sd[p] = dr[k];
+    if (gq[k] < 0) continue;
+    const int q = w.lane + 64 * k;
+    const int g = q / no, p = q - g * no;
+    const size_t r = (size_t)(blockIdx.x * a.G + g) * n9 + p;
+    const double n = (double)(n0[k] + A);
+    a.s.nrm_mean[r] = mr[k];
+    a.s.nrm_S[r] = sr[k];
+    a.s.nrm_std[r] = n == 1.0 ? mr[k] : sqrt(sr[k] / n);  // the last update's std (at n = 1: x = mean)
+    if (snap) {  // the normaliser the episode's first returned obs starts from
+      a.o.snap[(size_t)(blockIdx.x * a.G + g) * 2 * n9 + p] = mr[k];
+      a.o.snap[(size_t)(blockIdx.x * a.G + g) * 2 * n9 + n9 + p] = sr[k];
     }
   }
-}
-
-__device__ void fill_lds(const EnvArgs& a, int e, EnvLds& L) {
-  const int lane = threadIdx.x & 63;
-  if (lane < a.A) {
-    AgentView v;
-    load_agent(a, e, lane, v);
-    L.mec[lane] = v.mec;
-    L.ack[lane] = v.ack;
-    agent_inf(a, v, L.inf[lane]);
+  __syncthreads();  // every item read L.n before the count moves on
+  if (w.lead) {
+    L.n[w.g] += A;
+    if (snap) a.o.snap_n[w.e] = L.n[w.g];
   }
-  __builtin_amdgcn_wave_barrier();
   __syncthreads();
 }
 
-__device__ void write_state_avail(const EnvArgs& a, int e, const EnvLds& L) {
-  const int A = a.A, lane = threadIdx.x & 63, nA = a.C + 1;
+__device__ __forceinline__ void fill_lds(const EnvArgs& a, const Who& w, EnvLds& L) {
+  if (w.agent) {
+    AgentView v;
+    load_agent(a, w.e, w.ag, v);
+    L.mec[w.lane] = v.mec;
+    L.ack[w.lane] = v.ack;
+    agent_inf(a, v, L.inf[w.lane]);
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void write_state_avail(const EnvArgs& a, const Who& w, const EnvLds& L) {
+  const int A = a.A, nA = a.C + 1, ns = 8 * A;
   if (a.o.state) {
-    for (int p = lane; p < 8 * A; p += 64) {
+    for (int q = w.lane; q < a.G * ns; q += 64) {
+      const int g = q / ns, p = q - g * ns;
+      const int e = blockIdx.x * a.G + g;
+      if (e >= a.NE) break;
+      const int gb = g * a.apad;
       float v;
       if (p < 3 * A) {
         const int j = p / 3, f = p % 3;
-        v = (f == L.ack[j] + 1) ? 1.f : 0.f;
+        v = (f == L.ack[gb + j] + 1) ? 1.f : 0.f;
       } else {
-        const int q = p - 3 * A;
-        v = (float)L.inf[q / 5][q % 5];
+        const int r = p - 3 * A;
+        v = (float)L.inf[gb + r / 5][r % 5];
       }
-      a.o.state[(size_t)e * 8 * A + p] = v;
+      a.o.state[(size_t)e * ns + p] = v;
     }
   }
-  if (a.o.avail && lane < A) {
-    const bool has = a.s.q_len[e * A + lane] > 0;
+  if (a.o.avail && w.agent) {
+    const bool has = a.s.q_len[w.e * A + w.ag] > 0;
     for (int k = 0; k < nA; ++k)
-      a.o.avail[((size_t)e * A + lane) * nA + k] = has ? (a.sp.edge_only ? k != 0 : 1) : k == 0;
+      a.o.avail[((size_t)w.e * A + w.ag) * nA + k] = has ? (a.sp.edge_only ? k != 0 : 1) : k == 0;
   }
 }
 
-__device__ void generate_job(const EnvArgs& a, int i, double u1, double u2) {
+__device__ __forceinline__ void generate_job(const EnvArgs& a, int i, double u1, double u2) {
   if (u1 < a.sp.arrival_p) {
     const int len = a.s.q_len[i];
     const int slot = (a.s.q_head[i] + len) % a.QMAX;
@@ -322,17 +501,18 @@ __device__ void generate_job(const EnvArgs& a, int i, double u1, double u2) {
   }
 }
 
-__global__ __launch_bounds__(64) void env_kernel(EnvArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void env_kernel(EnvArgs a) {
   __shared__ EnvLds L;
-  const int e = blockIdx.x;
-  const int A = a.A, M = a.M, C = a.C, lane = threadIdx.x;
-  if (e >= a.NE) return;
-  const int64_t base = a.mode == 0 ? 0 : a.s.draw[e];
+  const Who w = who(a);
+  const int A = a.A, M = a.M, C = a.C, FS = M * (C + 1);
+  if (blockIdx.x * a.G >= a.NE) return;
+  const bool live = w.g < a.G && w.e < a.NE;
+  const int64_t base = a.mode == 0 || !live ? 0 : a.s.draw[w.e];
   if (a.mode == 0) {  // construction (:25-40): mec_index + position per agent
-    if (lane < A) {
-      const int i = e * A + lane;
-      const double u0 = uniform(a.seed, e, base + 3 * lane), u1 = uniform(a.seed, e, base + 3 * lane + 1),
-                   u2 = uniform(a.seed, e, base + 3 * lane + 2);
+    if (w.agent) {
+      const int i = w.e * A + w.ag;
+      const double u0 = uniform(a.seed, w.e, base + 3 * w.ag), u1 = uniform(a.seed, w.e, base + 3 * w.ag + 1),
+                   u2 = uniform(a.seed, w.e, base + 3 * w.ag + 2);
       const int m = (int)(u0 * (double)M);
       a.s.mec_index[i] = m;
       position(a, m, u1, u2, a.s.x[i], a.s.y[i]);
@@ -341,82 +521,76 @@ __global__ __launch_bounds__(64) void env_kernel(EnvArgs a) {
       a.s.remain_delay[i] = 0.0;
       a.s.last_ack[i] = 0;
     }
-    for (int p = lane; p < 9 * A; p += 64) {
-      const size_t q = (size_t)e * 9 * A + p;
-      a.s.nrm_mean[q] = a.s.nrm_S[q] = a.s.nrm_std[q] = 0.0;
+    const int n9 = 9 * A;
+    for (int q = w.lane; q < a.G * n9; q += 64) {
+      const int e = blockIdx.x * a.G + q / n9;
+      if (e >= a.NE) break;
+      const size_t r = (size_t)e * n9 + q % n9;
+      a.s.nrm_mean[r] = a.s.nrm_S[r] = a.s.nrm_std[r] = 0.0;
     }
-    if (lane == 0) {
-      a.s.nrm_n[e] = 0;
-      a.s.time_slot[e] = 0;
-      a.s.draw[e] = base + 3 * A;
+    if (w.lead) {
+      a.s.nrm_n[w.e] = 0;
+      a.s.time_slot[w.e] = 0;
+      a.s.draw[w.e] = base + 3 * A;
     }
     return;
   }
+  if (w.lead) L.n[w.g] = a.s.nrm_n[w.e];
   if (a.mode == 3) {  // get_env_info (:421-439): two get_obs calls (one without entity obs, :425,431-434)
-    int64_t n = a.s.nrm_n[e];
-    fill_lds(a, e, L);
-    get_obs(a, e, L, false, n);
-    if (a.sp.obs_entity) get_obs(a, e, L, false, n);
-    if (lane == 0) a.s.nrm_n[e] = n;
+    fill_lds(a, w, L);
+    get_obs<false>(a, w, L, false);
+    if (a.sp.obs_entity) get_obs<false>(a, w, L, false);
+    if (w.lead) a.s.nrm_n[w.e] = L.n[w.g];
     return;
   }
   if (a.mode == 1) {  // reset (:219-227), then the worker's get_state/get_avail/get_obs
-    if (lane < A) {
-      const int i = e * A + lane;
-      const int64_t b = base + 5 * lane;
-      const int m = (int)(uniform(a.seed, e, b) * (double)M);
-      position(a, m, uniform(a.seed, e, b + 1), uniform(a.seed, e, b + 2), a.s.x[i], a.s.y[i]);
+    if (w.agent) {
+      const int i = w.e * A + w.ag;
+      const int64_t b = base + 5 * w.ag;
+      const int m = (int)(uniform(a.seed, w.e, b) * (double)M);
+      position(a, m, uniform(a.seed, w.e, b + 1), uniform(a.seed, w.e, b + 2), a.s.x[i], a.s.y[i]);
       a.s.q_head[i] = a.s.q_len[i] = 0;
       a.s.task_num[i] = a.s.task_success[i] = 0;
       a.s.remain_delay[i] = 0.0;
-      generate_job(a, i, uniform(a.seed, e, b + 3), uniform(a.seed, e, b + 4));
+      generate_job(a, i, uniform(a.seed, w.e, b + 3), uniform(a.seed, w.e, b + 4));
       a.s.last_ack[i] = 0;
     }
-    if (lane == 0) {
-      a.s.time_slot[e] = 0;
-      a.s.draw[e] = base + 5 * A;
+    if (w.lead) {
+      a.s.time_slot[w.e] = 0;
+      a.s.draw[w.e] = base + 5 * A;
     }
     __syncthreads();
-    int64_t n = a.s.nrm_n[e];
-    fill_lds(a, e, L);
-    get_obs(a, e, L, false, n);  // reset()'s own get_obs
-    write_state_avail(a, e, L);
-    if (a.o.snap) {  // the normaliser the episode's first returned obs starts from
-      const int n9 = 9 * A;
-      for (int p = lane; p < n9; p += 64) {
-        a.o.snap[(size_t)e * 2 * n9 + p] = a.s.nrm_mean[(size_t)e * n9 + p];
-        a.o.snap[(size_t)e * 2 * n9 + n9 + p] = a.s.nrm_S[(size_t)e * n9 + p];
-      }
-      if (lane == 0) a.o.snap_n[e] = n;
-    }
-    write_wire(a, e, L);
-    get_obs(a, e, L, true, n);   // the worker's get_obs
-    if (lane == 0) a.s.nrm_n[e] = n;
+    fill_lds(a, w, L);
+    get_obs<false>(a, w, L, a.o.snap != nullptr);  // reset()'s own get_obs
+    write_state_avail(a, w, L);
+    write_wire(a, w, L);
+    get_obs<true>(a, w, L, false);  // the worker's get_obs
+    if (w.lead) a.s.nrm_n[w.e] = L.n[w.g];
     return;
   }
   // ---- step (:309-366)
-  for (int k = lane; k < 16 * 17; k += 64) (&L.freq[0][0])[k] = 0;
+  for (int k = w.lane; k < a.G * FS; k += 64) L.freq[k] = 0;
   __syncthreads();
   AgentView v;
   int act = 0;
-  if (lane < A) {
-    load_agent(a, e, lane, v);
-    act = (int)a.actions[(int64_t)e * a.act_se + lane];
+  int* freq = L.freq + w.g * FS;
+  if (w.agent) {
+    load_agent(a, w.e, w.ag, v);
+    act = (int)a.actions[(int64_t)w.e * a.act_se + w.ag];
     act = act < 0 ? 0 : (act > C ? C : act);  // actions come from avail-masked selection; clamp keeps LDS in bounds
-    atomicAdd(&L.freq[v.mec][act], 1);
+    atomicAdd(&freq[v.mec * (C + 1) + act], 1);
   }
   __syncthreads();
   int ack = 0;
-  if (lane < A) {
+  if (w.agent) {
     if (act == 0) ack = 0;
-    else ack = (L.freq[v.mec][act] == 1) ? 1 : -1;
+    else ack = (freq[v.mec * (C + 1) + act] == 1) ? 1 : -1;
   }
-  const unsigned long long confl = __ballot(lane < A && ack == -1);
   // get_reward (:229-293): per-agent terms, summed in agent order below
   double dr = 0.0, rd_inc = 0.0;
   int over = 0, succ = 0;
   bool has_dr = false;
-  if (lane < A && v.len) {
+  if (w.agent && v.len) {
     const double local = round2_python(((double)(a.sp.comp_cycles * v.size) / a.sp.user_cap) * 1000.0);
     if (ack == 0) {
       if ((double)v.thr - local > 0) {
@@ -439,50 +613,51 @@ __global__ __launch_bounds__(64) void env_kernel(EnvArgs a) {
       }
     }
   }
-  if (lane < A) {
-    L.dr[lane] = has_dr ? dr : NAN;
-    L.ack[lane] = ack;
-    L.mec[lane] = v.mec;
-    L.tn[lane] = over;
+  if (w.agent) {
+    L.dr[w.lane] = has_dr ? dr : NAN;
+    L.ack[w.lane] = ack;
+    L.mec[w.lane] = v.mec;
+    L.tn[w.lane] = over;
   }
   __syncthreads();
-  if (lane == 0) {
+  if (w.lead) {
     // channel utilisation (:321-329): counts > 1 zeroed, Python sums in order
     double util = 0.0;
     for (int m = 0; m < M; ++m) {
       double s = 0.0;
       for (int c = 0; c <= C; ++c) {
-        const int f = L.freq[m][c] > 1 ? 0 : L.freq[m][c];
+        const int f = freq[m * (C + 1) + c] > 1 ? 0 : freq[m * (C + 1) + c];
         s = s + (double)f / (double)C;
       }
       util = util + s;
     }
     util = util / (double)M;
     double delay_reward = 0.0;
-    int overtime = 0;
+    int overtime = 0, confl = 0;
     for (int ag = 0; ag < A; ++ag) {
-      if (!isnan(L.dr[ag])) delay_reward = delay_reward + L.dr[ag];
-      overtime += L.tn[ag];
+      if (!isnan(L.dr[w.gb + ag])) delay_reward = delay_reward + L.dr[w.gb + ag];
+      overtime += L.tn[w.gb + ag];
+      confl += L.ack[w.gb + ag] == -1;
     }
-    a.o.reward[e] = delay_reward - (double)overtime;
-    double* info = a.o.info + (size_t)e * 6;
+    a.o.reward[w.e] = delay_reward - (double)overtime;
+    double* info = a.o.info + (size_t)w.e * 6;
     info[0] = delay_reward;
     info[1] = (double)overtime;
     info[2] = util;
-    info[3] = (double)__popcll(confl) / (double)A;
+    info[3] = (double)confl / (double)A;
     info[4] = info[5] = NAN;
   }
   __syncthreads();
   // update_users (:295-307) after the reward, agent by agent (independent)
-  if (lane < A) {
-    const int i = e * A + lane;
+  if (w.agent) {
+    const int i = w.e * A + w.ag;
     a.s.last_ack[i] = ack;
     if (a.o.ack) a.o.ack[i] = ack;
     a.s.task_success[i] += succ;
     a.s.remain_delay[i] = a.s.remain_delay[i] + rd_inc;
-    const int64_t b = base + 5 * lane;
-    const int m = (int)(uniform(a.seed, e, b) * (double)M);
-    position(a, m, uniform(a.seed, e, b + 1), uniform(a.seed, e, b + 2), a.s.x[i], a.s.y[i]);
+    const int64_t b = base + 5 * w.ag;
+    const int m = (int)(uniform(a.seed, w.e, b) * (double)M);
+    position(a, m, uniform(a.seed, w.e, b + 1), uniform(a.seed, w.e, b + 2), a.s.x[i], a.s.y[i]);
     int head = a.s.q_head[i], len = a.s.q_len[i];
     if (ack != -1 && len > 0) {
       head = (head + 1) % a.QMAX;
@@ -495,39 +670,38 @@ __global__ __launch_bounds__(64) void env_kernel(EnvArgs a) {
     }
     a.s.q_head[i] = head;
     a.s.q_len[i] = len;
-    generate_job(a, i, uniform(a.seed, e, b + 3), uniform(a.seed, e, b + 4));
-    L.tn[lane] = a.s.task_num[i];
-    L.ts[lane] = a.s.task_success[i];
-    L.rd[lane] = a.s.remain_delay[i];
+    generate_job(a, i, uniform(a.seed, w.e, b + 3), uniform(a.seed, w.e, b + 4));
+    L.tn[w.lane] = a.s.task_num[i];
+    L.ts[w.lane] = a.s.task_success[i];
+    L.rd[w.lane] = a.s.remain_delay[i];
   }
   __syncthreads();
-  if (lane == 0) {
-    a.s.draw[e] = base + 5 * A;
-    const int ts = a.s.time_slot[e] + 1;
-    a.s.time_slot[e] = ts;
+  if (w.lead) {
+    a.s.draw[w.e] = base + 5 * A;
+    const int ts = a.s.time_slot[w.e] + 1;
+    a.s.time_slot[w.e] = ts;
     const bool term = ts == a.T;
-    a.o.terminated[e] = term ? 1 : 0;
+    a.o.terminated[w.e] = term ? 1 : 0;
     if (term) {  // get_task_num (:368-415)
       int tn = 0, tsu = 0;
       double rd = 0.0;
       for (int ag = 0; ag < A; ++ag) {
-        tn += L.tn[ag];
-        tsu += L.ts[ag];
-        rd = rd + L.rd[ag];
+        tn += L.tn[w.gb + ag];
+        tsu += L.ts[w.gb + ag];
+        rd = rd + L.rd[w.gb + ag];
       }
-      double* info = a.o.info + (size_t)e * 6;
+      double* info = a.o.info + (size_t)w.e * 6;
       info[4] = (double)tsu / (double)tn;
       info[5] = tsu != 0 ? rd / (double)tsu : 0.0;
     }
   }
   __syncthreads();
   // the worker's get_state / get_avail_actions / get_obs on the new state
-  int64_t n = a.s.nrm_n[e];
-  fill_lds(a, e, L);
-  write_state_avail(a, e, L);
-  write_wire(a, e, L);
-  get_obs(a, e, L, true, n);
-  if (lane == 0) a.s.nrm_n[e] = n;
+  fill_lds(a, w, L);
+  write_state_avail(a, w, L);
+  write_wire(a, w, L);
+  get_obs<true>(a, w, L, false);
+  if (w.lead) a.s.nrm_n[w.e] = L.n[w.g];
 }
 
 // ---- t2o_obs_expand: wire records -> dense normalised obs --------------------
@@ -653,7 +827,10 @@ extern "C" int t2o_env_run_ex(int mode, const double* spec, void* const* state, 
   a.T = T;
   a.seed = seed;
   a.mode = mode;
-  hipLaunchKernelGGL(env_kernel, dim3(NE), dim3(64), 0, (hipStream_t)stream, a);
+  const LaneMap lm = lane_map(A, M, C);
+  a.apad = lm.apad;
+  a.G = lm.G;
+  hipLaunchKernelGGL(env_kernel, dim3((NE + lm.G - 1) / lm.G), dim3(64), 0, (hipStream_t)stream, a);
   return (int)hipGetLastError();
 }
 

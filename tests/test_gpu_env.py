@@ -121,6 +121,14 @@ def test_env_single_agent_and_channel_extremes():
     _rollout_vs_oracle(NE=4, M=3, A=5, T=12, eps=1, seed=12)
 
 
+def test_env_partial_waves_vs_oracle():
+    """Several envs share a wave (t2o_env.hip lane map): env counts that leave the last
+    wave partly empty, and G capped by the collision counters (16 MEC: 13 envs per wave)."""
+    _rollout_vs_oracle(NE=7, M=2, A=16, T=5, eps=1, seed=13)
+    _rollout_vs_oracle(NE=11, M=2, A=3, T=5, eps=1, seed=14)
+    _rollout_vs_oracle(NE=30, M=16, A=3, T=4, eps=1, seed=15)
+
+
 def test_env_flat_obs_mode_vs_oracle():
     """obs_entity_mode=False: get_obs_agent's flat branch (:172-182), 6 features per agent
     normalised by a 6-long running normaliser; get_env_info makes one get_obs call."""
