@@ -179,6 +179,7 @@ __device__ __forceinline__ void agent_inf(const EnvArgs& a, const AgentView& v, 
 // all 64 lanes.  One env per wave left 48 of 64 lanes idle at 16 AGVs and, at
 // 139 VGPRs (3 waves / SIMD), needed 8192 / 3072 -> three rounds of waves.
 constexpr int FREQ_CAP = 1088;  // int counters: G * M * (C + 1)
+constexpr int QR = 16;          // job queues up to this capacity are updated in registers
 
 struct LaneMap {
   int apad, G;
@@ -288,6 +289,32 @@ __device__ __forceinline__ double sqrt_nn(double t) {
   return t == 0.0 ? t : g;
 }
 
+// a / z correctly rounded for operands that need no range scaling: the f64
+// division expansion the compiler emits (v_rcp_f64, two Newton steps on the
+// reciprocal, one quotient correction) without v_div_scale / v_div_fmas /
+// v_div_fixup, which only change the result for exponents near the ends of the
+// range, zeros, infinities and NaNs.  Here z = std + 1e-8 in [1e-8, 1e7] and a =
+// x - mean, |a| < 1e7, is +0 or >= 1e-34 (see sqrt_nn), so the results are the
+// library's bit for bit.
+__device__ __forceinline__ double div_lean(double a, double z) {
+  double y = __builtin_amdgcn_rcp(z);
+  double e = fma(-z, y, 1.0);
+  y = fma(y, e, y);
+  e = fma(-z, y, 1.0);
+  y = fma(y, e, y);
+  const double q = a * y;
+  const double r = fma(-z, q, a);
+  return fma(r, y, q);
+}
+
+// (q / d, q % d) for 0 <= q < 1024 and 1 <= d < 1024 through one fp32 multiply:
+// (q + 1/2) / d keeps >= 1/(2d) >= 4.9e-4 from any integer, the product's error is
+// below 1024 * 2^-23 = 1.2e-4 (rd = RN(1/d)).  Replaces a runtime integer division.
+__device__ __forceinline__ void divmod_small(int q, int d, float rd, int& g, int& p) {
+  g = (int)(((float)q + 0.5f) * rd);
+  p = q - g * d;
+}
+
 // The fast normaliser loop of get_obs (every env of the wave at the same count
 // n0 >= 1, so each update divides by the wave-uniform n >= 2: one reciprocal per
 // update and Markstein's correction, div_by, instead of one IEEE division per
@@ -309,12 +336,13 @@ __device__ __attribute__((always_inline)) void norm_fast(const EnvArgs& a, const
       __builtin_amdgcn_make_buffer_rsrc(obase, (short)0, a.o.obs ? ne * A * no * (int)sizeof(float) : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t orsrc64 = __builtin_amdgcn_make_buffer_rsrc(
       obase64, (short)0, a.o.obs64 ? ne * A * no * (int)sizeof(double) : 0, 0x00020000);
+  const float rno = 1.0f / (float)no;
   int ooff[OBS_SLOTS];  // bytes into the float obs; 2 * ooff (unsigned) into the fp64 copy
   int lb[OBS_SLOTS];    // LDS lane of agent 0 of the item's env
 #pragma unroll
   for (int k = 0; k < OBS_SLOTS; ++k) {
-    const int q = w.lane + 64 * k;
-    const int g = q / no, p = q - g * no;
+    int g, p;
+    divmod_small(w.lane + 64 * k, no, rno, g, p);
     ooff[k] = gq[k] < 0 ? 0x40000000 : (g * A * no + p) * (int)sizeof(float);
     lb[k] = gq[k] < 0 ? 0 : gq[k];
   }
@@ -330,8 +358,8 @@ __device__ __attribute__((always_inline)) void norm_fast(const EnvArgs& a, const
         const int mi = L.mec[lb[k] + i];
         x = (mi == key[k] || self == key[k]) ? xv[k] : 0.0;
       } else {
-        const int q = w.lane + 64 * k;
-        const int p = q - (q / no) * no;
+        int g, p;
+        divmod_small(w.lane + 64 * k, no, rno, g, p);
         x = p == 0 ? (double)L.ack[lb[k] + i] : L.inf[lb[k] + i][p - 1];  // [last_ack (raw -1/0/1), get_agent_inf]
       }
       const double old = mr[k], dx = x - old;
@@ -340,7 +368,7 @@ __device__ __attribute__((always_inline)) void norm_fast(const EnvArgs& a, const
       mr[k] = m;
       sr[k] = sn;
       if constexpr (OUT) {
-        const double v = (x - m) / (sqrt_nn(div_by(sn, n, y)) + 1e-8);
+        const double v = div_lean(x - m, sqrt_nn(div_by(sn, n, y)) + 1e-8);
         if (a.o.obs)
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(int, (float)v), orsrc, ooff[k],
                                                 i * no * (int)sizeof(float), 0);
@@ -354,27 +382,54 @@ __device__ __attribute__((always_inline)) void norm_fast(const EnvArgs& a, const
   }
 }
 
+// This lane's normaliser items (mean, S), loaded once per launch (in step mode at
+// the kernel's start, so the loads overlap the step) and carried across get_obs
+// calls in registers.
+struct NormPre {
+  double mr[OBS_SLOTS], sr[OBS_SLOTS];
+};
+
+__device__ __forceinline__ void load_norm(const EnvArgs& a, const Who& w, NormPre& pre) {
+  const int A = a.A, n9 = 9 * A, no = obs_len(a.sp.obs_entity, A), items = a.G * no;
+  const float rno = 1.0f / (float)no;
+#pragma unroll
+  for (int k = 0; k < OBS_SLOTS; ++k) {
+    const int q = w.lane + 64 * k;
+    int g, p;
+    divmod_small(q, no, rno, g, p);
+    const int e = blockIdx.x * a.G + g;
+    pre.mr[k] = pre.sr[k] = 0.0;
+    if (q < items && e < a.NE) {
+      pre.mr[k] = a.s.nrm_mean[(size_t)e * n9 + p];
+      pre.sr[k] = a.s.nrm_S[(size_t)e * n9 + p];
+    }
+  }
+}
+
 template <bool OUT>
-__device__ __attribute__((always_inline)) void get_obs(const EnvArgs& a, const Who& w, EnvLds& L, bool snap) {
+__device__ __attribute__((always_inline)) void get_obs(const EnvArgs& a, const Who& w, EnvLds& L, NormPre& pre,
+                                                      bool snap) {
   // normaliser rows keep their [9A] stride in both modes (state[14..16])
   const int A = a.A, n9 = 9 * A, no = obs_len(a.sp.obs_entity, A);
   const int items = a.G * no;
-  double mr[OBS_SLOTS], sr[OBS_SLOTS], xv[OBS_SLOTS];
+  const float rno = 1.0f / (float)no;
+  double(&mr)[OBS_SLOTS] = pre.mr;
+  double(&sr)[OBS_SLOTS] = pre.sr;
+  double xv[OBS_SLOTS];
   int64_t n0[OBS_SLOTS];  // the env's update count before this call
   int key[OBS_SLOTS];  // entity mode: j's MEC, or -1 - j for is_self
   int gq[OBS_SLOTS];   // the item's group base lane (-1: no item)
 #pragma unroll
   for (int k = 0; k < OBS_SLOTS; ++k) {
     const int q = w.lane + 64 * k;
-    const int g = q / no, p = q - g * no;
+    int g, p;
+    divmod_small(q, no, rno, g, p);
     const int e = blockIdx.x * a.G + g;
     gq[k] = -1;
-    mr[k] = sr[k] = xv[k] = 0.0;
+    xv[k] = 0.0;
     key[k] = n0[k] = 0;
     if (q < items && e < a.NE) {
       gq[k] = g * a.apad;
-      mr[k] = a.s.nrm_mean[(size_t)e * n9 + p];
-      sr[k] = a.s.nrm_S[(size_t)e * n9 + p];
       n0[k] = L.n[g];
       if (a.sp.obs_entity) {
         const int j = p / 9, f = p - 9 * (p / 9), lj = gq[k] + j;
@@ -399,8 +454,8 @@ __device__ __attribute__((always_inline)) void get_obs(const EnvArgs& a, const W
   #pragma unroll
       for (int k = 0; k < OBS_SLOTS; ++k) {
         if (gq[k] < 0) continue;
-        const int q = w.lane + 64 * k;
-        const int g = q / no, p = q - g * no;
+        int g, p;
+        divmod_small(w.lane + 64 * k, no, rno, g, p);
         const int li = gq[k] + i;
         double x;
         if (a.sp.obs_entity) {
@@ -430,19 +485,23 @@ __device__ __attribute__((always_inline)) void get_obs(const EnvArgs& a, const W
       }
     }
   }
+  // (validity and counts re-derived here, so the per-item arrays above need not
+  // stay live through the update loop)
 #pragma unroll
   for (int k = 0; k < OBS_SLOTS; ++k) {
-    if (gq[k] < 0) continue;
     const int q = w.lane + 64 * k;
-    const int g = q / no, p = q - g * no;
-    const size_t r = (size_t)(blockIdx.x * a.G + g) * n9 + p;
-    const double n = (double)(n0[k] + A);
+    int g, p;
+    divmod_small(q, no, rno, g, p);
+    const int e = blockIdx.x * a.G + g;
+    if (q >= items || e >= a.NE) continue;
+    const size_t r = (size_t)e * n9 + p;
+    const double n = (double)(L.n[g] + A);
     a.s.nrm_mean[r] = mr[k];
     a.s.nrm_S[r] = sr[k];
     a.s.nrm_std[r] = n == 1.0 ? mr[k] : sqrt(sr[k] / n);  // the last update's std (at n = 1: x = mean)
     if (snap) {  // the normaliser the episode's first returned obs starts from
-      a.o.snap[(size_t)(blockIdx.x * a.G + g) * 2 * n9 + p] = mr[k];
-      a.o.snap[(size_t)(blockIdx.x * a.G + g) * 2 * n9 + n9 + p] = sr[k];
+      a.o.snap[(size_t)e * 2 * n9 + p] = mr[k];
+      a.o.snap[(size_t)e * 2 * n9 + n9 + p] = sr[k];
     }
   }
   __syncthreads();  // every item read L.n before the count moves on
@@ -467,38 +526,43 @@ __device__ __forceinline__ void fill_lds(const EnvArgs& a, const Who& w, EnvLds&
 __device__ __forceinline__ void write_state_avail(const EnvArgs& a, const Who& w, const EnvLds& L) {
   const int A = a.A, nA = a.C + 1, ns = 8 * A;
   if (a.o.state) {
-    for (int q = w.lane; q < a.G * ns; q += 64) {
-      const int g = q / ns, p = q - g * ns;
+    for (int g = 0; g < a.G; ++g) {
       const int e = blockIdx.x * a.G + g;
       if (e >= a.NE) break;
       const int gb = g * a.apad;
-      float v;
-      if (p < 3 * A) {
-        const int j = p / 3, f = p % 3;
-        v = (f == L.ack[gb + j] + 1) ? 1.f : 0.f;
-      } else {
-        const int r = p - 3 * A;
-        v = (float)L.inf[gb + r / 5][r % 5];
+      for (int p = w.lane; p < ns; p += 64) {
+        float v;
+        if (p < 3 * A) {
+          const int j = p / 3, f = p % 3;
+          v = (f == L.ack[gb + j] + 1) ? 1.f : 0.f;
+        } else {
+          const int r = p - 3 * A;
+          v = (float)L.inf[gb + r / 5][r % 5];
+        }
+        a.o.state[(size_t)e * ns + p] = v;
       }
-      a.o.state[(size_t)e * ns + p] = v;
     }
   }
   if (a.o.avail && w.agent) {
-    const bool has = a.s.q_len[w.e * A + w.ag] > 0;
+    const bool has = L.inf[w.lane][4] > 0.0;  // get_agent_inf's queue length
     for (int k = 0; k < nA; ++k)
       a.o.avail[((size_t)w.e * A + w.ag) * nA + k] = has ? (a.sp.edge_only ? k != 0 : 1) : k == 0;
   }
 }
 
-__device__ __forceinline__ void generate_job(const EnvArgs& a, int i, double u1, double u2) {
+// appends a job with probability arrival_p to the queue (head, len); returns its
+// size, 0 if none arrived (sizes are >= size_min >= 1)
+__device__ __forceinline__ int generate_job(const EnvArgs& a, int i, int head, int len, double u1, double u2) {
   if (u1 < a.sp.arrival_p) {
-    const int len = a.s.q_len[i];
-    const int slot = (a.s.q_head[i] + len) % a.QMAX;
-    a.s.q_size[(size_t)i * a.QMAX + slot] = a.sp.size_min + (int)(u2 * (double)(a.sp.size_max - a.sp.size_min + 1));
+    const int slot = (head + len) % a.QMAX;
+    const int size = a.sp.size_min + (int)(u2 * (double)(a.sp.size_max - a.sp.size_min + 1));
+    a.s.q_size[(size_t)i * a.QMAX + slot] = size;
     a.s.q_thr[(size_t)i * a.QMAX + slot] = a.sp.latency_max;
     a.s.q_len[i] = len + 1;
     a.s.task_num[i] += 1;
+    return size;
   }
+  return 0;
 }
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void env_kernel(EnvArgs a) {
@@ -536,10 +600,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void en
     return;
   }
   if (w.lead) L.n[w.g] = a.s.nrm_n[w.e];
+  NormPre pre;
   if (a.mode == 3) {  // get_env_info (:421-439): two get_obs calls (one without entity obs, :425,431-434)
+    load_norm(a, w, pre);
     fill_lds(a, w, L);
-    get_obs<false>(a, w, L, false);
-    if (a.sp.obs_entity) get_obs<false>(a, w, L, false);
+    get_obs<false>(a, w, L, pre, false);
+    if (a.sp.obs_entity) get_obs<false>(a, w, L, pre, false);
     if (w.lead) a.s.nrm_n[w.e] = L.n[w.g];
     return;
   }
@@ -552,7 +618,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void en
       a.s.q_head[i] = a.s.q_len[i] = 0;
       a.s.task_num[i] = a.s.task_success[i] = 0;
       a.s.remain_delay[i] = 0.0;
-      generate_job(a, i, uniform(a.seed, w.e, b + 3), uniform(a.seed, w.e, b + 4));
+      generate_job(a, i, 0, 0, uniform(a.seed, w.e, b + 3), uniform(a.seed, w.e, b + 4));
       a.s.last_ack[i] = 0;
     }
     if (w.lead) {
@@ -560,15 +626,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void en
       a.s.draw[w.e] = base + 5 * A;
     }
     __syncthreads();
+    load_norm(a, w, pre);
     fill_lds(a, w, L);
-    get_obs<false>(a, w, L, a.o.snap != nullptr);  // reset()'s own get_obs
+    get_obs<false>(a, w, L, pre, a.o.snap != nullptr);  // reset()'s own get_obs
     write_state_avail(a, w, L);
     write_wire(a, w, L);
-    get_obs<true>(a, w, L, false);  // the worker's get_obs
+    get_obs<true>(a, w, L, pre, false);  // the worker's get_obs
     if (w.lead) a.s.nrm_n[w.e] = L.n[w.g];
     return;
   }
   // ---- step (:309-366)
+  load_norm(a, w, pre);
   for (int k = w.lane; k < a.G * FS; k += 64) L.freq[k] = 0;
   __syncthreads();
   AgentView v;
@@ -649,6 +717,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void en
   }
   __syncthreads();
   // update_users (:295-307) after the reward, agent by agent (independent)
+  AgentView nv{};
   if (w.agent) {
     const int i = w.e * A + w.ag;
     a.s.last_ack[i] = ack;
@@ -657,20 +726,59 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void en
     a.s.remain_delay[i] = a.s.remain_delay[i] + rd_inc;
     const int64_t b = base + 5 * w.ag;
     const int m = (int)(uniform(a.seed, w.e, b) * (double)M);
-    position(a, m, uniform(a.seed, w.e, b + 1), uniform(a.seed, w.e, b + 2), a.s.x[i], a.s.y[i]);
+    double px, py;
+    position(a, m, uniform(a.seed, w.e, b + 1), uniform(a.seed, w.e, b + 2), px, py);
+    a.s.x[i] = px;
+    a.s.y[i] = py;
     int head = a.s.q_head[i], len = a.s.q_len[i];
+    int* thr_ring = a.s.q_thr + (size_t)i * a.QMAX;
     if (ack != -1 && len > 0) {
       head = (head + 1) % a.QMAX;
       --len;
     }
-    for (int k = 0; k < len; ++k) a.s.q_thr[(size_t)i * a.QMAX + (head + k) % a.QMAX] -= 5;
-    while (len > 0 && a.s.q_thr[(size_t)i * a.QMAX + head] <= 0) {  // expired jobs are a FIFO prefix
-      head = (head + 1) % a.QMAX;
-      --len;
+    // every queued job's threshold drops by t_length (5); the expired ones are a
+    // FIFO prefix (thresholds grow from head to tail: jobs arrive with latency_max
+    // and age together), so they are counted, not searched.  The head job's
+    // threshold is kept for the obs that follow.
+    int hthr = 0;
+    if (a.QMAX <= QR) {
+      int thr[QR];
+#pragma unroll
+      for (int k = 0; k < QR; ++k) thr[k] = k < a.QMAX ? thr_ring[k] : 0;  // independent loads
+      int nexp = 0;
+#pragma unroll
+      for (int k = 0; k < QR; ++k) {
+        int rel = k - head;
+        rel = rel < 0 ? rel + a.QMAX : rel;
+        if (k < a.QMAX && rel < len) {
+          thr[k] -= 5;
+          thr_ring[k] = thr[k];
+          nexp += thr[k] <= 0;
+        }
+      }
+      head = (head + nexp) % a.QMAX;
+      len -= nexp;
+#pragma unroll
+      for (int k = 0; k < QR; ++k) hthr = k == head ? thr[k] : hthr;
+    } else {
+      for (int k = 0; k < len; ++k) thr_ring[(head + k) % a.QMAX] -= 5;
+      while (len > 0 && (hthr = thr_ring[head]) <= 0) {
+        head = (head + 1) % a.QMAX;
+        --len;
+      }
     }
     a.s.q_head[i] = head;
     a.s.q_len[i] = len;
-    generate_job(a, i, uniform(a.seed, w.e, b + 3), uniform(a.seed, w.e, b + 4));
+    const int nsize = generate_job(a, i, head, len, uniform(a.seed, w.e, b + 3), uniform(a.seed, w.e, b + 4));
+    // the new state as get_agent_inf sees it (load_agent without re-reading it);
+    // the draw m only places the AGV, its mec_index stays (:295-307)
+    nv.mec = v.mec;
+    nv.x = px;
+    nv.y = py;
+    nv.ack = ack;
+    nv.len = len + (nsize > 0);
+    nv.size = len > 0 ? a.s.q_size[(size_t)i * a.QMAX + head] : nsize;
+    nv.thr = len > 0 ? hthr : (nsize > 0 ? a.sp.latency_max : 0);
     L.tn[w.lane] = a.s.task_num[i];
     L.ts[w.lane] = a.s.task_success[i];
     L.rd[w.lane] = a.s.remain_delay[i];
@@ -697,10 +805,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void en
   }
   __syncthreads();
   // the worker's get_state / get_avail_actions / get_obs on the new state
-  fill_lds(a, w, L);
+  if (w.agent) {
+    L.mec[w.lane] = nv.mec;
+    L.ack[w.lane] = nv.ack;
+    agent_inf(a, nv, L.inf[w.lane]);
+  }
+  __syncthreads();
   write_state_avail(a, w, L);
   write_wire(a, w, L);
-  get_obs<true>(a, w, L, false);
+  get_obs<true>(a, w, L, pre, false);
   if (w.lead) a.s.nrm_n[w.e] = L.n[w.g];
 }
 
