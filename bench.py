@@ -72,6 +72,8 @@ def parse():
     ap.add_argument("--no-cpu-configs0", action="store_true",
                     help="skip the configs[0]-shape (16 AGVs, T=150) CPU-baseline figure")
     ap.add_argument("--mecs", type=int, default=2, help="rollout mode: MEC servers")
+    ap.add_argument("--rollout-precision", choices=("fp32", "bf16"), default="fp32",
+                    help="rollout / loop modes: the agent step's MFMA operands (fp32 = the reference's precision)")
     ap.add_argument("--qmix-pos-func", choices=("abs", "softplus", "quadratic", "identity"), default="abs",
                     help="the mixer head's positivity function (n_transf_mixer.py:95-103); the exact mixer "
                          "instances compute abs only, so softplus / quadratic / identity run the runtime-entity "
@@ -297,7 +299,7 @@ def rollout_bench(args, world, rank, dev):
     torch.manual_seed(0)
     agent = TransformerAgent(None, make_args(A, device=str(dev))).to(dev)
     env = VecEnv(n, mec_num=args.mecs, agv_num=A, episode_limit=T, seed=1, device=dev, wire=args.compact_obs)
-    runner = RolloutRunner(agent, env, seed=0, compact_obs=args.compact_obs)
+    runner = RolloutRunner(agent, env, seed=0, compact_obs=args.compact_obs, precision=args.rollout_precision)
     for _ in range(args.warmup):
         runner.run(new_buffers=False)
     timer = KernelTimer()
@@ -326,7 +328,8 @@ def rollout_bench(args, world, rank, dev):
     # bytes per agent-step x n x A per launch) and the one-step agent forward (MFMA:
     # §8(d)'s F_agent per sequence x n x A); the dominant one carries `roofline`
     env_bytes = env_step_bytes(A) * n * A
-    agent_flops = agent_row_step_flops(n=A) * n * A  # what the fp32 kernel executes per launch
+    agent_flops = agent_row_step_flops(n=A) * n * A  # what the agent kernel executes per launch
+    agent_peak = PEAK_BF16_TFLOPS if args.rollout_precision == "bf16" else PEAK_FP32_TFLOPS
     agent_ref_flops = ref_order_network_flops(A)[0] * n * A
     rl = {}
     if "env_step" in kern:
@@ -337,13 +340,13 @@ def rollout_bench(args, world, rank, dev):
                           "basis": "SURVEY.md §8(d): (16+4+64+4 + 9A*4) B per agent-step (perfmodel.env_step_bytes)"}
     if "agent_fwd" in kern:
         ach = agent_flops / (kern["agent_fwd"] * 1e-3) / 1e12
-        rl["agent_fwd"] = {"bound": "mfma", "kernel": "agent_fwd", "achieved": ach, "peak": PEAK_FP32_TFLOPS,
-                           "unit": "TFLOP/s", "frac": ach / PEAK_FP32_TFLOPS,
+        rl["agent_fwd"] = {"bound": "mfma", "kernel": "agent_fwd", "achieved": ach, "peak": agent_peak,
+                           "unit": "TFLOP/s", "frac": ach / agent_peak,
                            "traffic": traffic_for("agent_fwd", rollout_tag(args)),
                            "algorithmic_flops_per_launch": agent_flops, "avg_launch_ms": kern["agent_fwd"],
                            "basis": "executed algorithm (perfmodel.agent_row_step_flops: folded projections, "
-                                    "observation-space attention, token 0 only) vs the fp32 MFMA peak (the rollout "
-                                    "agent runs fp32)",
+                                    f"observation-space attention, token 0 only) vs the {args.rollout_precision} "
+                                    "MFMA peak (the rollout agent's operand precision)",
                            "reference_order": {"flops_per_launch": agent_ref_flops,
                                                "achieved": agent_ref_flops / (kern["agent_fwd"] * 1e-3) / 1e12,
                                                "note": "SURVEY.md §8(d) F_agent: the reference association order "
@@ -354,7 +357,7 @@ def rollout_bench(args, world, rank, dev):
            "value": env_steps * A / elapsed, "unit": "agent-transitions/s", "env_steps_per_s": env_steps / elapsed,
            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-           "vs_baseline": None, "dtype": "fp32 agent, fp64 env", "data": "simulated (VecEnv, env_spec stand-ins)",
+           "vs_baseline": None, "dtype": f"{args.rollout_precision} agent, fp64 env", "data": "simulated (VecEnv, env_spec stand-ins)",
            "config": {"workload": f"configs[4]: {n} envs/GPU x {A} AGVs x {args.mecs} MEC, episode {T} steps, "
                                   "one rollout per step" + (", compact obs wire format" if args.compact_obs else ""),
                       "global_envs": n * world, "agents": A, "compact_obs": bool(args.compact_obs)},
@@ -455,7 +458,7 @@ def loop_bench(args, world, rank, dev):
     learner = TDLearner(agent, mixer, precision=args.dtype, priorities_to_cpu=False, td_algo=args.td_algo)
     env = VecEnv(n, mec_num=args.mecs, agv_num=A, episode_limit=T, seed=1, device=dev, wire=args.compact_obs)
     env.get_env_info()
-    runner = RolloutRunner(agent, env, seed=0, compact_obs=args.compact_obs)
+    runner = RolloutRunner(agent, env, seed=0, compact_obs=args.compact_obs, precision=args.rollout_precision)
     buf = None
     episode = 0
     marks = []
@@ -518,7 +521,7 @@ def loop_bench(args, world, rank, dev):
                      "TD update -> update_priorities)",
            "value": learned / elapsed, "unit": "agent-transitions/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": f"{args.dtype} learner, fp32 rollout agent, fp64 env",
+           "scaling": "weak", "vs_baseline": None, "dtype": f"{args.dtype} learner, {args.rollout_precision} rollout agent, fp64 env",
            "data": "simulated (VecEnv, env_spec stand-ins) + device PER replay",
            "config": {"workload": f"configs[4] feeding the learner: {n} envs/GPU x {A} AGVs x {args.mecs} MEC, "
                                   f"episode {T} steps; per rollout {U} TD updates of {B} PER-sampled episodes "
@@ -546,7 +549,8 @@ def loop_bench(args, world, rank, dev):
 
 
 def rollout_tag(args):
-    return f"rollout_n{args.envs}_t{args.T}_a{args.agents}_m{args.mecs}" + ("_wire" if args.compact_obs else "")
+    return (f"rollout_n{args.envs}_t{args.T}_a{args.agents}_m{args.mecs}" + ("_wire" if args.compact_obs else "")
+            + ("_bf16" if args.rollout_precision == "bf16" else ""))
 
 
 def expand_bench(args, world, rank, dev):

@@ -224,6 +224,18 @@ __device__ __forceinline__ Who who(const EnvArgs& a) {
   return w;
 }
 
+// The env workgroups are one wave: an LDS read after other lanes' LDS writes needs
+// program order only (a wave's LDS instructions complete in order), so the
+// kernel's hand-overs between lanes are compiler fences.  __syncthreads() would
+// also wait for every outstanding global load — at the step's first hand-over,
+// the whole prefetched state.  (Global data is only ever re-read by the lane that
+// wrote it.)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ---- compact observation wire format ---------------------
 // Everything get_obs_agent (:148-182) reads about entity j, as 4 int32:
 //   w0 size, w1 data_delay (get_agent_inf's round() to int), w2 the offload
@@ -504,12 +516,12 @@ __device__ __attribute__((always_inline)) void get_obs(const EnvArgs& a, const W
       a.o.snap[(size_t)e * 2 * n9 + n9 + p] = sr[k];
     }
   }
-  __syncthreads();  // every item read L.n before the count moves on
+  wave_sync();  // every item read L.n before the count moves on
   if (w.lead) {
     L.n[w.g] += A;
     if (snap) a.o.snap_n[w.e] = L.n[w.g];
   }
-  __syncthreads();
+  wave_sync();
 }
 
 __device__ __forceinline__ void fill_lds(const EnvArgs& a, const Who& w, EnvLds& L) {
@@ -520,7 +532,7 @@ __device__ __forceinline__ void fill_lds(const EnvArgs& a, const Who& w, EnvLds&
     L.ack[w.lane] = v.ack;
     agent_inf(a, v, L.inf[w.lane]);
   }
-  __syncthreads();
+  wave_sync();
 }
 
 __device__ __forceinline__ void write_state_avail(const EnvArgs& a, const Who& w, const EnvLds& L) {
@@ -565,13 +577,251 @@ __device__ __forceinline__ int generate_job(const EnvArgs& a, int i, int head, i
   return 0;
 }
 
+// One step (:309-366) of the wave's envs.  Every per-agent state the step reads
+// — position, MEC, job queue (thresholds and sizes, in registers when the queue
+// capacity is <= QR), counters, the action — is loaded up front in one batch, the
+// normaliser items after them, so the step pays about one memory round trip;
+// everything after computes from registers and only stores.
+__device__ __forceinline__ void env_step(const EnvArgs& a, const Who& w, EnvLds& L, NormPre& pre) {
+  const int A = a.A, M = a.M, C = a.C, FS = M * (C + 1), Q = a.QMAX;
+  const bool ring = Q <= QR;
+  const int i = w.e * A + w.ag;
+  int mec = 0, len = 0, head = 0, act = 0, tnum = 0, tsucc = 0;
+  double x = 0.0, y = 0.0, rdel = 0.0;
+  int thr[QR], size[QR];
+#pragma unroll
+  for (int k = 0; k < QR; ++k) thr[k] = size[k] = 0;
+  int* thr_ring = a.s.q_thr + (size_t)i * Q;
+  int* size_ring = a.s.q_size + (size_t)i * Q;
+  if (w.agent) {
+    mec = a.s.mec_index[i];
+    x = a.s.x[i];
+    y = a.s.y[i];
+    len = a.s.q_len[i];
+    head = a.s.q_head[i];
+    act = (int)a.actions[(int64_t)w.e * a.act_se + w.ag];
+    tnum = a.s.task_num[i];
+    tsucc = a.s.task_success[i];
+    rdel = a.s.remain_delay[i];
+    if (ring) {
+#pragma unroll
+      for (int k = 0; k < QR; ++k)
+        if (k < Q) {
+          thr[k] = thr_ring[k];
+          size[k] = size_ring[k];
+        }
+    }
+  }
+  int64_t base = 0, nrm = 0;
+  int tslot = 0;
+  if (w.agent) base = a.s.draw[w.e];
+  if (w.lead) {
+    nrm = a.s.nrm_n[w.e];
+    tslot = a.s.time_slot[w.e];
+  }
+  load_norm(a, w, pre);
+  for (int k = w.lane; k < a.G * FS; k += 64) L.freq[k] = 0;
+  if (w.lead) L.n[w.g] = nrm;
+  wave_sync();
+  // the head job (load_agent)
+  int hsize = 0, hthr = 0;
+  if (w.agent && len) {
+    if (ring) {
+#pragma unroll
+      for (int k = 0; k < QR; ++k) {
+        hsize = k == head ? size[k] : hsize;
+        hthr = k == head ? thr[k] : hthr;
+      }
+    } else {
+      hsize = size_ring[head];
+      hthr = thr_ring[head];
+    }
+  }
+  int* freq = L.freq + w.g * FS;
+  if (w.agent) {
+    act = act < 0 ? 0 : (act > C ? C : act);  // actions come from avail-masked selection; clamp keeps LDS in bounds
+    atomicAdd(&freq[mec * (C + 1) + act], 1);
+  }
+  wave_sync();
+  int ack = 0;
+  if (w.agent) {
+    if (act == 0) ack = 0;
+    else ack = (freq[mec * (C + 1) + act] == 1) ? 1 : -1;
+  }
+  // get_reward (:229-293): per-agent terms, summed in agent order below
+  double dr = 0.0, rd_inc = 0.0;
+  int over = 0, succ = 0;
+  bool has_dr = false;
+  if (w.agent && len) {
+    const double local = round2_python(((double)(a.sp.comp_cycles * hsize) / a.sp.user_cap) * 1000.0);
+    if (ack == 0) {
+      if ((double)hthr - local > 0) {
+        succ = 1;
+        rd_inc = (double)(a.sp.latency_max - hthr) + local;
+      } else {
+        over = a.sp.latency_max;
+      }
+    } else if (ack == -1) {
+      if (hthr - a.sp.t_length <= 0) over = a.sp.latency_max;
+    } else {
+      const double off = offload_delay(a, mec, x, y, hsize);
+      dr = local - off;
+      has_dr = true;
+      if ((double)hthr - off > 0) {
+        succ = 1;
+        rd_inc = (double)(a.sp.latency_max - hthr) + off;
+      } else {
+        over = a.sp.latency_max;
+      }
+    }
+  }
+  if (w.agent) {
+    L.dr[w.lane] = has_dr ? dr : NAN;
+    L.ack[w.lane] = ack;
+    L.mec[w.lane] = mec;
+    L.tn[w.lane] = over;
+  }
+  wave_sync();
+  if (w.lead) {
+    // channel utilisation (:321-329): counts > 1 zeroed, Python sums in order
+    double util = 0.0;
+    for (int m = 0; m < M; ++m) {
+      double su = 0.0;
+      for (int c = 0; c <= C; ++c) {
+        const int f = freq[m * (C + 1) + c] > 1 ? 0 : freq[m * (C + 1) + c];
+        su = su + (double)f / (double)C;
+      }
+      util = util + su;
+    }
+    util = util / (double)M;
+    double delay_reward = 0.0;
+    int overtime = 0, confl = 0;
+    for (int ag = 0; ag < A; ++ag) {
+      if (!isnan(L.dr[w.gb + ag])) delay_reward = delay_reward + L.dr[w.gb + ag];
+      overtime += L.tn[w.gb + ag];
+      confl += L.ack[w.gb + ag] == -1;
+    }
+    a.o.reward[w.e] = delay_reward - (double)overtime;
+    double* info = a.o.info + (size_t)w.e * 6;
+    info[0] = delay_reward;
+    info[1] = (double)overtime;
+    info[2] = util;
+    info[3] = (double)confl / (double)A;
+    info[4] = info[5] = NAN;
+  }
+  wave_sync();
+  // update_users (:295-307) after the reward, agent by agent (independent)
+  AgentView nv{};
+  if (w.agent) {
+    a.s.last_ack[i] = ack;
+    if (a.o.ack) a.o.ack[i] = ack;
+    tsucc += succ;
+    a.s.task_success[i] = tsucc;
+    rdel = rdel + rd_inc;
+    a.s.remain_delay[i] = rdel;
+    const int64_t b = base + 5 * w.ag;
+    const int m = (int)(uniform(a.seed, w.e, b) * (double)M);  // only places the AGV: mec_index stays
+    double px, py;
+    position(a, m, uniform(a.seed, w.e, b + 1), uniform(a.seed, w.e, b + 2), px, py);
+    a.s.x[i] = px;
+    a.s.y[i] = py;
+    if (ack != -1 && len > 0) {
+      head = (head + 1) % Q;
+      --len;
+    }
+    // every queued job's threshold drops by t_length (5); the expired ones are a
+    // FIFO prefix (thresholds grow from head to tail: jobs arrive with latency_max
+    // and age together), so they are counted, not searched
+    if (ring) {
+      int nexp = 0;
+#pragma unroll
+      for (int k = 0; k < QR; ++k) {
+        int rel = k - head;
+        rel = rel < 0 ? rel + Q : rel;
+        if (k < Q && rel < len) {
+          thr[k] -= 5;
+          thr_ring[k] = thr[k];
+          nexp += thr[k] <= 0;
+        }
+      }
+      head = (head + nexp) % Q;
+      len -= nexp;
+    } else {
+      for (int k = 0; k < len; ++k) thr_ring[(head + k) % Q] -= 5;
+      while (len > 0 && thr_ring[head] <= 0) {
+        head = (head + 1) % Q;
+        --len;
+      }
+    }
+    a.s.q_head[i] = head;
+    a.s.q_len[i] = len;
+    const int nsize = generate_job(a, i, head, len, uniform(a.seed, w.e, b + 3), uniform(a.seed, w.e, b + 4));
+    tnum += nsize > 0;
+    // the new state as get_agent_inf sees it (load_agent without re-reading it)
+    int nh_size = nsize, nh_thr = nsize > 0 ? a.sp.latency_max : 0;
+    if (len > 0) {
+      if (ring) {
+#pragma unroll
+        for (int k = 0; k < QR; ++k) {
+          nh_size = k == head ? size[k] : nh_size;
+          nh_thr = k == head ? thr[k] : nh_thr;
+        }
+      } else {
+        nh_size = size_ring[head];
+        nh_thr = thr_ring[head];
+      }
+    }
+    nv.mec = mec;
+    nv.x = px;
+    nv.y = py;
+    nv.ack = ack;
+    nv.len = len + (nsize > 0);
+    nv.size = nh_size;
+    nv.thr = nh_thr;
+    L.tn[w.lane] = tnum;
+    L.ts[w.lane] = tsucc;
+    L.rd[w.lane] = rdel;
+  }
+  wave_sync();
+  if (w.lead) {
+    a.s.draw[w.e] = base + 5 * A;
+    const int ts = tslot + 1;
+    a.s.time_slot[w.e] = ts;
+    const bool term = ts == a.T;
+    a.o.terminated[w.e] = term ? 1 : 0;
+    if (term) {  // get_task_num (:368-415)
+      int tn = 0, tsu = 0;
+      double rd = 0.0;
+      for (int ag = 0; ag < A; ++ag) {
+        tn += L.tn[w.gb + ag];
+        tsu += L.ts[w.gb + ag];
+        rd = rd + L.rd[w.gb + ag];
+      }
+      double* info = a.o.info + (size_t)w.e * 6;
+      info[4] = (double)tsu / (double)tn;
+      info[5] = tsu != 0 ? rd / (double)tsu : 0.0;
+    }
+  }
+  // the worker's get_state / get_avail_actions / get_obs on the new state
+  if (w.agent) {
+    L.mec[w.lane] = nv.mec;
+    L.ack[w.lane] = nv.ack;
+    agent_inf(a, nv, L.inf[w.lane]);
+  }
+  wave_sync();
+  write_state_avail(a, w, L);
+  write_wire(a, w, L);
+  get_obs<true>(a, w, L, pre, false);
+  if (w.lead) a.s.nrm_n[w.e] = L.n[w.g];
+}
+
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void env_kernel(EnvArgs a) {
   __shared__ EnvLds L;
   const Who w = who(a);
-  const int A = a.A, M = a.M, C = a.C, FS = M * (C + 1);
+  const int A = a.A, M = a.M;
   if (blockIdx.x * a.G >= a.NE) return;
   const bool live = w.g < a.G && w.e < a.NE;
-  const int64_t base = a.mode == 0 || !live ? 0 : a.s.draw[w.e];
+  const int64_t base = a.mode == 0 || a.mode == 2 || !live ? 0 : a.s.draw[w.e];
   if (a.mode == 0) {  // construction (:25-40): mec_index + position per agent
     if (w.agent) {
       const int i = w.e * A + w.ag;
@@ -599,7 +849,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void en
     }
     return;
   }
-  if (w.lead) L.n[w.g] = a.s.nrm_n[w.e];
+  if (w.lead && a.mode != 2) L.n[w.g] = a.s.nrm_n[w.e];
   NormPre pre;
   if (a.mode == 3) {  // get_env_info (:421-439): two get_obs calls (one without entity obs, :425,431-434)
     load_norm(a, w, pre);
@@ -625,7 +875,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void en
       a.s.time_slot[w.e] = 0;
       a.s.draw[w.e] = base + 5 * A;
     }
-    __syncthreads();
+    wave_sync();
     load_norm(a, w, pre);
     fill_lds(a, w, L);
     get_obs<false>(a, w, L, pre, a.o.snap != nullptr);  // reset()'s own get_obs
@@ -636,185 +886,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void en
     return;
   }
   // ---- step (:309-366)
-  load_norm(a, w, pre);
-  for (int k = w.lane; k < a.G * FS; k += 64) L.freq[k] = 0;
-  __syncthreads();
-  AgentView v;
-  int act = 0;
-  int* freq = L.freq + w.g * FS;
-  if (w.agent) {
-    load_agent(a, w.e, w.ag, v);
-    act = (int)a.actions[(int64_t)w.e * a.act_se + w.ag];
-    act = act < 0 ? 0 : (act > C ? C : act);  // actions come from avail-masked selection; clamp keeps LDS in bounds
-    atomicAdd(&freq[v.mec * (C + 1) + act], 1);
-  }
-  __syncthreads();
-  int ack = 0;
-  if (w.agent) {
-    if (act == 0) ack = 0;
-    else ack = (freq[v.mec * (C + 1) + act] == 1) ? 1 : -1;
-  }
-  // get_reward (:229-293): per-agent terms, summed in agent order below
-  double dr = 0.0, rd_inc = 0.0;
-  int over = 0, succ = 0;
-  bool has_dr = false;
-  if (w.agent && v.len) {
-    const double local = round2_python(((double)(a.sp.comp_cycles * v.size) / a.sp.user_cap) * 1000.0);
-    if (ack == 0) {
-      if ((double)v.thr - local > 0) {
-        succ = 1;
-        rd_inc = (double)(a.sp.latency_max - v.thr) + local;
-      } else {
-        over = a.sp.latency_max;
-      }
-    } else if (ack == -1) {
-      if (v.thr - a.sp.t_length <= 0) over = a.sp.latency_max;
-    } else {
-      const double off = offload_delay(a, v.mec, v.x, v.y, v.size);
-      dr = local - off;
-      has_dr = true;
-      if ((double)v.thr - off > 0) {
-        succ = 1;
-        rd_inc = (double)(a.sp.latency_max - v.thr) + off;
-      } else {
-        over = a.sp.latency_max;
-      }
-    }
-  }
-  if (w.agent) {
-    L.dr[w.lane] = has_dr ? dr : NAN;
-    L.ack[w.lane] = ack;
-    L.mec[w.lane] = v.mec;
-    L.tn[w.lane] = over;
-  }
-  __syncthreads();
-  if (w.lead) {
-    // channel utilisation (:321-329): counts > 1 zeroed, Python sums in order
-    double util = 0.0;
-    for (int m = 0; m < M; ++m) {
-      double s = 0.0;
-      for (int c = 0; c <= C; ++c) {
-        const int f = freq[m * (C + 1) + c] > 1 ? 0 : freq[m * (C + 1) + c];
-        s = s + (double)f / (double)C;
-      }
-      util = util + s;
-    }
-    util = util / (double)M;
-    double delay_reward = 0.0;
-    int overtime = 0, confl = 0;
-    for (int ag = 0; ag < A; ++ag) {
-      if (!isnan(L.dr[w.gb + ag])) delay_reward = delay_reward + L.dr[w.gb + ag];
-      overtime += L.tn[w.gb + ag];
-      confl += L.ack[w.gb + ag] == -1;
-    }
-    a.o.reward[w.e] = delay_reward - (double)overtime;
-    double* info = a.o.info + (size_t)w.e * 6;
-    info[0] = delay_reward;
-    info[1] = (double)overtime;
-    info[2] = util;
-    info[3] = (double)confl / (double)A;
-    info[4] = info[5] = NAN;
-  }
-  __syncthreads();
-  // update_users (:295-307) after the reward, agent by agent (independent)
-  AgentView nv{};
-  if (w.agent) {
-    const int i = w.e * A + w.ag;
-    a.s.last_ack[i] = ack;
-    if (a.o.ack) a.o.ack[i] = ack;
-    a.s.task_success[i] += succ;
-    a.s.remain_delay[i] = a.s.remain_delay[i] + rd_inc;
-    const int64_t b = base + 5 * w.ag;
-    const int m = (int)(uniform(a.seed, w.e, b) * (double)M);
-    double px, py;
-    position(a, m, uniform(a.seed, w.e, b + 1), uniform(a.seed, w.e, b + 2), px, py);
-    a.s.x[i] = px;
-    a.s.y[i] = py;
-    int head = a.s.q_head[i], len = a.s.q_len[i];
-    int* thr_ring = a.s.q_thr + (size_t)i * a.QMAX;
-    if (ack != -1 && len > 0) {
-      head = (head + 1) % a.QMAX;
-      --len;
-    }
-    // every queued job's threshold drops by t_length (5); the expired ones are a
-    // FIFO prefix (thresholds grow from head to tail: jobs arrive with latency_max
-    // and age together), so they are counted, not searched.  The head job's
-    // threshold is kept for the obs that follow.
-    int hthr = 0;
-    if (a.QMAX <= QR) {
-      int thr[QR];
-#pragma unroll
-      for (int k = 0; k < QR; ++k) thr[k] = k < a.QMAX ? thr_ring[k] : 0;  // independent loads
-      int nexp = 0;
-#pragma unroll
-      for (int k = 0; k < QR; ++k) {
-        int rel = k - head;
-        rel = rel < 0 ? rel + a.QMAX : rel;
-        if (k < a.QMAX && rel < len) {
-          thr[k] -= 5;
-          thr_ring[k] = thr[k];
-          nexp += thr[k] <= 0;
-        }
-      }
-      head = (head + nexp) % a.QMAX;
-      len -= nexp;
-#pragma unroll
-      for (int k = 0; k < QR; ++k) hthr = k == head ? thr[k] : hthr;
-    } else {
-      for (int k = 0; k < len; ++k) thr_ring[(head + k) % a.QMAX] -= 5;
-      while (len > 0 && (hthr = thr_ring[head]) <= 0) {
-        head = (head + 1) % a.QMAX;
-        --len;
-      }
-    }
-    a.s.q_head[i] = head;
-    a.s.q_len[i] = len;
-    const int nsize = generate_job(a, i, head, len, uniform(a.seed, w.e, b + 3), uniform(a.seed, w.e, b + 4));
-    // the new state as get_agent_inf sees it (load_agent without re-reading it);
-    // the draw m only places the AGV, its mec_index stays (:295-307)
-    nv.mec = v.mec;
-    nv.x = px;
-    nv.y = py;
-    nv.ack = ack;
-    nv.len = len + (nsize > 0);
-    nv.size = len > 0 ? a.s.q_size[(size_t)i * a.QMAX + head] : nsize;
-    nv.thr = len > 0 ? hthr : (nsize > 0 ? a.sp.latency_max : 0);
-    L.tn[w.lane] = a.s.task_num[i];
-    L.ts[w.lane] = a.s.task_success[i];
-    L.rd[w.lane] = a.s.remain_delay[i];
-  }
-  __syncthreads();
-  if (w.lead) {
-    a.s.draw[w.e] = base + 5 * A;
-    const int ts = a.s.time_slot[w.e] + 1;
-    a.s.time_slot[w.e] = ts;
-    const bool term = ts == a.T;
-    a.o.terminated[w.e] = term ? 1 : 0;
-    if (term) {  // get_task_num (:368-415)
-      int tn = 0, tsu = 0;
-      double rd = 0.0;
-      for (int ag = 0; ag < A; ++ag) {
-        tn += L.tn[w.gb + ag];
-        tsu += L.ts[w.gb + ag];
-        rd = rd + L.rd[w.gb + ag];
-      }
-      double* info = a.o.info + (size_t)w.e * 6;
-      info[4] = (double)tsu / (double)tn;
-      info[5] = tsu != 0 ? rd / (double)tsu : 0.0;
-    }
-  }
-  __syncthreads();
-  // the worker's get_state / get_avail_actions / get_obs on the new state
-  if (w.agent) {
-    L.mec[w.lane] = nv.mec;
-    L.ack[w.lane] = nv.ack;
-    agent_inf(a, nv, L.inf[w.lane]);
-  }
-  __syncthreads();
-  write_state_avail(a, w, L);
-  write_wire(a, w, L);
-  get_obs<true>(a, w, L, pre, false);
-  if (w.lead) a.s.nrm_n[w.e] = L.n[w.g];
+  env_step(a, w, L, pre);
 }
 
 // ---- t2o_obs_expand: wire records -> dense normalised obs --------------------

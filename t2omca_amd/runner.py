@@ -33,6 +33,8 @@ batch carries the observation wire format instead of the dense obs —
 to a one-step scratch buffer the agent reads.  ``ops.obs_expand`` (called by
 TDLearner.train when the batch has no ``obs``) rebuilds the dense obs exactly.
 """
+import dataclasses
+
 import torch
 
 from . import ops
@@ -53,7 +55,14 @@ class LinearSchedule:
 
 class RolloutRunner:
     def __init__(self, agent, env, *, epsilon_start=1.0, epsilon_finish=0.05, epsilon_anneal_time=50000,
-                 seed=None, compact_obs=False):
+                 seed=None, compact_obs=False, precision="fp32"):
+        """precision: the agent step's MFMA operands — "fp32" (the reference's
+        precision, default) or "bf16" (bf16 weight / activation operands, fp32
+        accumulation, LayerNorm, softmax and recurrent state, as the learner's bf16
+        mode; greedy actions can differ from fp32's where two Q values are within
+        bf16 rounding)."""
+        if precision not in ("fp32", "bf16"):
+            raise ValueError(f"precision must be 'fp32' or 'bf16', not {precision!r}")
         # seed (None = 0) mixed with the data-parallel rank (distributed.rank_seed)
         # the data-parallel rank is always mixed in (rank 0 keeps `seed`), so ranks given
         # the same explicit seed still draw different streams
@@ -66,6 +75,8 @@ class RolloutRunner:
         if env.A != agent.shape.n_ent or env.n_actions != agent.shape.NA:
             raise ValueError("agent and env disagree on agents / actions")
         self.agent, self.env = agent, env
+        self.precision = precision
+        self.shape = dataclasses.replace(agent.shape, prec=1) if precision == "bf16" else agent.shape
         self.n, self.T, self.A, self.NA = env.n_envs, env.T, env.A, env.n_actions
         self.device = env.device
         self.schedule = LinearSchedule(epsilon_start, epsilon_finish, epsilon_anneal_time)
@@ -105,7 +116,7 @@ class RolloutRunner:
         if self._bufs is None or new_buffers:
             self._bufs = self._alloc()
         tm = self._bufs
-        env, shape = self.env, self.agent.shape
+        env, shape = self.env, self.shape
         pack = ops.pack_params(shape, torch.cat([p.detach().reshape(-1) for p in self.agent.parameters()]))
         eps = 0.0 if test_mode else self.schedule.eval(self.t_env)
         env.reset(dest=self._dest(tm, 0))

@@ -48,15 +48,18 @@ def _agent(A, seed=0):
     return TransformerAgent(None, make_args(A)).cuda()
 
 
-@pytest.mark.parametrize("A,M,n,T", [(3, 2, 5, 4), (8, 4, 6, 6)])
-def test_rollout_matches_env_replay_and_agent_unroll(A, M, n, T):
+@pytest.mark.parametrize("A,M,n,T,prec", [(3, 2, 5, 4, "fp32"), (8, 4, 6, 6, "fp32"), (8, 4, 6, 6, "bf16"),
+                                          (16, 2, 9, 5, "bf16")])
+def test_rollout_matches_env_replay_and_agent_unroll(A, M, n, T, prec):
+    """The runner's per-step agent launches equal one unroll over the recorded obs
+    (fp32, and the bf16 agent step of RolloutRunner(precision="bf16"))."""
     require_gpu()
     from t2omca_amd import ops
     from t2omca_amd.env import VecEnv
     from t2omca_amd.runner import RolloutRunner
     agent = _agent(A)
     env = VecEnv(n, mec_num=M, agv_num=A, episode_limit=T, seed=11)
-    runner = RolloutRunner(agent, env, seed=3)
+    runner = RolloutRunner(agent, env, seed=3, precision=prec)
     batch = runner.run(test_mode=True)
     ret = runner.last_returns
     torch.cuda.synchronize()
@@ -78,10 +81,16 @@ def test_rollout_matches_env_replay_and_agent_unroll(A, M, n, T):
     assert torch.equal(ret, ret2)
     assert int(batch["terminated"].sum()) == 0 and bool((batch["filled"] == 1).all())
     # greedy actions = masked argmax of the unrolled agent's Q on the recorded observations
-    pack = ops.pack_params(agent.shape, torch.cat([p.detach().reshape(-1) for p in agent.parameters()]))
-    q, _ = ops.agent_unroll_fwd(agent.shape, pack, batch["obs"])
+    flat = torch.cat([p.detach().reshape(-1) for p in agent.parameters()])
+    pack = ops.pack_params(runner.shape, flat)
+    q, _ = ops.agent_unroll_fwd(runner.shape, pack, batch["obs"])
     masked = q.masked_fill(batch["avail_actions"] == 0, -float("inf"))
     assert torch.equal(masked.argmax(-1), batch["actions"][..., 0])
+    if prec == "bf16":  # the bf16 step against fp32 operands on the same observations
+        q32, _ = ops.agent_unroll_fwd(agent.shape, ops.pack_params(agent.shape, flat), batch["obs"])
+        err = float((q - q32).abs().max() / q32.abs().max())
+        print(f"bf16 rollout agent step: Q normwise {err:.2e} vs fp32")
+        assert err < 2e-2
 
 
 def test_rollout_batch_feeds_learner():

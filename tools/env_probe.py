@@ -25,14 +25,14 @@ for t in range(20):
 torch.cuda.synchronize()
 nw = (NE + 3) // 4
 buf = np.zeros((4096, 16), np.uint64)
-_lib.lib.t2o_env_probe_read.restype = ctypes.c_int
-rc = _lib.lib.t2o_env_probe_read(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes))
+_lib.lib().t2o_env_probe_read.restype = ctypes.c_int
+rc = _lib.lib().t2o_env_probe_read(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(buf.nbytes))
 assert rc == 0, rc
 b = buf[:nw].astype(np.int64)
 clk = b[:, 1:12]  # clock64 at probe points 0..10
-names = ["normaliser prefetch", "reset freq + actions + load_agent + atomics", "per-agent reward + leader sums",
-         "update_users", "terminal sums", "fill L from registers", "state/avail/wire + get_obs prologue",
-         "get_obs update loop", "get_obs epilogue + counts", "(unused)"]
+names = ["state + normaliser loads (wait at the 1st barrier)", "head job + collision counts",
+         "per-agent reward + leader sums", "update_users", "terminal sums", "fill L from registers",
+         "state/avail/wire + get_obs prologue", "get_obs update loop", "get_obs epilogue + counts", "(unused)"]
 d = np.diff(clk, axis=1)
 out = {"waves": int(nw),
        "wall_us_100MHz": {"start_spread": float((b[:, 0].max() - b[:, 0].min()) / 100.0),
@@ -44,6 +44,7 @@ order = [(0, 1, names[0]), (1, 2, names[1]), (2, 3, names[2]), (3, 4, names[3]),
          (5, 6, names[5]), (6, 8, names[6]), (8, 9, names[7]), (9, 10, names[8])]
 for i, j, n in order:
     c = clk[:, j] - clk[:, i]
+    c = c[(c >= 0) & (c < 1 << 30)]  # waves that took the slow normaliser path skip probe 8
     out["phase_cycles_mean"][n] = float(c.mean())
     out["phase_cycles_p90"][n] = float(np.percentile(c, 90))
 print(json.dumps(out, indent=1))

@@ -6,15 +6,15 @@ import sys
 src = open(__file__.replace("tools/make_env_probe.py", "t2omca_amd/csrc/t2o_env.hip")).read()
 pts = [
     ("  const Who w = who(a);\n", "after", 0),
-    ("  // ---- step (:309-366)\n  load_norm(a, w, pre);\n", "after", 1),
+    ("  // the head job (load_agent)\n", "before", 1),
     ("  int ack = 0;\n  if (w.agent) {\n    if (act == 0)", "before", 2),
     ("  // update_users (:295-307)", "before", 3),
     ("  if (w.lead) {\n    a.s.draw[w.e] = base + 5 * A;", "before", 4),
-    ("  // the worker's get_state / get_avail_actions / get_obs on the new state", "before", 5),
-    ("  write_state_avail(a, w, L);\n  write_wire(a, w, L);\n  get_obs<true>(a, w, L, pre, false);", "before", 6),
-    ("  get_obs<true>(a, w, L, pre, false);\n  if (w.lead) a.s.nrm_n[w.e] = L.n[w.g];\n}", "before", 7),
+    ("  // the worker's get_state / get_avail_actions / get_obs on the new state\n  if (w.agent) {", "before", 5),
+    ("  write_state_avail(a, w, L);\n  write_wire(a, w, L);\n  get_obs<true>(a, w, L, pre, false);\n  if (w.lead) a.s.nrm_n", "before", 6),
+    ("  get_obs<true>(a, w, L, pre, false);\n  if (w.lead) a.s.nrm_n[w.e] = L.n[w.g];\n}\n\n__global__", "before", 7),
     ("  const double n0 = (double)nref;\n", "before", 8),
-    ("  if (w.lead) a.s.nrm_n[w.e] = L.n[w.g];\n}\n\n// ---- t2o_obs_expand", "before", 10),
+    ("  if (w.lead) a.s.nrm_n[w.e] = L.n[w.g];\n}\n\n__global__", "before", 10),
 ]
 for pat, where, k in pts:
     assert src.count(pat) == 1, (k, src.count(pat))
