@@ -25,6 +25,10 @@ python3 tools/timeline_trace.py $(find "$OUT/prof/trace" -name "*kernel_trace.cs
 tail -1 "$OUT/prof/timeline.txt"
 step rollout
 timeout -k 10 300 python bench.py --mode rollout > "$OUT/rollout.json" 2> "$OUT/rollout.err" || { tail -5 "$OUT/rollout.err"; exit 1; }
+timeout -k 10 300 python bench.py --mode rollout --rollout-precision bf16 > "$OUT/rollout_bf16.json" 2> "$OUT/rollout_bf16.err" || { tail -5 "$OUT/rollout_bf16.err"; exit 1; }
+for f in "$OUT"/rollout.json "$OUT"/rollout_bf16.json; do
+  python -c "import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[1],round(d['value']/1e6,1),'M/s',d['kernels_ms'])" "$f"
+done
 step dropin
 timeout -k 10 300 python bench.py --mode dropin > "$OUT/dropin.json" 2> "$OUT/dropin.err" || { tail -5 "$OUT/dropin.err"; exit 1; }
 step loop
