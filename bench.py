@@ -887,7 +887,13 @@ def main():
                                             "frac": flops[dom] / (dom_ms * 1e-3) / 1e12 / peak_tf},
                      "whole_update": {"flops": upd_flops, "ms": ms_step,
                                       "achieved": upd_flops / (ms_step * 1e-3) / 1e12,
-                                      "frac": upd_flops / (ms_step * 1e-3) / 1e12 / peak_tf}},
+                                      "frac": upd_flops / (ms_step * 1e-3) / 1e12 / peak_tf},
+                     # every network kernel on the same basis (the two BPTT kernels run within a
+                     # few µs of each other, so which one is "dominant" flips between runs)
+                     "per_kernel": {k: {"avg_launch_ms": kern[k],
+                                        "achieved": ref_flops[k] / (kern[k] * 1e-3) / 1e12,
+                                        "frac": ref_flops[k] / (kern[k] * 1e-3) / 1e12 / peak_tf}
+                                    for k in sorted(ref_flops) if k in kern}},
         "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items())},
         "flops_per_transition": {"executed_algorithm": sum(flops.values()) / (B * T * A),
                                  "reference_order": ref_order_flops_per_transition(A)},

@@ -512,8 +512,9 @@ T2O_DEV void mixer_head_bwd(const Wts<WT>& P, const t2o_layout& L, const float* 
   (void)mixer_head<E, A, WT, LDO>(P, L, OUT, qv, pre_h, pre2, na, pf, pb);
   const float hidden = elu1(pre_h);
   const float xw2 = OUT[(na + 1) * LDO + f];
-  const float sgn_w2 = dposf(xw2, pf, pb);
-  const float gpre = gyv * posf(xw2, pf, pb) * (pre_h > 0.f ? 1.f : expf(pre_h));
+  float pw2, sgn_w2;
+  posd(xw2, pf, pb, pw2, sgn_w2);
+  const float gpre = gyv * pw2 * (pre_h > 0.f ? 1.f : expf(pre_h));
   const float gpre2 = pre2 > 0.f ? gyv : 0.f;
   // gout[0, A): the agents' weight rows (entries >= na unused); gout[A + k]: hyper row na + k
   float gout[A + 3];
@@ -522,8 +523,10 @@ T2O_DEV void mixer_head_bwd(const Wts<WT>& P, const t2o_layout& L, const float* 
   for (int ag = 0; ag < A; ++ag) {
     if (ag < na) {
       const float xa = OUT[ag * LDO + f];
-      gout[ag] = qv[ag] * gpre * dposf(xa, pf, pb);
-      const float gq = feat_sum<E>(fv ? gpre * posf(xa, pf, pb) : 0.f);
+      float pa, da;
+      posd(xa, pf, pb, pa, da);
+      gout[ag] = qv[ag] * gpre * da;
+      const float gq = feat_sum<E>(fv ? gpre * pa : 0.f);
       gqm = lane == ag ? gq : gqm;
     }
   }
