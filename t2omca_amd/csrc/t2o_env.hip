@@ -683,14 +683,13 @@ __device__ __forceinline__ void env_step(const EnvArgs& a, const Who& w, EnvLds&
   }
   wave_sync();
   if (w.lead) {
-    // channel utilisation (:321-329): counts > 1 zeroed, Python sums in order
+    // channel utilisation (:321-329): counts > 1 zeroed, Python sums in order; a
+    // kept count is 0 or 1, so each term is +0 or the one quotient 1 / C
+    const double inv_c = 1.0 / (double)C;
     double util = 0.0;
     for (int m = 0; m < M; ++m) {
       double su = 0.0;
-      for (int c = 0; c <= C; ++c) {
-        const int f = freq[m * (C + 1) + c] > 1 ? 0 : freq[m * (C + 1) + c];
-        su = su + (double)f / (double)C;
-      }
+      for (int c = 0; c <= C; ++c) su = su + (freq[m * (C + 1) + c] == 1 ? inv_c : 0.0);
       util = util + su;
     }
     util = util / (double)M;
