@@ -44,6 +44,7 @@ struct AgentFwdArgs {
 inline int rows_per_wave(int R) { return (void)R, 16; }
 
 constexpr int AG_FWD_WAVES = 4;  // waves per workgroup sharing one LDS copy of the weights
+constexpr int AG_FWD_LOOP_T = 4;  // unrolls this short loop resident workgroups over the tiles
 
 // Up to 8 entities the forward fits 256 VGPRs: capping it there (2 waves per
 // SIMD's worth of registers) keeps the MFMA results in VGPRs instead of
@@ -53,7 +54,7 @@ constexpr int agent_fwd_waves_per_eu() { return NE <= 8 ? 2 : 1; }
 
 // RT: runtime-entity instance (t2o_dispatch.hpp) — NE is a capacity, the real
 // entity count is args.A (n_entities = n_agents on the tuned path)
-template <int E, int H, int D, int NE, int FF, bool RT, bool WLDS, typename WT>
+template <int E, int H, int D, int NE, int FF, bool RT, bool WLDS, bool LOOP, typename WT>
 __global__ __launch_bounds__(64 * AG_FWD_WAVES) __attribute__((amdgpu_waves_per_eu(agent_fwd_waves_per_eu<NE>())))
 void agent_fwd_kernel(AgentFwdArgs args) {
   constexpr int ET = E / 16;
@@ -72,80 +73,94 @@ void agent_fwd_kernel(AgentFwdArgs args) {
   const int A = args.A, F = args.F;
   const int ne = RT ? A : NE;
   const int R = args.B * A;
-  const int rt = blockIdx.x * AG_FWD_WAVES + wave_id();
-  if (rt * args.rpw >= R) return;  // wave-uniform: no barriers after this point
-  const int c = lane_c(), g = lane_g();
-  const int row_raw = rt * args.rpw + c;
-  const bool valid = c < args.rpw && row_raw < R;
-  const int row = valid ? row_raw : R - 1;
-  const int b = row / A, a = row % A;
+  // 16-row tiles, one per wave.  LOOP (a short unroll: the rollout's one step):
+  // launch_fwd starts only as many workgroups as are resident and each wave loops
+  // over tiles, so the weights are staged once per workgroup rather than once per
+  // four tiles (rollout agent step 0.210 -> 0.179 ms fp32, 0.125 -> 0.105 ms bf16,
+  // profiles/r4_agloop/); a long unroll keeps one tile per wave (the loop raised
+  // the 8-entity kernel's registers 202 -> 256 with spills).  Wave-uniform: no
+  // barriers after this point.
+  const int tiles = (R + args.rpw - 1) / args.rpw;
+  auto run_tile = [&](const int rt) {
+    const int c = lane_c(), g = lane_g();
+    const int row_raw = rt * args.rpw + c;
+    const bool valid = c < args.rpw && row_raw < R;
+    const int row = valid ? row_raw : R - 1;
+    const int b = row / A, a = row % A;
 
-  f4 h[ET];
+    f4 h[ET];
 #pragma unroll
-  for (int t = 0; t < ET; ++t) h[t] = net.h0 ? ld4(net.h0 + (size_t)row * E + 16 * t + 4 * g) : zero4();
+    for (int t = 0; t < ET; ++t) h[t] = net.h0 ? ld4(net.h0 + (size_t)row * E + 16 * t + 4 * g) : zero4();
 
-  // few entities: the observations live in registers, the next step's loaded
-  // while the current one computes; many entities: streamed per block in
-  // chunks (t2o_agent_block_ch.hpp)
-  constexpr bool CHUNK = NE > AG_CHUNK_MIN;
-  constexpr int NO = CHUNK ? 1 : NE;
-  auto row_obs = [&](int step) {
-    return args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * ne * F;
+    // few entities: the observations live in registers, the next step's loaded
+    // while the current one computes; many entities: streamed per block in
+    // chunks (t2o_agent_block_ch.hpp)
+    constexpr bool CHUNK = NE > AG_CHUNK_MIN;
+    constexpr int NO = CHUNK ? 1 : NE;
+    auto row_obs = [&](int step) {
+      return args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * ne * F;
+    };
+    auto load_obs = [&](int step, f4 (&o)[NO]) {
+      const float* ob = row_obs(step);
+#pragma unroll
+      for (int j = 0; j < NO; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int f = 4 * g + r;
+          o[j][r] = (f < F && j < ne) ? ob[j * F + f] : 0.f;
+        }
+    };
+    f4 on[NO];
+    if constexpr (!CHUNK) load_obs(0, on);
+    for (int step = 0; step < args.T; ++step) {
+      const Wts<WT> P = step_view(P0);
+      f4 o[NO];
+      if constexpr (!CHUNK) {
+#pragma unroll
+        for (int j = 0; j < NE; ++j) o[j] = on[j];
+        if (step + 1 < args.T) load_obs(step + 1, on);
+      }
+      const ObsRow orow{row_obs(step), F, ne, RT && ne % AG_CHUNK != 0};
+      f4 x[ET];
+#pragma unroll
+      for (int t = 0; t < ET; ++t) x[t] = h[t];
+#pragma unroll
+      for (int d = 0; d < D; ++d) {
+        if (d > 0 && net.hmid && valid) {
+          float* hm = net.hmid + ((((size_t)b * args.T + step) * (D - 1) + d - 1) * A + a) * E;
+#pragma unroll
+          for (int t = 0; t < ET; ++t) st4(hm + 16 * t + 4 * g, x[t]);
+        }
+        if constexpr (CHUNK) {
+          agent_block_fwd_ch<E, H, NE, FF, false>(P, L, d, h, orow, x, nullptr);
+        } else {
+          (void)orow;
+          agent_block_fwd<E, H, NE, FF, false>(P, L, d, h, o, ne, x, nullptr);
+        }
+      }
+      f4 q = zero4();
+#pragma unroll
+      for (int i = 0; i < ET; ++i) q = mma_tile(P.w + L.Wo, E, 0, i, x[i], q, P.vol);
+      q += vec_t(P.v + L.bo, 0);
+#pragma unroll
+      for (int t = 0; t < ET; ++t) h[t] = x[t];
+      if (valid) {
+        const size_t base = ((size_t)b * args.T + step) * A + a;
+        float* qo = net.q + base * L.NA;
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * g + r < L.NA) qo[4 * g + r] = q[r];
+        float* ho = net.h + base * E;
+#pragma unroll
+        for (int t = 0; t < ET; ++t) st4(ho + 16 * t + 4 * g, h[t]);
+      }
+    }
   };
-  auto load_obs = [&](int step, f4 (&o)[NO]) {
-    const float* ob = row_obs(step);
-#pragma unroll
-    for (int j = 0; j < NO; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int f = 4 * g + r;
-        o[j][r] = (f < F && j < ne) ? ob[j * F + f] : 0.f;
-      }
-  };
-  f4 on[NO];
-  if constexpr (!CHUNK) load_obs(0, on);
-  for (int step = 0; step < args.T; ++step) {
-    const Wts<WT> P = step_view(P0);
-    f4 o[NO];
-    if constexpr (!CHUNK) {
-#pragma unroll
-      for (int j = 0; j < NE; ++j) o[j] = on[j];
-      if (step + 1 < args.T) load_obs(step + 1, on);
-    }
-    const ObsRow orow{row_obs(step), F, ne, RT && ne % AG_CHUNK != 0};
-    f4 x[ET];
-#pragma unroll
-    for (int t = 0; t < ET; ++t) x[t] = h[t];
-#pragma unroll
-    for (int d = 0; d < D; ++d) {
-      if (d > 0 && net.hmid && valid) {
-        float* hm = net.hmid + ((((size_t)b * args.T + step) * (D - 1) + d - 1) * A + a) * E;
-#pragma unroll
-        for (int t = 0; t < ET; ++t) st4(hm + 16 * t + 4 * g, x[t]);
-      }
-      if constexpr (CHUNK) {
-        agent_block_fwd_ch<E, H, NE, FF, false>(P, L, d, h, orow, x, nullptr);
-      } else {
-        (void)orow;
-        agent_block_fwd<E, H, NE, FF, false>(P, L, d, h, o, ne, x, nullptr);
-      }
-    }
-    f4 q = zero4();
-#pragma unroll
-    for (int i = 0; i < ET; ++i) q = mma_tile(P.w + L.Wo, E, 0, i, x[i], q, P.vol);
-    q += vec_t(P.v + L.bo, 0);
-#pragma unroll
-    for (int t = 0; t < ET; ++t) h[t] = x[t];
-    if (valid) {
-      const size_t base = ((size_t)b * args.T + step) * A + a;
-      float* qo = net.q + base * L.NA;
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (4 * g + r < L.NA) qo[4 * g + r] = q[r];
-      float* ho = net.h + base * E;
-#pragma unroll
-      for (int t = 0; t < ET; ++t) st4(ho + 16 * t + 4 * g, h[t]);
-    }
+  const int rt0 = blockIdx.x * AG_FWD_WAVES + wave_id();
+  if constexpr (LOOP) {
+    for (int rt = rt0; rt < tiles; rt += gridDim.x * AG_FWD_WAVES) run_tile(rt);
+  } else {
+    if (rt0 < tiles) run_tile(rt0);
   }
 }
 
@@ -160,8 +175,20 @@ int launch_fwd(const AgentFwdArgs& args, int nnet, hipStream_t stream) {
   size_t lds = sizeof(float) * (size_t)lds_weight_floats<WT>(args.L, args.L.fwd_total);
   a.wlds = lds <= 160 * 1024;
   if (!a.wlds) lds = 0;
-  auto kern = a.wlds ? agent_fwd_kernel<E, H, D, NE, FF, RT, true, WT> : agent_fwd_kernel<E, H, D, NE, FF, RT, false, WT>;
+  const bool loop = args.T <= AG_FWD_LOOP_T && a.wlds;
+  auto kern = loop ? agent_fwd_kernel<E, H, D, NE, FF, RT, true, true, WT>
+              : a.wlds ? agent_fwd_kernel<E, H, D, NE, FF, RT, true, false, WT>
+                       : agent_fwd_kernel<E, H, D, NE, FF, RT, false, false, WT>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (loop) {  // resident workgroups only, looping over the tiles
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 64 * AG_FWD_WAVES, lds) == hipSuccess &&
+        hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && per_cu > 0 && cus > 0) {
+      const unsigned cap = (unsigned)((per_cu * cus + nnet - 1) / nnet);
+      if (grid.x > cap) grid.x = cap;
+    }
+  }
   hipLaunchKernelGGL(kern, grid, dim3(64 * AG_FWD_WAVES), lds, stream, a);
   return (int)hipGetLastError();
 }
