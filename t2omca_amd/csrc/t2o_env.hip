@@ -273,7 +273,8 @@ constexpr int OBS_SLOTS = 9;  // ceil(G * 9A / 64) <= 9 for every A <= 64
 // operands meet: finite, far from the subnormal range, and never -0 (a = +0
 // gives +0; x and the running mean are never -0, so neither is x - mean, and S
 // is a sum of non-negative products from +0).  Checked against IEEE division on
-// 5.9e7 random (a, n <= 3e5) pairs with gcc.
+// 5.9e7 random (a, n <= 3e5) pairs with gcc; tests/test_env_division.py keeps a
+// 2e6-pair version of that check.
 __device__ __forceinline__ double div_by(double a, double n, double y) {
   double q = a * y;
   double r = fma(-q, n, a);
