@@ -134,3 +134,37 @@ def test_env_flat_obs_mode_vs_oracle():
     normalised by a 6-long running normaliser; get_env_info makes one get_obs call."""
     _rollout_vs_oracle(NE=6, M=2, A=8, T=10, eps=2, seed=21, obs_entity_mode=False)
     _rollout_vs_oracle(NE=3, M=4, A=64, T=4, eps=1, seed=22, obs_entity_mode=False)
+
+
+def test_env_queue_capacity_beyond_register_ring(monkeypatch):
+    """Job queues of capacity <= 16 are updated in registers (t2o_env.hip env_step, QR),
+    larger ones through memory; the logical queue never holds more than
+    latency_max / t_length + 1 = 11 jobs, so a capacity of 20 must give the same
+    trajectories bit for bit as the default 11 (and exercises the memory path)."""
+    from t2omca_amd import env_spec
+    from t2omca_amd.env import VecEnv
+    NE, M, A, T = 10, 2, 16, 12
+    envs = [VecEnv(NE, mec_num=M, agv_num=A, episode_limit=T, seed=31, keep_obs64=True)]
+    monkeypatch.setattr(env_spec, "QMAX", 20)
+    envs.append(VecEnv(NE, mec_num=M, agv_num=A, episode_limit=T, seed=31, keep_obs64=True))
+    assert (envs[0].qmax, envs[1].qmax) == (env_spec.LATENCY_MAX // env_spec.T_LENGTH + 1, 20)
+    rng = np.random.default_rng(5)
+    for ep in range(2):
+        outs = [e.reset() for e in envs]
+        for a_, b_ in zip(outs[0], outs[1]):
+            _eq(b_.cpu().numpy(), a_.cpu().numpy(), f"reset{ep}")
+        for t in range(T):
+            avn = outs[0][1].cpu().numpy()
+            acts = torch.from_numpy(np.array([[rng.choice(np.nonzero(avn[e, i])[0]) for i in range(A)]
+                                              for e in range(NE)])).cuda()
+            outs = [e.step(acts) for e in envs]
+            r0, d0, i0, s0, a0, _ = outs[0]
+            r1, d1, i1, s1, a1, _ = outs[1]
+            _eq(r1.cpu().numpy(), r0.cpu().numpy(), "reward")
+            _eq(s1.cpu().numpy(), s0.cpu().numpy(), "state")
+            _eq(a1.cpu().numpy(), a0.cpu().numpy(), "avail")
+            _eq(envs[1].obs64.cpu().numpy(), envs[0].obs64.cpu().numpy(), f"obs t{t}")
+            for k in INFO:
+                _eq(i1[k].cpu().numpy(), i0[k].cpu().numpy(), k)
+            outs = [(None, a0), (None, a1)]  # avail drives the next draw
+        assert torch.equal(envs[0].queue_len, envs[1].queue_len)
