@@ -1,7 +1,15 @@
 """GPU, data parallel on the PRODUCT learner: two ranks (gloo, both on cuda:0, spawned
 before any GPU call in the children) each run TDLearner.train on their episode shard;
-after every update the post-Adam parameters equal a single-rank full-batch TDLearner
-update (<= 1e-6 normwise) and stay identical across ranks.
+every update's post-Adam parameters equal a single-rank full-batch TDLearner update
+from the same state (<= 1e-6 normwise), and the ranks stay identical.
+
+Each update is compared from the replicas' own state (parameters, target network,
+Adam moments): over several updates the two trajectories differ by gradient
+summation order (~1e-7), and once the parameters differ, an FFN pre-activation
+within that distance of 0 can take the other ReLU branch and move one unit's
+gradients by O(1) — profiles/r4_elu/diag_dp_*.log show it: after two updates
+1.2e-7 apart, the third update's gradients of one mixer FFN unit differ by 1.3e-4
+normwise, with the first two updates' gradients 1.1e-7 apart.
 
 The ranks deliberately build their modules from different seeds: the learner's
 rank-0 broadcast (distributed.broadcast_state) must make the replicas identical
@@ -54,11 +62,16 @@ def _worker(rank, world, port, out):
         batch, w = _batch(dev)
         lo, hi = shard_bounds(B, rank, world)
         shard = {k: v[lo:hi] for k, v in batch.items()}
-        hist = [learner.params.detach().cpu().clone()]
+
+        def state():
+            return torch.stack([learner.params, learner.target_params, learner.exp_avg,
+                                learner.exp_avg_sq]).detach().cpu().clone()
+
+        hist = [state()]
         for u in range(UPDATES):
             learner.train(shard, 0, u, per_weight=w[lo:hi])
             torch.cuda.synchronize()
-            hist.append(learner.params.detach().cpu().clone())
+            hist.append(state())
         out.put((rank, torch.stack(hist).numpy()))
     finally:
         dist.destroy_process_group()
@@ -81,15 +94,20 @@ def test_dp_two_ranks_equal_full_batch_learner():
             p.join(timeout=60)
     for p in procs:
         assert p.exitcode == 0
-    r0, r1 = torch.from_numpy(res[0]), torch.from_numpy(res[1])
+    r0, r1 = torch.from_numpy(res[0]), torch.from_numpy(res[1])  # [update, (params, target, m, v), n]
     # replicas are identical from the start (rank 0's init) and stay identical
     assert torch.equal(r0, r1)
     dev = torch.device("cuda", 0)
     full = _learner(100, dev)  # rank 0's init
     batch, w = _batch(dev)
-    assert torch.equal(full.params.cpu(), r0[0])
+    assert torch.equal(full.params.cpu(), r0[0, 0])
     for u in range(UPDATES):
+        # the full-batch update from the replicas' state before update u
+        for buf, k in ((full.params, 0), (full.target_params, 1), (full.exp_avg, 2), (full.exp_avg_sq, 3)):
+            buf.copy_(r0[u, k].to(dev))
+        full._params_written()
+        full._pack_targets()
         full.train(batch, 0, u, per_weight=w)
         torch.cuda.synchronize()
-        err = normwise(r0[u + 1], full.params.cpu())
+        err = normwise(r0[u + 1, 0], full.params.cpu())
         assert err < 1e-6, (u, err)
