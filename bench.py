@@ -675,6 +675,16 @@ def dropin_bench(args, world, rank, dev):
         print(json.dumps(out), flush=True)
 
 
+def dist_info(world, rank_seconds, steps):
+    """What the process group itself reports (so a SCALE line shows that RCCL saw N
+    ranks, not only what WORLD_SIZE said) and every rank's ms per step."""
+    ms = [t / steps * 1e3 for t in rank_seconds]
+    up = dist.is_available() and dist.is_initialized()
+    return {"world_size": dist.get_world_size() if up else 1, "backend": dist.get_backend() if up else None,
+            "env_world_size": world, "devices_visible": torch.cuda.device_count(),
+            "rank_ms_per_step": {"max": max(ms), "min": min(ms), "per_rank": [round(v, 4) for v in ms]}}
+
+
 def free_port():
     import socket
     with socket.socket() as s:
@@ -815,10 +825,18 @@ def main():
         el = time.perf_counter() - t0
         learner.timer = None
         if world > 1:
-            t = torch.tensor([el], device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t)
+            # every rank's time (the line reports the max; the spread shows the ranks ran together)
+            ts = [torch.zeros(1, device=dev) for _ in range(world)]
+            dist.all_gather(ts, torch.tensor([el], device=dev))
+            per_rank = [float(t) for t in ts]
+            el = max(per_rank)
+        else:
+            per_rank = [el]
+        rank_times.clear()
+        rank_times.extend(per_rank)
         return el
+
+    rank_times = []
 
     timer = KernelTimer()
     elapsed = timed(step, timer, args.kernel_timer_every)
@@ -899,6 +917,7 @@ def main():
                                         "frac": ref_flops[k] / (kern[k] * 1e-3) / 1e12 / peak_tf}
                                     for k in sorted(ref_flops) if k in kern}},
         "kernels_ms": {k: round(v, 4) for k, v in sorted(kern.items())},
+        "distributed": dist_info(world, rank_times, args.steps),
         "flops_per_transition": {"executed_algorithm": sum(flops.values()) / (B * T * A),
                                  "reference_order": ref_order_flops_per_transition(A)},
     }

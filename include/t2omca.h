@@ -331,6 +331,12 @@ int t2o_adam_workspace_floats(void);
  * (tests/test_gpu_primitives.py). */
 int t2o_probe_lane_ops(const float* in, float* out, void* stream);
 
+/* Diagnostic: the mixing head's positivity function pos_func (T2O_POS_*,
+ * n_transf_mixer.py:95-103) with beta on x[n]: out[0:n] posf, out[n:2n] its
+ * derivative, out[2n:4n] the fused value / derivative pair the BPTT kernels
+ * evaluate (tests/test_gpu_primitives.py checks them element by element). */
+int t2o_probe_posf(const float* x, int n, int pos_func, float beta, float* out, void* stream);
+
 /* Diagnostic: the XOR (in bf16 elements, a multiple of 8) applied to the
  * columns of row `row` of a bf16 weight-image matrix with row length ld: element
  * (r, col) of the image sits at r*ld + (col ^ t2o_bf_swz(r, ld)). */

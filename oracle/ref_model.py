@@ -62,7 +62,11 @@ def block(p, pre, q, k, heads, keep=None):
     attended = mha(p, pre + "attention.", q, k, heads)
     x = F.layer_norm(attended + q, (e,), p[pre + "norm1.weight"], p[pre + "norm1.bias"])
     ff = F.linear(x, p[pre + "ff.0.weight"], p[pre + "ff.0.bias"])
-    ff = F.relu(ff) if _ffn_relu is None else _ffn_relu(ff, keep)
+    if _ffn_relu is None:
+        ff = F.relu(ff)
+    else:  # (the hook also gets Σ_e |W1[j,e] x_e| + |c1[j]|: the pre-activation's rounding scale)
+        scale = F.linear(x.detach().abs(), p[pre + "ff.0.weight"].detach().abs(), p[pre + "ff.0.bias"].detach().abs())
+        ff = _ffn_relu(ff, keep, scale)
     ff = F.linear(ff, p[pre + "ff.2.weight"], p[pre + "ff.2.bias"])
     x = F.layer_norm(ff + x, (e,), p[pre + "norm2.weight"], p[pre + "norm2.bias"])
     return x
@@ -215,8 +219,11 @@ class TieAwareRelu:
     def __init__(self, margin):
         self.margin = margin
         self.ties = []  # (mask tensor, flat index, fp64 pre-activation)
+        self.scales = []  # per tie: Σ_e |W1[j,e] x_e| + |c1[j]| (0 when the caller gave none)
+        self.where = []  # per tie: (hook call number, [token, unit] shape of the call, flat index)
+        self.calls = 0
 
-    def __call__(self, x, keep):
+    def __call__(self, x, keep, scale=None):
         mask = (x.detach() > 0).to(x.dtype)
         if x.requires_grad:
             near = x.detach().abs() < self.margin
@@ -226,6 +233,9 @@ class TieAwareRelu:
                 near &= kept
             for i in near.reshape(-1).nonzero().reshape(-1).tolist():
                 self.ties.append((mask, i, float(x.detach().reshape(-1)[i])))
+                self.scales.append(0.0 if scale is None else float(scale.reshape(-1)[i]))
+                self.where.append((self.calls, tuple(x.shape), i))
+        self.calls += 1
         return _MaskedRelu.apply(x, mask)
 
     def branches(self):

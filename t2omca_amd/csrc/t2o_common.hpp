@@ -456,14 +456,18 @@ T2O_DEV float rowsum16_fast(float v) {
   return v;
 }
 
-// log(1 + e) for e >= 0 (softplus): v_log_f32 of 1 + e (log2, ~1 ulp) times ln 2,
-// and the series e - e²/2 + e³/3 where 1 + e would round e away (e < 2^-10:
-// relative error < 1e-9).  libm's log1pf / expf made a non-abs mixer head cost
-// its kernels as much as the rest of the step (mixer BPTT 0.95 vs 0.54 ms).
+// log(1 + e) for e >= 0 (softplus), Goldberg's form: u = RN(1 + e) is exact
+// as 1 + (u - 1), so log(u) · e / (u - 1) carries only the ~1 ulp relative errors
+// of v_log_f32 (log2), the ln 2 product and v_rcp_f32; e itself where u rounds
+// to 1.  (log(1 + e) alone lost up to 2^-24 / e relative to the rounding of 1 + e:
+// 6e-5 at e = 2^-10, x·β near -7 — ADVICE r4.)  libm's log1pf / expf made a
+// non-abs mixer head cost its kernels as much as the rest of the step (mixer
+// BPTT 0.95 vs 0.54 ms).
 T2O_DEV float log1p_fast(float e) {
-  const float big = __builtin_amdgcn_logf(1.f + e) * 0.6931471805599453f;
-  const float small = e * (1.f - e * (0.5f - e * (1.f / 3.f)));
-  return e < 9.765625e-4f ? small : big;
+  const float u = 1.f + e;
+  const float um1 = u - 1.f;
+  const float r = __builtin_amdgcn_logf(u) * 0.6931471805599453f * (e * rcp_fast(um1));
+  return um1 == 0.f ? e : r;
 }
 
 // ---- mixing-head positivity (n_transf_mixer.py:95-103; the generic kernels) --

@@ -387,7 +387,10 @@ __device__ __attribute__((always_inline)) void norm_fast(const EnvArgs& a, const
                                                 i * no * (int)sizeof(float), 0);
         if (a.o.obs64) {
           typedef int v2i __attribute__((ext_vector_type(2)));
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i, v), orsrc64, 2 * ooff[k],
+          // (doubled in unsigned arithmetic: the drop sentinel 0x40000000 becomes
+          // 0x80000000, still past the range-checked buffer's end)
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2i, v), orsrc64,
+                                                __builtin_bit_cast(int, (unsigned)ooff[k] << 1),
                                                 i * no * (int)sizeof(double), 0);
         }
       }

@@ -9,15 +9,18 @@ DP update equal to the full-batch update:
 
     loss = Σ_b w_b Σ_t ½ td² m / Σ_all m   ->   grad = Σ_r g_r / Σ_r M_r
 
-At E = 32 that buffer is 84,007 floats (336 KB): latency-bound over xGMI, so
-it is one all-reduce, issued after both unfolds (the default learner path).
-It cannot be hidden under the BPTT kernels: they hold every SIMD (the agent
-BPTT one 503-register wave per SIMD), and an RCCL kernel, like any kernel
-issued on another stream, needs a wave slot — the round-3 trace shows a side-
-stream copy issued at the agent BPTT's start waiting until its end
-(profiles/r3_f5/prof/timeline.txt).  The learner's ``contract="side"`` mode
-still issues the mixer half from the side stream before the agent BPTT; it
-runs when that BPTT drains, not under it.
+At E = 32 that buffer is 84,007 floats (336 KB), latency-bound over xGMI.  The
+default learner path (``TDLearner(contract="side")``, learner.py step 6) issues
+it in TWO halves on two streams: the mixer half [mixer grads, Σ mask] from the
+side stream as soon as the mixer's tape contraction and unfold finish there, the
+agent half [agent grads] from the main stream after the agent's; the main stream
+waits for both before Adam.  (``contract="pair"`` contracts both tapes in one
+launch after the agent BPTT and issues the whole buffer as one all-reduce.)
+Neither half runs under a BPTT kernel: those hold every SIMD (the agent BPTT
+one 503-register wave per SIMD), and an RCCL kernel, like any kernel issued on
+another stream, needs a wave slot — the round-3 trace shows a side-stream copy
+issued at the agent BPTT's start waiting until its end
+(profiles/r3_f5/prof/timeline.txt); the mixer half runs as that BPTT drains.
 
 Replicas start identical and stay identical: the learner broadcasts its
 parameters, target parameters and Adam moments from rank 0 when it is built

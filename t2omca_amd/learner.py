@@ -57,11 +57,16 @@ class TDLearner:
                  target_update_interval=200, optim_betas=(0.9, 0.999), optim_eps=1e-8, weight_decay=0.0,
                  detach_mixer_hidden=False, process_group=None, priorities_to_cpu=True, precision="fp32",
                  overlap=True, td_algo="auto", contract="side"):
+        # options first (a bad value fails here, not inside the first train())
+        if precision not in ("fp32", "bf16"):
+            raise ValueError("precision must be 'fp32' or 'bf16'")
+        if contract not in ("pair", "side"):
+            raise ValueError("contract must be 'pair' or 'side'")
+        if td_algo not in ops.TD_ALGOS:
+            raise ValueError(f"td_algo must be one of {sorted(ops.TD_ALGOS)}, got {td_algo!r}")
         dev = next(agent.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("TDLearner needs the modules on a HIP device (no CPU fallback)")
-        if precision not in ("fp32", "bf16"):
-            raise ValueError("precision must be 'fp32' or 'bf16'")
         self.agent, self.mixer = agent, mixer
         # bf16: MFMA operands (weights, activations entering a matrix product) in
         # bf16; accumulation, LayerNorm, softmax, recurrent state, TD targets, grads
@@ -98,8 +103,6 @@ class TDLearner:
         # every SIMD) but its workgroups take the CUs the BPTT's last waves free;
         # "pair": both contractions in one launch after the agent BPTT, measured
         # 15 us slower per update (profiles/r4_b/: 2.455 vs 2.438 ms)
-        if contract not in ("pair", "side"):
-            raise ValueError("contract must be 'pair' or 'side'")
         self.contract = contract
         self.step_count = 0
         self.last_target_update_episode = 0

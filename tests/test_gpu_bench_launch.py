@@ -30,4 +30,9 @@ def test_bench_gpus2_launches_two_ranks():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 32
     assert d["value"] > 0 and d["steps"] == 2 and d["warmup"] == 1
+    # what the process group itself saw (a SCALE line shows RCCL's rank count the same way)
+    di = d["distributed"]
+    assert di["world_size"] == 2 and di["backend"] == "gloo" and di["env_world_size"] == 2, di
+    rm = di["rank_ms_per_step"]
+    assert len(rm["per_rank"]) == 2 and rm["min"] <= rm["max"] and abs(rm["max"] - d["ms_per_step"]) < 1e-6 * rm["max"] + 1e-9
     print("bench --gpus 2 (gloo, one device):", {k: d[k] for k in ("value", "ms_per_step", "n_gpus")})

@@ -4,7 +4,8 @@ every update's post-Adam parameters equal a single-rank full-batch TDLearner upd
 from the same state (<= 1e-6 normwise), and the ranks stay identical.
 
 Each update is compared from the replicas' own state (parameters, target network,
-Adam moments): over several updates the two trajectories differ by gradient
+Adam moments; gradients and post-Adam parameters <= 1e-6), then the two
+trajectories are run freely (<= 1e-4): over several updates they differ by gradient
 summation order (~1e-7), and once the parameters differ, an FFN pre-activation
 within that distance of 0 can take the other ReLU branch and move one unit's
 gradients by O(1) — profiles/r4_elu/diag_dp_*.log show it: after two updates
@@ -63,15 +64,15 @@ def _worker(rank, world, port, out):
         lo, hi = shard_bounds(B, rank, world)
         shard = {k: v[lo:hi] for k, v in batch.items()}
 
-        def state():
+        def state(grad):
             return torch.stack([learner.params, learner.target_params, learner.exp_avg,
-                                learner.exp_avg_sq]).detach().cpu().clone()
+                                learner.exp_avg_sq, grad]).detach().cpu().clone()
 
-        hist = [state()]
+        hist = [state(torch.zeros_like(learner.params))]
         for u in range(UPDATES):
             learner.train(shard, 0, u, per_weight=w[lo:hi])
             torch.cuda.synchronize()
-            hist.append(state())
+            hist.append(state(learner.grad[:-1] / learner.grad[-1]))  # the all-reduced, Σmask-normalised grad
         out.put((rank, torch.stack(hist).numpy()))
     finally:
         dist.destroy_process_group()
@@ -94,7 +95,7 @@ def test_dp_two_ranks_equal_full_batch_learner():
             p.join(timeout=60)
     for p in procs:
         assert p.exitcode == 0
-    r0, r1 = torch.from_numpy(res[0]), torch.from_numpy(res[1])  # [update, (params, target, m, v), n]
+    r0, r1 = torch.from_numpy(res[0]), torch.from_numpy(res[1])  # [update, (params, target, m, v, grad), n]
     # replicas are identical from the start (rank 0's init) and stay identical
     assert torch.equal(r0, r1)
     dev = torch.device("cuda", 0)
@@ -109,5 +110,20 @@ def test_dp_two_ranks_equal_full_batch_learner():
         full._pack_targets()
         full.train(batch, 0, u, per_weight=w)
         torch.cuda.synchronize()
+        gerr = normwise(r0[u + 1, 4], (full.grad[:-1] / full.grad[-1]).cpu())
         err = normwise(r0[u + 1, 0], full.params.cpu())
+        print(f"update {u} from the replicas' state: grad {gerr:.2e}, params {err:.2e}")
+        assert gerr < 1e-6, (u, gerr)
         assert err < 1e-6, (u, err)
+    # ... and the two trajectories run freely: they separate only by summation
+    # order, plus at most an O(1) move of one FFN unit's gradient once a ReLU tie
+    # flips (the third update: 4.6e-5 on the parameters, tools/diag_dp_adam.py
+    # names the pre-activation, profiles/r5_dp/diag_dp.log); a systematic DP error
+    # (Σ mask or Adam state handled per rank) moves every parameter by ~lr
+    free = _learner(100, dev)
+    for u in range(UPDATES):
+        free.train(batch, 0, u, per_weight=w)
+        torch.cuda.synchronize()
+        err = normwise(r0[u + 1, 0], free.params.cpu())
+        print(f"update {u} free-running: params {err:.2e}")
+        assert err < 1e-4, (u, err)

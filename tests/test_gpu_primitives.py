@@ -34,3 +34,53 @@ def test_lane_primitives():
     assert torch.equal(out[6:13], out[13:20])
     b = torch.stack([x.cpu()[(torch.arange(64) + 9 * k) % 64] * (k + 1) for k in range(7)])
     torch.testing.assert_close(out[6:13], b.view(7, 4, 16).sum(1).repeat(1, 4), rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("beta", [1.0, 0.5, 2.0])
+def test_softplus_head_elementwise(beta):
+    """The mixing head's softplus (n_transf_mixer.py:96-97, torch's Softplus with
+    threshold 20) element by element over x·β in [-20, 20] and past the threshold,
+    against the fp64 value: relative error <= 2e-6 for the value and the derivative
+    (v_exp_f32 of x·β·log2e rounds its argument: ~7e-7 relative at |x·β| = 20; the
+    Goldberg-form log1p adds ~2 ulp — plain log(1 + e) was 6e-5 near x·β = -7),
+    for posf, dposf and the fused pair the BPTT kernels call."""
+    require_gpu()
+    from t2omca_amd._lib import POS_FUNCS, check, lib, ptr, stream_ptr
+    xb = torch.cat([torch.linspace(-20.0, 20.0, 40001, dtype=torch.float64),
+                    torch.tensor([-19.999, -7.0, -6.93, -1e-3, 0.0, 1e-3, 19.999, 20.5, 25.0], dtype=torch.float64)])
+    x = (xb / beta).float()
+    out = torch.full((4 * x.numel(),), float("nan"), device="cuda")
+    check(lib().t2o_probe_posf(ptr(x.cuda()), x.numel(), POS_FUNCS["softplus"], beta, ptr(out), stream_ptr()),
+          "probe_posf")
+    torch.cuda.synchronize()
+    p, d, p2, d2 = out.cpu().double().view(4, -1)
+    xd = x.double()
+    z = xd * beta
+    ref_p = torch.where(z > 20, xd, torch.log1p(torch.exp(z)) / beta)
+    ref_d = torch.where(z > 20, torch.ones_like(xd), torch.sigmoid(z))
+    for name, got, ref in (("posf", p, ref_p), ("dposf", d, ref_d), ("posd.p", p2, ref_p), ("posd.d", d2, ref_d)):
+        rel = ((got - ref).abs() / ref.abs()).max().item()
+        print(f"beta {beta} {name}: max relative error {rel:.2e}")
+        assert rel <= 2e-6, (name, rel)
+
+
+@pytest.mark.parametrize("name", ["abs", "quadratic", "identity"])
+def test_other_heads_elementwise(name):
+    """abs / quadratic / identity heads (n_transf_mixer.py:98-103) and their derivatives: exact."""
+    require_gpu()
+    from t2omca_amd._lib import POS_FUNCS, check, lib, ptr, stream_ptr
+    x = torch.randn(4096, generator=torch.Generator().manual_seed(1))
+    x[:3] = torch.tensor([0.0, -0.0, 1e-30])
+    out = torch.full((4 * x.numel(),), float("nan"), device="cuda")
+    check(lib().t2o_probe_posf(ptr(x.cuda()), x.numel(), POS_FUNCS.get(name, 3), 1.0, ptr(out), stream_ptr()),
+          "probe_posf")
+    torch.cuda.synchronize()
+    p, d, p2, d2 = out.cpu().view(4, -1)
+    if name == "abs":
+        ref_p, ref_d = x.abs(), torch.sign(x)
+    elif name == "quadratic":
+        ref_p, ref_d = 0.5 * x * x, x
+    else:
+        ref_p, ref_d = x, torch.ones_like(x)
+    assert torch.equal(p, ref_p) and torch.equal(p2, ref_p)
+    assert torch.equal(d, ref_d) and torch.equal(d2, ref_d)

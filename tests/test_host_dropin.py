@@ -74,3 +74,20 @@ def test_mixer_shape_options():
     assert (s.n_ent, s.agents) == (6, 4)
     s = TransformerMixer(_args(env_args={"state_entity_mode": False}, state_entity_feats=9)).shape
     assert (s.n_ent, s.agents, s.F) == (16, 4, 9)  # obs branch: n_agents * n_entities tokens
+
+
+def test_learner_rejects_bad_options_before_any_device_work():
+    """TDLearner validates precision / contract / td_algo up front (a bad td_algo used
+    to surface as a KeyError inside the first train())."""
+    import pytest
+    from t2omca_amd.learner import TDLearner
+    from t2omca_amd.modules import TransformerAgent, TransformerMixer
+    from t2omca_amd.synthetic import make_args
+    args = make_args(3)
+    agent, mixer = TransformerAgent(None, args), TransformerMixer(args)
+    for kw, msg in (({"td_algo": "scan"}, "td_algo"), ({"contract": "both"}, "contract"),
+                    ({"precision": "fp16"}, "precision")):
+        with pytest.raises(ValueError, match=msg):
+            TDLearner(agent, mixer, **kw)
+    with pytest.raises(RuntimeError, match="HIP device"):  # valid options, CPU modules: no fallback
+        TDLearner(agent, mixer, td_algo="wave")
