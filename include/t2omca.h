@@ -46,7 +46,7 @@ extern "C" {
  * library (tuned one-tile mixers write one compact tape stream per block,
  * ceil(B*T*(A+3)/16) tiles; records of 4E + 2HE features); 4 = t2o_td_loss_ex2,
  * t2o_bwd_tape_contract_pair, t2o_abi_version. */
-#define T2O_ABI_VERSION 4
+#define T2O_ABI_VERSION 5
 int t2o_abi_version(void);
 
 enum {
@@ -201,7 +201,8 @@ int t2o_agent_bwd_tape_format(const t2o_layout* L, int has_hmid);
  * strides av_sb, av_st; NULL = all available), ties -> lowest index.
  * Outputs per network: y[B][T], hw[B][T][3][E] (hyper tokens after step t),
  * qvo[B][T][A] (qvals used, may be NULL), xout[B][T][A+3][E] (final query
- * rows, may be NULL; required by the backward), xmid[B][T][D-1][A+3][E]
+ * rows, may be NULL; required by the backward, and by a decoupled multi-tile
+ * mixer for every network: t2o_mixer_split), xmid[B][T][D-1][A+3][E]
  * (inputs of blocks 1..D-1, may be NULL; lets the backward skip recomputing
  * them). */
 int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, const float* pack_tg,
@@ -230,6 +231,28 @@ int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, const float* st
                          float* ghid, float* ghw0, float* gslabs, int max_slabs, int* nslab, void* tape,
                          int B, int T, void* stream);
 int t2o_mixer_bwd_max_slabs(int B);
+
+/* The same with a workspace: work (work_floats floats, caller-owned,
+ * t2o_mixer_bwd_work_floats(L, B, T) of them; NULL / short = none) lets a
+ * multi-tile mixer (A + 3 > 16 query rows) at a small replay batch run its
+ * recurrence decoupled from the rest (t2o_mixer_split.hip: the window of the
+ * last 16 query rows carries the hyper tokens' recurrence, every (episode,
+ * step)'s other rows run in parallel).  Same outputs; the key-gradient sums run
+ * in another order.  Replaces the reference's per-timestep mixer backward
+ * through autograd (n_transf_mixer.py:55-91 driven by per_run.py:224). */
+int t2o_mixer_unroll_bwd_ex(const t2o_layout* L, const float* pack, const float* states,
+                            int64_t st_sb, int64_t st_st, const float* hid, int64_t hid_sb,
+                            int64_t hid_st, const float* hw0, const float* qv, const float* hw,
+                            const float* xout, const float* xmid, const float* gy, const float* ghw_ext,
+                            float* gqv, float* ghid, float* ghw0, float* gslabs, int max_slabs, int* nslab,
+                            void* tape, float* work, int64_t work_floats, int B, int T, void* stream);
+/* Workspace floats t2o_mixer_unroll_bwd_ex can use for this layout and batch
+ * (0: the layout has one query tile, nothing to decouple; -1 bad argument). */
+int64_t t2o_mixer_bwd_work_floats(const t2o_layout* L, int B, int T);
+/* 1 when a mixer of this layout runs decoupled at batch B (forward: when every
+ * network's xout is given; backward: with the workspace), else 0.
+ * T2O_MIXER_SPLIT=0 / 1 in the environment forces it off / on. */
+int t2o_mixer_split(const t2o_layout* L, int B);
 
 /* Tiles of 16 weight-gradient records per block that one backward call writes
  * (agent: T * ceil(B*A/16); mixer, A = L->n_agents: B*T*ceil((A+3)/16), or for

@@ -11,7 +11,7 @@ import torch
 from .build import LIB
 
 MAX_DEPTH = 4
-ABI_VERSION = 4  # include/t2omca.h T2O_ABI_VERSION this binding mirrors
+ABI_VERSION = 5  # include/t2omca.h T2O_ABI_VERSION this binding mirrors
 _I64x = ctypes.c_int64 * MAX_DEPTH
 
 
@@ -64,6 +64,13 @@ EXPORTS = {
                              [ctypes.c_int64] * 2 + [ctypes.c_void_p] + [ctypes.c_int64] * 2 +
                              [ctypes.c_void_p] * 11 + [ctypes.c_int, ctypes.POINTER(ctypes.c_int)] +
                              [ctypes.c_void_p] + [ctypes.c_int] * 2 + [ctypes.c_void_p]),
+    "t2o_mixer_unroll_bwd_ex": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_void_p] * 2 +
+                                [ctypes.c_int64] * 2 + [ctypes.c_void_p] + [ctypes.c_int64] * 2 +
+                                [ctypes.c_void_p] * 11 + [ctypes.c_int, ctypes.POINTER(ctypes.c_int)] +
+                                [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64] + [ctypes.c_int] * 2 +
+                                [ctypes.c_void_p]),
+    "t2o_mixer_bwd_work_floats": (ctypes.c_int64, [ctypes.POINTER(Layout), ctypes.c_int, ctypes.c_int]),
+    "t2o_mixer_split": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_int]),
     "t2o_mixer_bwd_max_slabs": (ctypes.c_int, [ctypes.c_int]),
     "t2o_bwd_tape_floats": (ctypes.c_int64, [ctypes.POINTER(Layout), ctypes.c_int64]),
     "t2o_bwd_tape_tiles": (ctypes.c_int64, [ctypes.POINTER(Layout), ctypes.c_int, ctypes.c_int, ctypes.c_int]),

@@ -296,11 +296,13 @@ class TDLearner:
         # 4. mixer BPTT (its weight-grad tape is contracted after the agent BPTT)
         tape_m = self._slab("tape_m", ops.tape_floats(self.sm, ops.mixer_tape_tiles(B, T, A, self.sm)))
         tape_a = self._slab("tape_a", ops.tape_floats(self.sa, ops.agent_tape_tiles(B, T, A)))
-        slabs_m = self._slab("m", int(ops.lib().t2o_mixer_bwd_max_slabs(B)) * self.sm.layout().grad_total)
+        slabs_m = self._slab("m", ops.mixer_slab_count(B) * self.sm.layout().grad_total)
+        nwork = ops.mixer_work_floats(self.sm, B, T)
+        work_m = self._slab("work_m", nwork) if nwork else None
         contract_m, gqv, ghid, _ = ops.mixer_unroll_bwd(self.sm, self.pack_m, state, h_on, o_on, td["gq"],
                                                         slabs=slabs_m, timer=self.timer, tape=tape_m,
-                                                        defer_contract=True)
-        slabs_a = self._slab("a", int(ops.lib().t2o_agent_bwd_max_slabs(B, A)) * self.sa.layout().grad_total)
+                                                        defer_contract=True, work=work_m)
+        slabs_a = self._slab("a", ops.agent_slab_count(B, A) * self.sa.layout().grad_total)
         gh = None if self.detach_mixer_hidden else ghid
         if self.contract == "pair":
             # 5. agent BPTT (grads of the chosen Q and, unless detached, of the hidden

@@ -172,6 +172,35 @@ def _tape(shape, tiles, tape, device):
     return tape
 
 
+# The tape contraction runs one workgroup per slab (split-K over the tape's
+# tiles).  A backward over a small replay batch fills few slabs (the mixer BPTT
+# one per 1-4 episodes, the agent BPTT one per two 16-row tiles: 8 and 16 at
+# configs[0]'s 32 episodes), so its contraction would stream the whole tape
+# through those few workgroups; it gets at least CONTRACT_MIN_WG instead, the
+# extra slabs zeroed first (they receive no BPTT flush; the contraction writes
+# everything else of a slab itself).
+CONTRACT_MIN_WG = 256
+
+
+def mixer_work_floats(shape: NetShape, B, T):
+    """Workspace floats of a decoupled multi-tile mixer backward (0 when it does not
+    run decoupled at this batch: t2o_mixer_split)."""
+    L = shape.layout()
+    if int(lib().t2o_mixer_split(ctypes.byref(L), int(B))) != 1:
+        return 0
+    return max(0, int(lib().t2o_mixer_bwd_work_floats(ctypes.byref(L), int(B), int(T))))
+
+
+def mixer_slab_count(B):
+    """Slabs a mixer backward over B episodes needs (its BPTT's + the widened contraction's)."""
+    return max(int(lib().t2o_mixer_bwd_max_slabs(B)), CONTRACT_MIN_WG)
+
+
+def agent_slab_count(B, A):
+    """Slabs an agent backward over B episodes of A agents needs."""
+    return max(int(lib().t2o_agent_bwd_max_slabs(B, A)), CONTRACT_MIN_WG)
+
+
 class DeferredContraction:
     """A backward call's weight-gradient tape, not yet contracted: call it (on the
     stream that should run the contraction + slab sum) for the compact gradient
@@ -181,7 +210,20 @@ class DeferredContraction:
         self.shape, self.pack, self.tape, self.tiles = shape, pack, tape, tiles
         self.slabs, self.nslab, self.timer, self.tag, self.fmt = slabs, nslab, timer, tag, fmt
 
+    def widen(self):
+        """Raise the contraction's workgroup count to CONTRACT_MIN_WG where the slab
+        buffer holds them (tuned layouts): zero the slabs past the BPTT's on the
+        current stream.  Idempotent."""
+        L = self.shape.layout()
+        cap = self.slabs.numel() // L.grad_total
+        nc = min(max(self.nslab, CONTRACT_MIN_WG), cap)
+        if L.generic or nc <= self.nslab:
+            return
+        self.slabs[self.nslab * L.grad_total:nc * L.grad_total].zero_()
+        self.nslab = nc
+
     def __call__(self):
+        self.widen()
         return tape_contract(self.shape, self.pack, self.tape, self.tiles, self.slabs, self.nslab, self.timer,
                              self.tag, self.fmt)
 
@@ -207,6 +249,7 @@ def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchose
         act_sb, act_st = actions.stride(0), actions.stride(1)
     nmax = int(lib().t2o_agent_bwd_max_slabs(B, A))
     if slabs is None or slabs.numel() < nmax * L.grad_total:
+        nmax = agent_slab_count(B, A)
         slabs = torch.empty(nmax * L.grad_total, device=obs.device)
     gh0 = torch.empty(B, A, shape.E, device=obs.device) if want_gh0 else None
     tiles = agent_tape_tiles(B, T, A)
@@ -262,11 +305,16 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
                     xout=torch.empty(B, T, A + 3, E, device=dev) if bwd else None,
                     xmid=torch.empty(B, T, shape.D - 1, A + 3, E, device=dev) if (bwd and shape.D > 1) else None)
 
-    o_on = outs(T_on, want_xout)
+    # a multi-tile mixer at a small batch runs decoupled (t2o_mixer_split.hip): its
+    # parallel kernel reads the recurrent kernel's window rows back from xout
+    split = bool(lib().t2o_mixer_split(ctypes.byref(L), B) == 1)
+    o_on = outs(T_on, want_xout or split)
     o_tg = None
     if pack_tg is not None:
         T_tg = T_tg or hid_tg.shape[1]
         o_tg = outs(T_tg, False)
+        if split:
+            o_tg["xout"] = torch.empty(B, T_tg, A + 3, E, device=dev)
     n_actions = q_on.shape[3] if q_on is not None else 0
     act_sb, act_st = _mstrides(actions)
     av_sb, av_st = _mstrides(avail)
@@ -303,6 +351,8 @@ def tape_contract_pair(dm: DeferredContraction, da: DeferredContraction, timer=N
     """Both backwards' tape contractions in one launch (t2o_bwd_tape_contract_pair;
     dm the mixer's, da the agent's), then each slab sum.  Returns (gpack_m, gpack_a)."""
     Lm, La = dm.shape.layout(), da.shape.layout()
+    dm.widen()
+    da.widen()
     _mark(timer, "begin:dw_pair")
     check(lib().t2o_bwd_tape_contract_pair(ctypes.byref(Lm), ptr(dm.pack), ptr(dm.tape), int(dm.tiles), ptr(dm.slabs),
                                            int(dm.nslab), ctypes.byref(La), ptr(da.pack), ptr(da.tape), int(da.tiles),
@@ -318,12 +368,13 @@ def tape_contract_pair(dm: DeferredContraction, da: DeferredContraction, timer=N
 
 
 def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_ext=None,
-                     want_ghw0=False, slabs=None, timer=None, tape=None, defer_contract=False):
+                     want_ghw0=False, slabs=None, timer=None, tape=None, defer_contract=False, work=None):
     """BPTT of mixer_unroll_fwd (one network, `fwd` = its output dict).
     Returns (gpack, gqv [B,T,A], ghid [B,T,A,E], ghw0 or None).  With
     defer_contract the first item is instead a zero-argument callable that runs
     the tape contraction + slab sum (on whatever stream is current when called)
-    and returns gpack."""
+    and returns gpack.  work: optional float buffer for the decoupled multi-tile
+    mixer (t2o_mixer_bwd_work_floats; allocated here when needed and not given)."""
     _dev(pack, states, hid, gy, hw0, ghw_ext)
     B, T = gy.shape
     A, E = hid.shape[2], shape.E
@@ -334,6 +385,7 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
     assert gy.is_contiguous() and fwd["xout"] is not None
     nmax = int(lib().t2o_mixer_bwd_max_slabs(B))
     if slabs is None or slabs.numel() < nmax * L.grad_total:
+        nmax = mixer_slab_count(B)
         slabs = torch.empty(nmax * L.grad_total, device=dev)
     gqv = torch.empty(B, T, A, device=dev)
     ghid = torch.empty(B, T, A, E, device=dev)
@@ -341,12 +393,15 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
     tiles = mixer_tape_tiles(B, T, A, shape)
     tape = _tape(shape, tiles, tape, dev)
     nslab = ctypes.c_int(0)
+    nwork = mixer_work_floats(shape, B, T)
+    if nwork and (work is None or work.numel() < nwork):
+        work = torch.empty(nwork, device=dev)
     _mark(timer, "begin:mixer_bwd")
-    check(lib().t2o_mixer_unroll_bwd(
+    check(lib().t2o_mixer_unroll_bwd_ex(
         ctypes.byref(L), ptr(pack), ptr(states), states.stride(0), states.stride(1), ptr(hid),
         hid.stride(0), hid.stride(1), ptr(hw0), ptr(fwd["qv"]), ptr(fwd["hw"]), ptr(fwd["xout"]),
         ptr(fwd.get("xmid")), ptr(gy), ptr(ghw_ext), ptr(gqv), ptr(ghid), ptr(ghw0), ptr(slabs), nmax, ctypes.byref(nslab),
-        ptr(tape), B, T, stream_ptr()), "mixer_unroll_bwd")
+        ptr(tape), ptr(work) if nwork else None, nwork, B, T, stream_ptr()), "mixer_unroll_bwd")
     _mark(timer, "end:mixer_bwd")
     contract = DeferredContraction(shape, pack, tape, tiles, slabs, nslab.value, timer, "mixer_dw", 0)
     return (contract if defer_contract else contract()), gqv, ghid, ghw0
