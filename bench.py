@@ -135,6 +135,7 @@ class KernelTimer:
 
     def __init__(self):
         self.events = []
+        self.updates = 0  # instrumented updates (a pipelined update times each step range of a kernel)
 
     def __call__(self, name):
         ev = torch.cuda.Event(enable_timing=True)
@@ -675,6 +676,11 @@ def dropin_bench(args, world, rank, dev):
         print(json.dumps(out), flush=True)
 
 
+def mixer_decoupled(learner, B):
+    from t2omca_amd import ops
+    return int(ops.lib().t2o_mixer_split(ops.ctypes.byref(learner.sm.layout()), int(B))) == 1
+
+
 def dist_info(world, rank_seconds, steps):
     """What the process group itself reports (so a SCALE line shows that RCCL saw N
     ranks, not only what WORLD_SIZE said) and every rank's ms per step."""
@@ -767,9 +773,11 @@ def main():
         margs = make_args(A, device=str(dev), qmix_pos_func=args.qmix_pos_func)
         agent = TransformerAgent(None, margs).to(dev)
         mixer = TransformerMixer(margs).to(dev)
+        pipe = {"0": False, "1": True}.get(os.environ.get("T2O_PIPELINE", "auto"), "auto")
         return TDLearner(agent, mixer, target_update_interval=10 ** 9, precision=precision,
                          overlap=not args.serial, priorities_to_cpu=args.priorities == "cpu",
-                         td_algo=args.td_algo, contract=args.contract)
+                         td_algo=args.td_algo, contract=args.contract, pipeline=pipe,
+                         pipeline_ranges=int(os.environ.get("T2O_PIPELINE_RANGES", "10")))
 
     learner = make_learner(args.dtype)
     batch, w = make_batch(B, T, A, seed=1 + rank, device=dev)
@@ -817,6 +825,8 @@ def main():
         t0 = time.perf_counter()
         for i in range(args.steps):
             learner.timer = timer if every > 0 and i % every == 0 else None
+            if learner.timer is not None:
+                timer.updates += 1
             step(i)
         torch.cuda.synchronize()
         if world > 1:
@@ -857,7 +867,9 @@ def main():
         return
     transitions = world * B * T * A * args.steps
     value = transitions / elapsed
-    kern = {k: sum(v) / len(v) for k, v in timer.durations().items()}
+    # per update: a pipelined update (TDLearner._pipelined) runs each recurrence in
+    # step ranges on two streams, so its kernels' sums overlap in time
+    kern = {k: sum(v) / max(1, timer.updates) for k, v in timer.durations().items()}
     flops = td_update_flops(B, T, A)
     ref_flops = ref_order_kernel_flops(B, T, A)
     bytes_ = td_update_bytes(B, T, A, elem=2 if args.dtype == "bf16" else 4)
@@ -889,7 +901,11 @@ def main():
                                f"batch {B} episodes/GPU x T={T}",
                    "global_batch": B * world, "seq_len": T, "agents": A, "emb": 32, "heads": 3, "depth": 2,
                    "parallelism": f"dp{world}", "priorities": args.priorities, "kernels": kernels,
-                   "mixer_head": args.qmix_pos_func},
+                   "mixer_head": args.qmix_pos_func,
+                   # small batches: the multi-tile mixer's recurrence decoupled from its other
+                   # rows (t2o_mixer_split) and the two networks' recurrences in step ranges
+                   # on two streams (TDLearner._pipelined)
+                   "mixer_decoupled": mixer_decoupled(learner, B), "pipelined": learner._pipelined(B)},
         "roofline": {"bound": "mfma", "kernel": dom, "achieved": achieved, "peak": peak_tf,
                      "unit": "TFLOP/s", "frac": achieved / peak_tf, "traffic": traffic_for(dom, workload_tag(args)),
                      "basis": "SURVEY.md §8(d) reference-order necessary FLOPs of the kernel's share "

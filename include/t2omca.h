@@ -183,6 +183,28 @@ int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack,
                          float* gslabs, int max_slabs, int* nslab, void* tape, float* gh0,
                          int B, int T, int A, void* stream);
 int t2o_agent_bwd_max_slabs(int B, int A);
+
+/* Step ranges of the two unrolls, for running the agent and mixer recurrences
+ * of one TD update side by side on two streams (the learner's pipelined mode at
+ * small replay batches).  Forward: steps [t0, t1) of T; t0 > 0 continues from
+ * h_on / h_tg at step t0 - 1 (what the range before wrote); outputs indexed by
+ * the full T.  Backward (the pipelined BPTT: depth 2, hmid given; else
+ * T2O_EUNSUPPORTED for a partial range): steps t_hi - 1 .. t_lo; ranges run from
+ * the last one down on the same slabs (the first, t_hi = T, clears them) and
+ * tape; gcarry [B*A][E] carries dL/dh between ranges (read at t_hi < T, written
+ * at t_lo > 0; gh0 gets it at t_lo = 0). */
+int t2o_agent_unroll_fwd_range(const t2o_layout* L, const float* pack_on, const float* pack_tg,
+                               const float* obs, int64_t obs_sb, int64_t obs_st,
+                               const float* h0_on, const float* h0_tg,
+                               float* q_on, float* h_on, float* hmid_on, float* q_tg, float* h_tg, float* hmid_tg,
+                               int B, int T, int A, int t0, int t1, void* stream);
+int t2o_agent_unroll_bwd_range(const t2o_layout* L, const float* pack,
+                               const float* obs, int64_t obs_sb, int64_t obs_st,
+                               const float* h0, const float* h_seq, const float* hmid, int h_ts,
+                               const float* gq, const float* gchosen, const int64_t* actions,
+                               int64_t act_sb, int64_t act_st, const float* gh,
+                               float* gslabs, int max_slabs, int* nslab, void* tape, float* gh0, float* gcarry,
+                               int B, int T, int A, int t_lo, int t_hi, void* stream);
 /* The record format t2o_agent_unroll_bwd writes to its tape for this layout
  * (has_hmid: the call passes hmid): 0 the full record; 1 (bf16, the pipelined
  * kernel, up to 8 entities) the lean record — dM and dN were accumulated in
@@ -246,6 +268,33 @@ int t2o_mixer_unroll_bwd_ex(const t2o_layout* L, const float* pack, const float*
                             const float* xout, const float* xmid, const float* gy, const float* ghw_ext,
                             float* gqv, float* ghid, float* ghw0, float* gslabs, int max_slabs, int* nslab,
                             void* tape, float* work, int64_t work_floats, int B, int T, void* stream);
+/* The decoupled mixer's phases, for running them beside the agent's step
+ * ranges on another stream (ranges as t2o_agent_unroll_fwd_range's).  Forward:
+ * phase 1 = the recurrence over steps [t0, t1) (the window's rows, hw, the
+ * window's xout / xmid), every range in order; then phase 2 = every (episode,
+ * step)'s other rows and the mixing head (y, qvo, the rest of xout / xmid).
+ * Backward: phase 1 = every (episode, step)'s parallel part; then phase 2 = the
+ * recurrence over steps t_hi - 1 .. t_lo, ranges from the last down, ghw_carry
+ * [B][3][E] carrying the hyper grads between them; *nslab is the same for every
+ * call.  T2O_EUNSUPPORTED when the layout / batch does not run decoupled
+ * (t2o_mixer_split). */
+int t2o_mixer_unroll_fwd_split(const t2o_layout* L, const float* pack_on, const float* pack_tg,
+                               const float* states, int64_t st_sb, int64_t st_st,
+                               const float* hid_on, const float* hid_tg, int64_t hid_sb, int64_t hid_st,
+                               const float* hw0_on, const float* hw0_tg, int qmode_on, int qmode_tg,
+                               const float* qv_on, const float* qv_tg, const float* q_on, const float* q_tg,
+                               int q_ts, int n_actions, const int64_t* actions, int64_t act_sb, int64_t act_st,
+                               const int32_t* avail, int64_t av_sb, int64_t av_st,
+                               float* y_on, float* hw_on, float* qvo_on, float* xout_on, float* xmid_on,
+                               float* y_tg, float* hw_tg, float* qvo_tg, float* xout_tg, float* xmid_tg,
+                               int B, int T_on, int T_tg, int phase, int t0, int t1, void* stream);
+int t2o_mixer_unroll_bwd_split(const t2o_layout* L, const float* pack, const float* states,
+                               int64_t st_sb, int64_t st_st, const float* hid, int64_t hid_sb,
+                               int64_t hid_st, const float* hw0, const float* qv, const float* hw,
+                               const float* xout, const float* xmid, const float* gy, const float* ghw_ext,
+                               float* gqv, float* ghid, float* ghw0, float* gslabs, int max_slabs, int* nslab,
+                               void* tape, float* work, int64_t work_floats, float* ghw_carry, int phase,
+                               int t_lo, int t_hi, int B, int T, void* stream);
 /* Workspace floats t2o_mixer_unroll_bwd_ex can use for this layout and batch
  * (0: the layout has one query tile, nothing to decouple; -1 bad argument). */
 int64_t t2o_mixer_bwd_work_floats(const t2o_layout* L, int B, int T);

@@ -54,6 +54,14 @@ EXPORTS = {
                              [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_void_p, ctypes.c_void_p] +
                              [ctypes.c_int] * 3 + [ctypes.c_void_p]),
     "t2o_agent_bwd_max_slabs": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    "t2o_agent_unroll_fwd_range": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_void_p] * 3 +
+                                   [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 8 + [ctypes.c_int] * 5 +
+                                   [ctypes.c_void_p]),
+    "t2o_agent_unroll_bwd_range": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_void_p] * 2 +
+                                   [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 3 + [ctypes.c_int] +
+                                   [ctypes.c_void_p] * 3 + [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 2 +
+                                   [ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p] + [ctypes.c_int] * 5 + [ctypes.c_void_p]),
     "t2o_mixer_unroll_fwd": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_void_p] * 3 +
                              [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 2 + [ctypes.c_int64] * 2 +
                              [ctypes.c_void_p] * 2 + [ctypes.c_int] * 2 + [ctypes.c_void_p] * 4 +
@@ -69,6 +77,17 @@ EXPORTS = {
                                 [ctypes.c_void_p] * 11 + [ctypes.c_int, ctypes.POINTER(ctypes.c_int)] +
                                 [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64] + [ctypes.c_int] * 2 +
                                 [ctypes.c_void_p]),
+    "t2o_mixer_unroll_fwd_split": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_void_p] * 3 +
+                                   [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 2 + [ctypes.c_int64] * 2 +
+                                   [ctypes.c_void_p] * 2 + [ctypes.c_int] * 2 + [ctypes.c_void_p] * 4 +
+                                   [ctypes.c_int] * 2 + [ctypes.c_void_p] + [ctypes.c_int64] * 2 +
+                                   [ctypes.c_void_p] + [ctypes.c_int64] * 2 + [ctypes.c_void_p] * 10 +
+                                   [ctypes.c_int] * 6 + [ctypes.c_void_p]),
+    "t2o_mixer_unroll_bwd_split": (ctypes.c_int, [ctypes.POINTER(Layout)] + [ctypes.c_void_p] * 2 +
+                                   [ctypes.c_int64] * 2 + [ctypes.c_void_p] + [ctypes.c_int64] * 2 +
+                                   [ctypes.c_void_p] * 11 + [ctypes.c_int, ctypes.POINTER(ctypes.c_int)] +
+                                   [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p] +
+                                   [ctypes.c_int] * 5 + [ctypes.c_void_p]),
     "t2o_mixer_bwd_work_floats": (ctypes.c_int64, [ctypes.POINTER(Layout), ctypes.c_int, ctypes.c_int]),
     "t2o_mixer_split": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_int]),
     "t2o_mixer_bwd_max_slabs": (ctypes.c_int, [ctypes.c_int]),

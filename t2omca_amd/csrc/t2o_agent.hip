@@ -34,6 +34,7 @@ struct AgentFwdArgs {
   const float* obs;
   int64_t obs_sb, obs_st;
   int B, T, A, F;
+  int t0, t1;  // steps [t0, t1) of the T (outputs indexed by the full T; t0 > 0 starts from h[t0 - 1])
   int wlds;  // weights staged in LDS (set by the launcher)
   int rpw;   // rows per wave: 16, or 8 when 16-row tiles would leave SIMDs idle
 };
@@ -89,8 +90,11 @@ void agent_fwd_kernel(AgentFwdArgs args) {
     const int b = row / A, a = row % A;
 
     f4 h[ET];
+    // a range's first step continues from the hidden state the previous range wrote
+    const float* hs = args.t0 > 0 ? net.h + (((size_t)b * args.T + args.t0 - 1) * A + a) * E
+                                  : net.h0 ? net.h0 + (size_t)row * E : nullptr;
 #pragma unroll
-    for (int t = 0; t < ET; ++t) h[t] = net.h0 ? ld4(net.h0 + (size_t)row * E + 16 * t + 4 * g) : zero4();
+    for (int t = 0; t < ET; ++t) h[t] = hs ? ld4(hs + 16 * t + 4 * g) : zero4();
 
     // few entities: the observations live in registers, the next step's loaded
     // while the current one computes; many entities: streamed per block in
@@ -111,14 +115,14 @@ void agent_fwd_kernel(AgentFwdArgs args) {
         }
     };
     f4 on[NO];
-    if constexpr (!CHUNK) load_obs(0, on);
-    for (int step = 0; step < args.T; ++step) {
+    if constexpr (!CHUNK) load_obs(args.t0, on);
+    for (int step = args.t0; step < args.t1; ++step) {
       const Wts<WT> P = step_view(P0);
       f4 o[NO];
       if constexpr (!CHUNK) {
 #pragma unroll
         for (int j = 0; j < NE; ++j) o[j] = on[j];
-        if (step + 1 < args.T) load_obs(step + 1, on);
+        if (step + 1 < args.t1) load_obs(step + 1, on);
       }
       const ObsRow orow{row_obs(step), F, ne, RT && ne % AG_CHUNK != 0};
       f4 x[ET];
@@ -175,7 +179,7 @@ int launch_fwd(const AgentFwdArgs& args, int nnet, hipStream_t stream) {
   size_t lds = sizeof(float) * (size_t)lds_weight_floats<WT>(args.L, args.L.fwd_total);
   a.wlds = lds <= 160 * 1024;
   if (!a.wlds) lds = 0;
-  const bool loop = args.T <= AG_FWD_LOOP_T && a.wlds;
+  const bool loop = args.t1 - args.t0 <= AG_FWD_LOOP_T && a.wlds;
   auto kern = loop ? agent_fwd_kernel<E, H, D, NE, FF, RT, true, true, WT>
               : a.wlds ? agent_fwd_kernel<E, H, D, NE, FF, RT, true, false, WT>
                        : agent_fwd_kernel<E, H, D, NE, FF, RT, false, false, WT>;
@@ -224,6 +228,12 @@ struct AgentBwdArgs {
   float* gh0;
   int B, T, A, F;
   int rpw;  // rows per wave (rows_per_wave)
+  // steps t_hi-1 .. t_lo (pipelined kernel): a range below T starts from the grad
+  // wrt h[t_hi - 1] a previous range left in gcarry [B*A][E]; one above 0 leaves
+  // the grad wrt h[t_lo - 1] there (gh0 gets it at t_lo = 0); only the range
+  // that starts at T - 1 clears the slab regions the flushes add into
+  int t_lo, t_hi;
+  float* gcarry;
 };
 
 constexpr int AG_BWD_WAVES = 2;  // (each wave needs a SIMD's full 512-register file)
@@ -473,7 +483,7 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
   float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
   Wts<WT> P0 = stage_weights(smem, args.pack, L, nw, WT{});
   P0.vol = NE <= 8;  // (Wts::vol: 16+ entities measured slower with volatile reads)
-  zero_flushed_regions(gs, G, ACC);  // (lean record: dM / dN flushed from registers)
+  if (args.t_hi == args.T) zero_flushed_regions(gs, G, ACC);  // (lean record: dM / dN flushed from registers)
   int* const flags = reinterpret_cast<int*>(smem + lds_w + 2 * AGP_TILES * STAGE + AGP_TILES * agp_xch_floats<E>());
   if (threadIdx.x < PAIR_FLAG_FLOATS) flags[threadIdx.x] = 0;
   __syncthreads();
@@ -570,9 +580,10 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
       }
     }
   };
-  load_step(T - 1);
+  const int t_lo = args.t_lo, t_hi = args.t_hi;
+  load_step(t_hi - 1);
   if (d == 0) pb.sync();
-  for (int step = T - 1; step >= 0; --step) {
+  for (int step = t_hi - 1; step >= t_lo; --step) {
 #ifdef T2O_TIMELINE
     T2O_STAMP(2 * (T - 1 - step), 0);
 #endif
@@ -609,8 +620,11 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             if (4 * g + r == act) gq[r] += gc;
-          if (step < T - 1) xget(2, gx);
-          else {
+          if (step < t_hi - 1) xget(2, gx);
+          else if (t_hi < T) {  // the grad wrt h[t_hi - 1] from the range after this one
+#pragma unroll
+            for (int t = 0; t < ET; ++t) gx[t] = ld4(args.gcarry + (size_t)row * E + 16 * t + 4 * g);
+          } else {
 #pragma unroll
             for (int t = 0; t < ET; ++t) gx[t] = zero4();
           }
@@ -656,12 +670,13 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
 #pragma unroll
           for (int t = 0; t < ET; ++t) grec[t] = gx[t] + ghi[t];
           xput(2, grec);
-          if (step == 0 && args.gh0 && valid) {
+          float* const gout = step > 0 ? args.gcarry : args.gh0;
+          if (step == t_lo && gout && valid) {
 #pragma unroll
-            for (int t = 0; t < ET; ++t) st4(args.gh0 + (size_t)row * E + 16 * t + 4 * g, grec[t]);
+            for (int t = 0; t < ET; ++t) st4(gout + (size_t)row * E + 16 * t + 4 * g, grec[t]);
           }
         }
-        if (step > 0) load_step(step - 1);
+        if (step > t_lo) load_step(step - 1);
       }
       T2O_MARK(3);
 #ifdef T2O_TIMELINE
@@ -735,6 +750,7 @@ int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream
       return (int)hipGetLastError();
     }
   }
+  if (args.t_lo != 0 || args.t_hi != args.T) return T2O_EUNSUPPORTED;  // (step ranges: the pipelined kernel)
   const int64_t nw = args.L.fwd_total;
   const size_t lds =
       sizeof(float) * ((size_t)(lds_weight_floats<WT>(args.L, nw) + 15) / 16 * 16 + AG_BWD_WAVES * StageDims<1>::FLOATS);
@@ -752,12 +768,23 @@ extern "C" int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, c
                                     const float* obs, int64_t obs_sb, int64_t obs_st, const float* h0_on,
                                     const float* h0_tg, float* q_on, float* h_on, float* hmid_on, float* q_tg,
                                     float* h_tg, float* hmid_tg, int B, int T, int A, void* stream) {
+  return t2o_agent_unroll_fwd_range(L, pack_on, pack_tg, obs, obs_sb, obs_st, h0_on, h0_tg, q_on, h_on, hmid_on,
+                                    q_tg, h_tg, hmid_tg, B, T, A, 0, T, stream);
+}
+
+extern "C" int t2o_agent_unroll_fwd_range(const t2o_layout* L, const float* pack_on, const float* pack_tg,
+                                          const float* obs, int64_t obs_sb, int64_t obs_st, const float* h0_on,
+                                          const float* h0_tg, float* q_on, float* h_on, float* hmid_on,
+                                          float* q_tg, float* h_tg, float* hmid_tg, int B, int T, int A, int t0,
+                                          int t1, void* stream) {
   if (!L || L->kind != 0 || !pack_on || !obs || !q_on || !h_on || B < 1 || T < 1 || A < 1 ||
-      (!L->generic && L->n_ent != A))
+      (!L->generic && L->n_ent != A) || t0 < 0 || t1 > T || t0 >= t1)
     return T2O_EINVAL;
-  if (L->generic)
+  if (L->generic) {
+    if (t0 != 0 || t1 != T) return T2O_EUNSUPPORTED;
     return gen_agent_unroll_fwd(L, pack_on, pack_tg, obs, obs_sb, obs_st, h0_on, h0_tg, q_on, h_on, hmid_on, q_tg,
                                 h_tg, hmid_tg, B, T, A, (hipStream_t)stream);
+  }
   AgentFwdArgs args{};
   args.L = *L;
   args.net[0] = AgentNet{pack_on, h0_on, q_on, h_on, hmid_on};
@@ -774,6 +801,8 @@ extern "C" int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, c
   args.T = T;
   args.A = A;
   args.F = L->F;
+  args.t0 = t0;
+  args.t1 = t1;
   int rc = T2O_EUNSUPPORTED;
   T2O_DISPATCH_AGENT(L->E, L->H, L->D, L->n_ent, L->FF,
                      rc = (L->prec ? launch_fwd<E_, H_, D_, NE_, FF_, RT_, __bf16>(args, nnet, (hipStream_t)stream)
@@ -787,9 +816,21 @@ extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, cons
                                     int64_t act_sb, int64_t act_st, const float* gh, float* gslabs,
                                     int max_slabs, int* nslab, void* tape, float* gh0, int B, int T, int A,
                                     void* stream) {
+  return t2o_agent_unroll_bwd_range(L, pack, obs, obs_sb, obs_st, h0, h_seq, hmid, h_ts, gq, gchosen, actions, act_sb,
+                                    act_st, gh, gslabs, max_slabs, nslab, tape, gh0, nullptr, B, T, A, 0, T, stream);
+}
+
+extern "C" int t2o_agent_unroll_bwd_range(const t2o_layout* L, const float* pack, const float* obs, int64_t obs_sb,
+                                          int64_t obs_st, const float* h0, const float* h_seq, const float* hmid,
+                                          int h_ts, const float* gq, const float* gchosen, const int64_t* actions,
+                                          int64_t act_sb, int64_t act_st, const float* gh, float* gslabs,
+                                          int max_slabs, int* nslab, void* tape, float* gh0, float* gcarry, int B,
+                                          int T, int A, int t_lo, int t_hi, void* stream) {
   if (!L || L->kind != 0 || !pack || !obs || !h_seq || !gslabs || !nslab || !tape || B < 1 || T < 1 || A < 1 ||
-      (!L->generic && L->n_ent != A) || h_ts < T || (gchosen && !actions))
+      (!L->generic && L->n_ent != A) || h_ts < T || (gchosen && !actions) || t_lo < 0 || t_hi > T ||
+      t_lo >= t_hi || ((t_lo > 0 || t_hi < T) && !gcarry))
     return T2O_EINVAL;
+  if (L->generic && (t_lo != 0 || t_hi != T)) return T2O_EUNSUPPORTED;
   if (L->generic)
     return gen_agent_unroll_bwd(L, pack, obs, obs_sb, obs_st, h0, h_seq, hmid, h_ts, gq, gchosen, actions, act_sb,
                                 act_st, gh, gslabs, max_slabs, nslab, tape, gh0, B, T, A, (hipStream_t)stream);
@@ -817,6 +858,9 @@ extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, cons
   args.T = T;
   args.A = A;
   args.F = L->F;
+  args.t_lo = t_lo;
+  args.t_hi = t_hi;
+  args.gcarry = gcarry;
   int rc = T2O_EUNSUPPORTED;
   T2O_DISPATCH_AGENT(L->E, L->H, L->D, L->n_ent, L->FF,
                      rc = (L->prec ? launch_bwd<E_, H_, D_, NE_, FF_, RT_, __bf16>(args, max_slabs, nslab, (hipStream_t)stream)

@@ -888,19 +888,20 @@ int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t 
 // diagnostic builds only (-DT2O_PHASE_PROF, tools/phase_prof.py)
 T2O_PROF_READER(t2o_prof_read_mixer)
 
-extern "C" int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, const float* pack_tg,
-                                    const float* states, int64_t st_sb, int64_t st_st,
-                                    const float* hid_on, const float* hid_tg, int64_t hid_sb, int64_t hid_st,
-                                    const float* hw0_on, const float* hw0_tg, int qmode_on, int qmode_tg,
-                                    const float* qv_on, const float* qv_tg, const float* q_on,
-                                    const float* q_tg, int q_ts, int n_actions, const int64_t* actions,
-                                    int64_t act_sb, int64_t act_st, const int32_t* avail, int64_t av_sb,
-                                    int64_t av_st, float* y_on, float* hw_on, float* qvo_on, float* xout_on,
-                                    float* xmid_on, float* y_tg, float* hw_tg, float* qvo_tg, float* xout_tg,
-                                    float* xmid_tg, int B, int T_on, int T_tg, void* stream) {
+static int mixer_fwd_impl(const t2o_layout* L, const float* pack_on, const float* pack_tg,
+                          const float* states, int64_t st_sb, int64_t st_st,
+                          const float* hid_on, const float* hid_tg, int64_t hid_sb, int64_t hid_st,
+                          const float* hw0_on, const float* hw0_tg, int qmode_on, int qmode_tg,
+                          const float* qv_on, const float* qv_tg, const float* q_on,
+                          const float* q_tg, int q_ts, int n_actions, const int64_t* actions,
+                          int64_t act_sb, int64_t act_st, const int32_t* avail, int64_t av_sb,
+                          int64_t av_st, float* y_on, float* hw_on, float* qvo_on, float* xout_on,
+                          float* xmid_on, float* y_tg, float* hw_tg, float* qvo_tg, float* xout_tg,
+                          float* xmid_tg, int B, int T_on, int T_tg, int phase, int t0, int t1, void* stream) {
   if (!L || L->kind != 1 || !pack_on || !states || !hid_on || !y_on || !hw_on || B < 1 || T_on < 1 ||
       L->E > 64)
     return T2O_EINVAL;
+  if (phase && (L->generic || !t2o::mixer_split_taken(*L, B))) return T2O_EUNSUPPORTED;
   if (L->generic) {
     auto ok = [&](int mode, const float* qv, const float* qsel) {
       return mode == 0 ? qv != nullptr : mode == 1 ? (qsel && actions) : mode == 2 ? (qsel && q_on) : false;
@@ -948,12 +949,49 @@ extern "C" int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, c
     nnet = 2;
   }
   // multi-tile mixers at a small batch: the recurrence decoupled (t2o_mixer_split.hip)
-  if (const int r = t2o::mixer_split_fwd(a, nnet, (hipStream_t)stream); r != 1) return r;
+  a.t0 = phase == 1 ? t0 : 0;
+  a.t1 = phase == 1 ? t1 : 0;
+  if (const int r = t2o::mixer_split_fwd(a, nnet, (hipStream_t)stream, phase); r != 1) return r;
+  if (phase) return T2O_EUNSUPPORTED;
   int rc = T2O_EUNSUPPORTED;
   T2O_DISPATCH_MIXER(L->E, L->H, L->D, L->n_ent, L->FF, L->pos_func == T2O_POS_ABS,
                      rc = (L->prec ? launch_mixer_fwd<E_, H_, D_, NE_, FF_, RTM_, __bf16>(a, nnet, (hipStream_t)stream)
                                    : launch_mixer_fwd<E_, H_, D_, NE_, FF_, RTM_, float>(a, nnet, (hipStream_t)stream)));
   return rc;
+}
+
+extern "C" int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, const float* pack_tg,
+                                    const float* states, int64_t st_sb, int64_t st_st,
+                                    const float* hid_on, const float* hid_tg, int64_t hid_sb, int64_t hid_st,
+                                    const float* hw0_on, const float* hw0_tg, int qmode_on, int qmode_tg,
+                                    const float* qv_on, const float* qv_tg, const float* q_on,
+                                    const float* q_tg, int q_ts, int n_actions, const int64_t* actions,
+                                    int64_t act_sb, int64_t act_st, const int32_t* avail, int64_t av_sb,
+                                    int64_t av_st, float* y_on, float* hw_on, float* qvo_on, float* xout_on,
+                                    float* xmid_on, float* y_tg, float* hw_tg, float* qvo_tg, float* xout_tg,
+                                    float* xmid_tg, int B, int T_on, int T_tg, void* stream) {
+  return mixer_fwd_impl(L, pack_on, pack_tg, states, st_sb, st_st, hid_on, hid_tg, hid_sb, hid_st, hw0_on, hw0_tg,
+                        qmode_on, qmode_tg, qv_on, qv_tg, q_on, q_tg, q_ts, n_actions, actions, act_sb, act_st,
+                        avail, av_sb, av_st, y_on, hw_on, qvo_on, xout_on, xmid_on, y_tg, hw_tg, qvo_tg, xout_tg,
+                        xmid_tg, B, T_on, T_tg, 0, 0, 0, stream);
+}
+
+extern "C" int t2o_mixer_unroll_fwd_split(const t2o_layout* L, const float* pack_on, const float* pack_tg,
+                                          const float* states, int64_t st_sb, int64_t st_st,
+                                          const float* hid_on, const float* hid_tg, int64_t hid_sb, int64_t hid_st,
+                                          const float* hw0_on, const float* hw0_tg, int qmode_on, int qmode_tg,
+                                          const float* qv_on, const float* qv_tg, const float* q_on,
+                                          const float* q_tg, int q_ts, int n_actions, const int64_t* actions,
+                                          int64_t act_sb, int64_t act_st, const int32_t* avail, int64_t av_sb,
+                                          int64_t av_st, float* y_on, float* hw_on, float* qvo_on, float* xout_on,
+                                          float* xmid_on, float* y_tg, float* hw_tg, float* qvo_tg, float* xout_tg,
+                                          float* xmid_tg, int B, int T_on, int T_tg, int phase, int t0, int t1,
+                                          void* stream) {
+  if (phase < 1 || phase > 2 || (phase == 1 && (t0 < 0 || t0 >= t1))) return T2O_EINVAL;
+  return mixer_fwd_impl(L, pack_on, pack_tg, states, st_sb, st_st, hid_on, hid_tg, hid_sb, hid_st, hw0_on, hw0_tg,
+                        qmode_on, qmode_tg, qv_on, qv_tg, q_on, q_tg, q_ts, n_actions, actions, act_sb, act_st,
+                        avail, av_sb, av_st, y_on, hw_on, qvo_on, xout_on, xmid_on, y_tg, hw_tg, qvo_tg, xout_tg,
+                        xmid_tg, B, T_on, T_tg, phase, t0, t1, stream);
 }
 
 // worst case: 1 episode per workgroup, plus the decoupled multi-tile mixer's
@@ -986,6 +1024,20 @@ extern "C" int t2o_mixer_unroll_bwd_ex(const t2o_layout* L, const float* pack, c
                                        const float* xmid, const float* gy, const float* ghw_ext, float* gqv,
                                        float* ghid, float* ghw0, float* gslabs, int max_slabs, int* nslab,
                                        void* tape, float* work, int64_t work_floats, int B, int T, void* stream) {
+  return t2o_mixer_unroll_bwd_split(L, pack, states, st_sb, st_st, hid, hid_sb, hid_st, hw0, qv, hw, xout, xmid, gy,
+                                    ghw_ext, gqv, ghid, ghw0, gslabs, max_slabs, nslab, tape, work, work_floats,
+                                    nullptr, 0, 0, 0, B, T, stream);
+}
+
+extern "C" int t2o_mixer_unroll_bwd_split(const t2o_layout* L, const float* pack, const float* states,
+                                          int64_t st_sb, int64_t st_st, const float* hid, int64_t hid_sb,
+                                          int64_t hid_st, const float* hw0, const float* qv, const float* hw,
+                                          const float* xout, const float* xmid, const float* gy,
+                                          const float* ghw_ext, float* gqv, float* ghid, float* ghw0,
+                                          float* gslabs, int max_slabs, int* nslab, void* tape, float* work,
+                                          int64_t work_floats, float* ghw_carry, int phase, int t_lo, int t_hi,
+                                          int B, int T, void* stream) {
+  if (phase < 0 || phase > 2) return T2O_EINVAL;
   if (!L || L->kind != 1 || !pack || !states || !hid || !qv || !hw || !xout || !gy || !gqv || !ghid ||
       !gslabs || !nslab || !tape || B < 1 || T < 1 || L->E > 64)
     return T2O_EINVAL;
@@ -1013,8 +1065,11 @@ extern "C" int t2o_mixer_unroll_bwd_ex(const t2o_layout* L, const float* pack, c
   a.ghw0 = ghw0;
   a.slabs = gslabs;
   a.tape = tape;
-  if (const int r = t2o::mixer_split_bwd(a, work, work_floats, max_slabs, nslab, (hipStream_t)stream); r != 1)
+  if (const int r = t2o::mixer_split_bwd(a, work, work_floats, max_slabs, nslab, (hipStream_t)stream, phase, t_lo,
+                                         phase == 2 ? t_hi : 0, ghw_carry);
+      r != 1)
     return r;
+  if (phase) return T2O_EUNSUPPORTED;
   int rc = T2O_EUNSUPPORTED;
   T2O_DISPATCH_MIXER(L->E, L->H, L->D, L->n_ent, L->FF, L->pos_func == T2O_POS_ABS,
                      rc = (L->prec ? launch_mixer_bwd<E_, H_, D_, NE_, FF_, RTM_, __bf16>(a, max_slabs, nslab, (hipStream_t)stream)

@@ -39,6 +39,7 @@ struct MixerFwdArgs {
   int B, Fs;
   int na;           // agents = state entities (n_entities = n_agents)
   int waves, wlds;  // set by the launcher
+  int t0, t1;       // decoupled recurrence only (t2o_mixer_split.hip): steps [t0, t1); t1 = 0: all
 };
 
 // Compile-time dims of an instance for A agents — the exact count, or the
@@ -412,9 +413,14 @@ namespace t2o {
 // t2o_mixer_split.hip: the multi-tile mixers' recurrence decoupled from the rest
 // (small replay batches).  The entry points return 1 when the split does not
 // apply (t2o_mixer.hip's one-wave kernels run instead), else a status.
-int mixer_split_fwd(const MixerFwdArgs& a, int nnet, hipStream_t stream);
+// phase (both): 0 the whole unroll; forward 1 the recurrence over steps
+// [a.t0, a.t1) only, 2 the parallel rows only (after every range of the
+// recurrence); backward 1 the parallel rows only, 2 the recurrence over steps
+// t_hi - 1 .. t_lo only (ranges from the last down; ghw_carry [B][3][E] carries
+// the hyper grads between them)
+int mixer_split_fwd(const MixerFwdArgs& a, int nnet, hipStream_t stream, int phase = 0);
 int mixer_split_bwd(const MixerBwdArgs& m, float* work, int64_t work_floats, int max_slabs, int* nslab,
-                    hipStream_t stream);
+                    hipStream_t stream, int phase = 0, int t_lo = 0, int t_hi = 0, float* ghw_carry = nullptr);
 int64_t mixer_split_work_floats(const t2o_layout& L, int B, int T);
 bool mixer_split_taken(const t2o_layout& L, int B);
 int mixer_split_extra_slabs(int B);

@@ -95,20 +95,24 @@ __global__ __launch_bounds__(512) void mixs_fwd_rec_kernel(MixerFwdArgs args) {
     P0 = global_weights(n.pack, L, WT{});
   }
   const int b = blockIdx.x * args.waves + w;
-  if (b >= args.B) return;  // wave-uniform; no block barriers after this point
+  // steps [ts, te) of this network (a range; the target network runs one step more)
+  const int ts = args.t0, te = args.t1 > 0 ? min(args.t1, n.T) : n.T;
+  if (b >= args.B || ts >= te) return;  // wave-uniform; no block barriers after this point
   float* X0 = smem + lds_w + w * MixsFwdDims<E, A>::PERW;
   float* OUT = X0 + Dm::X0F;  // window row c at OUT + c * LDO
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
   for (int i = lane; i < Dm::X0F; i += 64) X0[i] = 0.f;
-  for (int i = lane; i < 3 * E; i += 64) X0[(2 * na + i / E) * Dm::LDX + i % E] = n.hw0 ? n.hw0[(size_t)b * 3 * E + i] : 0.f;
+  // the hyper tokens entering step ts: hw0 / zeros, or what the range before wrote
+  const float* hws = ts > 0 ? n.hw + ((size_t)b * n.T + ts - 1) * 3 * E : n.hw0 ? n.hw0 + (size_t)b * 3 * E : nullptr;
+  for (int i = lane; i < 3 * E; i += 64) X0[(2 * na + i / E) * Dm::LDX + i % E] = hws ? hws[i] : 0.f;
   MixIn<E, A> in;
-  mixs_load_keys<E, A>(args, n, b, 0, in, na);
+  mixs_load_keys<E, A>(args, n, b, ts, in, na);
   const int q = q0 + c;  // this lane's query row (always < nq)
-  for (int t = 0; t < n.T; ++t) {
+  for (int t = ts; t < te; ++t) {
     const Wts<WT> P = step_view(P0);
     mix_keys<E, A>(P, L, in, X0, na);
     __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < n.T) mixs_load_keys<E, A>(args, n, b, t + 1, in, na);
+    if (t + 1 < te) mixs_load_keys<E, A>(args, n, b, t + 1, in, na);
     __builtin_amdgcn_wave_barrier();
     KeyFrags<E, Dm::KT, sizeof(WT) == 2> K;
     K.template load<Dm::LDX>(X0);
@@ -277,6 +281,11 @@ struct MixsBwdArgs {
   float* goutl;
   float* pghw;
   int slab0;  // first slab of this kernel's workgroups
+  // the recurrent kernel: steps t_hi - 1 .. t_lo; ghw_carry [B][3][E] hands the
+  // hyper grads from one range to the next (ranges run from the last down); the
+  // range starting at T - 1 clears its slabs and zeroes the tape's tail
+  int t_lo, t_hi;
+  float* ghw_carry;
 };
 
 template <int E, int H, int D, int A, int FF, int RT, bool WLDS, typename WT>
@@ -509,14 +518,15 @@ __global__ __launch_bounds__(256) void mixs_bwd_rec_kernel(MixsBwdArgs sa) {
   float* gs = args.slabs + (size_t)(sa.slab0 + blockIdx.x) * G.grad_total;
   Wts<WT> P0 = WLDS ? stage_weights(smem, n.pack, L, L.fwd_total, WT{}) : global_weights(n.pack, L, WT{});
   P0.vol = false;
-  zero_flushed_regions(gs, G, false);
+  const int T = n.T;
+  const int t_lo = sa.t_lo, t_hi = sa.t_hi > 0 ? sa.t_hi : T;
+  if (t_hi == T) zero_flushed_regions(gs, G, false);
   __syncthreads();
   const int b = blockIdx.x * args.waves + w;
   const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
   using Rec = TapeRec<E, H, FF>;
-  const int T = n.T;
   const size_t nrec = (size_t)fa.B * T * nq, ctiles = (nrec + 15) / 16;
-  if (blockIdx.x == 0 && w == 0) {  // zero each block's compact stream past its last record
+  if (blockIdx.x == 0 && w == 0 && t_hi == T) {  // zero each block's compact stream past its last record
     const int tail = (int)(ctiles * 16 - nrec) * Rec::SIZE;
     for (int d = 0; d < D; ++d) {
       WT* z = static_cast<WT*>(args.tape) + ((size_t)d * ctiles * 16 + nrec) * Rec::SIZE;
@@ -536,10 +546,14 @@ __global__ __launch_bounds__(256) void mixs_bwd_rec_kernel(MixsBwdArgs sa) {
   if (b < fa.B) {
     for (int i = lane; i < Dm::X0F; i += 64) X0[i] = 0.f;
     float ghw[3] = {0.f, 0.f, 0.f};  // grad wrt this step's hyper outputs, lane = feature
+    if (t_hi < T) {  // from the range after this one
+#pragma unroll
+      for (int k = 0; k < 3; ++k) ghw[k] = fv ? sa.ghw_carry[((size_t)b * 3 + k) * E + f] : 0.f;
+    }
     const int q = q0 + c;            // this lane's window row
     MixsRecIn<E, A> cur;
-    mixs_rec_load<E, A>(sa, n, b, T - 1, cur, na);
-    for (int t = T - 1; t >= 0; --t) {
+    mixs_rec_load<E, A>(sa, n, b, t_hi - 1, cur, na);
+    for (int t = t_hi - 1; t >= t_lo; --t) {
       const Wts<WT> P = step_view(P0);
       const size_t bt = (size_t)b * T + t;
       mix_keys<E, A>(P, L, cur.m, X0, na);
@@ -564,7 +578,7 @@ __global__ __launch_bounds__(256) void mixs_bwd_rec_kernel(MixsBwdArgs sa) {
       }
       const MixsRecIn<E, A> now = cur;  // (the prefetch below overwrites cur)
       __builtin_amdgcn_sched_barrier(0);
-      if (t > 0) mixs_rec_load<E, A>(sa, n, b, t - 1, cur, na);
+      if (t > t_lo) mixs_rec_load<E, A>(sa, n, b, t - 1, cur, na);
       __builtin_amdgcn_wave_barrier();
       KeyFrags<E, KT, sizeof(WT) == 2> K;
       K.template load<Dm::LDX>(X0);
@@ -636,9 +650,10 @@ __global__ __launch_bounds__(256) void mixs_bwd_rec_kernel(MixsBwdArgs sa) {
       for (int k = 0; k < 3; ++k) ghw[k] = fv ? GX0[(2 * na + k) * Bd::LDB + f] + now.ph[k] : 0.f;
       __builtin_amdgcn_wave_barrier();
     }
-    if (args.ghw0 && fv) {
+    float* const gout = t_lo > 0 ? sa.ghw_carry : args.ghw0;
+    if (gout && fv) {
 #pragma unroll
-      for (int k = 0; k < 3; ++k) args.ghw0[((size_t)b * 3 + k) * E + f] = ghw[k];
+      for (int k = 0; k < 3; ++k) gout[((size_t)b * 3 + k) * E + f] = ghw[k];
     }
   }
   flush_in_wave_order([&] {
@@ -683,12 +698,12 @@ inline int resident_grid(const void* kern, int threads, size_t lds, int want) {
 }
 
 template <int E, int H, int D, int A, int FF, int RT, typename WT>
-int mixs_launch_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
+int mixs_launch_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream, int phase) {
   using Dm = MixDims<E, A>;
   if (!kernel_layout_matches<E, H, D, FF, WT>(args.L)) return T2O_EINVAL;
   const size_t wfl = (lds_weight_floats<WT>(args.L, args.L.fwd_total) + 15) / 16 * 16;
   // recurrent part
-  {
+  if (phase != 2) {
     MixerFwdArgs a = args;
     constexpr size_t perw = MixsFwdDims<E, A>::PERW;
     size_t lds = 0;
@@ -712,6 +727,7 @@ int mixs_launch_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
     if (rc) return rc;
   }
   // every (episode, step)
+  if (phase == 1) return 0;
   {
     MixerFwdArgs a = args;
     constexpr size_t perw = MixsRowsDims<E, A>::PERW;
@@ -738,7 +754,7 @@ int mixs_launch_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
 }
 
 template <int E, int H, int D, int A, int FF, int RT, typename WT>
-int mixs_launch_bwd(MixsBwdArgs& sa, int max_slabs, int* nslab, hipStream_t stream) {
+int mixs_launch_bwd(MixsBwdArgs& sa, int max_slabs, int* nslab, hipStream_t stream, int phase) {
   using Bd = MixBwdDims<E, A>;
   MixerBwdArgs& args = sa.m;
   if (!kernel_layout_matches<E, H, D, FF, WT>(args.f.L)) return T2O_EINVAL;
@@ -773,9 +789,11 @@ int mixs_launch_bwd(MixsBwdArgs& sa, int max_slabs, int* nslab, hipStream_t stre
     g2 = std::min(resident_grid((const void*)kern, 64 * waves, lds, want), MIXS_ROWS_MAX_WG);
     sa.slab0 = 0;
     if (g2 > max_slabs) return T2O_EINVAL;
-    hipLaunchKernelGGL(kern, dim3(g2), dim3(64 * waves), lds, stream, sa);
-    const int rc = (int)hipGetLastError();
-    if (rc) return rc;
+    if (phase != 2) {
+      hipLaunchKernelGGL(kern, dim3(g2), dim3(64 * waves), lds, stream, sa);
+      const int rc = (int)hipGetLastError();
+      if (rc) return rc;
+    }
   }
   // the recurrence over the window
   {
@@ -790,26 +808,27 @@ int mixs_launch_bwd(MixsBwdArgs& sa, int max_slabs, int* nslab, hipStream_t stre
     const int g1 = (B + waves - 1) / waves;
     sa.slab0 = g2;
     if (g2 + g1 > max_slabs) return T2O_EINVAL;
+    *nslab = g2 + g1;
+    if (phase == 1) return 0;
     auto kern = wlds ? mixs_bwd_rec_kernel<E, H, D, A, FF, RT, true, WT> : mixs_bwd_rec_kernel<E, H, D, A, FF, RT, false, WT>;
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3(g1), dim3(64 * waves), lds, stream, sa);
-    *nslab = g2 + g1;
     return (int)hipGetLastError();
   }
 }
 
 template <int E, int H, int D, int NE, int FF, int RTM>
-int mixs_fwd_dispatch(const MixerFwdArgs& a, int nnet, hipStream_t stream) {
+int mixs_fwd_dispatch(const MixerFwdArgs& a, int nnet, hipStream_t stream, int phase) {
   if constexpr (MixDims<E, NE>::QT > 1)
-    return a.L.prec ? mixs_launch_fwd<E, H, D, NE, FF, RTM, __bf16>(a, nnet, stream)
-                    : mixs_launch_fwd<E, H, D, NE, FF, RTM, float>(a, nnet, stream);
+    return a.L.prec ? mixs_launch_fwd<E, H, D, NE, FF, RTM, __bf16>(a, nnet, stream, phase)
+                    : mixs_launch_fwd<E, H, D, NE, FF, RTM, float>(a, nnet, stream, phase);
   return 1;
 }
 template <int E, int H, int D, int NE, int FF, int RTM>
-int mixs_bwd_dispatch(MixsBwdArgs& sa, int max_slabs, int* nslab, hipStream_t stream) {
+int mixs_bwd_dispatch(MixsBwdArgs& sa, int max_slabs, int* nslab, hipStream_t stream, int phase) {
   if constexpr (MixDims<E, NE>::QT > 1)
-    return sa.m.f.L.prec ? mixs_launch_bwd<E, H, D, NE, FF, RTM, __bf16>(sa, max_slabs, nslab, stream)
-                         : mixs_launch_bwd<E, H, D, NE, FF, RTM, float>(sa, max_slabs, nslab, stream);
+    return sa.m.f.L.prec ? mixs_launch_bwd<E, H, D, NE, FF, RTM, __bf16>(sa, max_slabs, nslab, stream, phase)
+                         : mixs_launch_bwd<E, H, D, NE, FF, RTM, float>(sa, max_slabs, nslab, stream, phase);
   return 1;
 }
 
@@ -819,11 +838,11 @@ namespace t2o {
 
 // t2o_mixer.hip's entry points call these for the multi-tile instances; 1 = not
 // taken (the one-wave kernels run)
-int mixer_split_fwd(const MixerFwdArgs& a, int nnet, hipStream_t stream) {
+int mixer_split_fwd(const MixerFwdArgs& a, int nnet, hipStream_t stream, int phase) {
   if (!mixs_wanted(a.B) || !a.net[0].xout || (nnet > 1 && !a.net[1].xout)) return 1;
   int rc = 1;
   T2O_DISPATCH_MIXER(a.L.E, a.L.H, a.L.D, a.L.n_ent, a.L.FF, a.L.pos_func == T2O_POS_ABS,
-                     rc = (mixs_fwd_dispatch<E_, H_, D_, NE_, FF_, RTM_>(a, nnet, stream)));
+                     rc = (mixs_fwd_dispatch<E_, H_, D_, NE_, FF_, RTM_>(a, nnet, stream, phase)));
   return rc;
 }
 
@@ -833,17 +852,22 @@ int64_t mixer_split_work_floats(const t2o_layout& L, int B, int T) {
 }
 
 int mixer_split_bwd(const MixerBwdArgs& m, float* work, int64_t work_floats, int max_slabs, int* nslab,
-                    hipStream_t stream) {
+                    hipStream_t stream, int phase, int t_lo, int t_hi, float* ghw_carry) {
   const int B = m.f.B, T = m.f.net[0].T;
   const int64_t need = mixer_split_work_floats(m.f.L, B, T);
   if (!mixs_wanted(B) || !work || need <= 0 || work_floats < need) return 1;
+  if (t_hi <= 0) t_hi = T;
+  if (t_lo < 0 || t_lo >= t_hi || t_hi > T || ((t_lo > 0 || t_hi < T) && !ghw_carry)) return T2O_EINVAL;
   MixsBwdArgs sa{};
   sa.m = m;
   sa.goutl = work;
   sa.pghw = work + (int64_t)B * T * 16 * m.f.L.E;
+  sa.t_lo = t_lo;
+  sa.t_hi = t_hi;
+  sa.ghw_carry = ghw_carry;
   int rc = 1;
   T2O_DISPATCH_MIXER(m.f.L.E, m.f.L.H, m.f.L.D, m.f.L.n_ent, m.f.L.FF, m.f.L.pos_func == T2O_POS_ABS,
-                     rc = (mixs_bwd_dispatch<E_, H_, D_, NE_, FF_, RTM_>(sa, max_slabs, nslab, stream)));
+                     rc = (mixs_bwd_dispatch<E_, H_, D_, NE_, FF_, RTM_>(sa, max_slabs, nslab, stream, phase)));
   return rc;
 }
 

@@ -56,7 +56,7 @@ class TDLearner:
     def __init__(self, agent, mixer, *, lr=1e-3, gamma=0.99, td_lambda=0.6, grad_norm_clip=10.0,
                  target_update_interval=200, optim_betas=(0.9, 0.999), optim_eps=1e-8, weight_decay=0.0,
                  detach_mixer_hidden=False, process_group=None, priorities_to_cpu=True, precision="fp32",
-                 overlap=True, td_algo="auto", contract="side"):
+                 overlap=True, td_algo="auto", contract="side", pipeline="auto", pipeline_ranges=10):
         # options first (a bad value fails here, not inside the first train())
         if precision not in ("fp32", "bf16"):
             raise ValueError("precision must be 'fp32' or 'bf16'")
@@ -64,6 +64,8 @@ class TDLearner:
             raise ValueError("contract must be 'pair' or 'side'")
         if td_algo not in ops.TD_ALGOS:
             raise ValueError(f"td_algo must be one of {sorted(ops.TD_ALGOS)}, got {td_algo!r}")
+        if pipeline not in ("auto", True, False) or int(pipeline_ranges) < 1:
+            raise ValueError("pipeline must be 'auto', True or False and pipeline_ranges >= 1")
         dev = next(agent.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("TDLearner needs the modules on a HIP device (no CPU fallback)")
@@ -104,6 +106,9 @@ class TDLearner:
         # "pair": both contractions in one launch after the agent BPTT, measured
         # 15 us slower per update (profiles/r4_b/: 2.455 vs 2.438 ms)
         self.contract = contract
+        # small replay batches: the agent and the (decoupled) mixer recurrences run
+        # side by side on two streams in step ranges (_pipelined)
+        self.pipeline, self.pipeline_ranges = pipeline, int(pipeline_ranges)
         self.step_count = 0
         self.last_target_update_episode = 0
         self.timer = None   # optional callable(tag) recording HIP events around the big kernels
@@ -236,6 +241,20 @@ class TDLearner:
         self._pack_targets()
 
     # -- the TD update -------------------------------------------------------
+    def _pipelined(self, B):
+        """Run the update's recurrences in step ranges on two streams?  Only where the
+        mixer runs decoupled (a multi-tile mixer at a small batch, t2o_mixer_split)
+        and the agent BPTT is the pipelined kernel (depth 2), which take ranges."""
+        if self.pipeline is False or self.sa.D != 2 or self.sa.generic or self.sm.generic:
+            return False
+        return int(ops.lib().t2o_mixer_split(ops.ctypes.byref(self.sm.layout()), int(B))) == 1
+
+    def _ranges(self, n):
+        """pipeline_ranges step ranges covering [0, n), in order."""
+        k = min(self.pipeline_ranges, n)
+        cuts = [round(i * n / k) for i in range(k + 1)]
+        return [(cuts[i], cuts[i + 1]) for i in range(k) if cuts[i] < cuts[i + 1]]
+
     def train(self, batch, t_env=0, episode_num=0, per_weight=None):
         if "obs" in _keys(batch):
             obs = batch["obs"]
@@ -277,16 +296,40 @@ class TDLearner:
             ops.pack_params(self.sm, self.params[self.na:], self.pack_m)  # beside the agent's pack + forward
             mixer_packed = side.record_event()  # (main waits for it before the mixer: grad is clear by then too)
         ops.pack_params(self.sa, self.params[:self.na], self.pack_a)
-        # 1. agents: online + target over t = 0..T
         hmid = self._buf("hmid", (B, T1, self.sa.D - 1, A, self.sa.E)) if self.sa.D > 1 else None
-        q_on, h_on, q_tg, h_tg = ops.agent_unroll_fwd(self.sa, self.pack_a, obs, pack_tg=self.pack_at,
-                                                      timer=self.timer, hmid_on=hmid)
-        # 2. mixers: online on chosen Q (t < T), target on double-Q (t <= T)
-        main.wait_event(mixer_packed)
-        o_on, o_tg = ops.mixer_unroll_fwd(self.sm, self.pack_m, state, h_on, qmode_on=1, q_on=q_on,
-                                          actions=act, avail=avail, T_on=T, pack_tg=self.pack_mt,
-                                          hid_tg=h_tg, qmode_tg=2, q_tg=q_tg, T_tg=T1,
-                                          timer=self.timer)
+        piped = self._pipelined(B) and side is not main
+        mixer_kw = dict(qmode_on=1, actions=act, avail=avail, T_on=T, pack_tg=self.pack_mt, qmode_tg=2, T_tg=T1,
+                        timer=self.timer)
+        if piped:
+            # 1+2 in step ranges: agent range k (main) || mixer recurrence range k-1
+            # (side), then every (episode, step)'s mixer rows (side)
+            E = self.sa.E
+            q_on, q_tg = (self._buf(k, (B, T1, A, self.sa.NA)) for k in ("q_on", "q_tg"))
+            h_on, h_tg = (self._buf(k, (B, T1, A, E)) for k in ("h_on", "h_tg"))
+            o_on, o_tg = ({"y": self._buf("y" + n, (B, Tn)), "hw": self._buf("hw" + n, (B, Tn, 3, E)),
+                           "qv": self._buf("qv" + n, (B, Tn, A)), "xout": self._buf("xo" + n, (B, Tn, A + 3, E)),
+                           "xmid": (self._buf("xm" + n, (B, Tn, self.sm.D - 1, A + 3, E)) if n == "on" else None)}
+                          for n, Tn in (("on", T), ("tg", T1)))
+            for t0, t1 in self._ranges(T1):
+                ops.agent_unroll_fwd(self.sa, self.pack_a, obs, pack_tg=self.pack_at, timer=self.timer,
+                                     hmid_on=hmid, steps=(t0, t1), outs=(q_on, h_on, q_tg, h_tg))
+                agent_done = main.record_event()
+                with torch.cuda.stream(side):
+                    side.wait_event(agent_done)
+                    ops.mixer_unroll_fwd(self.sm, self.pack_m, state, h_on, q_on=q_on, hid_tg=h_tg, q_tg=q_tg,
+                                         phase=1, steps=(t0, t1), outs=(o_on, o_tg), **mixer_kw)
+            with torch.cuda.stream(side):
+                ops.mixer_unroll_fwd(self.sm, self.pack_m, state, h_on, q_on=q_on, hid_tg=h_tg, q_tg=q_tg,
+                                     phase=2, outs=(o_on, o_tg), **mixer_kw)
+            main.wait_stream(side)
+        else:
+            # 1. agents: online + target over t = 0..T
+            q_on, h_on, q_tg, h_tg = ops.agent_unroll_fwd(self.sa, self.pack_a, obs, pack_tg=self.pack_at,
+                                                          timer=self.timer, hmid_on=hmid)
+            # 2. mixers: online on chosen Q (t < T), target on double-Q (t <= T)
+            main.wait_event(mixer_packed)
+            o_on, o_tg = ops.mixer_unroll_fwd(self.sm, self.pack_m, state, h_on, q_on=q_on, hid_tg=h_tg, q_tg=q_tg,
+                                              **mixer_kw)
         # 3. TD(λ) targets / loss (un-normalised: Σ mask is applied in Adam so the
         #    data-parallel sum over ranks divides by the GLOBAL Σ mask)
         #    (Σ mask also lands in grad[-1] straight from the kernel: grad was cleared
@@ -299,10 +342,40 @@ class TDLearner:
         slabs_m = self._slab("m", ops.mixer_slab_count(B) * self.sm.layout().grad_total)
         nwork = ops.mixer_work_floats(self.sm, B, T)
         work_m = self._slab("work_m", nwork) if nwork else None
+        slabs_a = self._slab("a", ops.agent_slab_count(B, A) * self.sa.layout().grad_total)
+        if piped:
+            # 4+5 in step ranges: the mixer's parallel part, then per range from the
+            # last down its recurrence (side) || the agent BPTT of the range after (main)
+            gqv, ghid = self._buf("gqv", (B, T, A)), self._buf("ghid", (B, T, A, self.sm.E))
+            carry_m, carry_a = self._buf("carry_m", (B, 3, self.sm.E)), self._buf("carry_a", (B * A, self.sa.E))
+            mkw = dict(slabs=slabs_m, timer=self.timer, tape=tape_m, work=work_m, outs=(gqv, ghid))
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                contract_m, _, _, _ = ops.mixer_unroll_bwd(self.sm, self.pack_m, state, h_on, o_on, td["gq"],
+                                                           phase=1, **mkw)
+            for t_lo, t_hi in reversed(self._ranges(T)):
+                with torch.cuda.stream(side):
+                    ops.mixer_unroll_bwd(self.sm, self.pack_m, state, h_on, o_on, td["gq"], phase=2,
+                                         steps=(t_lo, t_hi), carry=carry_m, **mkw)
+                    mixer_done = side.record_event()
+                main.wait_event(mixer_done)
+                contract_a, _ = ops.agent_unroll_bwd(self.sa, self.pack_a, obs, h_on, gchosen=gqv, actions=act,
+                                                     gh=None if self.detach_mixer_hidden else ghid, slabs=slabs_a,
+                                                     timer=self.timer, hmid=hmid, tape=tape_a, steps=(t_lo, t_hi),
+                                                     gcarry=carry_a)
+            with torch.cuda.stream(side):
+                gm = contract_m()
+                ops.unpack_grads(self.sm, self.params[self.na:], gm, self.grad[self.na:self.na + self.nm])
+                work_m_ = allreduce_async(self.grad[self.na:], self.pg)
+            ga = contract_a()
+            ops.unpack_grads(self.sa, self.params[:self.na], ga, self.grad[:self.na])
+            work_a = allreduce_async(self.grad[:self.na], self.pg)
+            main.wait_stream(side)
+            wait_all((work_m_, work_a))
+            return self._finish(episode_num, td, {"y": o_on["y"].clone()})  # (o_on: reused buffers)
         contract_m, gqv, ghid, _ = ops.mixer_unroll_bwd(self.sm, self.pack_m, state, h_on, o_on, td["gq"],
                                                         slabs=slabs_m, timer=self.timer, tape=tape_m,
                                                         defer_contract=True, work=work_m)
-        slabs_a = self._slab("a", ops.agent_slab_count(B, A) * self.sa.layout().grad_total)
         gh = None if self.detach_mixer_hidden else ghid
         if self.contract == "pair":
             # 5. agent BPTT (grads of the chosen Q and, unless detached, of the hidden
@@ -328,6 +401,9 @@ class TDLearner:
             work_a = allreduce_async(self.grad[:self.na], self.pg)
             main.wait_stream(side)
             wait_all((work_m, work_a))
+        return self._finish(episode_num, td, o_on)
+
+    def _finish(self, episode_num, td, o_on):
         # 7. clip + Adam
         self.step_count += 1
         ops.adam_step(self.params, self.grad[:-1], self.exp_avg, self.exp_avg_sq, self.step_count, lr=self.lr,

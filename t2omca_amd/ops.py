@@ -112,31 +112,37 @@ def _mark(timer, tag):
 
 
 def agent_unroll_fwd(shape: NetShape, pack_on, obs, h0_on=None, pack_tg=None, h0_tg=None, timer=None,
-                     hmid_on=None):
+                     hmid_on=None, steps=None, outs=None):
     """Unroll the agent over obs [B, T, A, n_ent*F] (any stride over B, T; inner
     [A, n_ent*F] contiguous).  Returns (q_on, h_on[, q_tg, h_tg]) with
     q [B, T, A, NA], h [B, T, A, E].  hmid_on: optional [B, T, D-1, A, E]
-    output buffer for the inter-block activations (used by the backward)."""
+    output buffer for the inter-block activations (used by the backward).
+    steps=(t0, t1): only those steps (t2o_agent_unroll_fwd_range: t0 > 0 continues
+    from h[t0 - 1]) into the given outs=(q_on, h_on, q_tg, h_tg)."""
     _dev(pack_on, obs, h0_on, pack_tg, h0_tg)
     B, T, A, nf = obs.shape
     assert obs.dtype == torch.float32 and nf == shape.n_ent * shape.F
     assert obs.stride(3) == 1 and obs.stride(2) == nf, "obs rows must be contiguous per timestep"
     L = shape.layout()
     dev = obs.device
-    q_on = torch.empty(B, T, A, shape.NA, device=dev)
-    h_on = torch.empty(B, T, A, shape.E, device=dev)
-    q_tg = h_tg = None
-    if pack_tg is not None:
-        q_tg = torch.empty_like(q_on)
-        h_tg = torch.empty_like(h_on)
+    if outs is not None:
+        q_on, h_on, q_tg, h_tg = outs
+    else:
+        q_on = torch.empty(B, T, A, shape.NA, device=dev)
+        h_on = torch.empty(B, T, A, shape.E, device=dev)
+        q_tg = h_tg = None
+        if pack_tg is not None:
+            q_tg = torch.empty_like(q_on)
+            h_tg = torch.empty_like(h_on)
     for h0 in (h0_on, h0_tg):
         if h0 is not None:
             assert h0.is_contiguous() and h0.numel() == B * A * shape.E
+    t0, t1 = steps if steps is not None else (0, T)
     _mark(timer, "begin:agent_fwd")
-    check(lib().t2o_agent_unroll_fwd(ctypes.byref(L), ptr(pack_on), ptr(pack_tg), ptr(obs),
-                                     obs.stride(0), obs.stride(1), ptr(h0_on), ptr(h0_tg),
-                                     ptr(q_on), ptr(h_on), ptr(hmid_on), ptr(q_tg), ptr(h_tg), None,
-                                     B, T, A, stream_ptr()), "agent_unroll_fwd")
+    check(lib().t2o_agent_unroll_fwd_range(ctypes.byref(L), ptr(pack_on), ptr(pack_tg), ptr(obs),
+                                           obs.stride(0), obs.stride(1), ptr(h0_on), ptr(h0_tg),
+                                           ptr(q_on), ptr(h_on), ptr(hmid_on), ptr(q_tg), ptr(h_tg), None,
+                                           B, T, A, int(t0), int(t1), stream_ptr()), "agent_unroll_fwd")
     _mark(timer, "end:agent_fwd")
     if pack_tg is not None:
         return q_on, h_on, q_tg, h_tg
@@ -229,13 +235,17 @@ class DeferredContraction:
 
 
 def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchosen=None, actions=None,
-                     gh=None, want_gh0=False, slabs=None, timer=None, hmid=None, tape=None, defer_contract=False):
+                     gh=None, want_gh0=False, slabs=None, timer=None, hmid=None, tape=None, defer_contract=False,
+                     steps=None, gcarry=None):
     """BPTT of agent_unroll_fwd over the first T = len(grads) steps.
 
     obs [B, >=T, A, nF]; h_seq [B, Ts>=T, A, E] (forward output); gq [B,T,A,NA],
     gchosen [B,T,A] + actions (int64 [B, >=T, A], a-stride 1), gh [B,T,A,E].
     Returns (gpack, gh0) with gpack the compact weight-gradient block (with
-    defer_contract, a DeferredContraction instead)."""
+    defer_contract, a DeferredContraction instead).  steps=(t_lo, t_hi): only
+    steps t_hi - 1 .. t_lo (t2o_agent_unroll_bwd_range; ranges from the last down
+    on the same slabs / tape, gcarry [B*A, E] between them); the contraction is
+    then always deferred (call it after the range that ends at step 0)."""
     _dev(pack, obs, h_seq, h0, gq, gchosen, actions, gh)
     B, _, A, _ = obs.shape
     T = next(t.shape[1] for t in (gq, gchosen, gh) if t is not None)
@@ -255,16 +265,18 @@ def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchose
     tiles = agent_tape_tiles(B, T, A)
     tape = _tape(shape, tiles, tape, obs.device)
     nslab = ctypes.c_int(0)
+    t_lo, t_hi = steps if steps is not None else (0, T)
     _mark(timer, "begin:agent_bwd")
-    check(lib().t2o_agent_unroll_bwd(ctypes.byref(L), ptr(pack), ptr(obs), obs.stride(0), obs.stride(1),
-                                     ptr(h0), ptr(h_seq), ptr(hmid), h_seq.shape[1], ptr(gq), ptr(gchosen),
-                                     ptr(actions), act_sb, act_st, ptr(gh), ptr(slabs), nmax,
-                                     ctypes.byref(nslab), ptr(tape), ptr(gh0), B, T, A, stream_ptr()),
+    check(lib().t2o_agent_unroll_bwd_range(ctypes.byref(L), ptr(pack), ptr(obs), obs.stride(0), obs.stride(1),
+                                           ptr(h0), ptr(h_seq), ptr(hmid), h_seq.shape[1], ptr(gq), ptr(gchosen),
+                                           ptr(actions), act_sb, act_st, ptr(gh), ptr(slabs), nmax,
+                                           ctypes.byref(nslab), ptr(tape), ptr(gh0), ptr(gcarry), B, T, A,
+                                           int(t_lo), int(t_hi), stream_ptr()),
           "agent_unroll_bwd")
     _mark(timer, "end:agent_bwd")
     fmt = int(lib().t2o_agent_bwd_tape_format(ctypes.byref(L), int(hmid is not None)))
     dc = DeferredContraction(shape, pack, tape, tiles, slabs, nslab.value, timer, "agent_dw", fmt)
-    return (dc if defer_contract else dc()), gh0
+    return (dc if defer_contract or steps is not None else dc()), gh0
 
 
 def _mstrides(t):
@@ -274,11 +286,13 @@ def _mstrides(t):
 def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv_on=None, q_on=None,
                      actions=None, avail=None, hw0_on=None, T_on=None,
                      pack_tg=None, hid_tg=None, qmode_tg=2, qv_tg=None, q_tg=None, hw0_tg=None,
-                     T_tg=None, want_xout=True, timer=None):
+                     T_tg=None, want_xout=True, timer=None, phase=0, steps=None, outs=None):
     """Mixer unroll (see include/t2omca.h).  states [B, >=T, n_ent*F];
     hid_* [B, >=T, A, E] (contiguous inner [A, E]); q_on/q_tg [B, q_ts, A, NA]
     contiguous; actions int64 [B, >=T, A]; avail int32 [B, >=T, A, NA].
-    Returns dict of outputs per network: y [B,T], hw [B,T,3,E], qv [B,T,A], xout."""
+    Returns dict of outputs per network: y [B,T], hw [B,T,3,E], qv [B,T,A], xout.
+    phase 1 / 2 (a decoupled mixer, t2o_mixer_unroll_fwd_split): the recurrence
+    over steps=(t0, t1) / the parallel rows, into the given outs=(o_on, o_tg)."""
     _dev(pack_on, states, hid_on, qv_on, q_on, hw0_on, pack_tg, hid_tg, qv_tg, q_tg, hw0_tg)
     B = states.shape[0]
     A, E = hid_on.shape[2], shape.E
@@ -298,7 +312,7 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
     if avail is not None:
         assert avail.dtype == torch.int32 and avail.stride(3) == 1 and avail.stride(2) == avail.shape[3]
 
-    def outs(T, bwd):
+    def alloc(T, bwd):
         # xout / xmid only feed the backward: the target network skips them
         return dict(y=torch.empty(B, T, device=dev), hw=torch.empty(B, T, 3, E, device=dev),
                     qv=torch.empty(B, T, A, device=dev),
@@ -308,26 +322,36 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
     # a multi-tile mixer at a small batch runs decoupled (t2o_mixer_split.hip): its
     # parallel kernel reads the recurrent kernel's window rows back from xout
     split = bool(lib().t2o_mixer_split(ctypes.byref(L), B) == 1)
-    o_on = outs(T_on, want_xout or split)
-    o_tg = None
-    if pack_tg is not None:
-        T_tg = T_tg or hid_tg.shape[1]
-        o_tg = outs(T_tg, False)
-        if split:
-            o_tg["xout"] = torch.empty(B, T_tg, A + 3, E, device=dev)
+    given = outs
+    if given is not None:
+        o_on, o_tg = given
+        T_tg = T_tg or (hid_tg.shape[1] if hid_tg is not None else None)
+    else:
+        o_on = alloc(T_on, want_xout or split)
+        o_tg = None
+        if pack_tg is not None:
+            T_tg = T_tg or hid_tg.shape[1]
+            o_tg = alloc(T_tg, False)
+            if split:
+                o_tg["xout"] = torch.empty(B, T_tg, A + 3, E, device=dev)
     n_actions = q_on.shape[3] if q_on is not None else 0
     act_sb, act_st = _mstrides(actions)
     av_sb, av_st = _mstrides(avail)
     g = lambda d, k: ptr(d[k]) if d is not None else None  # noqa: E731
+    args = (ctypes.byref(L), ptr(pack_on), ptr(pack_tg), ptr(states), states.stride(0), states.stride(1),
+            ptr(hid_on), ptr(hid_tg), hid_on.stride(0), hid_on.stride(1), ptr(hw0_on), ptr(hw0_tg),
+            qmode_on, qmode_tg, ptr(qv_on), ptr(qv_tg), ptr(q_on), ptr(q_tg), q_ts, n_actions,
+            ptr(actions), act_sb, act_st, ptr(avail), av_sb, av_st,
+            g(o_on, "y"), g(o_on, "hw"), g(o_on, "qv"), g(o_on, "xout"), g(o_on, "xmid"),
+            g(o_tg, "y"), g(o_tg, "hw"), g(o_tg, "qv"), g(o_tg, "xout"), g(o_tg, "xmid"),
+            B, T_on, T_tg or 0)
     _mark(timer, "begin:mixer_fwd")
-    check(lib().t2o_mixer_unroll_fwd(
-        ctypes.byref(L), ptr(pack_on), ptr(pack_tg), ptr(states), states.stride(0), states.stride(1),
-        ptr(hid_on), ptr(hid_tg), hid_on.stride(0), hid_on.stride(1), ptr(hw0_on), ptr(hw0_tg),
-        qmode_on, qmode_tg, ptr(qv_on), ptr(qv_tg), ptr(q_on), ptr(q_tg), q_ts, n_actions,
-        ptr(actions), act_sb, act_st, ptr(avail), av_sb, av_st,
-        g(o_on, "y"), g(o_on, "hw"), g(o_on, "qv"), g(o_on, "xout"), g(o_on, "xmid"),
-        g(o_tg, "y"), g(o_tg, "hw"), g(o_tg, "qv"), g(o_tg, "xout"), g(o_tg, "xmid"),
-        B, T_on, T_tg or 0, stream_ptr()), "mixer_unroll_fwd")
+    if phase:
+        t0, t1 = steps if steps is not None else (0, 0)
+        check(lib().t2o_mixer_unroll_fwd_split(*args, int(phase), int(t0), int(t1), stream_ptr()),
+              "mixer_unroll_fwd_split")
+    else:
+        check(lib().t2o_mixer_unroll_fwd(*args, stream_ptr()), "mixer_unroll_fwd")
     _mark(timer, "end:mixer_fwd")
     return (o_on, o_tg) if pack_tg is not None else o_on
 
@@ -368,13 +392,18 @@ def tape_contract_pair(dm: DeferredContraction, da: DeferredContraction, timer=N
 
 
 def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_ext=None,
-                     want_ghw0=False, slabs=None, timer=None, tape=None, defer_contract=False, work=None):
+                     want_ghw0=False, slabs=None, timer=None, tape=None, defer_contract=False, work=None,
+                     phase=0, steps=None, carry=None, outs=None):
     """BPTT of mixer_unroll_fwd (one network, `fwd` = its output dict).
     Returns (gpack, gqv [B,T,A], ghid [B,T,A,E], ghw0 or None).  With
     defer_contract the first item is instead a zero-argument callable that runs
     the tape contraction + slab sum (on whatever stream is current when called)
     and returns gpack.  work: optional float buffer for the decoupled multi-tile
-    mixer (t2o_mixer_bwd_work_floats; allocated here when needed and not given)."""
+    mixer (t2o_mixer_bwd_work_floats; allocated here when needed and not given).
+    phase 1 / 2 (a decoupled mixer, t2o_mixer_unroll_bwd_split): the parallel
+    part / the recurrence over steps=(t_lo, t_hi) (ranges from the last down,
+    carry [B, 3, E] between them) into outs=(gqv, ghid), with the same slabs,
+    tape and work every call; the contraction is then always deferred."""
     _dev(pack, states, hid, gy, hw0, ghw_ext)
     B, T = gy.shape
     A, E = hid.shape[2], shape.E
@@ -387,8 +416,11 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
     if slabs is None or slabs.numel() < nmax * L.grad_total:
         nmax = mixer_slab_count(B)
         slabs = torch.empty(nmax * L.grad_total, device=dev)
-    gqv = torch.empty(B, T, A, device=dev)
-    ghid = torch.empty(B, T, A, E, device=dev)
+    if outs is not None:
+        gqv, ghid = outs
+    else:
+        gqv = torch.empty(B, T, A, device=dev)
+        ghid = torch.empty(B, T, A, E, device=dev)
     ghw0 = torch.empty(B, 3, E, device=dev) if want_ghw0 else None
     tiles = mixer_tape_tiles(B, T, A, shape)
     tape = _tape(shape, tiles, tape, dev)
@@ -396,15 +428,17 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
     nwork = mixer_work_floats(shape, B, T)
     if nwork and (work is None or work.numel() < nwork):
         work = torch.empty(nwork, device=dev)
+    t_lo, t_hi = steps if steps is not None else (0, 0)
     _mark(timer, "begin:mixer_bwd")
-    check(lib().t2o_mixer_unroll_bwd_ex(
+    check(lib().t2o_mixer_unroll_bwd_split(
         ctypes.byref(L), ptr(pack), ptr(states), states.stride(0), states.stride(1), ptr(hid),
         hid.stride(0), hid.stride(1), ptr(hw0), ptr(fwd["qv"]), ptr(fwd["hw"]), ptr(fwd["xout"]),
         ptr(fwd.get("xmid")), ptr(gy), ptr(ghw_ext), ptr(gqv), ptr(ghid), ptr(ghw0), ptr(slabs), nmax, ctypes.byref(nslab),
-        ptr(tape), ptr(work) if nwork else None, nwork, B, T, stream_ptr()), "mixer_unroll_bwd")
+        ptr(tape), ptr(work) if nwork else None, nwork, ptr(carry), int(phase), int(t_lo), int(t_hi), B, T,
+        stream_ptr()), "mixer_unroll_bwd")
     _mark(timer, "end:mixer_bwd")
     contract = DeferredContraction(shape, pack, tape, tiles, slabs, nslab.value, timer, "mixer_dw", 0)
-    return (contract if defer_contract else contract()), gqv, ghid, ghw0
+    return (contract if defer_contract or phase else contract()), gqv, ghid, ghw0
 
 
 # t2o_td_loss_ex mask element types (include/t2omca.h T2O_DT_*)

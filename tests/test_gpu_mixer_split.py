@@ -103,3 +103,35 @@ def test_split_learner_update_is_reproducible_and_close():
     # (Adam's m / sqrt(v) turns gradient rounding on near-zero entries into steps of
     # up to lr: the parameters after two updates sit 6.5e-6 apart for 1.8e-7 in the grads)
     assert normwise(g1, g0) < 1e-5 and normwise(p1, p0) < 5e-5
+
+
+@pytest.mark.parametrize("A,precision,ranges", [(16, "fp32", 4), (16, "bf16", 7), (20, "fp32", 3)])
+def test_pipelined_update_matches_sequential(A, precision, ranges):
+    """TDLearner's pipelined mode (agent and decoupled-mixer recurrences in step ranges
+    on two streams: h, the hyper tokens and their grads carried between ranges through
+    memory) against the same update with one launch per recurrence.  Forward outputs are
+    bit-identical (the same per-step code); the weight gradients are flushed per range,
+    so they agree to rounding; run to run the pipelined update is bit-reproducible."""
+    require_gpu()
+    from t2omca_amd.learner import TDLearner
+    B, T = 4, 13
+
+    def run(pipeline):
+        learner, batch, w = _setup(A, B, T, precision, seed=9)
+        learner = TDLearner(learner.agent, learner.mixer, precision=precision, priorities_to_cpu=False,
+                            pipeline=pipeline, pipeline_ranges=ranges)
+        assert learner._pipelined(B) == (pipeline is True)
+        infos = [learner.train(batch, 0, u, per_weight=w) for u in range(2)]
+        torch.cuda.synchronize()
+        return (infos[0]["qtot"].clone(), infos[0]["td_errors_abs"].clone(),
+                (learner.grad[:-1] / learner.grad[-1]).clone(), learner.params.clone())
+
+    q1, p1, g1, w1 = run(True)
+    q1b, p1b, g1b, w1b = run(True)
+    q0, p0, g0, w0 = run(False)
+    assert torch.equal(q1, q0) and torch.equal(p1, p0), "forward / priorities of the first update"
+    assert torch.equal(g1, g1b) and torch.equal(w1, w1b), "pipelined update not reproducible"
+    errs = {"grads": normwise(g1, g0), "params": normwise(w1, w0)}
+    print(f"A={A} {precision} ranges={ranges} pipelined vs sequential:", {k: f"{v:.1e}" for k, v in errs.items()})
+    bar = (1e-5, 5e-5) if precision == "fp32" else (2e-3, 5e-3)
+    assert errs["grads"] < bar[0] and errs["params"] < bar[1], errs

@@ -110,6 +110,7 @@ def main():
         torch.cuda.synchronize()
         fst.append(_state(full))
         fgs.append((full.grad[:-1] / full.grad[-1]).detach().cpu().clone())
+    fst, fgs = torch.stack(fst), torch.stack(fgs)
     gerrs = []
     for u in range(UPDATES):
         gerr = normwise(dgs[u], fgs[u])
