@@ -464,6 +464,7 @@ struct MixsRecIn {
   float ph[3];      // pghw of step t, lane = feature
   float ghx[3];     // ghw_ext of step t, lane = feature
   f4 stT[MixDims<E, A>::ST];
+  f4 gh[MixIn<E, A>::HV];  // ghid of step t as the parallel kernel left it, f4 i = lane + 64k of [A][E]
 };
 
 template <int E, int A>
@@ -497,6 +498,10 @@ T2O_DEV void mixs_rec_load(const MixsBwdArgs& sa, const MixerNet& n, int b, int 
       if (j < na && c == fa.Fs) v = 1.f;
       in.stT[s][r] = v;
     }
+  // (a step ahead: read-modify-written at the step's end, a dependent load there
+  // would expose its latency on the recurrence)
+#pragma unroll
+  for (int k = 0; k < MixIn<E, A>::HV; ++k) in.gh[k] = ld4(args.ghid + bt * na * E + 4 * min(lane + 64 * k, na * E / 4 - 1));
 }
 
 template <int E, int H, int D, int A, int FF, int RT, bool WLDS, typename WT>
@@ -641,9 +646,11 @@ __global__ __launch_bounds__(256) void mixs_bwd_rec_kernel(MixsBwdArgs sa) {
       }
       __builtin_amdgcn_wave_barrier();
       // agent hidden tokens: the parallel kernel's share + this one's
-      for (int i = lane; i < na * E / 4; i += 64) {
-        float* gh = args.ghid + bt * na * E + 4 * i;
-        st4(gh, ld4(gh) + ld4(GX0 + (na + 4 * i / E) * Bd::LDB + (4 * i) % E));
+#pragma unroll
+      for (int k = 0; k < MixIn<E, A>::HV; ++k) {
+        const int i = lane + 64 * k;
+        if (i < na * E / 4)
+          st4(args.ghid + bt * na * E + 4 * i, now.gh[k] + ld4(GX0 + (na + 4 * i / E) * Bd::LDB + (4 * i) % E));
       }
       // the hyper keys' total: the grad wrt the hyper outputs of step t - 1
 #pragma unroll

@@ -310,17 +310,20 @@ class TDLearner:
                            "qv": self._buf("qv" + n, (B, Tn, A)), "xout": self._buf("xo" + n, (B, Tn, A + 3, E)),
                            "xmid": (self._buf("xm" + n, (B, Tn, self.sm.D - 1, A + 3, E)) if n == "on" else None)}
                           for n, Tn in (("on", T), ("tg", T1)))
+            # (launchers: each wrapper's arguments converted once, then one C call per
+            # range — the host must stay ahead of ranges of ~0.1 ms)
+            agent_go = ops.agent_unroll_fwd(self.sa, self.pack_a, obs, pack_tg=self.pack_at, timer=self.timer,
+                                            hmid_on=hmid, outs=(q_on, h_on, q_tg, h_tg), launcher=True)
+            mixer_go = ops.mixer_unroll_fwd(self.sm, self.pack_m, state, h_on, q_on=q_on, hid_tg=h_tg, q_tg=q_tg,
+                                            outs=(o_on, o_tg), launcher=True, **mixer_kw)
             for t0, t1 in self._ranges(T1):
-                ops.agent_unroll_fwd(self.sa, self.pack_a, obs, pack_tg=self.pack_at, timer=self.timer,
-                                     hmid_on=hmid, steps=(t0, t1), outs=(q_on, h_on, q_tg, h_tg))
+                agent_go(t0, t1)
                 agent_done = main.record_event()
                 with torch.cuda.stream(side):
                     side.wait_event(agent_done)
-                    ops.mixer_unroll_fwd(self.sm, self.pack_m, state, h_on, q_on=q_on, hid_tg=h_tg, q_tg=q_tg,
-                                         phase=1, steps=(t0, t1), outs=(o_on, o_tg), **mixer_kw)
+                    mixer_go(1, t0, t1)
             with torch.cuda.stream(side):
-                ops.mixer_unroll_fwd(self.sm, self.pack_m, state, h_on, q_on=q_on, hid_tg=h_tg, q_tg=q_tg,
-                                     phase=2, outs=(o_on, o_tg), **mixer_kw)
+                mixer_go(2)
             main.wait_stream(side)
         else:
             # 1. agents: online + target over t = 0..T
@@ -348,21 +351,22 @@ class TDLearner:
             # last down its recurrence (side) || the agent BPTT of the range after (main)
             gqv, ghid = self._buf("gqv", (B, T, A)), self._buf("ghid", (B, T, A, self.sm.E))
             carry_m, carry_a = self._buf("carry_m", (B, 3, self.sm.E)), self._buf("carry_a", (B * A, self.sa.E))
-            mkw = dict(slabs=slabs_m, timer=self.timer, tape=tape_m, work=work_m, outs=(gqv, ghid))
+            mixer_go = ops.mixer_unroll_bwd(self.sm, self.pack_m, state, h_on, o_on, td["gq"], slabs=slabs_m,
+                                            timer=self.timer, tape=tape_m, work=work_m, outs=(gqv, ghid),
+                                            carry=carry_m, launcher=True)
+            agent_go, _ = ops.agent_unroll_bwd(self.sa, self.pack_a, obs, h_on, gchosen=gqv, actions=act,
+                                               gh=None if self.detach_mixer_hidden else ghid, slabs=slabs_a,
+                                               timer=self.timer, hmid=hmid, tape=tape_a, gcarry=carry_a,
+                                               launcher=True)
             side.wait_stream(main)
             with torch.cuda.stream(side):
-                contract_m, _, _, _ = ops.mixer_unroll_bwd(self.sm, self.pack_m, state, h_on, o_on, td["gq"],
-                                                           phase=1, **mkw)
+                contract_m = mixer_go(1)
             for t_lo, t_hi in reversed(self._ranges(T)):
                 with torch.cuda.stream(side):
-                    ops.mixer_unroll_bwd(self.sm, self.pack_m, state, h_on, o_on, td["gq"], phase=2,
-                                         steps=(t_lo, t_hi), carry=carry_m, **mkw)
+                    mixer_go(2, t_lo, t_hi)
                     mixer_done = side.record_event()
                 main.wait_event(mixer_done)
-                contract_a, _ = ops.agent_unroll_bwd(self.sa, self.pack_a, obs, h_on, gchosen=gqv, actions=act,
-                                                     gh=None if self.detach_mixer_hidden else ghid, slabs=slabs_a,
-                                                     timer=self.timer, hmid=hmid, tape=tape_a, steps=(t_lo, t_hi),
-                                                     gcarry=carry_a)
+                contract_a = agent_go(t_lo, t_hi)
             with torch.cuda.stream(side):
                 gm = contract_m()
                 ops.unpack_grads(self.sm, self.params[self.na:], gm, self.grad[self.na:self.na + self.nm])

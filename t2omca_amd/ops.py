@@ -112,7 +112,7 @@ def _mark(timer, tag):
 
 
 def agent_unroll_fwd(shape: NetShape, pack_on, obs, h0_on=None, pack_tg=None, h0_tg=None, timer=None,
-                     hmid_on=None, steps=None, outs=None):
+                     hmid_on=None, steps=None, outs=None, launcher=False):
     """Unroll the agent over obs [B, T, A, n_ent*F] (any stride over B, T; inner
     [A, n_ent*F] contiguous).  Returns (q_on, h_on[, q_tg, h_tg]) with
     q [B, T, A, NA], h [B, T, A, E].  hmid_on: optional [B, T, D-1, A, E]
@@ -137,13 +137,17 @@ def agent_unroll_fwd(shape: NetShape, pack_on, obs, h0_on=None, pack_tg=None, h0
     for h0 in (h0_on, h0_tg):
         if h0 is not None:
             assert h0.is_contiguous() and h0.numel() == B * A * shape.E
-    t0, t1 = steps if steps is not None else (0, T)
-    _mark(timer, "begin:agent_fwd")
-    check(lib().t2o_agent_unroll_fwd_range(ctypes.byref(L), ptr(pack_on), ptr(pack_tg), ptr(obs),
-                                           obs.stride(0), obs.stride(1), ptr(h0_on), ptr(h0_tg),
-                                           ptr(q_on), ptr(h_on), ptr(hmid_on), ptr(q_tg), ptr(h_tg), None,
-                                           B, T, A, int(t0), int(t1), stream_ptr()), "agent_unroll_fwd")
-    _mark(timer, "end:agent_fwd")
+    args = (ctypes.byref(L), ptr(pack_on), ptr(pack_tg), ptr(obs), obs.stride(0), obs.stride(1), ptr(h0_on),
+            ptr(h0_tg), ptr(q_on), ptr(h_on), ptr(hmid_on), ptr(q_tg), ptr(h_tg), None, B, T, A)
+    fn = lib().t2o_agent_unroll_fwd_range
+
+    def go(t0, t1):
+        _mark(timer, "begin:agent_fwd")
+        check(fn(*args, t0, t1, stream_ptr()), "agent_unroll_fwd")
+        _mark(timer, "end:agent_fwd")
+    if launcher:  # go(t0, t1) per step range, the arguments converted once (pipelined learner)
+        return go
+    go(*(steps if steps is not None else (0, T)))
     if pack_tg is not None:
         return q_on, h_on, q_tg, h_tg
     return q_on, h_on
@@ -236,7 +240,7 @@ class DeferredContraction:
 
 def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchosen=None, actions=None,
                      gh=None, want_gh0=False, slabs=None, timer=None, hmid=None, tape=None, defer_contract=False,
-                     steps=None, gcarry=None):
+                     steps=None, gcarry=None, launcher=False):
     """BPTT of agent_unroll_fwd over the first T = len(grads) steps.
 
     obs [B, >=T, A, nF]; h_seq [B, Ts>=T, A, E] (forward output); gq [B,T,A,NA],
@@ -265,17 +269,20 @@ def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchose
     tiles = agent_tape_tiles(B, T, A)
     tape = _tape(shape, tiles, tape, obs.device)
     nslab = ctypes.c_int(0)
-    t_lo, t_hi = steps if steps is not None else (0, T)
-    _mark(timer, "begin:agent_bwd")
-    check(lib().t2o_agent_unroll_bwd_range(ctypes.byref(L), ptr(pack), ptr(obs), obs.stride(0), obs.stride(1),
-                                           ptr(h0), ptr(h_seq), ptr(hmid), h_seq.shape[1], ptr(gq), ptr(gchosen),
-                                           ptr(actions), act_sb, act_st, ptr(gh), ptr(slabs), nmax,
-                                           ctypes.byref(nslab), ptr(tape), ptr(gh0), ptr(gcarry), B, T, A,
-                                           int(t_lo), int(t_hi), stream_ptr()),
-          "agent_unroll_bwd")
-    _mark(timer, "end:agent_bwd")
+    args = (ctypes.byref(L), ptr(pack), ptr(obs), obs.stride(0), obs.stride(1), ptr(h0), ptr(h_seq), ptr(hmid),
+            h_seq.shape[1], ptr(gq), ptr(gchosen), ptr(actions), act_sb, act_st, ptr(gh), ptr(slabs), nmax,
+            ctypes.byref(nslab), ptr(tape), ptr(gh0), ptr(gcarry), B, T, A)
+    fn = lib().t2o_agent_unroll_bwd_range
     fmt = int(lib().t2o_agent_bwd_tape_format(ctypes.byref(L), int(hmid is not None)))
-    dc = DeferredContraction(shape, pack, tape, tiles, slabs, nslab.value, timer, "agent_dw", fmt)
+
+    def go(t_lo, t_hi):
+        _mark(timer, "begin:agent_bwd")
+        check(fn(*args, t_lo, t_hi, stream_ptr()), "agent_unroll_bwd")
+        _mark(timer, "end:agent_bwd")
+        return DeferredContraction(shape, pack, tape, tiles, slabs, nslab.value, timer, "agent_dw", fmt)
+    if launcher:  # go(t_lo, t_hi) per step range -> the (deferred) contraction
+        return go, gh0
+    dc = go(*(steps if steps is not None else (0, T)))
     return (dc if defer_contract or steps is not None else dc()), gh0
 
 
@@ -286,7 +293,7 @@ def _mstrides(t):
 def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv_on=None, q_on=None,
                      actions=None, avail=None, hw0_on=None, T_on=None,
                      pack_tg=None, hid_tg=None, qmode_tg=2, qv_tg=None, q_tg=None, hw0_tg=None,
-                     T_tg=None, want_xout=True, timer=None, phase=0, steps=None, outs=None):
+                     T_tg=None, want_xout=True, timer=None, phase=0, steps=None, outs=None, launcher=False):
     """Mixer unroll (see include/t2omca.h).  states [B, >=T, n_ent*F];
     hid_* [B, >=T, A, E] (contiguous inner [A, E]); q_on/q_tg [B, q_ts, A, NA]
     contiguous; actions int64 [B, >=T, A]; avail int32 [B, >=T, A, NA].
@@ -345,14 +352,18 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
             g(o_on, "y"), g(o_on, "hw"), g(o_on, "qv"), g(o_on, "xout"), g(o_on, "xmid"),
             g(o_tg, "y"), g(o_tg, "hw"), g(o_tg, "qv"), g(o_tg, "xout"), g(o_tg, "xmid"),
             B, T_on, T_tg or 0)
-    _mark(timer, "begin:mixer_fwd")
-    if phase:
-        t0, t1 = steps if steps is not None else (0, 0)
-        check(lib().t2o_mixer_unroll_fwd_split(*args, int(phase), int(t0), int(t1), stream_ptr()),
-              "mixer_unroll_fwd_split")
-    else:
-        check(lib().t2o_mixer_unroll_fwd(*args, stream_ptr()), "mixer_unroll_fwd")
-    _mark(timer, "end:mixer_fwd")
+    fn_split, fn = lib().t2o_mixer_unroll_fwd_split, lib().t2o_mixer_unroll_fwd
+
+    def go(phase, t0=0, t1=0):
+        _mark(timer, "begin:mixer_fwd")
+        if phase:
+            check(fn_split(*args, phase, t0, t1, stream_ptr()), "mixer_unroll_fwd_split")
+        else:
+            check(fn(*args, stream_ptr()), "mixer_unroll_fwd")
+        _mark(timer, "end:mixer_fwd")
+    if launcher:  # go(phase, t0, t1) per phase / step range (pipelined learner)
+        return go
+    go(int(phase), *(steps if steps is not None else (0, 0)))
     return (o_on, o_tg) if pack_tg is not None else o_on
 
 
@@ -393,7 +404,7 @@ def tape_contract_pair(dm: DeferredContraction, da: DeferredContraction, timer=N
 
 def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_ext=None,
                      want_ghw0=False, slabs=None, timer=None, tape=None, defer_contract=False, work=None,
-                     phase=0, steps=None, carry=None, outs=None):
+                     phase=0, steps=None, carry=None, outs=None, launcher=False):
     """BPTT of mixer_unroll_fwd (one network, `fwd` = its output dict).
     Returns (gpack, gqv [B,T,A], ghid [B,T,A,E], ghw0 or None).  With
     defer_contract the first item is instead a zero-argument callable that runs
@@ -428,16 +439,20 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
     nwork = mixer_work_floats(shape, B, T)
     if nwork and (work is None or work.numel() < nwork):
         work = torch.empty(nwork, device=dev)
-    t_lo, t_hi = steps if steps is not None else (0, 0)
-    _mark(timer, "begin:mixer_bwd")
-    check(lib().t2o_mixer_unroll_bwd_split(
-        ctypes.byref(L), ptr(pack), ptr(states), states.stride(0), states.stride(1), ptr(hid),
-        hid.stride(0), hid.stride(1), ptr(hw0), ptr(fwd["qv"]), ptr(fwd["hw"]), ptr(fwd["xout"]),
-        ptr(fwd.get("xmid")), ptr(gy), ptr(ghw_ext), ptr(gqv), ptr(ghid), ptr(ghw0), ptr(slabs), nmax, ctypes.byref(nslab),
-        ptr(tape), ptr(work) if nwork else None, nwork, ptr(carry), int(phase), int(t_lo), int(t_hi), B, T,
-        stream_ptr()), "mixer_unroll_bwd")
-    _mark(timer, "end:mixer_bwd")
-    contract = DeferredContraction(shape, pack, tape, tiles, slabs, nslab.value, timer, "mixer_dw", 0)
+    args = (ctypes.byref(L), ptr(pack), ptr(states), states.stride(0), states.stride(1), ptr(hid),
+            hid.stride(0), hid.stride(1), ptr(hw0), ptr(fwd["qv"]), ptr(fwd["hw"]), ptr(fwd["xout"]),
+            ptr(fwd.get("xmid")), ptr(gy), ptr(ghw_ext), ptr(gqv), ptr(ghid), ptr(ghw0), ptr(slabs), nmax,
+            ctypes.byref(nslab), ptr(tape), ptr(work) if nwork else None, nwork, ptr(carry))
+    fn = lib().t2o_mixer_unroll_bwd_split
+
+    def go(phase, t_lo=0, t_hi=0):
+        _mark(timer, "begin:mixer_bwd")
+        check(fn(*args, phase, t_lo, t_hi, B, T, stream_ptr()), "mixer_unroll_bwd")
+        _mark(timer, "end:mixer_bwd")
+        return DeferredContraction(shape, pack, tape, tiles, slabs, nslab.value, timer, "mixer_dw", 0)
+    if launcher:  # go(phase, t_lo, t_hi) per phase / step range -> the (deferred) contraction
+        return go
+    contract = go(int(phase), *(steps if steps is not None else (0, 0)))
     return (contract if defer_contract or phase else contract()), gqv, ghid, ghw0
 
 
