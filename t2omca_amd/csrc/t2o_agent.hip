@@ -52,11 +52,21 @@ constexpr int AG_FWD_LOOP_T = 4;  // unrolls this short loop resident workgroups
 // accumulation registers the compiler would otherwise copy them out of.
 template <int NE>
 constexpr int agent_fwd_waves_per_eu() { return NE <= 8 ? 2 : 1; }
+// Observations of the next step prefetched into registers (NE f4 per lane) while
+// the current one computes.  T2O_AG16_LEAN: not at 16 entities, whose forward then
+// fits two waves per SIMD (the 64 prefetch registers were what kept it above 256).
+#ifndef T2O_AG16_LEAN
+#define T2O_AG16_LEAN 0
+#endif
+template <int NE>
+constexpr bool agent_fwd_prefetch() { return NE <= 8 || !T2O_AG16_LEAN; }
+template <int NE>
+constexpr int agent_fwd_wpe() { return agent_fwd_waves_per_eu<NE>() > 1 || (T2O_AG16_LEAN && NE <= 16) ? 2 : 1; }
 
 // RT: runtime-entity instance (t2o_dispatch.hpp) — NE is a capacity, the real
 // entity count is args.A (n_entities = n_agents on the tuned path)
 template <int E, int H, int D, int NE, int FF, bool RT, bool WLDS, bool LOOP, typename WT>
-__global__ __launch_bounds__(64 * AG_FWD_WAVES) __attribute__((amdgpu_waves_per_eu(agent_fwd_waves_per_eu<NE>())))
+__global__ __launch_bounds__(64 * AG_FWD_WAVES) __attribute__((amdgpu_waves_per_eu(agent_fwd_wpe<NE>())))
 void agent_fwd_kernel(AgentFwdArgs args) {
   constexpr int ET = E / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -101,6 +111,7 @@ void agent_fwd_kernel(AgentFwdArgs args) {
     // chunks (t2o_agent_block_ch.hpp)
     constexpr bool CHUNK = NE > AG_CHUNK_MIN;
     constexpr int NO = CHUNK ? 1 : NE;
+    constexpr bool PF = agent_fwd_prefetch<NE>();
     auto row_obs = [&](int step) {
       return args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * ne * F;
     };
@@ -114,15 +125,17 @@ void agent_fwd_kernel(AgentFwdArgs args) {
           o[j][r] = (f < F && j < ne) ? ob[j * F + f] : 0.f;
         }
     };
-    f4 on[NO];
-    if constexpr (!CHUNK) load_obs(args.t0, on);
+    f4 on[PF ? NO : 1];
+    if constexpr (!CHUNK && PF) load_obs(args.t0, on);
     for (int step = args.t0; step < args.t1; ++step) {
       const Wts<WT> P = step_view(P0);
       f4 o[NO];
-      if constexpr (!CHUNK) {
+      if constexpr (!CHUNK && PF) {
 #pragma unroll
         for (int j = 0; j < NE; ++j) o[j] = on[j];
         if (step + 1 < args.t1) load_obs(step + 1, on);
+      } else if constexpr (!CHUNK) {
+        load_obs(step, o);
       }
       const ObsRow orow{row_obs(step), F, ne, RT && ne % AG_CHUNK != 0};
       f4 x[ET];

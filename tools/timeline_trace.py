@@ -1,11 +1,14 @@
 """Print one TD update's kernel timeline (start/end/duration in µs, queue) from a
-rocprofv3 --kernel-trace CSV: the last complete update (agent_fwd to agent_fwd).
-   python tools/timeline_trace.py <run_kernel_trace.csv>"""
+rocprofv3 --kernel-trace CSV: the last complete update, from one launch of the
+anchor kernel to the next (default agent_fwd; a pipelined update launches the agent
+forward once per step range, so anchor it on the Adam kernel: `adam`).
+   python tools/timeline_trace.py <run_kernel_trace.csv> [anchor]"""
 import csv
 import sys
 
 r = sorted(csv.DictReader(open(sys.argv[1])), key=lambda x: int(x["Start_Timestamp"]))
-idx = [i for i, x in enumerate(r) if "agent_fwd" in x["Kernel_Name"]]
+anchor = sys.argv[2] if len(sys.argv) > 2 else "agent_fwd"
+idx = [i for i, x in enumerate(r) if anchor in x["Kernel_Name"]]
 i0, i1 = idx[-2], idx[-1]
 t0 = int(r[i0]["Start_Timestamp"])
 print("queue   start_us    end_us    dur_us  kernel")
