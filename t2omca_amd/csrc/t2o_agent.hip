@@ -52,21 +52,20 @@ constexpr int AG_FWD_LOOP_T = 4;  // unrolls this short loop resident workgroups
 // accumulation registers the compiler would otherwise copy them out of.
 template <int NE>
 constexpr int agent_fwd_waves_per_eu() { return NE <= 8 ? 2 : 1; }
-// Observations of the next step prefetched into registers (NE f4 per lane) while
-// the current one computes.  T2O_AG16_LEAN: not at 16 entities, whose forward then
-// fits two waves per SIMD (the 64 prefetch registers were what kept it above 256).
-#ifndef T2O_AG16_LEAN
-#define T2O_AG16_LEAN 0
-#endif
-template <int NE>
-constexpr bool agent_fwd_prefetch() { return NE <= 8 || !T2O_AG16_LEAN; }
-template <int NE>
-constexpr int agent_fwd_wpe() { return agent_fwd_waves_per_eu<NE>() > 1 || (T2O_AG16_LEAN && NE <= 16) ? 2 : 1; }
+// Observations of the next step are prefetched into registers (NE f4 per lane)
+// while the current one computes.  LEAN (9-16 entities, a grid of more waves than
+// SIMDs): not — the 64 prefetch registers were what kept the 16-entity forward
+// above 256, and without them it runs two waves per SIMD (222 VGPRs) where the
+// other wave covers the loads: 16 AGVs x 1024 episodes x T=150, agent_fwd 2.56 ->
+// 2.10 ms (profiles/r5_ag16/).  A small grid keeps the prefetch (one wave per SIMD
+// either way, the load latency would be exposed).
+template <int NE, bool LEAN>
+constexpr int agent_fwd_wpe() { return agent_fwd_waves_per_eu<NE>() > 1 || LEAN ? 2 : 1; }
 
 // RT: runtime-entity instance (t2o_dispatch.hpp) — NE is a capacity, the real
 // entity count is args.A (n_entities = n_agents on the tuned path)
-template <int E, int H, int D, int NE, int FF, bool RT, bool WLDS, bool LOOP, typename WT>
-__global__ __launch_bounds__(64 * AG_FWD_WAVES) __attribute__((amdgpu_waves_per_eu(agent_fwd_wpe<NE>())))
+template <int E, int H, int D, int NE, int FF, bool RT, bool WLDS, bool LOOP, typename WT, bool LEAN = false>
+__global__ __launch_bounds__(64 * AG_FWD_WAVES) __attribute__((amdgpu_waves_per_eu(agent_fwd_wpe<NE, LEAN>())))
 void agent_fwd_kernel(AgentFwdArgs args) {
   constexpr int ET = E / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -111,7 +110,7 @@ void agent_fwd_kernel(AgentFwdArgs args) {
     // chunks (t2o_agent_block_ch.hpp)
     constexpr bool CHUNK = NE > AG_CHUNK_MIN;
     constexpr int NO = CHUNK ? 1 : NE;
-    constexpr bool PF = agent_fwd_prefetch<NE>();
+    constexpr bool PF = !LEAN;
     auto row_obs = [&](int step) {
       return args.obs + b * args.obs_sb + step * args.obs_st + (int64_t)a * ne * F;
     };
@@ -196,6 +195,9 @@ int launch_fwd(const AgentFwdArgs& args, int nnet, hipStream_t stream) {
   auto kern = loop ? agent_fwd_kernel<E, H, D, NE, FF, RT, true, true, WT>
               : a.wlds ? agent_fwd_kernel<E, H, D, NE, FF, RT, true, false, WT>
                        : agent_fwd_kernel<E, H, D, NE, FF, RT, false, false, WT>;
+  if constexpr (NE > 8 && NE <= AG_CHUNK_MIN) {  // (LEAN: more waves than SIMDs)
+    if (!loop && a.wlds && (int64_t)tiles * nnet > 1024) kern = agent_fwd_kernel<E, H, D, NE, FF, RT, true, false, WT, true>;
+  }
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   if (loop) {  // resident workgroups only, looping over the tiles
     int per_cu = 0, dev = 0, cus = 0;

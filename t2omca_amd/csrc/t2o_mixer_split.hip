@@ -679,6 +679,330 @@ __global__ __launch_bounds__(256) void mixs_bwd_rec_kernel(MixsBwdArgs sa) {
 }
 
 // ---------------------------------------------------------------------------
+// The window's BPTT on two waves per episode, one per transformer block (depth
+// 2), as t2o_mixer.hip's mixer_bwd_pipe_kernel does for the one-tile mixers:
+//   block-1 wave: keys+fwd1(t) | bwd1(t) | keys+fwd1(t-1) | bwd1(t-1) | ...
+//   block-0 wave:      -       | fwd0(t) |     bwd0(t)    | fwd0(t-1) | ...
+// so the recomputes come off the dependent chain bwd1 -> bwd0 -> (hyper grads)
+// -> bwd1 ...  Per step the block-1 wave starts from the window rows' grads (the
+// parallel kernel's share + the carried hyper grads: no head here), the block-0
+// wave finishes with the step's key grads (its own + the parallel kernel's hyper
+// share) and the ghid read-modify-write.  One pair per workgroup: the two waves
+// land on two SIMDs and each may take the whole register file (the small batches
+// this runs at leave SIMDs idle anyway).  Pair LDS: the key block X0 (written by
+// the block-1 recompute, read by both recomputes) and a region R owned by the
+// wave in its backward phase: the window grads / dW staging, then the hand-over
+// 1 -> 0 (block-1 key grads in rows < lk, the grads wrt the block-1 input past
+// them), then the step's total key grads, whose hyper rows the block-1 wave reads
+// at its next backward phase.
+template <int E, int A>
+struct MixsPipeDims {
+  using Dm = MixDims<E, A>;
+  using Bd = MixBwdDims<E, A>;
+  static constexpr int LDR = E;
+  static constexpr int XCH = Dm::LKCAP * LDR;  // window-row grads after the key rows
+  static constexpr int R0 = Bd::STAGE > Dm::KT * 16 * LDR ? Bd::STAGE : Dm::KT * 16 * LDR;
+  static constexpr int REGION = R0 > XCH + 16 * LDR ? R0 : XCH + 16 * LDR;
+  static constexpr int PAIRF = Dm::X0F + REGION;
+};
+
+template <int E, int A>
+T2O_DEV void mixs_load_stT(const MixerFwdArgs& fa, int b, int t, f4 (&stT)[MixDims<E, A>::ST], int na) {
+  const int c = lane_c(), g = lane_g();
+  const float* st = fa.states + b * fa.st_sb + t * fa.st_st;
+#pragma unroll
+  for (int s = 0; s < MixDims<E, A>::ST; ++s)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * s + 4 * g + r;
+      float v = ld_or0(st, j * fa.Fs + c, j < na && c < fa.Fs);
+      if (j < na && c == fa.Fs) v = 1.f;
+      stT[s][r] = v;
+    }
+}
+
+template <int E, int H, int A, int FF, typename WT>
+T2O_DEV void mixs_pipe_block1(const MixsBwdArgs& sa, const Wts<WT>& P0, const t2o_layout& L, const t2o_layout& G,
+                              float* __restrict__ gs, float* X0, float* R, int b, PairBarrier& pbar, int na) {
+  const MixerBwdArgs& args = sa.m;
+  const t2o_layout Lb = block_view(L, 1), Gb = block_view(G, 1);
+  using Dm = MixDims<E, A>;
+  using Pd = MixsPipeDims<E, A>;
+  using Rec = TapeRec<E, H, FF>;
+  constexpr int ET = E / 16, KT = Dm::KT, HW = mixs_hw<E>(), GL = (16 * E + 63) / 64;
+  constexpr bool BF = sizeof(WT) == 2;
+  const MixerFwdArgs& fa = args.f;
+  const MixerNet& n = fa.net[0];
+  const int T = n.T, t_lo = sa.t_lo, t_hi = sa.t_hi;
+  const int nq = na + 3, lk = 2 * na + 3, q0 = mixs_q0(nq);
+  const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
+  const int f = lane < E ? lane : 0;
+  const bool fv = lane < E;
+  const size_t ctiles = ((size_t)fa.B * T * nq + 15) / 16;
+  f4 ln2[2 * ET];
+#pragma unroll
+  for (int i = 0; i < 2 * ET; ++i) ln2[i] = zero4();
+  for (int t = t_hi - 1; t >= t_lo; --t) {
+    const size_t bt = (size_t)b * T + t;
+    const MaskedRec<WT> rec(static_cast<WT*>(args.tape) + (1 * ctiles * 16 + ((size_t)t * fa.B + b) * nq + q0) * Rec::SIZE,
+                            16, Rec::SIZE);
+    MixerCacheLean<E, H, KT, FF> cache;
+    KeyFrags<E, KT, BF> K;
+    MixIn<E, A> in;
+    float hwp[HW], gl[GL], ghx[3];
+    f4 xm[ET];
+    {  // ---- recompute: the key block of step t, block-1 forward of the window rows
+      mixs_load_keys<E, A>(fa, n, b, t, in, na);
+#pragma unroll
+      for (int k = 0; k < HW; ++k) {
+        const int i = min(lane + 64 * k, 3 * E - 1);
+        hwp[k] = t > 0 ? args.hw[(bt - 1) * 3 * E + i] : (n.hw0 ? n.hw0[(size_t)b * 3 * E + i] : 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < GL; ++k) gl[k] = sa.goutl[bt * 16 * E + lane + 64 * k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) ghx[k] = args.ghw_ext ? args.ghw_ext[(bt * 3 + k) * E + f] : 0.f;
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft) xm[ft] = ld4(args.xmid + (bt * nq + q0 + c) * E + 16 * ft + 4 * g);
+      const Wts<WT> P = step_view(P0);
+      mix_keys<E, A>(P, L, in, X0, na);
+#pragma unroll
+      for (int k = 0; k < HW; ++k) {
+        const int i = lane + 64 * k;
+        if (i < 3 * E) X0[(2 * na + i / E) * Dm::LDX + i % E] = hwp[k];
+      }
+      __builtin_amdgcn_wave_barrier();
+      K.template load<Dm::LDX>(X0);
+      f4 x[ET];
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft) x[ft] = xm[ft];
+      mixer_block_fwd_lean<E, H, KT, FF>(P, Lb, 0, K, lk, x, cache, rec);
+    }
+    pbar.sync();
+    {  // ---- backward: the window rows' grads, block 1
+      const Wts<WT> P = step_view(P0);
+      float ghw[3];  // grad wrt this step's hyper outputs: the step after's key grads (block-0 wave), carried
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        ghw[k] = !fv ? 0.f : t < t_hi - 1 ? R[(2 * na + k) * Pd::LDR + f]
+                           : t_hi < T ? sa.ghw_carry[((size_t)b * 3 + k) * E + f] : 0.f;
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int k = 0; k < GL; ++k) {
+        const int i = lane + 64 * k;
+        R[(i / E) * Pd::LDR + i % E] = gl[k];
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (fv) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) R[(13 + k) * Pd::LDR + f] += ghw[k] + ghx[k];
+      }
+      __builtin_amdgcn_wave_barrier();
+      f4 gx[ET];
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft) gx[ft] = ld4(R + c * Pd::LDR + 16 * ft + 4 * g);
+      __builtin_amdgcn_wave_barrier();
+      f4 gX0[KT][ET];
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft) gX0[kt][ft] = zero4();
+      mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, lk, gX0, cache, gx, ln2);
+      __builtin_amdgcn_wave_barrier();
+      // hand-over to the block-0 wave
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * kt + 4 * g + r;
+            if (row < lk) R[row * Pd::LDR + 16 * ft + c] = gX0[kt][ft][r];
+          }
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft) st4(R + Pd::XCH + c * Pd::LDR + 16 * ft + 4 * g, gx[ft]);
+    }
+    pbar.sync();
+  }
+  pbar.sync();  // the block-0 wave's last backward phase
+  flush_in_wave_order([&] {
+    vec_accumulate_g<ET>(gs + Gb.g2[0], &ln2[0]);
+    vec_accumulate_g<ET>(gs + Gb.n2[0], &ln2[ET]);
+  });
+  (void)G;
+}
+
+template <int E, int H, int A, int FF, typename WT>
+T2O_DEV void mixs_pipe_block0(const MixsBwdArgs& sa, const Wts<WT>& P0, const t2o_layout& L, const t2o_layout& G,
+                              float* __restrict__ gs, const float* X0, float* R, int b, PairBarrier& pb, int na) {
+  const MixerBwdArgs& args = sa.m;
+  const t2o_layout Lb = block_view(L, 0), Gb = block_view(G, 0);
+  using Dm = MixDims<E, A>;
+  using Pd = MixsPipeDims<E, A>;
+  using Rec = TapeRec<E, H, FF>;
+  constexpr int ET = E / 16, KT = Dm::KT, HV = MixIn<E, A>::HV;
+  constexpr bool BF = sizeof(WT) == 2;
+  const MixerFwdArgs& fa = args.f;
+  const int T = fa.net[0].T, t_lo = sa.t_lo, t_hi = sa.t_hi;
+  const int nq = na + 3, lk = 2 * na + 3, q0 = mixs_q0(nq);
+  const size_t ctiles = ((size_t)fa.B * T * nq + 15) / 16;
+  const int c = lane_c(), g = lane_g(), lane = threadIdx.x & 63;
+  const int f = lane < E ? lane : 0;
+  const bool fv = lane < E;
+  f4 ln2[2 * ET], gWe[ET];
+#pragma unroll
+  for (int i = 0; i < ET; ++i) ln2[i] = ln2[ET + i] = gWe[i] = zero4();
+  pb.sync();  // one phase behind the block-1 wave
+  for (int t = t_hi - 1; t >= t_lo; --t) {
+    const size_t bt = (size_t)b * T + t;
+    const MaskedRec<WT> rec(static_cast<WT*>(args.tape) + (((size_t)t * fa.B + b) * nq + q0) * Rec::SIZE, 16,
+                            Rec::SIZE);
+    MixerCacheLean<E, H, KT, FF> cache;
+    KeyFrags<E, KT, BF> K;
+    f4 stT[Dm::ST], gh[HV];
+    float ph[3];
+    {  // ---- recompute: block-0 forward of the window rows (block inputs = X0 rows na + q)
+      mixs_load_stT<E, A>(fa, b, t, stT, na);
+#pragma unroll
+      for (int k = 0; k < HV; ++k) gh[k] = ld4(args.ghid + bt * na * E + 4 * min(lane + 64 * k, na * E / 4 - 1));
+#pragma unroll
+      for (int k = 0; k < 3; ++k) ph[k] = sa.pghw[(bt * 3 + k) * E + f];
+      const Wts<WT> P = step_view(P0);
+      K.template load<Dm::LDX>(X0);
+      f4 x[ET];
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft) x[ft] = ld4(X0 + (na + q0 + c) * Dm::LDX + 16 * ft + 4 * g);
+      mixer_block_fwd_lean<E, H, KT, FF>(P, Lb, 0, K, lk, x, cache, rec);
+    }
+    pb.sync();
+    {  // ---- backward: block 0, then the step's key-token grads
+      const Wts<WT> P = step_view(P0);
+      f4 gX0[KT][ET], gx[ET];
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 16 * kt + 4 * g + r;
+            gX0[kt][ft][r] = row < lk ? R[row * Pd::LDR + 16 * ft + c] : 0.f;
+          }
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft) gx[ft] = ld4(R + Pd::XCH + c * Pd::LDR + 16 * ft + 4 * g);
+      __builtin_amdgcn_wave_barrier();
+      mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, lk, gX0, cache, gx, ln2);
+#pragma unroll
+      for (int s = 0; s < Dm::ST; ++s)
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft) {
+          f4 am;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) am[r] = 16 * s + 4 * g + r < na ? gX0[s][ft][r] : 0.f;
+          if constexpr (BF) {
+            gWe[ft] = mfma_b16(to_bf4(am), to_bf4(stT[s]), gWe[ft]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) gWe[ft] = mfma4(am[r], stT[s][r], gWe[ft]);
+          }
+        }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) R[(16 * kt + 4 * g + r) * Pd::LDR + 16 * ft + c] = gX0[kt][ft][r];
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft) {  // the window rows' query path
+        float* dst = R + (na + q0 + c) * Pd::LDR + 16 * ft + 4 * g;
+        st4(dst, ld4(dst) + gx[ft]);
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int k = 0; k < HV; ++k) {  // agent hidden tokens: the parallel kernel's share + the window's
+        const int i = lane + 64 * k;
+        if (i < na * E / 4)
+          st4(args.ghid + bt * na * E + 4 * i, gh[k] + ld4(R + (na + 4 * i / E) * Pd::LDR + (4 * i) % E));
+      }
+      // the hyper keys' total (+ the parallel kernel's share): the block-1 wave's
+      // carried grads at t - 1, or what this range hands on
+      if (fv) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const float v = R[(2 * na + k) * Pd::LDR + f] + ph[k];
+          R[(2 * na + k) * Pd::LDR + f] = v;
+          if (t == t_lo) {
+            float* gout = t_lo > 0 ? sa.ghw_carry : args.ghw0;
+            if (gout) gout[((size_t)b * 3 + k) * E + f] = v;
+          }
+        }
+      }
+    }
+    pb.sync();
+  }
+  flush_in_wave_order([&] {
+#pragma unroll
+    for (int ft = 0; ft < ET; ++ft)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int fe = 16 * ft + 4 * g + r;
+        if (c < fa.Fs) unsafeAtomicAdd(gs + Gb.We + fe * 16 + c, gWe[ft][r]);
+        else if (c == fa.Fs) unsafeAtomicAdd(gs + Gb.be + fe, gWe[ft][r]);
+      }
+    vec_accumulate_g<ET>(gs + Gb.g2[0], &ln2[0]);
+    vec_accumulate_g<ET>(gs + Gb.n2[0], &ln2[ET]);
+  });
+  (void)G;
+}
+
+template <int E, int H, int D, int A, int FF, int RT, typename WT>
+__global__ __launch_bounds__(128) void mixs_bwd_rec_pipe_kernel(MixsBwdArgs sa) {
+  static_assert(D == 2, "one wave per block of a depth-2 stack");
+  using Dm = MixDims<E, A>;
+  using Pd = MixsPipeDims<E, A>;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const MixerBwdArgs& args = sa.m;
+  const t2o_layout& L = args.f.L;
+  const t2o_layout& G = args.G;
+  const int na = RT == 1 ? args.f.na : A;
+  const int w = __builtin_amdgcn_readfirstlane(wave_id());  // 0: block 1, 1: block 0
+  float* X0 = smem + args.lds_w;
+  float* R = X0 + Dm::X0F;
+  float* gs = args.slabs + (size_t)(sa.slab0 + blockIdx.x) * G.grad_total;
+  const int T = args.f.net[0].T;
+  const Wts<WT> P0 = stage_weights(smem, args.f.net[0].pack, L, sizeof(WT) == 4 ? L.fwd_total : L.total, WT{}, false);
+  if (sa.t_hi == T) zero_flushed_regions(gs, G, false);
+  for (int i = threadIdx.x; i < Dm::X0F; i += 128) X0[i] = 0.f;
+  int* const flags = reinterpret_cast<int*>(R + Pd::REGION);
+  if (threadIdx.x < PAIR_FLAG_FLOATS) flags[threadIdx.x] = 0;
+  if (blockIdx.x == 0 && threadIdx.x < 64 && sa.t_hi == T) {  // zero each block's compact stream past its last record
+    using Rec = TapeRec<E, H, FF>;
+    const size_t nrec = (size_t)args.f.B * T * (na + 3), ctiles = (nrec + 15) / 16;
+    const int tail = (int)(ctiles * 16 - nrec) * Rec::SIZE;
+    for (int dd = 0; dd < D; ++dd) {
+      WT* z = static_cast<WT*>(args.tape) + ((size_t)dd * ctiles * 16 + nrec) * Rec::SIZE;
+      for (int i = threadIdx.x; i < tail; i += 64) z[i] = WT(0.f);
+    }
+  }
+  __syncthreads();
+  PairBarrier pb = PairBarrier::make(flags, w);
+  const int b = blockIdx.x;
+  if (w == 0) {
+    __builtin_amdgcn_s_setprio(1);  // (the head of the dependent chain, as the one-tile pipeline's block-1 wave)
+    mixs_pipe_block1<E, H, A, FF, WT>(sa, P0, L, G, gs, X0, R, b, pb, na);
+  } else {
+    mixs_pipe_block0<E, H, A, FF, WT>(sa, P0, L, G, gs, X0, R, b, pb, na);
+  }
+}
+
+// T2O_MIXS_REC=single: the one-wave recurrent backward (A/B, cross-check)
+inline bool mixs_rec_single() {
+  const char* e = getenv("T2O_MIXS_REC");
+  return e && e[0] == 's';
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 
 // When the split runs: multi-tile instances, a replay batch small enough that
@@ -802,7 +1126,23 @@ int mixs_launch_bwd(MixsBwdArgs& sa, int max_slabs, int* nslab, hipStream_t stre
       if (rc) return rc;
     }
   }
-  // the recurrence over the window
+  // the recurrence over the window: two waves per episode (one per block) where the
+  // block inputs are stored and the weights fit LDS beside the pair's buffers
+  if constexpr (D == 2) {
+    const int lds_wp = (int)((lds_weight_floats<WT>(L, sizeof(WT) == 4 ? L.fwd_total : L.total) + 15) / 16 * 16);
+    const size_t lds = sizeof(float) * ((size_t)lds_wp + MixsPipeDims<E, A>::PAIRF + PAIR_FLAG_FLOATS);
+    if (args.xmid && lds <= 160 * 1024 && !mixs_rec_single()) {
+      args.lds_w = lds_wp;
+      sa.slab0 = g2;
+      if (g2 + B > max_slabs) return T2O_EINVAL;
+      *nslab = g2 + B;
+      if (phase == 1) return 0;
+      auto kern = mixs_bwd_rec_pipe_kernel<E, H, D, A, FF, RT, WT>;
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(kern, dim3(B), dim3(128), lds, stream, sa);
+      return (int)hipGetLastError();
+    }
+  }
   {
     int waves;
     bool wlds;

@@ -118,7 +118,7 @@ def test_dp_two_ranks_equal_full_batch_learner():
     # ... and the two trajectories run freely: they separate only by summation
     # order, plus at most an O(1) move of one FFN unit's gradient once a ReLU tie
     # flips (the third update: 4.6e-5 on the parameters, tools/diag_dp_adam.py
-    # names the pre-activation, profiles/r5_dp/diag_dp.log); a systematic DP error
+    # names the pre-activation, profiles/r5_split/diag_dp.log); a systematic DP error
     # (Σ mask or Adam state handled per rank) moves every parameter by ~lr
     free = _learner(100, dev)
     for u in range(UPDATES):
