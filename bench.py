@@ -777,7 +777,7 @@ def main():
         return TDLearner(agent, mixer, target_update_interval=10 ** 9, precision=precision,
                          overlap=not args.serial, priorities_to_cpu=args.priorities == "cpu",
                          td_algo=args.td_algo, contract=args.contract, pipeline=pipe,
-                         pipeline_ranges=int(os.environ.get("T2O_PIPELINE_RANGES", "10")))
+                         pipeline_ranges=int(os.environ.get("T2O_PIPELINE_RANGES", "6")))
 
     learner = make_learner(args.dtype)
     batch, w = make_batch(B, T, A, seed=1 + rank, device=dev)

@@ -13,19 +13,30 @@
 //   ô_h = Σ_j p_hj o_j;  P_h = Σ_j p_hj;  z_h = p_h0 h + We ô_h + P_h b_e
 // then the shared post-attention half (t2o_block.hpp).  Observation features
 // live in the T-layout over a 16-padded F axis: lane group g holds
-// o_j[4g .. 4g+3], so every per-entity dot product is 4 FMAs plus a 4-lane
-// all-reduce, and no entity embedding is ever materialised.
+// o_j[4g .. 4g+3], so every per-entity dot product is a packed multiply-add pair
+// plus a 4-lane reduction, and no entity embedding is ever materialised.  The
+// reduction scatters (rsum4_n): lane group g ends with entity 4i + g's score, the
+// softmax runs on ceil(NE/4) values per lane, and only the probabilities are
+// broadcast back (bcast4_n) for ô — the same per-row math with a quarter of the
+// softmax VALU (16 entities: agent forward step loop 3608 -> 3067 instructions).
 #pragma once
 #include "t2o_block.hpp"
 
 namespace t2o {
 
+// Entity batches of the softmax: after the score reduction (rsum4_n) lane group g
+// holds entity 4i + g of batch i, so a lane keeps NB = ceil(NE / 4) probabilities
+// per head, not NE + 1.
+template <int NE>
+constexpr int agent_nb() { return (NE + 3) / 4; }
+
 template <int E, int H, int NE, int FF, bool LEAN>
 struct AgentCacheT {
-  static constexpr int ET = E / 16, HET = H * ET;
+  static constexpr int ET = E / 16, HET = H * ET, NB = agent_nb<NE>();
   typename std::conditional<LEAN, PostCacheLean<E, H, FF>, PostCache<E, H, FF>>::type post;
   f4 u[HET];
-  float p[H][NE + 1];
+  float p0[H];      // probability of token 0 (the hidden state)
+  float pr[H][NB];  // entity probabilities, scattered: lane group g holds entity 4i + g
   f4 oh[H];
   float Ps[H];
 };
@@ -43,13 +54,13 @@ using AgentCacheLean = AgentCacheT<E, H, NE, FF, true>;
 template <int E, int H, int NE, int FF, bool LEAN, typename WT>
 T2O_DEV void agent_attn_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const f4* h, const f4 (&o)[NE], int ne,
                             const f4* x, f4* z, AgentCacheT<E, H, NE, FF, LEAN>* cache) {
-  constexpr int ET = E / 16, HET = H * ET;
+  constexpr int ET = E / 16, HET = H * ET, NB = agent_nb<NE>();
   const float* be = P.v + L.be;
+  const int g = lane_g();
   f4 u[HET];
   matvec<HET, ET>(P.w + L.M[d], E, x, u, P.vol);
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
-    float p[NE + 1];
     f4 w;
     matvec<1, ET>(P.w + L.WeT, E, &u[hh * ET], &w, P.vol);
     float cpart = 0.f, s0part = 0.f;
@@ -57,48 +68,53 @@ T2O_DEV void agent_attn_fwd(const Wts<WT>& P, const t2o_layout& L, int d, const 
     for (int t = 0; t < ET; ++t) {
       const f4 bt = vec_t(be, t);
       const f4 ut = u[hh * ET + t];
-      cpart += (ut[0] * bt[0] + ut[1] * bt[1]) + (ut[2] * bt[2] + ut[3] * bt[3]);
-      s0part += (ut[0] * h[t][0] + ut[1] * h[t][1]) + (ut[2] * h[t][2] + ut[3] * h[t][3]);
+      cpart += dot4_pk(ut, bt);
+      s0part += dot4_pk(ut, h[t]);
     }
-    // [c, s_0, w·o_1 .. w·o_NE] reduced over the lane groups in one batch
-    float red[NE + 2];
-    red[0] = cpart;
-    red[1] = s0part;
+    float cs[2] = {cpart, s0part};  // [c, s_0] in every lane
+    allsum4_n(cs);
+    // entity scores w·o_j reduce-scattered: lane group g gets entity 4i + g, so the
+    // softmax's max / exp / sum run on NB values per lane instead of NE + 1
+    float sp[4 * NB], s[NB];
 #pragma unroll
-    for (int j = 0; j < NE; ++j) red[j + 2] = (w[0] * o[j][0] + w[1] * o[j][1]) + (w[2] * o[j][2] + w[3] * o[j][3]);
-    allsum4_n(red);
-    const float cval = red[0];
-    p[0] = red[1];
+    for (int j = 0; j < 4 * NB; ++j)
+      sp[j] = j < NE ? dot4_pk(w, o[j]) : 0.f;
+    rsum4_n(sp, s);
+    const float cval = cs[0], s0 = cs[1];
+    float m = s0;
 #pragma unroll
-    for (int j = 0; j < NE; ++j) p[j + 1] = j < ne ? red[j + 2] + cval : -INFINITY;
-    float m = p[0];
-#pragma unroll
-    for (int j = 1; j <= NE; ++j) m = fmaxf(m, p[j]);
-    float l = 0.f;
-#pragma unroll
-    for (int j = 0; j <= NE; ++j) {
-      p[j] = exp_fast(p[j] - m);
-      l += p[j];
+    for (int i = 0; i < NB; ++i) {
+      s[i] = 4 * i + g < ne ? s[i] + cval : -INFINITY;
+      m = fmaxf(m, s[i]);
     }
-    const float il = rcp_fast(l);
+    m = allmax4(m);
+    const float e0 = exp_fast(s0 - m);
+    float lp = 0.f;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      s[i] = exp_fast(s[i] - m);
+      lp += s[i];
+    }
+    const float le = allsum4(lp);  // Σ over the entities
+    const float il = rcp_fast(e0 + le);
+    const float p0 = e0 * il, Ps = le * il;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) s[i] *= il;
+    float pa[4 * NB];  // every entity's probability in every lane (ô = Σ p_j o_j)
+    bcast4_n(s, pa);
     f4 oh = zero4();
-    float Ps = 0.f;
 #pragma unroll
-    for (int j = 0; j <= NE; ++j) p[j] *= il;
-#pragma unroll
-    for (int j = 0; j < NE; ++j) {
-      oh += p[j + 1] * o[j];
-      Ps += p[j + 1];
-    }
+    for (int j = 0; j < NE; ++j) oh += pa[j] * o[j];
     f4 zz[ET];
     matvec<ET, 1>(P.w + L.We, 16, &oh, zz, P.vol);
 #pragma unroll
-    for (int t = 0; t < ET; ++t) z[hh * ET + t] = zz[t] + p[0] * h[t] + Ps * vec_t(be, t);
+    for (int t = 0; t < ET; ++t) z[hh * ET + t] = zz[t] + p0 * h[t] + Ps * vec_t(be, t);
     if (cache) {
       cache->oh[hh] = oh;
       cache->Ps[hh] = Ps;
+      cache->p0[hh] = p0;
 #pragma unroll
-      for (int j = 0; j <= NE; ++j) cache->p[hh][j] = p[j];
+      for (int i = 0; i < NB; ++i) cache->pr[hh][i] = s[i];
     }
   }
   if (cache) {
@@ -224,14 +240,14 @@ T2O_DEV void agent_attn_bwd(const Wts<WT>& P, const t2o_layout& L, float* __rest
   for (int hh = 0; hh < H; ++hh) {
     const f4* gzh = &gz[hh * ET];
     const f4* uh = &c.u[hh * ET];
-    const float p0 = c.p[hh][0];
+    const float p0 = c.p0[hh];
     // z_h = p0 h + We oh + Ps be
     float gp0p = 0.f, gPp = 0.f;
 #pragma unroll
     for (int t = 0; t < ET; ++t) {
       const f4 bt = vec_t(be, t);
-      gp0p += (gzh[t][0] * h[t][0] + gzh[t][1] * h[t][1]) + (gzh[t][2] * h[t][2] + gzh[t][3] * h[t][3]);
-      gPp += (gzh[t][0] * bt[0] + gzh[t][1] * bt[1]) + (gzh[t][2] * bt[2] + gzh[t][3] * bt[3]);
+      gp0p += dot4_pk(gzh[t], h[t]);
+      gPp += dot4_pk(gzh[t], bt);
       gh_in[t] += p0 * gzh[t];
       gbe[t] += c.Ps[hh] * gzh[t];
     }
@@ -248,31 +264,35 @@ T2O_DEV void agent_attn_bwd(const Wts<WT>& P, const t2o_layout& L, float* __rest
     } else {
       dw_accumulate_regs<ET, 1, BF>(gWe, gzh, &c.oh[hh], stage);
     }
-    // softmax backward over [token 0, entities]; [gP, gp_0, goh·o_j] reduced in one batch
-    float red[NE + 2];
-    red[0] = gPp;
-    red[1] = gp0p;
+    // softmax backward over [token 0, entities], the entity terms in the forward's
+    // scattered form (lane group g: entity 4i + g)
+    constexpr int NB = agent_nb<NE>();
+    float cs[2] = {gPp, gp0p};
+    allsum4_n(cs);
+    const float gP = cs[0], gp0 = cs[1];
+    float gpart[4 * NB], gq[NB];
 #pragma unroll
-    for (int j = 0; j < NE; ++j)
-      red[j + 2] = (goh[0] * o[j][0] + goh[1] * o[j][1]) + (goh[2] * o[j][2] + goh[3] * o[j][3]);
-    allsum4_n(red);
-    const float gP = red[0];
-    float gp[NE + 1];
-    gp[0] = red[1];
+    for (int j = 0; j < 4 * NB; ++j)
+      gpart[j] = j < NE ? dot4_pk(goh, o[j]) : 0.f;
+    rsum4_n(gpart, gq);
+    float dl = 0.f;
 #pragma unroll
-    for (int j = 0; j < NE; ++j) gp[j + 1] = red[j + 2] + gP;
-    float dot = 0.f;
-#pragma unroll
-    for (int j = 0; j <= NE; ++j) dot += c.p[hh][j] * gp[j];
-    const float gs0 = p0 * (gp[0] - dot);
-    f4 gw = zero4();
-    float gc = 0.f;
-#pragma unroll
-    for (int j = 0; j < NE; ++j) {
-      const float gsj = c.p[hh][j + 1] * (gp[j + 1] - dot);
-      gw += gsj * o[j];
-      gc += gsj;
+    for (int i = 0; i < NB; ++i) {
+      gq[i] += gP;
+      dl += c.pr[hh][i] * gq[i];
     }
+    const float dot = p0 * gp0 + allsum4(dl);
+    const float gs0 = p0 * (gp0 - dot);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) gq[i] = c.pr[hh][i] * (gq[i] - dot);
+    float gsa[4 * NB], gcl = 0.f;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) gcl += gq[i];
+    const float gc = allsum4(gcl);  // Σ_j gs_j
+    bcast4_n(gq, gsa);
+    f4 gw = zero4();
+#pragma unroll
+    for (int j = 0; j < NE; ++j) gw += gsa[j] * o[j];
     // s_h0 = u_h·h ; s_hj = (WeT u_h)·o_j + u_h·be
     f4 t1[ET];
     matvec<ET, 1>(P.w + L.We, 16, &gw, t1, P.vol);

@@ -91,6 +91,14 @@ T2O_DEV f4 mfma4(float a, float b, f4 acc) {
 
 T2O_DEV f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+// a·b over 4 features as (a0 b0 + a2 b2) + (a1 b1 + a3 b3): one v_pk_mul_f32, one
+// v_pk_fma_f32 and an add (the lane's partial of an entity score)
+T2O_DEV float dot4_pk(f4 a, f4 b) {
+  const f2 t = __builtin_elementwise_fma(a.zw, b.zw, a.xy * b.xy);
+  return t.x + t.y;
+}
+
 // e^x for softmax arguments (x <= 0, -inf allowed): one v_exp_f32 (2^y, ~1 ulp)
 // of y = x·log2(e) instead of libm expf's range-reduced ~10-instruction expansion.
 // Relative error ≈ |x|·2^-24 + 1 ulp, far inside the fp32 parity bar.
@@ -440,6 +448,34 @@ T2O_DEV void allsum4_n(float (&v)[N]) {
     i += 2;
   }
   if constexpr (N % 2) v[i] = allsum4(v[i]);
+}
+
+// The two halves of allsum4_n on their own.  rsum4_n: reduce-scatter, out[i] in
+// lane group g = the row total of v[4i + g] (same pairing, so the same bits as
+// allsum4 of that value) — a row's 4N values become N per lane, and elementwise
+// work on them (a softmax over entities) runs once instead of in all 4 lanes.
+// bcast4_n: the inverse, v[4i + k] = lane group k's in[i] in every lane.
+template <int N>
+T2O_DEV void rsum4_n(const float (&v)[4 * N], float (&out)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float ab = pair_sum16(v[4 * i], v[4 * i + 1]), cd = pair_sum16(v[4 * i + 2], v[4 * i + 3]);
+    const auto q = __builtin_amdgcn_permlane32_swap(f2u(ab), f2u(cd), false, false);
+    out[i] = u2f(q[0]) + u2f(q[1]);
+  }
+}
+template <int N>
+T2O_DEV void bcast4_n(const float (&in)[N], float (&v)[4 * N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const auto x = __builtin_amdgcn_permlane16_swap(f2u(in[i]), f2u(in[i]), false, false);
+    const auto y = __builtin_amdgcn_permlane32_swap(x[0], x[0], false, false);
+    const auto z = __builtin_amdgcn_permlane32_swap(x[1], x[1], false, false);
+    v[4 * i] = u2f(y[0]);
+    v[4 * i + 1] = u2f(z[0]);
+    v[4 * i + 2] = u2f(y[1]);
+    v[4 * i + 3] = u2f(z[1]);
+  }
 }
 
 // Sum over the 16 lanes of a row with DPP (VALU only); the total lands in the

@@ -56,7 +56,7 @@ class TDLearner:
     def __init__(self, agent, mixer, *, lr=1e-3, gamma=0.99, td_lambda=0.6, grad_norm_clip=10.0,
                  target_update_interval=200, optim_betas=(0.9, 0.999), optim_eps=1e-8, weight_decay=0.0,
                  detach_mixer_hidden=False, process_group=None, priorities_to_cpu=True, precision="fp32",
-                 overlap=True, td_algo="auto", contract="side", pipeline="auto", pipeline_ranges=10):
+                 overlap=True, td_algo="auto", contract="side", pipeline="auto", pipeline_ranges=6):
         # options first (a bad value fails here, not inside the first train())
         if precision not in ("fp32", "bf16"):
             raise ValueError("precision must be 'fp32' or 'bf16'")
