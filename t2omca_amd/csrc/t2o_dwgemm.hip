@@ -72,6 +72,10 @@ T2O_DEV void dw_vec_store(float* __restrict__ v, const float (&acc)[NT]) {
 
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 
+#ifndef T2O_DW_TG_A
+#define T2O_DW_TG_A 4
+#endif
+
 template <typename TT> struct DwTraits;
 template <> struct DwTraits<__bf16> { static constexpr int TG = 2, PADC = 2; };  // tiles per group, pad chunks
 template <> struct DwTraits<float> { static constexpr int TG = 1, PADC = 1; };
@@ -84,7 +88,9 @@ struct DwDims {
   static constexpr bool MN = R::GU >= 0;  // dM / dN operands on the tape
   static constexpr int ET = E / 16, HET = H * ET, FT = FF / 16, FH = FT / 2;
   static constexpr bool BF = sizeof(TT) == 2;
-  static constexpr int TG = DwTraits<TT>::TG;
+  // tiles per group: the lean agent record is a third of the full one, so its
+  // groups take more tiles (the same bytes in flight per workgroup)
+  static constexpr int TG = (FMT == 1 && BF) ? T2O_DW_TG_A : DwTraits<TT>::TG;
   static constexpr int PER = 16 / (int)sizeof(TT);          // elements per 16-B chunk
   static constexpr int CPR = R::SIZE / PER;                  // chunks per record
   static constexpr int CPT = RT * CPR;                       // chunks per tile (HBM: RT records)
@@ -182,6 +188,7 @@ struct DwRole<0, E, H, FF, D, TT, FMT> {
   using Frag = typename std::conditional<Dm::BF, bf4, f4>::type;
   f4 acc[Dm::HET][Dm::ET];  // dM[gu feature][x feature]
   float vq[Dm::ET];         // Q = Σ gr2 ⊙ x̂1
+  T2O_DEV void ready() {}
   T2O_DEV void init(const DwGemmArgs&, int, const TT*) {
 #pragma unroll
     for (int o = 0; o < Dm::HET; ++o)
@@ -224,6 +231,7 @@ struct DwRole<1, E, H, FF, D, TT, FMT> {
   using Frag = typename std::conditional<Dm::BF, bf4, f4>::type;
   f4 acc[Dm::ET][Dm::HET];  // dN[gres feature][z feature]
   float vbu[Dm::ET];
+  T2O_DEV void ready() {}
   T2O_DEV void init(const DwGemmArgs&, int, const TT*) {
 #pragma unroll
     for (int o = 0; o < Dm::ET; ++o) {
@@ -255,27 +263,39 @@ struct DwRole<1, E, H, FF, D, TT, FMT> {
   }
 };
 
-// FFN half HALF: recompute y = x̂1 ⊙ g1 + n1, f1 = W1 y + c1 and gf1 = [f1 > 0] ⊙
-// W2ᵀ gr2 for the half's FH feature tiles as [records x features] MFMA tiles
-// (lane (g, c) = records 4g..4g+3 of feature 16J + c — already the K-slice
-// layout of the contraction), then dW2[e][J] += gr2 ⊗ relu(f1) and
+// FFN part PART of NPART: recompute y = x̂1 ⊙ g1 + n1, f1 = W1 y + c1 and gf1 =
+// [f1 > 0] ⊙ W2ᵀ gr2 for the part's FH feature tiles as [records x features]
+// MFMA tiles (lane (g, c) = records 4g..4g+3 of feature 16J + c — already the
+// K-slice layout of the contraction), then dW2[e][J] += gr2 ⊗ relu(f1) and
 // P[J][e] += gf1 ⊗ x̂1 (t2o_unpack_grads makes dW1 of P).
 // Weight fragments: bf16 from the workgroup's LDS copy of the pack's
 // (swizzled) bf16 image; fp32 straight from the pack (L2-resident).
-template <int HALF, int E, int H, int FF, int D, typename TT, int FMT>
+// NPART 2: roles 2 / 3 of the full record (roles 0 / 1 contract dM, dN).
+// NPART 4: the lean agent record (TapeRecA: dM / dN were accumulated by the
+// BPTT) — all four waves of a block take an FFN quarter, with their weight
+// fragments in registers for the launch, and the record's vector sums ride
+// along (part 0: Q, part 1: d bu, part 2: d c2).  Round 4's split left two of
+// the four waves with only those sums: the agent contraction ran 0.275 ms for
+// 207 MB at the headline (0.75 TB/s, profiles/r4_h/prof/timeline.txt).
+template <int PART, int NPART, int E, int H, int FF, int D, typename TT, int FMT>
 struct DwFfn {
   using Dm = DwDims<E, H, FF, D, TT, 16, FMT>;
   using R = typename Dm::R;
-  static constexpr int ET = Dm::ET, FH = Dm::FH;
+  static constexpr int ET = Dm::ET, FH = Dm::FT / NPART;
+  static constexpr bool WREG = NPART == 4 && Dm::BF;  // weight fragments held in registers
+  static_assert(Dm::FT % NPART == 0, "FF must split into NPART parts of 16-feature tiles");
   using Frag = typename std::conditional<Dm::BF, bf4, f4>::type;
-  f4 acc1[FH][ET];  // P rows of this half
-  f4 acc2[ET][FH];  // dW2 columns of this half
+  f4 acc1[FH][ET];  // P rows of this part
+  f4 acc2[ET][FH];  // dW2 columns of this part
   float vc1[FH], vc2[ET];
+  float vq[ET], vbu[ET];  // NPART 4: Q (part 0), d bu (part 1)
   float c1v[FH];
   f4 g1r[ET], n1r[ET];  // fp32: LN1 affine of this lane's record-major features 16s + 4g .. +3
+  Frag w1r[WREG ? FH : 1][ET], w2r[WREG ? FH : 1][ET];
   const TT* wl;     // bf16: LDS W1 [FF][E] then W2ᵀ [FF][E] of this block
   const float* wsrc;
   int64_t o1, o2;
+  static constexpr bool DO_C2 = NPART == 2 ? PART == 0 : PART == 2;
   T2O_DEV void init(const DwGemmArgs& a, int d, const TT* wlds) {
     const int c = lane_c();
 #pragma unroll
@@ -285,17 +305,17 @@ struct DwFfn {
       for (int i = 0; i < ET; ++i) acc1[o][i] = acc2[i][o] = zero4();
     }
 #pragma unroll
-    for (int i = 0; i < ET; ++i) vc2[i] = 0.f;
+    for (int i = 0; i < ET; ++i) vc2[i] = vq[i] = vbu[i] = 0.f;
     wl = wlds + (size_t)d * 2 * FF * E;
     wsrc = a.pack;
     o1 = a.L.W1[d];
     o2 = a.L.W2T[d];
 #pragma unroll
-    for (int jt = 0; jt < FH; ++jt) c1v[jt] = a.pack[a.L.c1[d] + 16 * (HALF * FH + jt) + c];
+    for (int jt = 0; jt < FH; ++jt) c1v[jt] = a.pack[a.L.c1[d] + 16 * (PART * FH + jt) + c];
     if constexpr (Dm::BF) {  // the LDS W1 image carries g1; fold n1 into the bias
 #pragma unroll
       for (int jt = 0; jt < FH; ++jt) {
-        const float* w = a.pack + a.L.W1[d] + (int64_t)(16 * (HALF * FH + jt) + c) * E;
+        const float* w = a.pack + a.L.W1[d] + (int64_t)(16 * (PART * FH + jt) + c) * E;
         float acc = 0.f;
         for (int e = 0; e < E; ++e) acc = fmaf(w[e], a.pack[a.L.n1[d] + e], acc);
         c1v[jt] += acc;
@@ -310,9 +330,26 @@ struct DwFfn {
         }
     }
   }
-  // fragment of W (0: W1, 1: W2ᵀ): row 16J + c, features 16s + 4g .. +3
+  // after the first barrier (the LDS weight image is visible): the part's
+  // fragments into registers
+  T2O_DEV void ready() {
+    if constexpr (WREG) {
+#pragma unroll
+      for (int jt = 0; jt < FH; ++jt)
+#pragma unroll
+        for (int s2 = 0; s2 < ET; ++s2) {
+          w1r[jt][s2] = wfrag_lds(0, jt, s2);
+          w2r[jt][s2] = wfrag_lds(1, jt, s2);
+        }
+    }
+  }
   T2O_DEV Frag wfrag(int m, int jt, int s) const {
-    const int row = 16 * (HALF * FH + jt) + lane_c();
+    if constexpr (WREG) return m ? w2r[jt][s] : w1r[jt][s];
+    else return wfrag_lds(m, jt, s);
+  }
+  // fragment of W (0: W1, 1: W2ᵀ): row 16J + c, features 16s + 4g .. +3
+  T2O_DEV Frag wfrag_lds(int m, int jt, int s) const {
+    const int row = 16 * (PART * FH + jt) + lane_c();
     if constexpr (Dm::BF) {
       const TT* base = wl + (size_t)m * FF * E + (size_t)row * E;
       return ldb4(base + ((16 * s + 4 * lane_g()) ^ bf_swz(row, E)));
@@ -342,7 +379,9 @@ struct DwFfn {
       gr[s] = rslice<S>(t, R::GR2 + 16 * s);
       xk[s] = kslice<S>(t, R::XH1 + 16 * s);
       gk[s] = kslice<S>(t, R::GR2 + 16 * s);
-      if (HALF == 0) vc2[s] += bsum4(gk[s]);
+      if (DO_C2) vc2[s] += bsum4(gk[s]);
+      if (NPART == 4 && PART == 0) vq[s] += bdot4(gk[s], xk[s]);
+      if (NPART == 4 && PART == 1) vbu[s] += bsum4(kslice<S>(t, R::GRES + 16 * s));
     }
 #pragma unroll
     for (int jt = 0; jt < FH; ++jt) {
@@ -377,16 +416,33 @@ struct DwFfn {
     }
   }
   T2O_DEV void finish(const DwGemmArgs& a, float* slab, int d) {
-    dw_tiles_store<FH, ET>(slab + a.G.W1[d] + (int64_t)16 * HALF * FH * E, E, acc1);
-    dw_tiles_store<ET, FH>(slab + a.G.W2[d] + 16 * HALF * FH, FF, acc2);
-    dw_vec_store<FH>(slab + a.G.c1[d] + 16 * HALF * FH, vc1);
-    if (HALF == 0) dw_vec_store<ET>(slab + a.G.c2[d], vc2);
+    dw_tiles_store<FH, ET>(slab + a.G.W1[d] + (int64_t)16 * PART * FH * E, E, acc1);
+    dw_tiles_store<ET, FH>(slab + a.G.W2[d] + 16 * PART * FH, FF, acc2);
+    dw_vec_store<FH>(slab + a.G.c1[d] + 16 * PART * FH, vc1);
+    if (DO_C2) dw_vec_store<ET>(slab + a.G.c2[d], vc2);
+    if constexpr (NPART == 4 && PART == 0) {  // as role 0 of the full record
+      dw_vec_store<ET>(slab + a.G.g1[d], vq);
+      if (lane_g() == 0) {
+#pragma unroll
+        for (int i = 0; i < ET; ++i) slab[a.G.n1[d] + 16 * i + lane_c()] = 0.f;
+      }
+    }
+    if constexpr (NPART == 4 && PART == 1) dw_vec_store<ET>(slab + a.G.bu[d], vbu);
   }
 };
 template <int E, int H, int FF, int D, typename TT, int FMT>
-struct DwRole<2, E, H, FF, D, TT, FMT> : DwFfn<0, E, H, FF, D, TT, FMT> {};
+struct DwRole<2, E, H, FF, D, TT, FMT> : DwFfn<0, 2, E, H, FF, D, TT, FMT> {};
 template <int E, int H, int FF, int D, typename TT, int FMT>
-struct DwRole<3, E, H, FF, D, TT, FMT> : DwFfn<1, E, H, FF, D, TT, FMT> {};
+struct DwRole<3, E, H, FF, D, TT, FMT> : DwFfn<1, 2, E, H, FF, D, TT, FMT> {};
+// the lean agent record: four FFN quarters (roles 4 + q)
+template <int E, int H, int FF, int D, typename TT, int FMT>
+struct DwRole<4, E, H, FF, D, TT, FMT> : DwFfn<0, 4, E, H, FF, D, TT, FMT> {};
+template <int E, int H, int FF, int D, typename TT, int FMT>
+struct DwRole<5, E, H, FF, D, TT, FMT> : DwFfn<1, 4, E, H, FF, D, TT, FMT> {};
+template <int E, int H, int FF, int D, typename TT, int FMT>
+struct DwRole<6, E, H, FF, D, TT, FMT> : DwFfn<2, 4, E, H, FF, D, TT, FMT> {};
+template <int E, int H, int FF, int D, typename TT, int FMT>
+struct DwRole<7, E, H, FF, D, TT, FMT> : DwFfn<3, 4, E, H, FF, D, TT, FMT> {};
 
 // One wave's whole launch for its role (every role runs the same pipeline and
 // the same barrier sequence; the roles only differ in what they read).
@@ -413,6 +469,7 @@ T2O_DEV void dw_run(const DwGemmArgs& a, int wg, int nwg, TT* buf0, TT* buf1, co
   if (nj > 2) dw_load<Dm, TT>(a, wg, nwg, 2, r0);
   if (nj > 3) dw_load<Dm, TT>(a, wg, nwg, 3, r1);
   __syncthreads();
+  st.ready();
   for (int64_t j = 0; j < nj; j += 2) {
     compute(buf0);
     __syncthreads();
@@ -472,14 +529,23 @@ T2O_DEV void dw_gemm_wg(const DwGemmArgs& a, int wg, int nwg, float* smem) {
   // plus the W1/W2ᵀ reads) weigh about 2.7x roles 0/1 (12 MFMAs), so block 1
   // rotates its roles by two: every SIMD holds one light and one heavy role.
   const int d = w >> 2, role = (w + 2 * d) & 3;
-  // the heavy (FFN-half) wave issues first on its SIMD, the light one fills its
-  // gaps (A/B: mixer_dw 0.256 -> 0.249 ms; prioritising the light roles: no gain)
-  if (role >= 2) __builtin_amdgcn_s_setprio(1);
-  switch (role) {  // wave-uniform; the four paths issue the same barriers
-    case 0: dw_run<0, E, H, FF, D, TT, RT, FMT>(a, wg, nwg, buf0, buf1, wlds, d); break;
-    case 1: dw_run<1, E, H, FF, D, TT, RT, FMT>(a, wg, nwg, buf0, buf1, wlds, d); break;
-    case 2: dw_run<2, E, H, FF, D, TT, RT, FMT>(a, wg, nwg, buf0, buf1, wlds, d); break;
-    default: dw_run<3, E, H, FF, D, TT, RT, FMT>(a, wg, nwg, buf0, buf1, wlds, d); break;
+  if constexpr (FMT == 1) {  // lean agent record: four equal FFN quarters
+    switch (w & 3) {
+      case 0: dw_run<4, E, H, FF, D, TT, RT, FMT>(a, wg, nwg, buf0, buf1, wlds, d); break;
+      case 1: dw_run<5, E, H, FF, D, TT, RT, FMT>(a, wg, nwg, buf0, buf1, wlds, d); break;
+      case 2: dw_run<6, E, H, FF, D, TT, RT, FMT>(a, wg, nwg, buf0, buf1, wlds, d); break;
+      default: dw_run<7, E, H, FF, D, TT, RT, FMT>(a, wg, nwg, buf0, buf1, wlds, d); break;
+    }
+  } else {
+    // the heavy (FFN-half) wave issues first on its SIMD, the light one fills its
+    // gaps (A/B: mixer_dw 0.256 -> 0.249 ms; prioritising the light roles: no gain)
+    if (role >= 2) __builtin_amdgcn_s_setprio(1);
+    switch (role) {  // wave-uniform; the four paths issue the same barriers
+      case 0: dw_run<0, E, H, FF, D, TT, RT, FMT>(a, wg, nwg, buf0, buf1, wlds, d); break;
+      case 1: dw_run<1, E, H, FF, D, TT, RT, FMT>(a, wg, nwg, buf0, buf1, wlds, d); break;
+      case 2: dw_run<2, E, H, FF, D, TT, RT, FMT>(a, wg, nwg, buf0, buf1, wlds, d); break;
+      default: dw_run<3, E, H, FF, D, TT, RT, FMT>(a, wg, nwg, buf0, buf1, wlds, d); break;
+    }
   }
 }
 
