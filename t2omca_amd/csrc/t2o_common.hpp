@@ -127,11 +127,12 @@ T2O_DEV f4 mma_tile(const float* __restrict__ W, int ldw, int o, int i, f4 x, f4
 
 // y[0..OT) = W[16*OT x 16*IT] · x[0..IT)  (T-layout in, T-layout out)
 // (HOIST: see the bf16 overload; nothing to hoist in fp32)
-template <int OT, int IT, bool HOIST = true>
+// ACC: accumulate onto y (the caller's bias / residual) instead of zero
+template <int OT, int IT, bool HOIST = true, bool ACC = false>
 T2O_DEV void matvec(const float* __restrict__ W, int ldw, const f4* x, f4* y, bool = true) {
 #pragma unroll
   for (int o = 0; o < OT; ++o) {
-    f4 acc = zero4();
+    f4 acc = ACC ? y[o] : zero4();
 #pragma unroll
     for (int i = 0; i < IT; ++i) acc = mma_tile(W, ldw, o, i, x[i], acc);
     y[o] = acc;
@@ -167,8 +168,25 @@ typedef __bf16 bf4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef short s4v __attribute__((ext_vector_type(4)));
 
+// f32 -> bf16 (round to nearest even).  hipcc (ROCm 7.2, gfx950) emits the
+// packed v_cvt_pk_bf16_f32 only for an 8-wide conversion; a lone f4 is
+// scalarised (four conversions with a dummy second source + two v_perm_b32: six
+// VALU for two).  Convert f4 PAIRS through cvt8 wherever two tiles are
+// converted together (to_bf4_pairs, the 16x16x32 operands of matvec / KeyFrags).
 T2O_DEV bf4 to_bf4(f4 x) { return __builtin_convertvector(x, bf4); }
+T2O_DEV bf8 cvt8(f4 a, f4 b) { return __builtin_convertvector(__builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7), bf8); }
+T2O_DEV bf4 lo4(bf8 v) { return __builtin_shufflevector(v, v, 0, 1, 2, 3); }
+T2O_DEV bf4 hi4(bf8 v) { return __builtin_shufflevector(v, v, 4, 5, 6, 7); }
 T2O_DEV bf4 ldb4(const __bf16* p) { return *reinterpret_cast<const bf4*>(p); }
+// ReLU of bf16 operands on their bit patterns: a bf16 is negative (or -0) iff
+// its sign bit is set, i.e. iff it is negative as an int16, so max_i16(x, 0) is
+// relu(x) — packed v_pk_max_i16, bit-identical to rounding relu(x) in fp32
+// (both give +0 for every x <= 0).
+typedef short s8v __attribute__((ext_vector_type(8)));
+T2O_DEV bf8 relu_bf8(bf8 x) {
+  const s8v v = __builtin_bit_cast(s8v, x);
+  return __builtin_bit_cast(bf8, __builtin_elementwise_max(v, s8v{0, 0, 0, 0, 0, 0, 0, 0}));
+}
 // A weight fragment (4 bf16 of one image row).  From LDS it is a volatile
 // ds_read_b64: the compiler then loads each half of a 16x16x32 operand straight
 // into its registers instead of fusing the fragments of two rows into one
@@ -233,8 +251,18 @@ T2O_DEV f4 mma_tile(const __bf16* __restrict__ W, int ldw, int o, int i, f4 x, f
 }
 
 // y[0..OT) = W · x[0..IT), bf16 weights and operands, fp32 accumulate
-template <int OT, int IT, bool HOIST = T2O_SWZ_HOIST>
+template <int OT, int IT, bool HOIST = T2O_SWZ_HOIST, bool ACC = false>
+T2O_DEV void matvec_b(const __bf16* __restrict__ W, int ldw, const bf4* xb, f4* y, bool vol = true);
+template <int OT, int IT, bool HOIST = T2O_SWZ_HOIST, bool ACC = false>
 T2O_DEV void matvec(const __bf16* __restrict__ W, int ldw, const f4* x, f4* y, bool vol = true) {
+  bf4 xb[IT];
+#pragma unroll
+  for (int i = 0; i < IT; ++i) xb[i] = to_bf4(x[i]);
+  matvec_b<OT, IT, HOIST, ACC>(W, ldw, xb, y, vol);
+}
+// the same product from operands already in bf16 (xb: T-layout tiles)
+template <int OT, int IT, bool HOIST, bool ACC>
+T2O_DEV void matvec_b(const __bf16* __restrict__ W, int ldw, const bf4* xb, f4* y, bool vol) {
   // HOIST false (T2O_SWZ_HOIST 0: the mixer BPTT kernels, register-bound at two
   // waves per SIMD): the lane's row swizzle is derived per product from an opaque
   // lane id, since hoisted out of the step loop one register per distinct row
@@ -245,14 +273,11 @@ T2O_DEV void matvec(const __bf16* __restrict__ W, int ldw, const f4* x, f4* y, b
   int l = threadIdx.x;
   if (!HOIST) asm volatile("" : "+v"(l));
   const int c = l & 15, g = (l >> 4) & 3;
-  bf4 xb[IT];
-#pragma unroll
-  for (int i = 0; i < IT; ++i) xb[i] = to_bf4(x[i]);
   const int xs = bf_swz(c, ldw);
 #pragma unroll
   for (int o = 0; o < OT; ++o) {
     const __bf16* row = W + (size_t)(16 * o + c) * ldw;
-    f4 acc = zero4();
+    f4 acc = ACC ? y[o] : zero4();
 #pragma unroll
     for (int i = 0; i + 1 < IT; i += 2) {
       const __bf16* p0 = row + ((16 * i + 4 * g) ^ xs);

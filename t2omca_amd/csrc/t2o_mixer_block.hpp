@@ -32,71 +32,131 @@ struct MixerCache {
 // block (and by the backward's products):
 //   dot[kt][ft]  = X0[key 16kt + c][features 16ft + 4g .. +3]   (Sᵀ = X0 · v)
 //   comb[kt][ft] = X0[keys 16kt + 4g .. +3][feature 16ft + c]    (Zᵀ = X0ᵀ · w)
-// bf16 mode holds them as bf16 (4 VGPRs per 16x16 tile pair), fp32 as f32.
+// fp32 holds them as f32.  bf16 pairs the contraction's 16-wide K tiles into
+// 16x16x32 operands — dot8[kt][p] = (dot[kt][2p], dot[kt][2p+1]) over feature
+// tiles, comb8[p][ft] = (comb[2p][ft], comb[2p+1][ft]) over key tiles (an odd
+// feature-tile count's last tile alone in dot1; an odd key-tile count: every
+// comb tile alone in comb1) — so each product takes half the MFMAs
+// and its B operand (u_h, gz_h; the probabilities) converts 8-wide, i.e. packed
+// (to_bf4: the 4-wide conversions of round 4 cost six VALU per tile).
 template <int E, int KT, bool BF>
 struct KeyFrags {
-  static constexpr int ET = E / 16;
-  using Frag = typename std::conditional<BF, bf4, f4>::type;
-  Frag dot[KT][ET], comb[KT][ET];
+  // (an odd key-tile count keeps every comb tile unpaired: paired tiles plus a
+  // lone tail made the one-wave multi-tile BPTT disagree with the split kernels
+  // at 16 / 20 / 64 AGVs in bf16 — profiles/r5_bis/ — while 8, 13 and 40 AGVs,
+  // even counts, agree; the pairing's gain is at the headline's 2 key tiles)
+  static constexpr int ET = E / 16, EP = ET / 2, KP = (KT & 1) ? 0 : KT / 2;
+  static constexpr bool EO = ET & 1, KO = KT & 1;
+  static constexpr int N_EP = EP > 0 ? EP : 1, N_KP = KP > 0 ? KP : 1;
+  // fp32
+  f4 dot[BF ? 1 : KT][BF ? 1 : ET], comb[BF ? 1 : KT][BF ? 1 : ET];
+  // bf16
+  bf8 dot8[BF ? KT : 1][N_EP], comb8[BF ? N_KP : 1][ET];
+  bf4 dot1[BF && EO ? KT : 1], comb1[BF && KO ? KT : 1][ET];
   template <int LDX>
   T2O_DEV void load(const float* __restrict__ X0) {
     const int c = lane_c(), g = lane_g();
+    auto arow = [&](int kt, int ft) { return ld4(X0 + (16 * kt + c) * LDX + 16 * ft + 4 * g); };
+    auto bcol = [&](int kt, int ft) {
+      f4 b;
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt)
+      for (int s = 0; s < 4; ++s) b[s] = X0[(16 * kt + 4 * g + s) * LDX + 16 * ft + c];
+      return b;
+    };
+    if constexpr (BF) {
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt) {
+#pragma unroll
+        for (int p = 0; p < EP; ++p) dot8[kt][p] = cvt8(arow(kt, 2 * p), arow(kt, 2 * p + 1));
+        if constexpr (EO) dot1[kt] = to_bf4(arow(kt, ET - 1));
+      }
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) {
-        const f4 a = ld4(X0 + (16 * kt + c) * LDX + 16 * ft + 4 * g);
-        f4 b;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) b[s] = X0[(16 * kt + 4 * g + s) * LDX + 16 * ft + c];
-        if constexpr (BF) {
-          dot[kt][ft] = to_bf4(a);
-          comb[kt][ft] = to_bf4(b);
-        } else {
-          dot[kt][ft] = a;
-          comb[kt][ft] = b;
-        }
+        for (int p = 0; p < KP; ++p) comb8[p][ft] = cvt8(bcol(2 * p, ft), bcol(2 * p + 1, ft));
+        if constexpr (KO)
+#pragma unroll
+          for (int kt = 0; kt < KT; ++kt) comb1[kt][ft] = to_bf4(bcol(kt, ft));
       }
+    } else {
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int ft = 0; ft < ET; ++ft) {
+          dot[kt][ft] = arow(kt, ft);
+          comb[kt][ft] = bcol(kt, ft);
+        }
+    }
   }
 };
+
+T2O_DEV f4 mfma_b8(bf8 a, bf8 b, f4 acc) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0); }
 
 // Sᵀ-style product: out[kt] (keys 16kt+4g+r, query c) = Σ_f X0[key][f] v[f]
 template <int E, int KT, bool BF>
 T2O_DEV void keys_dot(const KeyFrags<E, KT, BF>& K, const f4* v, f4* out) {
+  using KF = KeyFrags<E, KT, BF>;
   constexpr int ET = E / 16;
+  if constexpr (BF) {
+    bf8 vb[KF::N_EP];
+    bf4 vt;
 #pragma unroll
-  for (int kt = 0; kt < KT; ++kt) {
-    f4 acc = zero4();
+    for (int p = 0; p < KF::EP; ++p) vb[p] = cvt8(v[2 * p], v[2 * p + 1]);
+    if constexpr (KF::EO) vt = to_bf4(v[ET - 1]);
 #pragma unroll
-    for (int ft = 0; ft < ET; ++ft) {
-      if constexpr (BF) {
-        acc = mfma_b16(K.dot[kt][ft], to_bf4(v[ft]), acc);
-      } else {
+    for (int kt = 0; kt < KT; ++kt) {
+      f4 acc = zero4();
+#pragma unroll
+      for (int p = 0; p < KF::EP; ++p) acc = mfma_b8(K.dot8[kt][p], vb[p], acc);
+      if constexpr (KF::EO) acc = mfma_b16(K.dot1[kt], vt, acc);
+      out[kt] = acc;
+    }
+  } else {
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      f4 acc = zero4();
+#pragma unroll
+      for (int ft = 0; ft < ET; ++ft)
 #pragma unroll
         for (int s = 0; s < 4; ++s) acc = mfma4(K.dot[kt][ft][s], v[ft][s], acc);
-      }
+      out[kt] = acc;
     }
-    out[kt] = acc;
   }
 }
 
 // Zᵀ-style product: out[ft] (features 16ft+4g+r, query c) = Σ_key X0[key][f] w[key]
 template <int E, int KT, bool BF>
 T2O_DEV void keys_combine(const KeyFrags<E, KT, BF>& K, const f4* w, f4* out) {
+  using KF = KeyFrags<E, KT, BF>;
   constexpr int ET = E / 16;
+  if constexpr (BF) {
+    bf8 wb[KF::N_KP];
+    bf4 wt[KF::KO ? KT : 1];
 #pragma unroll
-  for (int ft = 0; ft < ET; ++ft) {
-    f4 acc = zero4();
+    for (int p = 0; p < KF::KP; ++p) wb[p] = cvt8(w[2 * p], w[2 * p + 1]);
+    if constexpr (KF::KO)
 #pragma unroll
-    for (int kt = 0; kt < KT; ++kt) {
-      if constexpr (BF) {
-        acc = mfma_b16(K.comb[kt][ft], to_bf4(w[kt]), acc);
-      } else {
+      for (int kt = 0; kt < KT; ++kt) wt[kt] = to_bf4(w[kt]);
+#pragma unroll
+    for (int ft = 0; ft < ET; ++ft) {
+      f4 acc = zero4();
+#pragma unroll
+      for (int p = 0; p < KF::KP; ++p) acc = mfma_b8(K.comb8[p][ft], wb[p], acc);
+      if constexpr (KF::KO)
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt) acc = mfma_b16(K.comb1[kt][ft], wt[kt], acc);
+      out[ft] = acc;
+    }
+  } else {
+#pragma unroll
+    for (int ft = 0; ft < ET; ++ft) {
+      f4 acc = zero4();
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
         for (int s = 0; s < 4; ++s) acc = mfma4(K.comb[kt][ft][s], w[kt][s], acc);
-      }
+      out[ft] = acc;
     }
-    out[ft] = acc;
   }
 }
 
