@@ -160,6 +160,19 @@ T2O_DEV void keys_combine(const KeyFrags<E, KT, BF>& K, const f4* w, f4* out) {
   }
 }
 
+// scores of keys >= Lk (padding) to -inf; only key tiles that reach Lk hold
+// any (a wave-uniform test per tile), so a full tile costs no VALU
+template <int KT>
+T2O_DEV void key_mask(f4* s, int Lk, int g) {
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt)
+    if (16 * kt + 16 > Lk) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (16 * kt + 4 * g + r >= Lk) s[kt][r] = -INFINITY;
+    }
+}
+
 // HOIST: matvec's swizzle hoisting (t2o_common.hpp), true from the forward kernel
 template <int E, int H, int KT, int FF, bool CACHE, typename WT, bool HOIST = T2O_SWZ_HOIST>
 T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
@@ -175,14 +188,12 @@ T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
   for (int hh = 0; hh < H; ++hh) {
     f4 s[KT];
     keys_dot<E, KT, BF>(K, &u[hh * ET], s);
+    key_mask<KT>(s, Lk, g);
     float m = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (16 * kt + 4 * g + r >= Lk) s[kt][r] = -INFINITY;
-        m = fmaxf(m, s[kt][r]);
-      }
+      for (int r = 0; r < 4; ++r) m = fmaxf(m, s[kt][r]);
     m = allmax4(m);
     float l = 0.f;
 #pragma unroll
@@ -269,14 +280,12 @@ template <int E, int KT, bool BF>
 T2O_DEV void attn_probs(const KeyFrags<E, KT, BF>& K, const f4* u, int Lk, f4* s) {
   const int g = lane_g();
   keys_dot<E, KT, BF>(K, u, s);
+  key_mask<KT>(s, Lk, g);
   float m = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (16 * kt + 4 * g + r >= Lk) s[kt][r] = -INFINITY;
-      m = fmaxf(m, s[kt][r]);
-    }
+    for (int r = 0; r < 4; ++r) m = fmaxf(m, s[kt][r]);
   m = allmax4(m);
   float l = 0.f;
 #pragma unroll
