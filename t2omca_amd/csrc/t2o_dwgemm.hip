@@ -75,6 +75,11 @@ typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 #ifndef T2O_DW_TG_A
 #define T2O_DW_TG_A 4
 #endif
+// bf16: contract tiles in pairs (K = 32 records per 16x16x32 MFMA; 0 = one tile
+// per 16x16x16 MFMA, the round-4 form)
+#ifndef T2O_DW_PAIR
+#define T2O_DW_PAIR 1
+#endif
 
 template <typename TT> struct DwTraits;
 template <> struct DwTraits<__bf16> { static constexpr int TG = 2, PADC = 2; };  // tiles per group, pad chunks
@@ -168,6 +173,10 @@ T2O_DEV float bdot4(bf4 a, bf4 b) {
 }
 T2O_DEV float bdot4(f4 a, f4 b) { return (a[0] * b[0] + a[1] * b[1]) + (a[2] * b[2] + a[3] * b[3]); }
 
+// two bf16 slices as one 16x16x32 operand (K = the first's 4 values, then the second's)
+T2O_DEV bf8 cat8(bf4 a, bf4 b) { return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7); }
+T2O_DEV f4 kmma8(bf8 a, bf8 b, f4 acc) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0); }
+
 // acc += A-slice ⊗ B-slice over the tile's 16 records (K-slices as above)
 T2O_DEV f4 kmma(bf4 a, bf4 b, f4 acc) { return mfma_b16(a, b, acc); }
 T2O_DEV f4 kmma(f4 a, f4 b, f4 acc) {
@@ -213,6 +222,25 @@ struct DwRole<0, E, H, FF, D, TT, FMT> {
 #pragma unroll
     for (int i = 0; i < Dm::ET; ++i) vq[i] += bdot4(kslice<S>(t, R::GR2 + 16 * i), kslice<S>(t, R::XH1 + 16 * i));
   }
+  // bf16, two tiles at once: K = their 32 records, one 16x16x32 MFMA per product
+  T2O_DEV void tile2(const TT* ta, const TT* tb) {
+    constexpr int S = Dm::RSTR;
+    if constexpr (Dm::MN) {
+      bf8 xb[Dm::ET];
+#pragma unroll
+      for (int i = 0; i < Dm::ET; ++i) xb[i] = cat8(kslice<S>(ta, R::X + 16 * i), kslice<S>(tb, R::X + 16 * i));
+#pragma unroll
+      for (int o = 0; o < Dm::HET; ++o) {
+        const bf8 ab = cat8(kslice<S>(ta, R::GU + 16 * o), kslice<S>(tb, R::GU + 16 * o));
+#pragma unroll
+        for (int i = 0; i < Dm::ET; ++i) acc[o][i] = kmma8(ab, xb[i], acc[o][i]);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < Dm::ET; ++i)
+      vq[i] += bdot4(kslice<S>(ta, R::GR2 + 16 * i), kslice<S>(ta, R::XH1 + 16 * i)) +
+               bdot4(kslice<S>(tb, R::GR2 + 16 * i), kslice<S>(tb, R::XH1 + 16 * i));
+  }
   T2O_DEV void finish(const DwGemmArgs& a, float* slab, int d) {
     if constexpr (Dm::MN) dw_tiles_store<Dm::HET, Dm::ET>(slab + a.G.M[d], E, acc);
     dw_vec_store<Dm::ET>(slab + a.G.g1[d], vq);
@@ -254,6 +282,24 @@ struct DwRole<1, E, H, FF, D, TT, FMT> {
         const Frag zb = kslice<S>(t, R::Z + 16 * i);
 #pragma unroll
         for (int o = 0; o < Dm::ET; ++o) acc[o][i] = kmma(gb[o], zb, acc[o][i]);
+      }
+    }
+  }
+  T2O_DEV void tile2(const TT* ta, const TT* tb) {
+    constexpr int S = Dm::RSTR;
+    bf8 gb[Dm::ET];
+#pragma unroll
+    for (int o = 0; o < Dm::ET; ++o) {
+      const bf4 a = kslice<S>(ta, R::GRES + 16 * o), b = kslice<S>(tb, R::GRES + 16 * o);
+      gb[o] = cat8(a, b);
+      vbu[o] += bsum4(a) + bsum4(b);
+    }
+    if constexpr (Dm::MN) {
+#pragma unroll
+      for (int i = 0; i < Dm::HET; ++i) {
+        const bf8 zb = cat8(kslice<S>(ta, R::Z + 16 * i), kslice<S>(tb, R::Z + 16 * i));
+#pragma unroll
+        for (int o = 0; o < Dm::ET; ++o) acc[o][i] = kmma8(gb[o], zb, acc[o][i]);
       }
     }
   }
@@ -415,6 +461,53 @@ struct DwFfn {
       }
     }
   }
+  // bf16, two tiles at once: the recompute contracts both feature tiles in one
+  // 16x16x32 MFMA (K = 32 features), the weight-grad products both tiles' 32
+  // records, and relu(f1) / gf1 of the two tiles convert 8-wide (packed)
+  T2O_DEV void tile2(const TT* ta, const TT* tb) {
+    static_assert(ET == 2, "the paired recompute contracts the two 16-feature tiles of E = 32");
+    constexpr int S = Dm::RSTR;
+    const TT* tt[2] = {ta, tb};
+    bf8 yr[2], gr[2], xk[ET], gk[ET];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      yr[k] = cat8(rslice<S>(tt[k], R::XH1), rslice<S>(tt[k], R::XH1 + 16));
+      gr[k] = cat8(rslice<S>(tt[k], R::GR2), rslice<S>(tt[k], R::GR2 + 16));
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < ET; ++s2) {
+      const bf4 xa = kslice<S>(ta, R::XH1 + 16 * s2), xbb = kslice<S>(tb, R::XH1 + 16 * s2);
+      const bf4 ga = kslice<S>(ta, R::GR2 + 16 * s2), gbb = kslice<S>(tb, R::GR2 + 16 * s2);
+      xk[s2] = cat8(xa, xbb);
+      gk[s2] = cat8(ga, gbb);
+      if (DO_C2) vc2[s2] += bsum4(ga) + bsum4(gbb);
+      if (NPART == 4 && PART == 0) vq[s2] += bdot4(ga, xa) + bdot4(gbb, xbb);
+      if (NPART == 4 && PART == 1)
+        vbu[s2] += bsum4(kslice<S>(ta, R::GRES + 16 * s2)) + bsum4(kslice<S>(tb, R::GRES + 16 * s2));
+    }
+#pragma unroll
+    for (int jt = 0; jt < FH; ++jt) {
+      const bf8 w1 = cat8(wfrag(0, jt, 0), wfrag(0, jt, 1)), w2 = cat8(wfrag(1, jt, 0), wfrag(1, jt, 1));
+      f4 fr[2], gf[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const f4 f1 = kmma8(yr[k], w1, zero4()), gp = kmma8(gr[k], w2, zero4());
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = f1[r] + c1v[jt];
+          fr[k][r] = fmaxf(v, 0.f);
+          gf[k][r] = v > 0.f ? gp[r] : 0.f;
+        }
+        vc1[jt] += (gf[k][0] + gf[k][1]) + (gf[k][2] + gf[k][3]);
+      }
+      const bf8 frb = cvt8(fr[0], fr[1]), gfb = cvt8(gf[0], gf[1]);
+#pragma unroll
+      for (int e = 0; e < ET; ++e) {
+        acc2[e][jt] = kmma8(gk[e], frb, acc2[e][jt]);  // dW2[e][J] += gr2 ⊗ relu(f1)
+        acc1[jt][e] = kmma8(gfb, xk[e], acc1[jt][e]);  // P[J][e] += gf1 ⊗ x̂1
+      }
+    }
+  }
   T2O_DEV void finish(const DwGemmArgs& a, float* slab, int d) {
     dw_tiles_store<FH, ET>(slab + a.G.W1[d] + (int64_t)16 * PART * FH * E, E, acc1);
     dw_tiles_store<ET, FH>(slab + a.G.W2[d] + 16 * PART * FH, FF, acc2);
@@ -455,10 +548,18 @@ T2O_DEV void dw_run(const DwGemmArgs& a, int wg, int nwg, TT* buf0, TT* buf1, co
   DwRole<ROLE, E, H, FF, D, TT, FMT> st;
   st.init(a, d, wlds);
   auto compute = [&](const TT* buf) {
+    if constexpr (Dm::BF && Dm::TG % 2 == 0 && E == 32 && T2O_DW_PAIR) {  // tile pairs: 16x16x32 products
 #pragma unroll
-    for (int tt = 0; tt < Dm::TG; ++tt) {
-      st.tile(buf + (d * Dm::TG + tt) * Dm::TSTR);
-      T2O_FENCE();  // keep the next tile's LDS reads from being hoisted over these MFMAs
+      for (int tt = 0; tt < Dm::TG; tt += 2) {
+        st.tile2(buf + (d * Dm::TG + tt) * Dm::TSTR, buf + (d * Dm::TG + tt + 1) * Dm::TSTR);
+        T2O_FENCE();
+      }
+    } else {
+#pragma unroll
+      for (int tt = 0; tt < Dm::TG; ++tt) {
+        st.tile(buf + (d * Dm::TG + tt) * Dm::TSTR);
+        T2O_FENCE();  // keep the next tile's LDS reads from being hoisted over these MFMAs
+      }
     }
   };
   u4v r0[Dm::NLD], r1[Dm::NLD];
