@@ -46,6 +46,10 @@ def test_td_update_bit_reproducible_across_runs(A, B, T, precision):
         assert torch.isfinite(a).all(), name
         ndiff = int((a != b).sum())
         print(f"A={A} B={B} T={T} {precision} {name}: {ndiff} differing elements of {a.numel()}")
+        if ndiff and name == "grad":  # where they sit: [agent params | mixer params | Σ mask]
+            idx = torch.nonzero(a != b).flatten().cpu()
+            print(f"  differing indices {int(idx.min())}..{int(idx.max())} (agent params {learner.na}, "
+                  f"mixer {learner.nm}); first {idx[:8].tolist()}; max |diff| {float((a - b).abs().max()):.3g}")
         assert torch.equal(a, b), (name, ndiff)
 
 
