@@ -13,3 +13,6 @@ echo "== profile"
 bash tools/profile_box.sh "$TAG/prof" || exit 1
 echo "== configs"
 bash tools/configs_box.sh "$TAG/configs" || exit 1
+echo "== SQ counters"
+bash tools/pmc_sq_box.sh "$TAG/sq" || exit 1
+head -8 "gpurun_out/$TAG/sq/sq_summary.csv" | cut -c1-200
