@@ -409,6 +409,12 @@ int t2o_probe_lane_ops(const float* in, float* out, void* stream);
  * evaluate (tests/test_gpu_primitives.py checks them element by element). */
 int t2o_probe_posf(const float* x, int n, int pos_func, float beta, float* out, void* stream);
 
+/* Diagnostic: the agent softmax's reduce-scatter / broadcast halves of the batched
+ * 4-lane all-reduce, the packed 4-feature dot product and the 8-wide bf16
+ * conversion with the bit-pattern ReLU, on in[64]; writes 23 x 64 results
+ * (tests/test_gpu_primitives.py). */
+int t2o_probe_scatter_ops(const float* in, float* out, void* stream);
+
 /* Diagnostic: the XOR (in bf16 elements, a multiple of 8) applied to the
  * columns of row `row` of a bf16 weight-image matrix with row length ld: element
  * (r, col) of the image sits at r*ld + (col ^ t2o_bf_swz(r, ld)). */

@@ -123,6 +123,7 @@ EXPORTS = {
                       [ctypes.c_float] * 3 + [ctypes.c_int64] + [ctypes.c_void_p] * 3),
     "t2o_adam_workspace_floats": (ctypes.c_int, []),
     "t2o_probe_lane_ops": (ctypes.c_int, [ctypes.c_void_p] * 3),
+    "t2o_probe_scatter_ops": (ctypes.c_int, [ctypes.c_void_p] * 3),
     "t2o_probe_posf": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_void_p,
                                       ctypes.c_void_p]),
     "t2o_bf_swz": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
@@ -147,7 +148,7 @@ EXPORTS = {
 
 # exports only tests / tools call (never on the product path), and the newest
 # reporting export: an older build loaded under A/B timing (T2O_LIB) may lack them
-_DIAGNOSTIC = {"t2o_bf_swz", "t2o_probe_lane_ops", "t2o_probe_posf", "t2o_layout_instance", "t2o_abi_version", "t2o_td_loss_ex2",
+_DIAGNOSTIC = {"t2o_bf_swz", "t2o_probe_lane_ops", "t2o_probe_scatter_ops", "t2o_probe_posf", "t2o_layout_instance", "t2o_abi_version", "t2o_td_loss_ex2",
                "t2o_bwd_tape_contract_pair"}
 
 _lib = None

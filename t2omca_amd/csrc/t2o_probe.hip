@@ -57,3 +57,40 @@ extern "C" int t2o_probe_posf(const float* x, int n, int pos_func, float beta, f
                      beta, out);
   return (int)hipGetLastError();
 }
+
+// The reduce-scatter / broadcast halves of the batched all-reduce (the agent's
+// scattered softmax), the packed 4-feature dot product, and the 8-wide bf16
+// conversion with the bit-pattern ReLU (tests/test_gpu_primitives.py).
+// out rows: 0-1 rsum4_n of 8 values, 2-9 bcast4_n of them, 10-17 allsum4_n of the
+// same 8 values, 18 dot4_pk, 19-22 relu_bf8(cvt8(a, b)) as packed bf16 words.
+namespace {
+__global__ void probe_scatter_kernel(const float* __restrict__ in, float* __restrict__ out) {
+  const int l = threadIdx.x;
+  float v[8], a8[8], r[2], bc[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = a8[k] = in[(l + 5 * k) % 64] * (float)(k + 1);
+  rsum4_n(v, r);
+  bcast4_n(r, bc);
+  allsum4_n(a8);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) out[k * 64 + l] = r[k];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    out[(2 + k) * 64 + l] = bc[k];
+    out[(10 + k) * 64 + l] = a8[k];
+  }
+  const f4 x{in[l], in[(l + 1) % 64], in[(l + 2) % 64], in[(l + 3) % 64]};
+  const f4 y{in[(l + 17) % 64], in[(l + 29) % 64], in[(l + 41) % 64], in[(l + 53) % 64]};
+  out[18 * 64 + l] = dot4_pk(x, y);
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  const u4 w = __builtin_bit_cast(u4, relu_bf8(cvt8(x, y)));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) out[(19 + k) * 64 + l] = __uint_as_float(w[k]);
+}
+}  // namespace
+
+extern "C" int t2o_probe_scatter_ops(const float* in, float* out, void* stream) {
+  if (!in || !out) return T2O_EINVAL;
+  hipLaunchKernelGGL(probe_scatter_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, in, out);
+  return (int)hipGetLastError();
+}

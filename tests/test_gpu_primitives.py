@@ -36,6 +36,34 @@ def test_lane_primitives():
     torch.testing.assert_close(out[6:13], b.view(7, 4, 16).sum(1).repeat(1, 4), rtol=1e-6, atol=1e-6)
 
 
+def test_scatter_dot_and_conversion_primitives():
+    """rsum4_n / bcast4_n (the agent's scattered softmax), dot4_pk, and relu_bf8(cvt8)."""
+    require_gpu()
+    from t2omca_amd._lib import check, lib, ptr, stream_ptr
+    x = torch.randn(64, generator=torch.Generator().manual_seed(1)).cuda()
+    out = torch.full((23 * 64,), float("nan"), device="cuda")
+    check(lib().t2o_probe_scatter_ops(ptr(x), ptr(out), stream_ptr()), "probe_scatter")
+    torch.cuda.synchronize()
+    out, xc = out.cpu().view(23, 64), x.cpu()
+    v = torch.stack([xc[(torch.arange(64) + 5 * k) % 64] * (k + 1) for k in range(8)])  # [k][lane]
+    tot = v.view(8, 4, 16).sum(1)                   # [k][c]: the row totals
+    g = torch.arange(64) // 16
+    for i in range(2):                             # lane group g holds value 4i + g
+        torch.testing.assert_close(out[i], tot[4 * i + g, torch.arange(64) % 16], rtol=1e-6, atol=1e-6)
+    # broadcast after scatter = the batched all-reduce, bit for bit
+    assert torch.equal(out[2:10], out[10:18])
+    torch.testing.assert_close(out[10:18], tot.repeat(1, 4), rtol=1e-6, atol=1e-6)
+    idx = torch.arange(64)
+    a = torch.stack([xc[(idx + k) % 64] for k in range(4)])
+    b = torch.stack([xc[(idx + k) % 64] for k in (17, 29, 41, 53)])
+    torch.testing.assert_close(out[18], (a * b).sum(0), rtol=1e-6, atol=1e-6)
+    # relu(bf16(a, b)) packed two per word, element order a0..a3, b0..b3
+    ref = torch.relu(torch.cat([a, b]).to(torch.bfloat16)).view(torch.int16).to(torch.int32) & 0xFFFF  # [8][lane]
+    words = out[19:23].contiguous().view(torch.int32)
+    got = torch.stack([words[k // 2] >> (16 * (k % 2)) & 0xFFFF for k in range(8)])
+    assert torch.equal(got, ref), int((got != ref).sum())
+
+
 @pytest.mark.parametrize("beta", [1.0, 0.5, 2.0])
 def test_softplus_head_elementwise(beta):
     """The mixing head's softplus (n_transf_mixer.py:96-97, torch's Softplus with
