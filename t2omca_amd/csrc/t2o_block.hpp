@@ -62,11 +62,14 @@ T2O_DEV void ffn_out_product(const Wts<WT>& P, int64_t off, int ld, const f4* f1
   }
 }
 
+#ifndef T2O_BF_BACC
+#define T2O_BF_BACC 1
+#endif
 // r1 = N z + bu + x, y = LN1(r1), f1 = W1 y + c1 (bf16: bias-first accumulation)
 template <int ET, int HET, int FT, bool HOIST, typename WT>
 T2O_DEV void ffn_half(const Wts<WT>& P, const t2o_layout& L, int d, const f4* z, const f4* x, f4* r1, f4* y,
                       f4* xh1, float& rs1, f4* f1) {
-  constexpr bool BACC = sizeof(WT) == 2;
+  constexpr bool BACC = sizeof(WT) == 2 && T2O_BF_BACC;
   if constexpr (BACC) {
 #pragma unroll
     for (int t = 0; t < ET; ++t) r1[t] = vec_t(P.v + L.bu[d], t) + x[t];

@@ -39,20 +39,23 @@ struct MixerCache {
 // comb tile alone in comb1) — so each product takes half the MFMAs
 // and its B operand (u_h, gz_h; the probabilities) converts 8-wide, i.e. packed
 // (to_bf4: the 4-wide conversions of round 4 cost six VALU per tile).
+#ifndef T2O_KF_PAIR
+#define T2O_KF_PAIR 1
+#endif
 template <int E, int KT, bool BF>
 struct KeyFrags {
   // (an odd key-tile count keeps every comb tile unpaired: paired tiles plus a
   // lone tail made the one-wave multi-tile BPTT disagree with the split kernels
   // at 16 / 20 / 64 AGVs in bf16 — profiles/r5_bis/ — while 8, 13 and 40 AGVs,
   // even counts, agree; the pairing's gain is at the headline's 2 key tiles)
-  static constexpr int ET = E / 16, EP = ET / 2, KP = (KT & 1) ? 0 : KT / 2;
-  static constexpr bool EO = ET & 1, KO = KT & 1;
-  static constexpr int N_EP = EP > 0 ? EP : 1, N_KP = KP > 0 ? KP : 1;
+  static constexpr int ET = E / 16, EP = T2O_KF_PAIR ? ET / 2 : 0, KP = (KT & 1) || !T2O_KF_PAIR ? 0 : KT / 2;
+  static constexpr bool EO = EP * 2 != ET, KO = KP * 2 != KT;
+  static constexpr int N_EP = EP > 0 ? EP : 1, N_KP = KP > 0 ? KP : 1, EU = ET - 2 * EP;  // EU unpaired feature tiles
   // fp32
   f4 dot[BF ? 1 : KT][BF ? 1 : ET], comb[BF ? 1 : KT][BF ? 1 : ET];
   // bf16
   bf8 dot8[BF ? KT : 1][N_EP], comb8[BF ? N_KP : 1][ET];
-  bf4 dot1[BF && EO ? KT : 1], comb1[BF && KO ? KT : 1][ET];
+  bf4 dot1[BF && EO ? KT : 1][EO ? EU : 1], comb1[BF && KO ? KT : 1][ET];
   template <int LDX>
   T2O_DEV void load(const float* __restrict__ X0) {
     const int c = lane_c(), g = lane_g();
@@ -68,7 +71,9 @@ struct KeyFrags {
       for (int kt = 0; kt < KT; ++kt) {
 #pragma unroll
         for (int p = 0; p < EP; ++p) dot8[kt][p] = cvt8(arow(kt, 2 * p), arow(kt, 2 * p + 1));
-        if constexpr (EO) dot1[kt] = to_bf4(arow(kt, ET - 1));
+        if constexpr (EO)
+#pragma unroll
+          for (int u = 0; u < EU; ++u) dot1[kt][u] = to_bf4(arow(kt, 2 * EP + u));
       }
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) {
@@ -99,16 +104,20 @@ T2O_DEV void keys_dot(const KeyFrags<E, KT, BF>& K, const f4* v, f4* out) {
   constexpr int ET = E / 16;
   if constexpr (BF) {
     bf8 vb[KF::N_EP];
-    bf4 vt;
+    bf4 vt[KF::EO ? KF::EU : 1];
 #pragma unroll
     for (int p = 0; p < KF::EP; ++p) vb[p] = cvt8(v[2 * p], v[2 * p + 1]);
-    if constexpr (KF::EO) vt = to_bf4(v[ET - 1]);
+    if constexpr (KF::EO)
+#pragma unroll
+      for (int u = 0; u < KF::EU; ++u) vt[u] = to_bf4(v[2 * KF::EP + u]);
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) {
       f4 acc = zero4();
 #pragma unroll
       for (int p = 0; p < KF::EP; ++p) acc = mfma_b8(K.dot8[kt][p], vb[p], acc);
-      if constexpr (KF::EO) acc = mfma_b16(K.dot1[kt], vt, acc);
+      if constexpr (KF::EO)
+#pragma unroll
+        for (int u = 0; u < KF::EU; ++u) acc = mfma_b16(K.dot1[kt][u], vt[u], acc);
       out[kt] = acc;
     }
   } else {
