@@ -169,17 +169,17 @@ T2O_DEV void keys_combine(const KeyFrags<E, KT, BF>& K, const f4* w, f4* out) {
   }
 }
 
-// scores of keys >= Lk (padding) to -inf; only key tiles that reach Lk hold
-// any (a wave-uniform test per tile), so a full tile costs no VALU
+// scores of keys >= Lk (padding) to -inf, per element and branch-free: a
+// wave-uniform "does this tile reach Lk" test in front of each tile measured
+// slower where Lk is a run-time value (32 AGVs, five key tiles: mixer_bwd 7.49 vs
+// 6.56 ms, profiles/r5_km/) and equal at the exact 8-AGV instance
 template <int KT>
 T2O_DEV void key_mask(f4* s, int Lk, int g) {
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt)
-    if (16 * kt + 16 > Lk) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (16 * kt + 4 * g + r >= Lk) s[kt][r] = -INFINITY;
-    }
+    for (int r = 0; r < 4; ++r)
+      if (16 * kt + 4 * g + r >= Lk) s[kt][r] = -INFINITY;
 }
 
 // HOIST: matvec's swizzle hoisting (t2o_common.hpp), true from the forward kernel
