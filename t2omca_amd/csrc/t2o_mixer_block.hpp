@@ -176,6 +176,9 @@ T2O_DEV void keys_combine(const KeyFrags<E, KT, BF>& K, const f4* w, f4* out) {
 // per-tile test: its branch-free build returned wrong gradients from the
 // capacity-64 instances (40 / 63 AGVs, profiles/r5_final4/pytest.log) although the
 // two forms mask the same elements; not root-caused
+#ifndef T2O_KM_FP32_FLAT  // diagnostic: bit 0 flat fp32 mask in mixer_block_fwd, bit 1 in attn_probs
+#define T2O_KM_FP32_FLAT 0
+#endif
 template <int KT, bool TILE_TEST>
 T2O_DEV void key_mask(f4* s, int Lk, int g) {
 #pragma unroll
@@ -202,7 +205,7 @@ T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
   for (int hh = 0; hh < H; ++hh) {
     f4 s[KT];
     keys_dot<E, KT, BF>(K, &u[hh * ET], s);
-    key_mask<KT, !BF>(s, Lk, g);
+    key_mask<KT, !BF && !(T2O_KM_FP32_FLAT & 1)>(s, Lk, g);
     float m = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt)
@@ -294,7 +297,7 @@ template <int E, int KT, bool BF>
 T2O_DEV void attn_probs(const KeyFrags<E, KT, BF>& K, const f4* u, int Lk, f4* s) {
   const int g = lane_g();
   keys_dot<E, KT, BF>(K, u, s);
-  key_mask<KT, !BF>(s, Lk, g);
+  key_mask<KT, !BF && !(T2O_KM_FP32_FLAT & 2)>(s, Lk, g);
   float m = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt)
