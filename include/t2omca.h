@@ -211,6 +211,12 @@ int t2o_agent_unroll_bwd_range(const t2o_layout* L, const float* pack,
  * registers and flushed into the slabs, the tape holds only the FFN / LN1 /
  * unify-bias operands.  Pass it to t2o_bwd_tape_contract_ex. */
 int t2o_agent_bwd_tape_format(const t2o_layout* L, int has_hmid);
+/* 1 when t2o_agent_unroll_bwd_range accepts a partial step range for this layout
+ * (has_hmid: the call passes hmid): the two-wave pipelined BPTT runs it (depth 2,
+ * its LDS fits, T2O_AGENT_BWD is not "single").  Otherwise 0, and the one-wave
+ * kernel takes only the whole unroll (a partial range returns T2O_EUNSUPPORTED).
+ * The learner's pipelined update (step ranges on two streams) asks this first. */
+int t2o_agent_bwd_ranges(const t2o_layout* L, int has_hmid);
 
 /* Mixer unroll forward for up to two networks (online + target) in one
  * launch; one wave per episode.  states[b][t][n_ent*F] (element strides

@@ -104,6 +104,7 @@ EXPORTS = {
                                                   ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                                   ctypes.c_void_p]),
     "t2o_agent_bwd_tape_format": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_int]),
+    "t2o_agent_bwd_ranges": (ctypes.c_int, [ctypes.POINTER(Layout), ctypes.c_int]),
     "t2o_td_loss": (ctypes.c_int, [ctypes.c_void_p] * 3 + [ctypes.c_int64] * 2 + [ctypes.c_void_p] +
                     [ctypes.c_int64] * 2 + [ctypes.c_void_p] + [ctypes.c_int64] * 2 +
                     [ctypes.c_void_p] + [ctypes.c_float] * 3 + [ctypes.c_void_p] * 4 +

@@ -69,6 +69,7 @@ __global__ __launch_bounds__(64 * AG_FWD_WAVES) __attribute__((amdgpu_waves_per_
 void agent_fwd_kernel(AgentFwdArgs args) {
   constexpr int ET = E / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   const AgentNet net = args.net[blockIdx.y];
   const t2o_layout& L = args.L;
   // the forward section of the pack lives in LDS for the whole unroll (when it fits)
@@ -259,6 +260,7 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
   constexpr int STAGE = StageDims<1>::FLOATS;
   using Rec = TapeRec<E, H, FF>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   const t2o_layout& L = args.L;
   const t2o_layout& G = args.G;
   // the forward section of the pack; transposed products read it transposed (matvec_tr)
@@ -431,12 +433,9 @@ __global__ __launch_bounds__(64 * AG_BWD_WAVES) void agent_bwd_kernel(AgentBwdAr
 // phase.  The backward of a block is the same code as in the single-wave
 // kernel, so records, slabs and the head grads are identical in meaning.
 // T2O_AGENT_BWD=single selects the single-wave kernel (A/B timing, parity cross-check)
-inline bool agent_bwd_single_wave() {
-  static const bool single = [] {
-    const char* e = getenv("T2O_AGENT_BWD");
-    return e && e[0] == 's';
-  }();
-  return single;
+inline bool agent_bwd_single_wave() {  // (read per call: a test switches it within one process)
+  const char* e = getenv("T2O_AGENT_BWD");
+  return e && e[0] == 's';
 }
 
 constexpr int AGP_TILES = AG_BWD_WAVES;  // tiles per workgroup (same slab count as the single-wave kernel)
@@ -477,6 +476,7 @@ __global__ __launch_bounds__(64 * 2 * AGP_TILES) void agent_bwd_pipe_kernel(Agen
   // written by the recompute phase) unless the entities are streamed in chunks
   using Cache = typename std::conditional<CHUNK, AgentCacheCh<E, H, NE, FF>, AgentCacheLean<E, H, NE, FF>>::type;
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   const int64_t nw = L.fwd_total;
   const int lds_w = (int)((lds_weight_floats<WT>(L, nw) + 15) / 16 * 16);
   // wave-uniform by construction; readfirstlane tells the compiler, so the block's
@@ -894,6 +894,16 @@ extern "C" int t2o_agent_bwd_tape_format(const t2o_layout* L, int has_hmid) {
                      fmt = (L->prec ? bwd_tape_format<E_, H_, D_, NE_, FF_, RT_, __bf16>(*L, has_hmid != 0)
                                     : bwd_tape_format<E_, H_, D_, NE_, FF_, RT_, float>(*L, has_hmid != 0)));
   return fmt;
+}
+
+extern "C" int t2o_agent_bwd_ranges(const t2o_layout* L, int has_hmid) {
+  if (!L || L->kind != 0) return T2O_EINVAL;
+  if (L->generic) return 0;
+  int ok = 0;
+  T2O_DISPATCH_AGENT(L->E, L->H, L->D, L->n_ent, L->FF,
+                     ok = (L->prec ? bwd_uses_pipe<E_, H_, D_, NE_, FF_, RT_, __bf16>(*L, has_hmid != 0)
+                                   : bwd_uses_pipe<E_, H_, D_, NE_, FF_, RT_, float>(*L, has_hmid != 0)));
+  return ok ? 1 : 0;
 }
 
 extern "C" int t2o_agent_bwd_max_slabs(int B, int A) {

@@ -85,6 +85,30 @@ __device__ long long t2o_prof_buf[128 * 8 * 4];  // [slot][wave][delta]
   } while (0)
 #endif
 
+// Debug builds only (python -m t2omca_amd.build --debug-poison): every kernel
+// first fills its launch's whole dynamic LDS allocation with 0xFFFFFFFF (a NaN
+// in fp32 and in both bf16 halves), so a read of LDS no code of the launch wrote
+// turns into a NaN in the results instead of whatever the previous workgroup on
+// that CU left there.  The group segment size comes from the dispatch packet
+// (hsa_kernel_dispatch_packet_t.group_segment_size, byte offset 28).
+#ifndef T2O_DEBUG_POISON
+#define T2O_DEBUG_POISON 0
+#endif
+#if T2O_DEBUG_POISON && defined(__HIP_DEVICE_COMPILE__)
+#define T2O_LDS_POISON(smem)                                                                          \
+  do {                                                                                               \
+    const uint32_t seg_ = reinterpret_cast<const uint32_t*>(__builtin_amdgcn_dispatch_ptr())[7];     \
+    const uint32_t n_ = (seg_ - __builtin_amdgcn_groupstaticsize()) / 4;                             \
+    const uint32_t nthr_ = blockDim.x * blockDim.y * blockDim.z;                                     \
+    for (uint32_t i_ = threadIdx.x + blockDim.x * (threadIdx.y + blockDim.y * threadIdx.z); i_ < n_; i_ += nthr_) reinterpret_cast<uint32_t*>(smem)[i_] = ~0u; \
+    __syncthreads();                                                                                 \
+  } while (0)
+#else
+#define T2O_LDS_POISON(smem) \
+  do {                      \
+  } while (0)
+#endif
+
 T2O_DEV f4 mfma4(float a, float b, f4 acc) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
 }

@@ -661,6 +661,7 @@ T2O_DEV void dw_gemm_wg(const DwGemmArgs& a, int wg, int nwg, float* smem) {
 template <int E, int H, int FF, int D, int KIND, typename TT, int RT, int FMT>
 __global__ __launch_bounds__(256 * D) void dw_gemm_kernel(DwGemmArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   dw_gemm_wg<E, H, FF, D, TT, RT, FMT>(a, blockIdx.x, gridDim.x, smem);
 }
 
@@ -672,6 +673,7 @@ __global__ __launch_bounds__(256 * D) void dw_gemm_kernel(DwGemmArgs a) {
 template <int E, int H, int FF, int D, typename TT, int FMT1>
 __global__ __launch_bounds__(256 * D) void dw_gemm_pair_kernel(DwGemmArgs a0, DwGemmArgs a1, int n0) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   if ((int)blockIdx.x < n0) {
     dw_gemm_wg<E, H, FF, D, TT, 16, 0>(a0, blockIdx.x, n0, smem);
   } else {

@@ -435,6 +435,7 @@ T2O_DEV void agent_tokens(const GNet& N, const float* __restrict__ ob, int n, fl
 
 __global__ __launch_bounds__(256) void gagent_fwd_kernel(GAgentArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   const t2o_layout& L = a.L;
   const GAgentNet net = a.net[blockIdx.y];
   const GNet N = make_net(L, a.g, net.pack);
@@ -468,6 +469,7 @@ __global__ __launch_bounds__(256) void gagent_fwd_kernel(GAgentArgs a) {
 
 __global__ __launch_bounds__(256) void gagent_bwd_kernel(GAgentArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   const t2o_layout& L = a.L;
   const GNet N = make_net(L, a.g, a.net[0].pack);
   const int w = threadIdx.x >> 6, l = ln();
@@ -644,6 +646,7 @@ T2O_DEV void mix_embed(const GNet& N, const MixLds& m, int ns, int XS) {
 
 __global__ __launch_bounds__(256) void gmixer_fwd_kernel(GMixArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   const t2o_layout& L = a.L;
   const GMixNet net = a.net[blockIdx.y];
   const GNet N = make_net(L, a.g, net.pack);
@@ -718,6 +721,7 @@ __global__ __launch_bounds__(256) void gmixer_fwd_kernel(GMixArgs a) {
 
 __global__ __launch_bounds__(256) void gmixer_bwd_kernel(GMixArgs a) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   const t2o_layout& L = a.L;
   const GMixNet& net = a.net[0];
   const GNet N = make_net(L, a.g, net.pack);

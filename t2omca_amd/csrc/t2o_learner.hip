@@ -66,6 +66,7 @@ __device__ float block_sum(float v, float* red) {
 //   mask[b][t] = filled[t] * (t == 0 ? 1 : 1 - term[t-1])   (PyMARL2 nq_learner)
 __global__ __launch_bounds__(256) void td_loss_kernel(TDArgs a, int EP) {
   extern __shared__ float sm[];
+  T2O_LDS_POISON(sm);
   __shared__ float red[8];
   const int T = a.T;
   const int b0 = blockIdx.x * EP;

@@ -28,6 +28,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
   using Dm = MixDims<E, A>;
   constexpr int ET = E / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   const int w = wave_id();
   const MixerNet n = args.net[blockIdx.y];
   // bf16: the pack offsets as compile-time constants (t2o_layout.hpp kernel_layout,
@@ -167,6 +168,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   using Bd = MixBwdDims<E, A>;
   constexpr int ET = E / 16, KT = Dm::KT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   const MixerFwdArgs& fa = args.f;
   const MixerNet& n = fa.net[0];
   const t2o_layout& L = fa.L;
@@ -769,6 +771,7 @@ T2O_DEV void mixer_bwd_pipe_body(const MixerBwdArgs& args, const t2o_layout& L, 
   static_assert(D == 2 && MixPipeDims<E, A>::OK, "one wave per block of a depth-2 stack, one query tile");
   using Dm = MixDims<E, A>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   const int na = RT == 1 ? args.f.na : A;
   const int w = __builtin_amdgcn_readfirstlane(wave_id());
   // the block this wave owns.  Waves w and w + 4 share a SIMD: with four pairs,
@@ -1041,9 +1044,11 @@ extern "C" int t2o_mixer_unroll_bwd_split(const t2o_layout* L, const float* pack
   if (!L || L->kind != 1 || !pack || !states || !hid || !qv || !hw || !xout || !gy || !gqv || !ghid ||
       !gslabs || !nslab || !tape || B < 1 || T < 1 || L->E > 64)
     return T2O_EINVAL;
-  if (L->generic)
+  if (L->generic) {  // (no decoupled form: phases and ranges are the split kernels')
+    if (phase) return T2O_EUNSUPPORTED;
     return gen_mixer_unroll_bwd(L, pack, states, st_sb, st_st, hid, hid_sb, hid_st, hw0, qv, hw, xout, xmid, gy,
                                 ghw_ext, gqv, ghid, ghw0, gslabs, max_slabs, nslab, tape, B, T, (hipStream_t)stream);
+  }
   MixerBwdArgs a{};
   a.f.L = *L;
   a.f.states = states;

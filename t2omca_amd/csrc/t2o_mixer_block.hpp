@@ -42,20 +42,25 @@ struct MixerCache {
 #ifndef T2O_KF_PAIR
 #define T2O_KF_PAIR 1
 #endif
+#ifndef T2O_KF_ODD_PAIR  // 1: an odd key-tile count pairs all but its last comb tile (A/B)
+#define T2O_KF_ODD_PAIR 0
+#endif
 template <int E, int KT, bool BF>
 struct KeyFrags {
   // (an odd key-tile count keeps every comb tile unpaired: paired tiles plus a
   // lone tail made the one-wave multi-tile BPTT disagree with the split kernels
   // at 16 / 20 / 64 AGVs in bf16 — profiles/r5_bis/ — while 8, 13 and 40 AGVs,
   // even counts, agree; the pairing's gain is at the headline's 2 key tiles)
-  static constexpr int ET = E / 16, EP = T2O_KF_PAIR ? ET / 2 : 0, KP = (KT & 1) || !T2O_KF_PAIR ? 0 : KT / 2;
+  static constexpr int ET = E / 16, EP = T2O_KF_PAIR ? ET / 2 : 0;
+  static constexpr int KP = !T2O_KF_PAIR || ((KT & 1) && !T2O_KF_ODD_PAIR) ? 0 : KT / 2;
   static constexpr bool EO = EP * 2 != ET, KO = KP * 2 != KT;
-  static constexpr int N_EP = EP > 0 ? EP : 1, N_KP = KP > 0 ? KP : 1, EU = ET - 2 * EP;  // EU unpaired feature tiles
+  // EU / KU unpaired feature / key tiles (the last ones: 2 EP .. ET-1, 2 KP .. KT-1)
+  static constexpr int N_EP = EP > 0 ? EP : 1, N_KP = KP > 0 ? KP : 1, EU = ET - 2 * EP, KU = KT - 2 * KP;
   // fp32
   f4 dot[BF ? 1 : KT][BF ? 1 : ET], comb[BF ? 1 : KT][BF ? 1 : ET];
   // bf16
   bf8 dot8[BF ? KT : 1][N_EP], comb8[BF ? N_KP : 1][ET];
-  bf4 dot1[BF && EO ? KT : 1][EO ? EU : 1], comb1[BF && KO ? KT : 1][ET];
+  bf4 dot1[BF && EO ? KT : 1][EO ? EU : 1], comb1[BF && KO ? KU : 1][ET];
   template <int LDX>
   T2O_DEV void load(const float* __restrict__ X0) {
     const int c = lane_c(), g = lane_g();
@@ -81,7 +86,7 @@ struct KeyFrags {
         for (int p = 0; p < KP; ++p) comb8[p][ft] = cvt8(bcol(2 * p, ft), bcol(2 * p + 1, ft));
         if constexpr (KO)
 #pragma unroll
-          for (int kt = 0; kt < KT; ++kt) comb1[kt][ft] = to_bf4(bcol(kt, ft));
+          for (int u = 0; u < KU; ++u) comb1[u][ft] = to_bf4(bcol(2 * KP + u, ft));
       }
     } else {
 #pragma unroll
@@ -140,12 +145,12 @@ T2O_DEV void keys_combine(const KeyFrags<E, KT, BF>& K, const f4* w, f4* out) {
   constexpr int ET = E / 16;
   if constexpr (BF) {
     bf8 wb[KF::N_KP];
-    bf4 wt[KF::KO ? KT : 1];
+    bf4 wt[KF::KO ? KF::KU : 1];
 #pragma unroll
     for (int p = 0; p < KF::KP; ++p) wb[p] = cvt8(w[2 * p], w[2 * p + 1]);
     if constexpr (KF::KO)
 #pragma unroll
-      for (int kt = 0; kt < KT; ++kt) wt[kt] = to_bf4(w[kt]);
+      for (int u = 0; u < KF::KU; ++u) wt[u] = to_bf4(w[2 * KF::KP + u]);
 #pragma unroll
     for (int ft = 0; ft < ET; ++ft) {
       f4 acc = zero4();
@@ -153,7 +158,7 @@ T2O_DEV void keys_combine(const KeyFrags<E, KT, BF>& K, const f4* w, f4* out) {
       for (int p = 0; p < KF::KP; ++p) acc = mfma_b8(K.comb8[p][ft], wb[p], acc);
       if constexpr (KF::KO)
 #pragma unroll
-        for (int kt = 0; kt < KT; ++kt) acc = mfma_b16(K.comb1[kt][ft], wt[kt], acc);
+        for (int u = 0; u < KF::KU; ++u) acc = mfma_b16(K.comb1[u][ft], wt[u], acc);
       out[ft] = acc;
     }
   } else {

@@ -82,6 +82,7 @@ __global__ __launch_bounds__(512) void mixs_fwd_rec_kernel(MixerFwdArgs args) {
   using Dm = MixDims<E, A>;
   constexpr int ET = E / 16, HW = mixs_hw<E>();
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   const int w = wave_id();
   const MixerNet n = args.net[blockIdx.y];
   const t2o_layout L = kernel_layout<E, H, D, FF, WT>(args.L);
@@ -191,6 +192,7 @@ __global__ __launch_bounds__(512) void mixs_fwd_rows_kernel(MixerFwdArgs args) {
   using Rd = MixsRowsDims<E, A>;
   constexpr int ET = E / 16, HW = mixs_hw<E>();
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   const int w = wave_id();
   const MixerNet n = args.net[blockIdx.y];
   const t2o_layout L = kernel_layout<E, H, D, FF, WT>(args.L);
@@ -295,6 +297,7 @@ __global__ __launch_bounds__(256) void mixs_bwd_rows_kernel(MixsBwdArgs sa) {
   constexpr int ET = E / 16, KT = Dm::KT;
   static_assert(Dm::QT > 1, "multi-tile mixers only");
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   const MixerBwdArgs& args = sa.m;
   const MixerFwdArgs& fa = args.f;
   const MixerNet& n = fa.net[0];
@@ -510,6 +513,7 @@ __global__ __launch_bounds__(256) void mixs_bwd_rec_kernel(MixsBwdArgs sa) {
   using Bd = MixBwdDims<E, A>;
   constexpr int ET = E / 16, KT = Dm::KT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   const MixerBwdArgs& args = sa.m;
   const MixerFwdArgs& fa = args.f;
   const MixerNet& n = fa.net[0];
@@ -962,6 +966,7 @@ __global__ __launch_bounds__(128) void mixs_bwd_rec_pipe_kernel(MixsBwdArgs sa) 
   using Dm = MixDims<E, A>;
   using Pd = MixsPipeDims<E, A>;
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  T2O_LDS_POISON(smem);
   const MixerBwdArgs& args = sa.m;
   const t2o_layout& L = args.f.L;
   const t2o_layout& G = args.G;

@@ -72,6 +72,7 @@ __global__ __launch_bounds__(256) void pack_kernel(TaskTable tab, const float* _
                                                    const float* __restrict__ src2, float* __restrict__ dst,
                                                    __bf16* __restrict__ dstb) {
   extern __shared__ float sm[];
+  T2O_LDS_POISON(sm);
   int k = 0;
   while ((int)blockIdx.x >= tab.blk[k + 1]) ++k;
   const Task tk = tab.t[k];

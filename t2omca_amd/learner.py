@@ -66,6 +66,9 @@ class TDLearner:
             raise ValueError(f"td_algo must be one of {sorted(ops.TD_ALGOS)}, got {td_algo!r}")
         if pipeline not in ("auto", True, False) or int(pipeline_ranges) < 1:
             raise ValueError("pipeline must be 'auto', True or False and pipeline_ranges >= 1")
+        if pipeline is True and (contract == "pair" or not overlap):
+            raise ValueError("pipeline=True runs the mixer's contraction on the side stream: it needs "
+                             "contract='side' and overlap=True")
         dev = next(agent.parameters()).device
         if dev.type != "cuda":
             raise RuntimeError("TDLearner needs the modules on a HIP device (no CPU fallback)")
@@ -107,7 +110,10 @@ class TDLearner:
         # 15 us slower per update (profiles/r4_b/: 2.455 vs 2.438 ms)
         self.contract = contract
         # small replay batches: the agent and the (decoupled) mixer recurrences run
-        # side by side on two streams in step ranges (_pipelined)
+        # side by side on two streams in step ranges (_pipelined).  "auto": wherever
+        # the layout and batch allow it (never with contract="pair", which contracts
+        # both tapes in one launch after the agent BPTT); True: required — train()
+        # raises when the update cannot be pipelined; False: never
         self.pipeline, self.pipeline_ranges = pipeline, int(pipeline_ranges)
         self.step_count = 0
         self.last_target_update_episode = 0
@@ -245,9 +251,12 @@ class TDLearner:
         """Run the update's recurrences in step ranges on two streams?  Only where the
         mixer runs decoupled (a multi-tile mixer at a small batch, t2o_mixer_split)
         and the agent BPTT is the pipelined kernel (depth 2), which take ranges."""
-        if self.pipeline is False or self.sa.D != 2 or self.sa.generic or self.sm.generic:
+        if self.pipeline is False or self.contract == "pair" or self.sa.D != 2 or self.sa.generic or self.sm.generic:
             return False
-        return int(ops.lib().t2o_mixer_split(ops.ctypes.byref(self.sm.layout()), int(B))) == 1
+        lib = ops.lib()
+        if int(lib.t2o_agent_bwd_ranges(ops.ctypes.byref(self.sa.layout()), 1)) != 1:
+            return False  # (e.g. T2O_AGENT_BWD=single: the one-wave BPTT takes only the whole unroll)
+        return int(lib.t2o_mixer_split(ops.ctypes.byref(self.sm.layout()), int(B))) == 1
 
     def _ranges(self, n):
         """pipeline_ranges step ranges covering [0, n), in order."""
@@ -298,6 +307,10 @@ class TDLearner:
         ops.pack_params(self.sa, self.params[:self.na], self.pack_a)
         hmid = self._buf("hmid", (B, T1, self.sa.D - 1, A, self.sa.E)) if self.sa.D > 1 else None
         piped = self._pipelined(B) and side is not main
+        if self.pipeline is True and not piped:
+            raise RuntimeError(f"pipeline=True, but this update cannot run in step ranges (layout instance "
+                               f"{self.sa.instance}/{self.sm.instance}, {B} episodes: the mixer must run decoupled "
+                               f"and the agent BPTT must be the pipelined kernel)")
         mixer_kw = dict(qmode_on=1, actions=act, avail=avail, T_on=T, pack_tg=self.pack_mt, qmode_tg=2, T_tg=T1,
                         timer=self.timer)
         if piped:

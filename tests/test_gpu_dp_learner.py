@@ -28,10 +28,10 @@ import torch.multiprocessing as mp
 from tests.gpu_util import normwise, require_gpu
 
 pytestmark = pytest.mark.gpu
-A, B, T, UPDATES = 8, 6, 7, 3
+B, T, UPDATES = 6, 7, 3
 
 
-def _batch(device):
+def _batch(device, A):
     from t2omca_amd.synthetic import make_batch
     batch, w = make_batch(B, T, A, seed=11, device=device)
     batch["terminated"][1, 3] = 1  # ragged masks: the shards' Σ mask differ
@@ -39,7 +39,7 @@ def _batch(device):
     return batch, w
 
 
-def _learner(seed, device, pg=None):
+def _learner(seed, device, A, pg=None):
     from t2omca_amd.learner import TDLearner
     from t2omca_amd.modules import TransformerAgent, TransformerMixer
     from t2omca_amd.synthetic import make_args
@@ -50,7 +50,7 @@ def _learner(seed, device, pg=None):
     return TDLearner(agent, mixer, process_group=pg, target_update_interval=2)
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, A):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -59,8 +59,8 @@ def _worker(rank, world, port, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from t2omca_amd.distributed import shard_bounds
-        learner = _learner(100 + rank, dev)  # different init per rank: the broadcast must fix it
-        batch, w = _batch(dev)
+        learner = _learner(100 + rank, dev, A)  # different init per rank: the broadcast must fix it
+        batch, w = _batch(dev, A)
         lo, hi = shard_bounds(B, rank, world)
         shard = {k: v[lo:hi] for k, v in batch.items()}
 
@@ -78,14 +78,19 @@ def _worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-def test_dp_two_ranks_equal_full_batch_learner():
+@pytest.mark.parametrize("A", [8, 16])
+def test_dp_two_ranks_equal_full_batch_learner(A):
+    """A = 8: the one-tile mixer, sequential update.  A = 16: the decoupled two-tile
+    mixer at these small shards, so both ranks and the full-batch learner run the
+    PIPELINED update (step ranges on two streams, learner._pipelined), whose
+    mixer-half all-reduce is issued on the side stream after the per-range flushes."""
     require_gpu()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, A)) for r in range(2)]
     for p in procs:
         p.start()
     try:
@@ -99,8 +104,10 @@ def test_dp_two_ranks_equal_full_batch_learner():
     # replicas are identical from the start (rank 0's init) and stay identical
     assert torch.equal(r0, r1)
     dev = torch.device("cuda", 0)
-    full = _learner(100, dev)  # rank 0's init
-    batch, w = _batch(dev)
+    full = _learner(100, dev, A)  # rank 0's init
+    if A == 16:
+        assert full._pipelined(B) and full._pipelined(B // 2)
+    batch, w = _batch(dev, A)
     assert torch.equal(full.params.cpu(), r0[0, 0])
     for u in range(UPDATES):
         # the full-batch update from the replicas' state before update u
@@ -120,7 +127,7 @@ def test_dp_two_ranks_equal_full_batch_learner():
     # flips (the third update: 4.6e-5 on the parameters, tools/diag_dp_adam.py
     # names the pre-activation, profiles/r5_split/diag_dp.log); a systematic DP error
     # (Σ mask or Adam state handled per rank) moves every parameter by ~lr
-    free = _learner(100, dev)
+    free = _learner(100, dev, A)
     for u in range(UPDATES):
         free.train(batch, 0, u, per_weight=w)
         torch.cuda.synchronize()

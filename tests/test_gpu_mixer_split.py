@@ -135,3 +135,41 @@ def test_pipelined_update_matches_sequential(A, precision, ranges):
     print(f"A={A} {precision} ranges={ranges} pipelined vs sequential:", {k: f"{v:.1e}" for k, v in errs.items()})
     bar = (1e-5, 5e-5) if precision == "fp32" else (2e-3, 5e-3)
     assert errs["grads"] < bar[0] and errs["params"] < bar[1], errs
+
+
+def test_pipeline_falls_back_when_agent_bwd_cannot_take_ranges():
+    """T2O_AGENT_BWD=single selects the one-wave agent BPTT, which takes only the
+    whole unroll (t2o_agent_bwd_ranges = 0): pipeline='auto' must then run the
+    sequential update (the same result as pipeline=False), and pipeline=True must
+    refuse rather than fail part way through the update."""
+    require_gpu()
+    from t2omca_amd import ops
+    from t2omca_amd.learner import TDLearner
+    A, B, T = 16, 4, 9
+    old = os.environ.get("T2O_AGENT_BWD")
+    os.environ["T2O_AGENT_BWD"] = "single"
+    try:
+        base, batch, w = _setup(A, B, T, "bf16", seed=9)
+        assert int(ops.lib().t2o_agent_bwd_ranges(ops.ctypes.byref(base.sa.layout()), 1)) == 0
+        outs = []
+        for pipeline in ("auto", False):
+            learner = TDLearner(base.agent, base.mixer, precision="bf16", priorities_to_cpu=False, pipeline=pipeline)
+            snap = learner.params.clone()
+            assert not learner._pipelined(B)
+            info = learner.train(batch, 0, 0, per_weight=w)
+            torch.cuda.synchronize()
+            outs.append((learner.grad.clone(), info["td_errors_abs"].clone()))
+            learner.params.copy_(snap)
+            learner._params_written()
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+        forced = TDLearner(base.agent, base.mixer, precision="bf16", priorities_to_cpu=False, pipeline=True)
+        with pytest.raises(RuntimeError, match="pipeline=True"):
+            forced.train(batch, 0, 0, per_weight=w)
+    finally:
+        if old is None:
+            del os.environ["T2O_AGENT_BWD"]
+        else:
+            os.environ["T2O_AGENT_BWD"] = old
+    with_ranges = TDLearner(base.agent, base.mixer, precision="bf16", priorities_to_cpu=False)
+    assert int(ops.lib().t2o_agent_bwd_ranges(ops.ctypes.byref(with_ranges.sa.layout()), 1)) == 1
+    assert with_ranges._pipelined(B)
