@@ -43,8 +43,8 @@ struct MixerCache {
 #define T2O_KF_PAIR 1
 #endif
 #ifndef T2O_KF_ODD_PAIR  // 1: an odd key-tile count pairs all but its last comb tile (A/B)
-#define T2O_KF_ODD_PAIR 0
-#endif
+#define T2O_KF_ODD_PAIR 0   // 2: ... the tail in its own accumulator, added by VALU
+#endif                      // 3: ... the tail chained after 16 wait states (diagnostic)
 template <int E, int KT, bool BF>
 struct KeyFrags {
   // (an odd key-tile count keeps every comb tile unpaired: paired tiles plus a
@@ -156,9 +156,16 @@ T2O_DEV void keys_combine(const KeyFrags<E, KT, BF>& K, const f4* w, f4* out) {
       f4 acc = zero4();
 #pragma unroll
       for (int p = 0; p < KF::KP; ++p) acc = mfma_b8(K.comb8[p][ft], wb[p], acc);
-      if constexpr (KF::KO)
+      if constexpr (KF::KO && KF::KP > 0 && T2O_KF_ODD_PAIR == 2) {
+        f4 tail = zero4();
+#pragma unroll
+        for (int u = 0; u < KF::KU; ++u) tail = mfma_b16(K.comb1[u][ft], wt[u], tail);
+        acc += tail;
+      } else if constexpr (KF::KO) {
+        if constexpr (KF::KP > 0 && T2O_KF_ODD_PAIR == 3) asm volatile("s_nop 15" : "+v"(acc));
 #pragma unroll
         for (int u = 0; u < KF::KU; ++u) acc = mfma_b16(K.comb1[u][ft], wt[u], acc);
+      }
       out[ft] = acc;
     }
   } else {

@@ -67,7 +67,10 @@ def test_paired_contraction_equals_separate_launches(A, B, T, precision):
     out = {}
     for mode in ("pair", "side"):
         agent, mixer, _, _ = _setup(A, seed=6)
-        learner = TDLearner(agent, mixer, precision=precision, priorities_to_cpu=False, contract=mode)
+        # (both sequential: the pipelined update, which small multi-tile batches run by
+        # default, flushes per step range and never takes contract="pair")
+        learner = TDLearner(agent, mixer, precision=precision, priorities_to_cpu=False, contract=mode,
+                            pipeline=False)
         info = learner.train(batch, 0, 0, per_weight=w)
         torch.cuda.synchronize()
         out[mode] = (learner.grad.clone(), info["td_errors_abs"].clone(), learner.params.clone())

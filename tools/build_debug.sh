@@ -6,6 +6,8 @@
 #   {,dbg_}kmf.so     the fp32 flat key mask at both mixer call sites (T2O_KM_FP32_FLAT=3)
 #   {,dbg_}pf.so      the full-record tile-pair contraction (T2O_DW_PAIR_FULL=1)
 #   {,dbg_}odd.so     odd key-tile counts paired, last comb tile alone (T2O_KF_ODD_PAIR=1)
+#   odd2.so / odd3.so the same with the tail in its own accumulator / chained after 16
+#                     wait states (T2O_KF_ODD_PAIR=2 / 3)
 # A variant recompiles only the translation units its switch reaches and links them
 # with the matching (product / debug) objects of the rest.
 set -eu
@@ -33,6 +35,8 @@ add kmf "-DT2O_KM_FP32_FLAT=3" $MIX
 add dbg_kmf "$DBG -DT2O_KM_FP32_FLAT=3" $MIX
 add odd "-DT2O_KF_ODD_PAIR=1" $MIX
 add dbg_odd "$DBG -DT2O_KF_ODD_PAIR=1" $MIX
+add odd2 "-DT2O_KF_ODD_PAIR=2" $MIX
+add odd3 "-DT2O_KF_ODD_PAIR=3" $MIX
 add pf "-DT2O_DW_PAIR_FULL=1" t2o_dwgemm.hip
 add dbg_pf "$DBG -DT2O_DW_PAIR_FULL=1" t2o_dwgemm.hip
 [ ${#jobs[@]} -gt 0 ] && printf '%s\n' "${jobs[@]}" | xargs -P "${JOBS:-8}" -I{} bash -c '
@@ -53,3 +57,4 @@ for v in kmf odd pf; do
   link $v "$P" $v
   link dbg_$v "$O/dbg" dbg_$v
 done
+for v in odd2 odd3; do link $v "$P" $v; done

@@ -34,5 +34,25 @@ case "${1:-all}" in
       [ $rc -gt 1 ] && exit $rc
     done
     ;;
+  two)  # after the first pass: which poison reaches the flat-mask failure; the odd-pair fixes;
+        # run-to-run stress of the product and the pair-full contraction
+    step x1_kmf_pypoison kmf 1 $T_KMF
+    for v in odd2 odd3; do
+      step x2_$v $v 0 $T_ODD
+      T2O_LIB=$L/$v.so timeout -k 10 300 python -u tools/diag_repro.py --repeats 10 16,4,6,bf16 64,2,3,bf16 \
+        > $OUT/x2_repro_$v.log 2>&1
+      rc=$?; echo "x2_repro_$v rc=$rc"; tail -2 $OUT/x2_repro_$v.log
+      [ $rc -gt 1 ] && exit $rc
+    done
+    for v in libt2omca pf; do
+      T2O_LIB=$L/$v.so timeout -k 10 400 python -u tools/diag_repro.py --repeats 30 8,64,12,bf16 16,4,6,bf16 \
+        8,1024,60,bf16 > $OUT/x3_stress_$v.log 2>&1
+      rc=$?; echo "x3_stress_$v rc=$rc"; tail -3 $OUT/x3_stress_$v.log
+      [ $rc -gt 1 ] && exit $rc
+    done
+    timeout -k 10 400 python -u -m pytest -m gpu -q -s --timeout 300 --timeout-method thread -p no:cacheprovider \
+      tests/test_gpu_fullgrid.py > $OUT/x4_fullgrid.log 2>&1
+    rc=$?; echo "x4_fullgrid rc=$rc $(tail -1 $OUT/x4_fullgrid.log)"
+    ;;
 esac
 exit 0
