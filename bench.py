@@ -83,7 +83,7 @@ def parse():
                     help="weight-gradient tape contractions: side (default) = the mixer's on a side stream "
                          "issued before the agent BPTT; pair = both in one launch after the agent BPTT")
     ap.add_argument("--td-algo", choices=("auto", "sequential", "wave"), default="auto",
-                    help="TD(lambda) target kernel (t2o_td_loss_ex2): the sequential per-episode recursion "
+                    help="TD(lambda) target kernel (t2o_td_args.algo): the sequential per-episode recursion "
                          "or the one-wave-per-episode suffix scan; auto = the library default")
     ap.add_argument("--priorities", choices=("device", "cpu"), default="device",
                     help="where each update's |TD errors| go: device (consumed by the device-resident "

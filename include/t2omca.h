@@ -45,8 +45,11 @@ extern "C" {
  * refuse a library built from another (t2o_abi_version).  History: 3 = round-3
  * library (tuned one-tile mixers write one compact tape stream per block,
  * ceil(B*T*(A+3)/16) tiles; records of 4E + 2HE features); 4 = t2o_td_loss_ex2,
- * t2o_bwd_tape_contract_pair, t2o_abi_version. */
-#define T2O_ABI_VERSION 5
+ * t2o_bwd_tape_contract_pair, t2o_abi_version; 5 = the step-range / split-phase
+ * entry points; 6 = one argument struct per unroll / BPTT / contraction / TD
+ * loss entry point (their _ex / _ex2 / _range / _split / _pair generations
+ * folded in), t2o_args_sizeof, t2o_agent_bwd_ranges. */
+#define T2O_ABI_VERSION 6
 int t2o_abi_version(void);
 
 enum {
@@ -150,158 +153,169 @@ int t2o_pack_params(const t2o_layout* L, const float* params, float* pack, void*
 int t2o_unpack_grads(const t2o_layout* L, const float* params, const float* gpack,
                      float* grad, void* stream);
 
-/* Agent unroll forward over T steps for up to two networks sharing the
- * observations (online + target).  obs[b][t][a][n_ent*F] with element strides
- * obs_sb, obs_st (a-stride = n_ent*F).  h0 may be NULL (zeros, init_hidden).
- * Outputs q[b][t][a][NA], h[b][t][a][E] (h after step t) and, if non-NULL,
- * hmid[b][t][D-1][a][E] (inputs of blocks 1..D-1, lets the backward skip
- * recomputing them).  pack_tg/q_tg/h_tg/hmid_tg may be NULL to run one network. */
-int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, const float* pack_tg,
-                         const float* obs, int64_t obs_sb, int64_t obs_st,
-                         const float* h0_on, const float* h0_tg,
-                         float* q_on, float* h_on, float* hmid_on, float* q_tg, float* h_tg,
-                         float* hmid_tg, int B, int T, int A, void* stream);
+/* ---- The unrolls, their BPTTs, the tape contraction and the TD loss take ONE
+ * argument struct each (ABI 6): named fields instead of 25-45 positional
+ * arguments, so a binding cannot shift a pointer into the wrong slot unnoticed.
+ * Bindings check their mirror of every struct with t2o_args_sizeof. */
+#define T2O_ARGS_AGENT_FWD 0
+#define T2O_ARGS_AGENT_BWD 1
+#define T2O_ARGS_MIXER_FWD 2
+#define T2O_ARGS_MIXER_BWD 3
+#define T2O_ARGS_TAPE 4
+#define T2O_ARGS_TD 5
+int t2o_args_sizeof(int which); /* sizeof the T2O_ARGS_* struct, -1 for an unknown one */
 
-/* Agent BPTT over steps T-1..0 of one network.  h_seq = forward h output
- * [b][h_ts][a][E] (h_ts >= T), hmid = forward hmid [b][h_ts][D-1][a][E] or
- * NULL, h0 as in the forward (NULL = zeros).  External
- * grads of the T steps: gq[b][t][a][NA] (may be NULL) plus, if gchosen != NULL,
- * gchosen[b][t][a] routed to q[action] (actions int64 [b][t][a] with element
- * strides act_sb, act_st, a-stride 1); gh[b][t][a][E] (may be NULL).
- * Outputs: gslabs[nslab][grad_total] per-workgroup partial gradients (compact
- * layout, overwritten; *nslab = number written, at most max_slabs =
- * t2o_agent_bwd_max_slabs(B, A)); gh0[b][a][E] = dL/dh0 (may be NULL).
- * Workspace: tape, t2o_bwd_tape_floats(L, tiles) floats with tiles =
- * t2o_bwd_tape_tiles(L, B, T, A) — the per-record operand pairs of the M/N/W1/W2
- * weight grads; the slabs are complete only after t2o_bwd_tape_contract(L, pack,
- * tape, tiles, gslabs, *nslab) on the same stream. */
-int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack,
-                         const float* obs, int64_t obs_sb, int64_t obs_st,
-                         const float* h0, const float* h_seq, const float* hmid, int h_ts,
-                         const float* gq, const float* gchosen, const int64_t* actions,
-                         int64_t act_sb, int64_t act_st, const float* gh,
-                         float* gslabs, int max_slabs, int* nslab, void* tape, float* gh0,
-                         int B, int T, int A, void* stream);
+/* Agent unroll forward (TransformerAgent.forward over t, transf_agent.py:54-76) for
+ * up to two networks sharing the observations (online + target). */
+typedef struct {
+  const t2o_layout* L;
+  const float* pack_on;
+  const float* pack_tg;       /* NULL: one network (q_tg / h_tg / hmid_tg unused) */
+  const float* obs;           /* [b][t][a][n_ent*F], element strides obs_sb, obs_st */
+  int64_t obs_sb, obs_st;
+  const float* h0_on;         /* [B][A][E]; NULL = zeros (init_hidden) */
+  const float* h0_tg;
+  float* q_on;                /* out [b][t][a][NA] */
+  float* h_on;                /* out [b][t][a][E]: h after step t */
+  float* hmid_on;             /* out [b][t][D-1][a][E] block inputs (NULL: not kept) */
+  float* q_tg;
+  float* h_tg;
+  float* hmid_tg;
+  int32_t B, T, A;
+  int32_t t0, t1;             /* steps [t0, t1) of T (t1 <= 0: T); t0 > 0 continues from h at t0 - 1
+                                 (what the range before wrote; outputs are indexed by the full T) */
+} t2o_agent_fwd_args;
+int t2o_agent_unroll_fwd(const t2o_agent_fwd_args* a, void* stream);
+
+/* Agent BPTT of one network over steps t_hi - 1 .. t_lo (default: T - 1 .. 0). */
+typedef struct {
+  const t2o_layout* L;
+  const float* pack;
+  const float* obs;           /* as the forward's */
+  int64_t obs_sb, obs_st;
+  const float* h0;            /* as the forward's (NULL = zeros) */
+  const float* h_seq;         /* forward h [b][h_ts][a][E], h_ts >= T */
+  const float* hmid;          /* forward hmid [b][h_ts][D-1][a][E] or NULL (recomputed) */
+  int32_t h_ts;
+  const float* gq;            /* dL/dq [b][t][a][NA] or NULL */
+  const float* gchosen;       /* dL/dq[action] [b][t][a] or NULL (needs actions) */
+  const int64_t* actions;     /* [b][t][a], element strides act_sb, act_st, a-stride 1 */
+  int64_t act_sb, act_st;
+  const float* gh;            /* dL/dh [b][t][a][E] or NULL */
+  float* gslabs;              /* out [nslab][grad_total] per-workgroup partial gradients (compact
+                                 layout, overwritten); complete after t2o_bwd_tape_contract */
+  int32_t max_slabs;          /* >= t2o_agent_bwd_max_slabs(B, A) */
+  int32_t* nslab;             /* out: slabs written */
+  void* tape;                 /* workspace t2o_bwd_tape_floats(L, t2o_bwd_tape_tiles(L, B, T, A)) floats */
+  float* gh0;                 /* out dL/dh0 [B][A][E] or NULL */
+  float* gcarry;              /* [B*A][E] dL/dh between step ranges (read at t_hi < T, written at t_lo > 0) */
+  int32_t B, T, A;
+  int32_t t_lo, t_hi;         /* t_hi <= 0: T.  A partial range needs the pipelined BPTT
+                                 (t2o_agent_bwd_ranges; else T2O_EUNSUPPORTED); ranges run from the
+                                 last one down on the same slabs (the first clears them) and tape */
+} t2o_agent_bwd_args;
+int t2o_agent_unroll_bwd(const t2o_agent_bwd_args* a, void* stream);
 int t2o_agent_bwd_max_slabs(int B, int A);
-
-/* Step ranges of the two unrolls, for running the agent and mixer recurrences
- * of one TD update side by side on two streams (the learner's pipelined mode at
- * small replay batches).  Forward: steps [t0, t1) of T; t0 > 0 continues from
- * h_on / h_tg at step t0 - 1 (what the range before wrote); outputs indexed by
- * the full T.  Backward (the pipelined BPTT: depth 2, hmid given; else
- * T2O_EUNSUPPORTED for a partial range): steps t_hi - 1 .. t_lo; ranges run from
- * the last one down on the same slabs (the first, t_hi = T, clears them) and
- * tape; gcarry [B*A][E] carries dL/dh between ranges (read at t_hi < T, written
- * at t_lo > 0; gh0 gets it at t_lo = 0). */
-int t2o_agent_unroll_fwd_range(const t2o_layout* L, const float* pack_on, const float* pack_tg,
-                               const float* obs, int64_t obs_sb, int64_t obs_st,
-                               const float* h0_on, const float* h0_tg,
-                               float* q_on, float* h_on, float* hmid_on, float* q_tg, float* h_tg, float* hmid_tg,
-                               int B, int T, int A, int t0, int t1, void* stream);
-int t2o_agent_unroll_bwd_range(const t2o_layout* L, const float* pack,
-                               const float* obs, int64_t obs_sb, int64_t obs_st,
-                               const float* h0, const float* h_seq, const float* hmid, int h_ts,
-                               const float* gq, const float* gchosen, const int64_t* actions,
-                               int64_t act_sb, int64_t act_st, const float* gh,
-                               float* gslabs, int max_slabs, int* nslab, void* tape, float* gh0, float* gcarry,
-                               int B, int T, int A, int t_lo, int t_hi, void* stream);
 /* The record format t2o_agent_unroll_bwd writes to its tape for this layout
  * (has_hmid: the call passes hmid): 0 the full record; 1 (bf16, the pipelined
  * kernel, up to 8 entities) the lean record — dM and dN were accumulated in
  * registers and flushed into the slabs, the tape holds only the FFN / LN1 /
- * unify-bias operands.  Pass it to t2o_bwd_tape_contract_ex. */
+ * unify-bias operands.  Pass it to the contraction (t2o_tape_args.rec_format). */
 int t2o_agent_bwd_tape_format(const t2o_layout* L, int has_hmid);
-/* 1 when t2o_agent_unroll_bwd_range accepts a partial step range for this layout
+/* 1 when t2o_agent_unroll_bwd accepts a partial step range for this layout
  * (has_hmid: the call passes hmid): the two-wave pipelined BPTT runs it (depth 2,
  * its LDS fits, T2O_AGENT_BWD is not "single").  Otherwise 0, and the one-wave
  * kernel takes only the whole unroll (a partial range returns T2O_EUNSUPPORTED).
  * The learner's pipelined update (step ranges on two streams) asks this first. */
 int t2o_agent_bwd_ranges(const t2o_layout* L, int has_hmid);
 
-/* Mixer unroll forward for up to two networks (online + target) in one
- * launch; one wave per episode.  states[b][t][n_ent*F] (element strides
- * st_sb, st_st); hid_*[b][t][a][E] agent hidden states (strides hid_sb,
- * hid_st, a-stride E); hw0 [B][3][E] initial hyper tokens (NULL = zeros).
- * qmode: 0 = qvals given (qv_* [B][T][A]); 1 = chosen-action gather from the
- * network's Q array (q_on / q_tg [b][q_ts][a][n_actions], actions int64
- * [b][t][a] with strides act_sb, act_st); 2 = double-Q: the network's Q
- * array at argmax_a' of q_on masked by avail (int32 [b][t][a][n_actions],
- * strides av_sb, av_st; NULL = all available), ties -> lowest index.
- * Outputs per network: y[B][T], hw[B][T][3][E] (hyper tokens after step t),
- * qvo[B][T][A] (qvals used, may be NULL), xout[B][T][A+3][E] (final query
- * rows, may be NULL; required by the backward, and by a decoupled multi-tile
- * mixer for every network: t2o_mixer_split), xmid[B][T][D-1][A+3][E]
- * (inputs of blocks 1..D-1, may be NULL; lets the backward skip recomputing
- * them). */
-int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, const float* pack_tg,
-                         const float* states, int64_t st_sb, int64_t st_st,
-                         const float* hid_on, const float* hid_tg, int64_t hid_sb, int64_t hid_st,
-                         const float* hw0_on, const float* hw0_tg, int qmode_on, int qmode_tg,
-                         const float* qv_on, const float* qv_tg, const float* q_on, const float* q_tg,
-                         int q_ts, int n_actions, const int64_t* actions, int64_t act_sb, int64_t act_st,
-                         const int32_t* avail, int64_t av_sb, int64_t av_st,
-                         float* y_on, float* hw_on, float* qvo_on, float* xout_on, float* xmid_on,
-                         float* y_tg, float* hw_tg, float* qvo_tg, float* xout_tg, float* xmid_tg,
-                         int B, int T_on, int T_tg, void* stream);
+/* Mixer unroll forward (TransformerMixer.forward over t, n_transf_mixer.py:55-91)
+ * for up to two networks (online + target) in one launch, with the learner's
+ * chosen-Q gather / double-Q argmax.  qmode: 0 = qvals given (qv_* [B][T][A]);
+ * 1 = chosen-action gather from the network's Q array (q_on / q_tg
+ * [b][q_ts][a][n_actions] at actions); 2 = double-Q: the network's Q array at
+ * argmax_a' of q_on masked by avail (NULL = all available), ties -> lowest index. */
+typedef struct {
+  const t2o_layout* L;
+  const float* pack_on;
+  const float* pack_tg;       /* NULL: one network */
+  const float* states;        /* [b][t][n_ent*F], element strides st_sb, st_st */
+  int64_t st_sb, st_st;
+  const float* hid_on;        /* agent hidden states [b][t][a][E], strides hid_sb, hid_st, a-stride E */
+  const float* hid_tg;
+  int64_t hid_sb, hid_st;
+  const float* hw0_on;        /* initial hyper tokens [B][3][E]; NULL = zeros */
+  const float* hw0_tg;
+  int32_t qmode_on, qmode_tg;
+  const float* qv_on;
+  const float* qv_tg;
+  const float* q_on;
+  const float* q_tg;
+  int32_t q_ts, n_actions;
+  const int64_t* actions;     /* [b][t][a], strides act_sb, act_st */
+  int64_t act_sb, act_st;
+  const int32_t* avail;       /* [b][t][a][n_actions], strides av_sb, av_st, or NULL */
+  int64_t av_sb, av_st;
+  float* y_on;                /* out [B][T] */
+  float* hw_on;               /* out [B][T][3][E] hyper tokens after step t */
+  float* qvo_on;              /* out [B][T][A] qvals used, or NULL */
+  float* xout_on;             /* out [B][T][A+3][E] final query rows, or NULL (the backward needs them,
+                                 and a decoupled multi-tile mixer needs them for every network) */
+  float* xmid_on;             /* out [B][T][D-1][A+3][E] block inputs, or NULL (recomputed) */
+  float* y_tg;
+  float* hw_tg;
+  float* qvo_tg;
+  float* xout_tg;
+  float* xmid_tg;
+  int32_t B, T_on, T_tg;
+  int32_t phase;              /* 0: the whole unroll.  A decoupled mixer (t2o_mixer_split) may run its
+                                 phases beside the agent's step ranges on another stream: 1 = the
+                                 recurrence over steps [t0, t1) (the window's rows, hw, their xout /
+                                 xmid), every range in order; then 2 = every (episode, step)'s other
+                                 rows and the mixing head.  T2O_EUNSUPPORTED when it does not run
+                                 decoupled. */
+  int32_t t0, t1;
+} t2o_mixer_fwd_args;
+int t2o_mixer_unroll_fwd(const t2o_mixer_fwd_args* a, void* stream);
 
-/* Mixer BPTT over steps T-1..0 of one network.  qv = forward qvo [B][T][A],
- * hw / xout / xmid = forward outputs (xmid may be NULL).  gy[B][T] = dL/dy; ghw_ext [B][T][3][E] optional
- * extra grad on the hyper outputs.  Outputs: gqv[B][T][A] (dL/dqvals),
- * ghid[B][T][A][E] (dL/dhidden states), ghw0[B][3][E] (may be NULL), partial
- * weight-grad slabs as for the agent (max_slabs = t2o_mixer_bwd_max_slabs(B)),
- * tape workspace of t2o_bwd_tape_floats(L, tiles) floats with
- * tiles = t2o_bwd_tape_tiles(L, B, T, A); pass the same `tiles` to the contraction
- * (it is the per-block stride of the tape). */
-int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, const float* states,
-                         int64_t st_sb, int64_t st_st, const float* hid, int64_t hid_sb,
-                         int64_t hid_st, const float* hw0, const float* qv, const float* hw,
-                         const float* xout, const float* xmid, const float* gy, const float* ghw_ext, float* gqv,
-                         float* ghid, float* ghw0, float* gslabs, int max_slabs, int* nslab, void* tape,
-                         int B, int T, void* stream);
+/* Mixer BPTT of one network over steps T-1..0. */
+typedef struct {
+  const t2o_layout* L;
+  const float* pack;
+  const float* states;
+  int64_t st_sb, st_st;
+  const float* hid;
+  int64_t hid_sb, hid_st;
+  const float* hw0;
+  const float* qv;            /* forward qvo [B][T][A] */
+  const float* hw;            /* forward hw */
+  const float* xout;          /* forward xout (required) */
+  const float* xmid;          /* forward xmid or NULL */
+  const float* gy;            /* dL/dy [B][T] */
+  const float* ghw_ext;       /* extra dL/dhw [B][T][3][E] or NULL */
+  float* gqv;                 /* out dL/dqvals [B][T][A] */
+  float* ghid;                /* out dL/dhidden states [B][T][A][E] */
+  float* ghw0;                /* out dL/dhw0 [B][3][E] or NULL */
+  float* gslabs;              /* out partial weight-grad slabs, as the agent's */
+  int32_t max_slabs;          /* >= t2o_mixer_bwd_max_slabs(B) */
+  int32_t* nslab;
+  void* tape;                 /* t2o_bwd_tape_floats(L, tiles) floats, tiles = t2o_bwd_tape_tiles(L, B, T, A) */
+  float* work;                /* t2o_mixer_bwd_work_floats(L, B, T) floats, or NULL: lets a multi-tile
+                                 mixer (A + 3 > 16 query rows) at a small batch run its recurrence
+                                 decoupled (the window of the last 16 query rows carries the hyper
+                                 tokens, every (episode, step)'s other rows run in parallel; the key
+                                 gradients sum in another order) */
+  int64_t work_floats;
+  float* ghw_carry;           /* [B][3][E] hyper grads between phase-2 step ranges */
+  int32_t B, T;
+  int32_t phase;              /* 0: the whole BPTT; decoupled: 1 = every (episode, step)'s parallel part,
+                                 then 2 = the recurrence over steps t_hi - 1 .. t_lo, ranges from the
+                                 last one down (*nslab the same for every call) */
+  int32_t t_lo, t_hi;         /* t_hi <= 0: T */
+} t2o_mixer_bwd_args;
+int t2o_mixer_unroll_bwd(const t2o_mixer_bwd_args* a, void* stream);
 int t2o_mixer_bwd_max_slabs(int B);
-
-/* The same with a workspace: work (work_floats floats, caller-owned,
- * t2o_mixer_bwd_work_floats(L, B, T) of them; NULL / short = none) lets a
- * multi-tile mixer (A + 3 > 16 query rows) at a small replay batch run its
- * recurrence decoupled from the rest (t2o_mixer_split.hip: the window of the
- * last 16 query rows carries the hyper tokens' recurrence, every (episode,
- * step)'s other rows run in parallel).  Same outputs; the key-gradient sums run
- * in another order.  Replaces the reference's per-timestep mixer backward
- * through autograd (n_transf_mixer.py:55-91 driven by per_run.py:224). */
-int t2o_mixer_unroll_bwd_ex(const t2o_layout* L, const float* pack, const float* states,
-                            int64_t st_sb, int64_t st_st, const float* hid, int64_t hid_sb,
-                            int64_t hid_st, const float* hw0, const float* qv, const float* hw,
-                            const float* xout, const float* xmid, const float* gy, const float* ghw_ext,
-                            float* gqv, float* ghid, float* ghw0, float* gslabs, int max_slabs, int* nslab,
-                            void* tape, float* work, int64_t work_floats, int B, int T, void* stream);
-/* The decoupled mixer's phases, for running them beside the agent's step
- * ranges on another stream (ranges as t2o_agent_unroll_fwd_range's).  Forward:
- * phase 1 = the recurrence over steps [t0, t1) (the window's rows, hw, the
- * window's xout / xmid), every range in order; then phase 2 = every (episode,
- * step)'s other rows and the mixing head (y, qvo, the rest of xout / xmid).
- * Backward: phase 1 = every (episode, step)'s parallel part; then phase 2 = the
- * recurrence over steps t_hi - 1 .. t_lo, ranges from the last down, ghw_carry
- * [B][3][E] carrying the hyper grads between them; *nslab is the same for every
- * call.  T2O_EUNSUPPORTED when the layout / batch does not run decoupled
- * (t2o_mixer_split). */
-int t2o_mixer_unroll_fwd_split(const t2o_layout* L, const float* pack_on, const float* pack_tg,
-                               const float* states, int64_t st_sb, int64_t st_st,
-                               const float* hid_on, const float* hid_tg, int64_t hid_sb, int64_t hid_st,
-                               const float* hw0_on, const float* hw0_tg, int qmode_on, int qmode_tg,
-                               const float* qv_on, const float* qv_tg, const float* q_on, const float* q_tg,
-                               int q_ts, int n_actions, const int64_t* actions, int64_t act_sb, int64_t act_st,
-                               const int32_t* avail, int64_t av_sb, int64_t av_st,
-                               float* y_on, float* hw_on, float* qvo_on, float* xout_on, float* xmid_on,
-                               float* y_tg, float* hw_tg, float* qvo_tg, float* xout_tg, float* xmid_tg,
-                               int B, int T_on, int T_tg, int phase, int t0, int t1, void* stream);
-int t2o_mixer_unroll_bwd_split(const t2o_layout* L, const float* pack, const float* states,
-                               int64_t st_sb, int64_t st_st, const float* hid, int64_t hid_sb,
-                               int64_t hid_st, const float* hw0, const float* qv, const float* hw,
-                               const float* xout, const float* xmid, const float* gy, const float* ghw_ext,
-                               float* gqv, float* ghid, float* ghw0, float* gslabs, int max_slabs, int* nslab,
-                               void* tape, float* work, int64_t work_floats, float* ghw_carry, int phase,
-                               int t_lo, int t_hi, int B, int T, void* stream);
-/* Workspace floats t2o_mixer_unroll_bwd_ex can use for this layout and batch
+/* Workspace floats t2o_mixer_unroll_bwd can use for this layout and batch
  * (0: the layout has one query tile, nothing to decouple; -1 bad argument). */
 int64_t t2o_mixer_bwd_work_floats(const t2o_layout* L, int B, int T);
 /* 1 when a mixer of this layout runs decoupled at batch B (forward: when every
@@ -313,84 +327,74 @@ int t2o_mixer_split(const t2o_layout* L, int B);
  * (agent: T * ceil(B*A/16); mixer, A = L->n_agents: B*T*ceil((A+3)/16), or for
  * a tuned mixer with A+3 > 16 query rows, whose records form one compact stream
  * per block, ceil(B*T*(A+3)/16)).  -1 on a bad argument.  Both the tape size
- * (t2o_bwd_tape_floats) and the contraction's `tiles` argument take this count. */
+ * (t2o_bwd_tape_floats) and the contraction's `tiles` take this count. */
 int64_t t2o_bwd_tape_tiles(const t2o_layout* L, int B, int T, int A);
 
 /* Floats of backward tape workspace for `tiles` tiles of 16 records:
  * D * tiles * 16 * (4E + 2HE) elements of 4 (fp32) or 2 (bf16) bytes. */
 int64_t t2o_bwd_tape_floats(const t2o_layout* L, int64_t tiles);
 
-/* Contract a backward tape (dM, dN, dW2, P = Σ_records dYᵀ X, split-K over
- * the nslab slabs the backward call returned) into the M/N/W1/W2 regions of
- * those slabs.  pack = the same kernel pack the backward used (g1, n1, W1, W2ᵀ,
- * c1 recompute the FFN operands the tape does not store).  The W1 / g1 regions
- * then hold P = Σ gf1 ⊗ x̂1 and Q = Σ gr2 ⊙ x̂1, which t2o_unpack_grads turns
- * into the W1 / norm1 grads (the LN1 output and its grad are not on the tape).
- * Must follow the t2o_*_unroll_bwd call that wrote the tape. */
-int t2o_bwd_tape_contract(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
-                          float* gslabs, int nslab, void* stream);
-/* t2o_bwd_tape_contract for a tape in record format rec_format
- * (t2o_agent_bwd_tape_format; 0 = the full record, what the mixer writes).
- * Format 1 adds only the FFN / LN1 / bu grads: the backward call already put
- * dM / dN into the slabs. */
-int t2o_bwd_tape_contract_ex(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
-                             float* gslabs, int nslab, int rec_format, void* stream);
+/* One backward call's weight-gradient tape, to be contracted into its slabs. */
+typedef struct {
+  const t2o_layout* L;
+  const float* pack;          /* the kernel pack the backward used (g1, n1, W1, W2ᵀ, c1 recompute the
+                                 FFN operands the tape does not store) */
+  const void* tape;
+  int64_t tiles;              /* the backward's t2o_bwd_tape_tiles (the tape's per-block stride) */
+  float* gslabs;              /* the backward's slabs */
+  int32_t nslab;              /* >= the backward's *nslab: slabs past it must be zeroed by the caller
+                                 (a small batch's contraction over more workgroups) */
+  int32_t rec_format;         /* t2o_agent_bwd_tape_format; 0 = the full record (every mixer's) */
+} t2o_tape_args;
+/* Contract a backward tape (dM, dN, dW2, P = Σ_records dYᵀ X, split-K over the
+ * slabs) into the M/N/W1/W2 regions of its slabs.  The W1 / g1 regions then hold
+ * P = Σ gf1 ⊗ x̂1 and Q = Σ gr2 ⊙ x̂1, which t2o_unpack_grads turns into the W1 /
+ * norm1 grads.  Format 1 adds only the FFN / LN1 / bu grads (the backward put dM /
+ * dN into the slabs).  With `second` (or NULL): BOTH backwards' tapes in one
+ * launch — `first` the mixer's (format 0), `second` the agent's — each exactly as
+ * alone, one grid of both slab counts (the two share the chip from the start);
+ * layouts that are not tuned instances of one network shape and precision run as
+ * two launches.  Must follow the t2o_*_unroll_bwd call(s) on the same stream. */
+int t2o_bwd_tape_contract(const t2o_tape_args* first, const t2o_tape_args* second, void* stream);
 
-/* Both backwards' tape contractions in one launch: the mixer's (record format 0)
- * and the agent's (rec_format_a, t2o_agent_bwd_tape_format), each exactly as
- * t2o_bwd_tape_contract_ex would, with one grid of nslab_m + nslab_a workgroups
- * (the two then share the chip from the start instead of the second waiting on
- * the first).  Both layouts must be tuned instances of the same network shape
- * and precision for the one-grid path; otherwise the two contractions run as two
- * launches.  Must follow both t2o_*_unroll_bwd calls on the same stream. */
-int t2o_bwd_tape_contract_pair(const t2o_layout* Lm, const float* pack_m, const void* tape_m, int64_t tiles_m,
-                               float* slabs_m, int nslab_m, const t2o_layout* La, const float* pack_a,
-                               const void* tape_a, int64_t tiles_a, float* slabs_a, int nslab_a, int rec_format_a,
-                               void* stream);
-
-/* TD(λ) targets, masked PER-weighted loss, dL/dQtot and priorities
- * (PyMARL2 NQLearner semantics; see t2o_learner.hip).  qtot [B][T] (online
- * mixer), qtot_tgt [B][T+1] (target mixer), reward/term/filled [b][t] with
- * element strides (term/filled may be NULL), per_weight [B] (NULL = 1);
- * mask_sum > 0 overrides the local Σ mask (data parallel).  Outputs gq[B][T],
- * targets[B][T] (may be NULL), prio[B], loss[2] = {loss, local Σ mask}. */
-int t2o_td_loss(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
-                int64_t rw_st, const float* term, int64_t tm_sb, int64_t tm_st,
-                const float* filled, int64_t fl_sb, int64_t fl_st, const float* per_weight,
-                float gamma, float td_lambda, float mask_sum, float* gq, float* targets,
-                float* prio, float* loss, int B, int T, void* stream);
-
-/* Element types of the mask inputs of t2o_td_loss_ex. */
+/* Element types of the TD loss's mask inputs. */
 #define T2O_DT_F32 0
 #define T2O_DT_U8 1   /* uint8 / bool: EpisodeBatch "terminated" */
 #define T2O_DT_I32 2
 #define T2O_DT_I64 3  /* int64: EpisodeBatch "filled" */
 
-/* t2o_td_loss with term / filled read in their own storage types (the
- * reference EpisodeBatch keeps terminated as uint8 and filled as int64,
- * per_run.py's scheme), so the learner passes the replay views as they are. */
-int t2o_td_loss_ex(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
-                   int64_t rw_st, const void* term, int term_dtype, int64_t tm_sb, int64_t tm_st,
-                   const void* filled, int filled_dtype, int64_t fl_sb, int64_t fl_st,
-                   const float* per_weight, float gamma, float td_lambda, float mask_sum, float* gq,
-                   float* targets, float* prio, float* loss, int B, int T, void* stream);
-
-/* t2o_td_loss_ex2 algorithms */
+/* TD loss algorithms */
 #define T2O_TD_AUTO 0        /* the library's default (currently T2O_TD_WAVE_SCAN, the faster) */
 #define T2O_TD_SEQUENTIAL 1  /* one thread per episode, the reference's backward order (T <= ~4900) */
 #define T2O_TD_WAVE_SCAN 2   /* one wave per episode: suffix scan of the linear TD(λ) recursion
                                 (reassociated: fp32 rounding differs by ~1e-7 relative; any T) */
 
-/* t2o_td_loss_ex with the algorithm chosen explicitly and, when mask_sum_acc is
- * non-NULL, the local Σ mask also added (atomically) into *mask_sum_acc — the
- * learner's flat gradient buffer keeps Σ mask in its last slot, so the data-parallel
- * all-reduce sums it with the grads and Adam divides by the global value. */
-int t2o_td_loss_ex2(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
-                    int64_t rw_st, const void* term, int term_dtype, int64_t tm_sb, int64_t tm_st,
-                    const void* filled, int filled_dtype, int64_t fl_sb, int64_t fl_st,
-                    const float* per_weight, float gamma, float td_lambda, float mask_sum, float* gq,
-                    float* targets, float* prio, float* loss, float* mask_sum_acc, int algo, int B, int T,
-                    void* stream);
+/* TD(λ) targets, masked PER-weighted loss, dL/dQtot and priorities (PyMARL2
+ * NQLearner semantics, learner.train at per_run.py:224-238; t2o_learner.hip). */
+typedef struct {
+  const float* qtot;          /* [B][T] online mixer */
+  const float* qtot_tgt;      /* [B][T+1] target mixer */
+  const float* reward;        /* [b][t], element strides rw_sb, rw_st */
+  int64_t rw_sb, rw_st;
+  const void* term;           /* [b][t] 0/1 (NULL: none), element type term_dtype, strides tm_* */
+  int64_t tm_sb, tm_st;
+  const void* filled;         /* [b][t] 0/1 (NULL: all), element type filled_dtype, strides fl_* */
+  int64_t fl_sb, fl_st;
+  const float* per_weight;    /* [B] or NULL (= 1) */
+  float* gq;                  /* out [B][T] dL/dQtot */
+  float* targets;             /* out [B][T] or NULL */
+  float* prio;                /* out [B] */
+  float* loss;                /* out [2] = {loss, local Σ mask} */
+  float* mask_sum_acc;        /* NULL, or += local Σ mask (the learner keeps Σ mask in its flat
+                                 gradient's last slot: the data-parallel all-reduce sums it with the
+                                 grads and Adam divides by the global value) */
+  float gamma, td_lambda;
+  float mask_sum;             /* > 0: normalise gq / loss by this global Σ mask; else by the local one */
+  int32_t term_dtype, filled_dtype;  /* T2O_DT_*: the EpisodeBatch's own types, read in place */
+  int32_t algo;               /* T2O_TD_* */
+  int32_t B, T;
+} t2o_td_args;
+int t2o_td_loss(const t2o_td_args* a, void* stream);
 
 /* clip_grad_norm_(max_grad_norm) + Adam (torch.optim.Adam semantics, L2
  * weight decay) over n floats.  workspace: t2o_adam_workspace_floats() floats
@@ -420,6 +424,13 @@ int t2o_probe_posf(const float* x, int n, int pos_func, float beta, float* out, 
  * conversion with the bit-pattern ReLU, on in[64]; writes 23 x 64 results
  * (tests/test_gpu_primitives.py). */
 int t2o_probe_scatter_ops(const float* in, float* out, void* stream);
+/* Diagnostic: MFMA result hand-offs after a fixed number of wait states (inline
+ * asm, unpadded by the compiler): a 16x16x4 f32 result stored to LDS / global
+ * memory from its AGPRs after 10 or 32 states, a 16x16x32 bf16 result read as
+ * srcC by a 16x16x16 bf16 MFMA after 0 / 4 / 32 states and by a 16x16x32 after
+ * 0 / 32, then the compiler-built references.  in [nwaves][64][12] floats, out
+ * [12][nwaves][64][4] floats (t2o_probe.hip). */
+int t2o_probe_xdl_hazards(const float* in, float* out, int nwaves, void* stream);
 
 /* Diagnostic: the XOR (in bf16 elements, a multiple of 8) applied to the
  * columns of row `row` of a bf16 weight-image matrix with row length ld: element

@@ -779,15 +779,7 @@ int launch_bwd(AgentBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream
 
 }  // namespace
 
-extern "C" int t2o_agent_unroll_fwd(const t2o_layout* L, const float* pack_on, const float* pack_tg,
-                                    const float* obs, int64_t obs_sb, int64_t obs_st, const float* h0_on,
-                                    const float* h0_tg, float* q_on, float* h_on, float* hmid_on, float* q_tg,
-                                    float* h_tg, float* hmid_tg, int B, int T, int A, void* stream) {
-  return t2o_agent_unroll_fwd_range(L, pack_on, pack_tg, obs, obs_sb, obs_st, h0_on, h0_tg, q_on, h_on, hmid_on,
-                                    q_tg, h_tg, hmid_tg, B, T, A, 0, T, stream);
-}
-
-extern "C" int t2o_agent_unroll_fwd_range(const t2o_layout* L, const float* pack_on, const float* pack_tg,
+static int agent_fwd_impl(const t2o_layout* L, const float* pack_on, const float* pack_tg,
                                           const float* obs, int64_t obs_sb, int64_t obs_st, const float* h0_on,
                                           const float* h0_tg, float* q_on, float* h_on, float* hmid_on,
                                           float* q_tg, float* h_tg, float* hmid_tg, int B, int T, int A, int t0,
@@ -825,17 +817,7 @@ extern "C" int t2o_agent_unroll_fwd_range(const t2o_layout* L, const float* pack
   return rc;
 }
 
-extern "C" int t2o_agent_unroll_bwd(const t2o_layout* L, const float* pack, const float* obs, int64_t obs_sb,
-                                    int64_t obs_st, const float* h0, const float* h_seq, const float* hmid, int h_ts,
-                                    const float* gq, const float* gchosen, const int64_t* actions,
-                                    int64_t act_sb, int64_t act_st, const float* gh, float* gslabs,
-                                    int max_slabs, int* nslab, void* tape, float* gh0, int B, int T, int A,
-                                    void* stream) {
-  return t2o_agent_unroll_bwd_range(L, pack, obs, obs_sb, obs_st, h0, h_seq, hmid, h_ts, gq, gchosen, actions, act_sb,
-                                    act_st, gh, gslabs, max_slabs, nslab, tape, gh0, nullptr, B, T, A, 0, T, stream);
-}
-
-extern "C" int t2o_agent_unroll_bwd_range(const t2o_layout* L, const float* pack, const float* obs, int64_t obs_sb,
+static int agent_bwd_impl(const t2o_layout* L, const float* pack, const float* obs, int64_t obs_sb,
                                           int64_t obs_st, const float* h0, const float* h_seq, const float* hmid,
                                           int h_ts, const float* gq, const float* gchosen, const int64_t* actions,
                                           int64_t act_sb, int64_t act_st, const float* gh, float* gslabs,
@@ -881,6 +863,20 @@ extern "C" int t2o_agent_unroll_bwd_range(const t2o_layout* L, const float* pack
                      rc = (L->prec ? launch_bwd<E_, H_, D_, NE_, FF_, RT_, __bf16>(args, max_slabs, nslab, (hipStream_t)stream)
                                    : launch_bwd<E_, H_, D_, NE_, FF_, RT_, float>(args, max_slabs, nslab, (hipStream_t)stream)));
   return rc;
+}
+
+extern "C" int t2o_agent_unroll_fwd(const t2o_agent_fwd_args* a, void* stream) {
+  if (!a) return T2O_EINVAL;
+  return agent_fwd_impl(a->L, a->pack_on, a->pack_tg, a->obs, a->obs_sb, a->obs_st, a->h0_on, a->h0_tg, a->q_on,
+                        a->h_on, a->hmid_on, a->q_tg, a->h_tg, a->hmid_tg, a->B, a->T, a->A, a->t0,
+                        a->t1 > 0 ? a->t1 : a->T, stream);
+}
+
+extern "C" int t2o_agent_unroll_bwd(const t2o_agent_bwd_args* a, void* stream) {
+  if (!a) return T2O_EINVAL;
+  return agent_bwd_impl(a->L, a->pack, a->obs, a->obs_sb, a->obs_st, a->h0, a->h_seq, a->hmid, a->h_ts, a->gq,
+                        a->gchosen, a->actions, a->act_sb, a->act_st, a->gh, a->gslabs, a->max_slabs, a->nslab, a->tape,
+                        a->gh0, a->gcarry, a->B, a->T, a->A, a->t_lo, a->t_hi > 0 ? a->t_hi : a->T, stream);
 }
 
 // diagnostic builds only (-DT2O_PHASE_PROF, tools/phase_prof.py)

@@ -665,7 +665,7 @@ __global__ __launch_bounds__(256 * D) void dw_gemm_kernel(DwGemmArgs a) {
   dw_gemm_wg<E, H, FF, D, TT, RT, FMT>(a, blockIdx.x, gridDim.x, smem);
 }
 
-// Both backwards' tapes in ONE grid (t2o_bwd_tape_contract_pair): workgroups
+// Both backwards' tapes in ONE grid (t2o_bwd_tape_contract with two tapes): workgroups
 // [0, n0) contract tape 0 (record format 0: the mixer's), the rest tape 1
 // (format FMT1: the agent's).  After the agent BPTT the two contractions are the
 // update's tail; as one launch their workgroups share the chip from the first
@@ -750,7 +750,7 @@ extern "C" int64_t t2o_bwd_tape_tiles(const t2o_layout* L, int B, int T, int A) 
   return (int64_t)B * T * ((Q + 15) / 16);
 }
 
-extern "C" int t2o_bwd_tape_contract_ex(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
+static int contract_one(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
                                         float* gslabs, int nslab, int rec_format, void* stream) {
   if (!L || !pack || !tape || !gslabs || tiles < 0 || nslab < 1 || rec_format < 0 || rec_format > 1 ||
       (rec_format == 1 && (L->kind != 0 || !L->prec || L->generic)))
@@ -773,12 +773,7 @@ extern "C" int t2o_bwd_tape_contract_ex(const t2o_layout* L, const float* pack, 
   return rc;
 }
 
-extern "C" int t2o_bwd_tape_contract(const t2o_layout* L, const float* pack, const void* tape, int64_t tiles,
-                                     float* gslabs, int nslab, void* stream) {
-  return t2o_bwd_tape_contract_ex(L, pack, tape, tiles, gslabs, nslab, 0, stream);
-}
-
-extern "C" int t2o_bwd_tape_contract_pair(const t2o_layout* Lm, const float* pack_m, const void* tape_m,
+static int contract_pair(const t2o_layout* Lm, const float* pack_m, const void* tape_m,
                                           int64_t tiles_m, float* slabs_m, int nslab_m, const t2o_layout* La,
                                           const float* pack_a, const void* tape_a, int64_t tiles_a,
                                           float* slabs_a, int nslab_a, int rec_format_a, void* stream) {
@@ -791,8 +786,8 @@ extern "C" int t2o_bwd_tape_contract_pair(const t2o_layout* Lm, const float* pac
                     Lm->FF == La->FF && Lm->prec == La->prec;
   hipStream_t s = (hipStream_t)stream;
   if (!same) {
-    int rc = t2o_bwd_tape_contract_ex(Lm, pack_m, tape_m, tiles_m, slabs_m, nslab_m, 0, stream);
-    return rc ? rc : t2o_bwd_tape_contract_ex(La, pack_a, tape_a, tiles_a, slabs_a, nslab_a, rec_format_a, stream);
+    int rc = contract_one(Lm, pack_m, tape_m, tiles_m, slabs_m, nslab_m, 0, stream);
+    return rc ? rc : contract_one(La, pack_a, tape_a, tiles_a, slabs_a, nslab_a, rec_format_a, stream);
   }
   const DwGemmArgs am = dw_args(tape_m, tiles_m, pack_m, slabs_m, *Lm);
   const DwGemmArgs aa = dw_args(tape_a, tiles_a, pack_a, slabs_a, *La);
@@ -803,4 +798,15 @@ extern "C" int t2o_bwd_tape_contract_pair(const t2o_layout* Lm, const float* pac
                                          : launch_dw_gemm_pair<E_, H_, FF_, D_, __bf16, 0>(am, nslab_m, aa, nslab_a, s))
                                   : launch_dw_gemm_pair<E_, H_, FF_, D_, float, 0>(am, nslab_m, aa, nslab_a, s)));
   return rc;
+}
+
+extern "C" int t2o_bwd_tape_contract(const t2o_tape_args* first, const t2o_tape_args* second, void* stream) {
+  if (!first) return T2O_EINVAL;
+  if (!second)
+    return contract_one(first->L, first->pack, first->tape, first->tiles, first->gslabs, first->nslab,
+                        first->rec_format, stream);
+  if (first->rec_format != 0) return T2O_EINVAL;  // (the first of a pair is the mixer's tape)
+  return contract_pair(first->L, first->pack, first->tape, first->tiles, first->gslabs, first->nslab, second->L,
+                       second->pack, second->tape, second->tiles, second->gslabs, second->nslab, second->rec_format,
+                       stream);
 }

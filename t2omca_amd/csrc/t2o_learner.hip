@@ -278,7 +278,7 @@ __global__ __launch_bounds__(256) void adam_kernel(AdamArgs a) {
 
 }  // namespace
 
-extern "C" int t2o_td_loss_ex2(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
+static int td_impl(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
                                int64_t rw_st, const void* term, int term_dtype, int64_t tm_sb, int64_t tm_st,
                                const void* filled, int filled_dtype, int64_t fl_sb, int64_t fl_st,
                                const float* per_weight, float gamma, float td_lambda, float mask_sum, float* gq,
@@ -315,23 +315,11 @@ extern "C" int t2o_td_loss_ex2(const float* qtot, const float* qtot_tgt, const f
   return (int)hipGetLastError();
 }
 
-extern "C" int t2o_td_loss_ex(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
-                              int64_t rw_st, const void* term, int term_dtype, int64_t tm_sb, int64_t tm_st,
-                              const void* filled, int filled_dtype, int64_t fl_sb, int64_t fl_st,
-                              const float* per_weight, float gamma, float td_lambda, float mask_sum, float* gq,
-                              float* targets, float* prio, float* loss, int B, int T, void* stream) {
-  return t2o_td_loss_ex2(qtot, qtot_tgt, reward, rw_sb, rw_st, term, term_dtype, tm_sb, tm_st, filled,
-                         filled_dtype, fl_sb, fl_st, per_weight, gamma, td_lambda, mask_sum, gq, targets, prio,
-                         loss, nullptr, T2O_TD_AUTO, B, T, stream);
-}
-
-extern "C" int t2o_td_loss(const float* qtot, const float* qtot_tgt, const float* reward, int64_t rw_sb,
-                           int64_t rw_st, const float* term, int64_t tm_sb, int64_t tm_st, const float* filled,
-                           int64_t fl_sb, int64_t fl_st, const float* per_weight, float gamma, float td_lambda,
-                           float mask_sum, float* gq, float* targets, float* prio, float* loss, int B, int T,
-                           void* stream) {
-  return t2o_td_loss_ex(qtot, qtot_tgt, reward, rw_sb, rw_st, term, T2O_DT_F32, tm_sb, tm_st, filled, T2O_DT_F32,
-                        fl_sb, fl_st, per_weight, gamma, td_lambda, mask_sum, gq, targets, prio, loss, B, T, stream);
+extern "C" int t2o_td_loss(const t2o_td_args* a, void* stream) {
+  if (!a) return T2O_EINVAL;
+  return td_impl(a->qtot, a->qtot_tgt, a->reward, a->rw_sb, a->rw_st, a->term, a->term_dtype, a->tm_sb, a->tm_st,
+                 a->filled, a->filled_dtype, a->fl_sb, a->fl_st, a->per_weight, a->gamma, a->td_lambda, a->mask_sum,
+                 a->gq, a->targets, a->prio, a->loss, a->mask_sum_acc, a->algo, a->B, a->T, stream);
 }
 
 extern "C" int t2o_adam_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq,

@@ -963,38 +963,14 @@ static int mixer_fwd_impl(const t2o_layout* L, const float* pack_on, const float
   return rc;
 }
 
-extern "C" int t2o_mixer_unroll_fwd(const t2o_layout* L, const float* pack_on, const float* pack_tg,
-                                    const float* states, int64_t st_sb, int64_t st_st,
-                                    const float* hid_on, const float* hid_tg, int64_t hid_sb, int64_t hid_st,
-                                    const float* hw0_on, const float* hw0_tg, int qmode_on, int qmode_tg,
-                                    const float* qv_on, const float* qv_tg, const float* q_on,
-                                    const float* q_tg, int q_ts, int n_actions, const int64_t* actions,
-                                    int64_t act_sb, int64_t act_st, const int32_t* avail, int64_t av_sb,
-                                    int64_t av_st, float* y_on, float* hw_on, float* qvo_on, float* xout_on,
-                                    float* xmid_on, float* y_tg, float* hw_tg, float* qvo_tg, float* xout_tg,
-                                    float* xmid_tg, int B, int T_on, int T_tg, void* stream) {
-  return mixer_fwd_impl(L, pack_on, pack_tg, states, st_sb, st_st, hid_on, hid_tg, hid_sb, hid_st, hw0_on, hw0_tg,
-                        qmode_on, qmode_tg, qv_on, qv_tg, q_on, q_tg, q_ts, n_actions, actions, act_sb, act_st,
-                        avail, av_sb, av_st, y_on, hw_on, qvo_on, xout_on, xmid_on, y_tg, hw_tg, qvo_tg, xout_tg,
-                        xmid_tg, B, T_on, T_tg, 0, 0, 0, stream);
-}
-
-extern "C" int t2o_mixer_unroll_fwd_split(const t2o_layout* L, const float* pack_on, const float* pack_tg,
-                                          const float* states, int64_t st_sb, int64_t st_st,
-                                          const float* hid_on, const float* hid_tg, int64_t hid_sb, int64_t hid_st,
-                                          const float* hw0_on, const float* hw0_tg, int qmode_on, int qmode_tg,
-                                          const float* qv_on, const float* qv_tg, const float* q_on,
-                                          const float* q_tg, int q_ts, int n_actions, const int64_t* actions,
-                                          int64_t act_sb, int64_t act_st, const int32_t* avail, int64_t av_sb,
-                                          int64_t av_st, float* y_on, float* hw_on, float* qvo_on, float* xout_on,
-                                          float* xmid_on, float* y_tg, float* hw_tg, float* qvo_tg, float* xout_tg,
-                                          float* xmid_tg, int B, int T_on, int T_tg, int phase, int t0, int t1,
-                                          void* stream) {
-  if (phase < 1 || phase > 2 || (phase == 1 && (t0 < 0 || t0 >= t1))) return T2O_EINVAL;
-  return mixer_fwd_impl(L, pack_on, pack_tg, states, st_sb, st_st, hid_on, hid_tg, hid_sb, hid_st, hw0_on, hw0_tg,
-                        qmode_on, qmode_tg, qv_on, qv_tg, q_on, q_tg, q_ts, n_actions, actions, act_sb, act_st,
-                        avail, av_sb, av_st, y_on, hw_on, qvo_on, xout_on, xmid_on, y_tg, hw_tg, qvo_tg, xout_tg,
-                        xmid_tg, B, T_on, T_tg, phase, t0, t1, stream);
+extern "C" int t2o_mixer_unroll_fwd(const t2o_mixer_fwd_args* a, void* stream) {
+  if (!a || a->phase < 0 || a->phase > 2 || (a->phase == 1 && (a->t0 < 0 || a->t0 >= a->t1))) return T2O_EINVAL;
+  const int ph = a->phase;
+  return mixer_fwd_impl(a->L, a->pack_on, a->pack_tg, a->states, a->st_sb, a->st_st, a->hid_on, a->hid_tg, a->hid_sb,
+                        a->hid_st, a->hw0_on, a->hw0_tg, a->qmode_on, a->qmode_tg, a->qv_on, a->qv_tg, a->q_on,
+                        a->q_tg, a->q_ts, a->n_actions, a->actions, a->act_sb, a->act_st, a->avail, a->av_sb,
+                        a->av_st, a->y_on, a->hw_on, a->qvo_on, a->xout_on, a->xmid_on, a->y_tg, a->hw_tg, a->qvo_tg,
+                        a->xout_tg, a->xmid_tg, a->B, a->T_on, a->T_tg, ph, ph ? a->t0 : 0, ph ? a->t1 : 0, stream);
 }
 
 // worst case: 1 episode per workgroup, plus the decoupled multi-tile mixer's
@@ -1011,28 +987,7 @@ extern "C" int t2o_mixer_split(const t2o_layout* L, int B) {
   return t2o::mixer_split_taken(*L, B) ? 1 : 0;
 }
 
-extern "C" int t2o_mixer_unroll_bwd(const t2o_layout* L, const float* pack, const float* states, int64_t st_sb,
-                                    int64_t st_st, const float* hid, int64_t hid_sb, int64_t hid_st,
-                                    const float* hw0, const float* qv, const float* hw, const float* xout,
-                                    const float* xmid, const float* gy, const float* ghw_ext, float* gqv,
-                                    float* ghid, float* ghw0, float* gslabs,
-                                    int max_slabs, int* nslab, void* tape, int B, int T, void* stream) {
-  return t2o_mixer_unroll_bwd_ex(L, pack, states, st_sb, st_st, hid, hid_sb, hid_st, hw0, qv, hw, xout, xmid, gy,
-                                 ghw_ext, gqv, ghid, ghw0, gslabs, max_slabs, nslab, tape, nullptr, 0, B, T, stream);
-}
-
-extern "C" int t2o_mixer_unroll_bwd_ex(const t2o_layout* L, const float* pack, const float* states, int64_t st_sb,
-                                       int64_t st_st, const float* hid, int64_t hid_sb, int64_t hid_st,
-                                       const float* hw0, const float* qv, const float* hw, const float* xout,
-                                       const float* xmid, const float* gy, const float* ghw_ext, float* gqv,
-                                       float* ghid, float* ghw0, float* gslabs, int max_slabs, int* nslab,
-                                       void* tape, float* work, int64_t work_floats, int B, int T, void* stream) {
-  return t2o_mixer_unroll_bwd_split(L, pack, states, st_sb, st_st, hid, hid_sb, hid_st, hw0, qv, hw, xout, xmid, gy,
-                                    ghw_ext, gqv, ghid, ghw0, gslabs, max_slabs, nslab, tape, work, work_floats,
-                                    nullptr, 0, 0, 0, B, T, stream);
-}
-
-extern "C" int t2o_mixer_unroll_bwd_split(const t2o_layout* L, const float* pack, const float* states,
+static int mixer_bwd_impl(const t2o_layout* L, const float* pack, const float* states,
                                           int64_t st_sb, int64_t st_st, const float* hid, int64_t hid_sb,
                                           int64_t hid_st, const float* hw0, const float* qv, const float* hw,
                                           const float* xout, const float* xmid, const float* gy,
@@ -1080,4 +1035,12 @@ extern "C" int t2o_mixer_unroll_bwd_split(const t2o_layout* L, const float* pack
                      rc = (L->prec ? launch_mixer_bwd<E_, H_, D_, NE_, FF_, RTM_, __bf16>(a, max_slabs, nslab, (hipStream_t)stream)
                                    : launch_mixer_bwd<E_, H_, D_, NE_, FF_, RTM_, float>(a, max_slabs, nslab, (hipStream_t)stream)));
   return rc;
+}
+
+extern "C" int t2o_mixer_unroll_bwd(const t2o_mixer_bwd_args* a, void* stream) {
+  if (!a) return T2O_EINVAL;
+  return mixer_bwd_impl(a->L, a->pack, a->states, a->st_sb, a->st_st, a->hid, a->hid_sb, a->hid_st, a->hw0, a->qv,
+                        a->hw, a->xout, a->xmid, a->gy, a->ghw_ext, a->gqv, a->ghid, a->ghw0, a->gslabs, a->max_slabs,
+                        a->nslab, a->tape, a->work, a->work_floats, a->ghw_carry, a->phase, a->t_lo, a->t_hi, a->B,
+                        a->T, stream);
 }

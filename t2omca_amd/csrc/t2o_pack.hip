@@ -336,6 +336,18 @@ extern "C" int t2o_layout_init_ex(t2o_layout* L, int kind, int E, int H, int D, 
 
 extern "C" int t2o_layout_sizeof(void) { return (int)sizeof(t2o_layout); }
 
+extern "C" int t2o_args_sizeof(int which) {
+  switch (which) {
+    case T2O_ARGS_AGENT_FWD: return (int)sizeof(t2o_agent_fwd_args);
+    case T2O_ARGS_AGENT_BWD: return (int)sizeof(t2o_agent_bwd_args);
+    case T2O_ARGS_MIXER_FWD: return (int)sizeof(t2o_mixer_fwd_args);
+    case T2O_ARGS_MIXER_BWD: return (int)sizeof(t2o_mixer_bwd_args);
+    case T2O_ARGS_TAPE: return (int)sizeof(t2o_tape_args);
+    case T2O_ARGS_TD: return (int)sizeof(t2o_td_args);
+    default: return -1;
+  }
+}
+
 extern "C" int t2o_abi_version(void) { return T2O_ABI_VERSION; }
 
 extern "C" int64_t t2o_param_count(int kind, int E, int H, int D, int F, int NA, int FF) {

@@ -9,7 +9,8 @@ from dataclasses import dataclass
 import torch
 
 from . import _lib
-from ._lib import check, lib, ptr, stream_ptr
+from ._lib import (AgentBwdArgs, AgentFwdArgs, MixerBwdArgs, MixerFwdArgs, TapeArgs, TDArgs, check, lib, ptr,
+                   stream_ptr)
 
 AGENT, MIXER = 0, 1
 
@@ -106,6 +107,11 @@ def reduce_slabs(slabs, nslab, out):
     return out
 
 
+def _p(t):
+    """Device address of a tensor for an argument struct's pointer field (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
 def _mark(timer, tag):
     if timer is not None:
         timer(tag)
@@ -117,7 +123,7 @@ def agent_unroll_fwd(shape: NetShape, pack_on, obs, h0_on=None, pack_tg=None, h0
     [A, n_ent*F] contiguous).  Returns (q_on, h_on[, q_tg, h_tg]) with
     q [B, T, A, NA], h [B, T, A, E].  hmid_on: optional [B, T, D-1, A, E]
     output buffer for the inter-block activations (used by the backward).
-    steps=(t0, t1): only those steps (t2o_agent_unroll_fwd_range: t0 > 0 continues
+    steps=(t0, t1): only those steps (t2o_agent_fwd_args.t0 / t1: t0 > 0 continues
     from h[t0 - 1]) into the given outs=(q_on, h_on, q_tg, h_tg)."""
     _dev(pack_on, obs, h0_on, pack_tg, h0_tg)
     B, T, A, nf = obs.shape
@@ -137,13 +143,15 @@ def agent_unroll_fwd(shape: NetShape, pack_on, obs, h0_on=None, pack_tg=None, h0
     for h0 in (h0_on, h0_tg):
         if h0 is not None:
             assert h0.is_contiguous() and h0.numel() == B * A * shape.E
-    args = (ctypes.byref(L), ptr(pack_on), ptr(pack_tg), ptr(obs), obs.stride(0), obs.stride(1), ptr(h0_on),
-            ptr(h0_tg), ptr(q_on), ptr(h_on), ptr(hmid_on), ptr(q_tg), ptr(h_tg), None, B, T, A)
-    fn = lib().t2o_agent_unroll_fwd_range
+    a = AgentFwdArgs(L=ctypes.pointer(L), pack_on=_p(pack_on), pack_tg=_p(pack_tg), obs=_p(obs),
+                     obs_sb=obs.stride(0), obs_st=obs.stride(1), h0_on=_p(h0_on), h0_tg=_p(h0_tg), q_on=_p(q_on),
+                     h_on=_p(h_on), hmid_on=_p(hmid_on), q_tg=_p(q_tg), h_tg=_p(h_tg), B=B, T=T, A=A)
+    fn = lib().t2o_agent_unroll_fwd
 
     def go(t0, t1):
+        a.t0, a.t1 = int(t0), int(t1)
         _mark(timer, "begin:agent_fwd")
-        check(fn(*args, t0, t1, stream_ptr()), "agent_unroll_fwd")
+        check(fn(ctypes.byref(a), stream_ptr()), "agent_unroll_fwd")
         _mark(timer, "end:agent_fwd")
     if launcher:  # go(t0, t1) per step range, the arguments converted once (pipelined learner)
         return go
@@ -247,7 +255,7 @@ def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchose
     gchosen [B,T,A] + actions (int64 [B, >=T, A], a-stride 1), gh [B,T,A,E].
     Returns (gpack, gh0) with gpack the compact weight-gradient block (with
     defer_contract, a DeferredContraction instead).  steps=(t_lo, t_hi): only
-    steps t_hi - 1 .. t_lo (t2o_agent_unroll_bwd_range; ranges from the last down
+    steps t_hi - 1 .. t_lo (t2o_agent_bwd_args.t_lo / t_hi; ranges from the last down
     on the same slabs / tape, gcarry [B*A, E] between them); the contraction is
     then always deferred (call it after the range that ends at step 0)."""
     _dev(pack, obs, h_seq, h0, gq, gchosen, actions, gh)
@@ -268,16 +276,18 @@ def agent_unroll_bwd(shape: NetShape, pack, obs, h_seq, h0=None, gq=None, gchose
     gh0 = torch.empty(B, A, shape.E, device=obs.device) if want_gh0 else None
     tiles = agent_tape_tiles(B, T, A)
     tape = _tape(shape, tiles, tape, obs.device)
-    nslab = ctypes.c_int(0)
-    args = (ctypes.byref(L), ptr(pack), ptr(obs), obs.stride(0), obs.stride(1), ptr(h0), ptr(h_seq), ptr(hmid),
-            h_seq.shape[1], ptr(gq), ptr(gchosen), ptr(actions), act_sb, act_st, ptr(gh), ptr(slabs), nmax,
-            ctypes.byref(nslab), ptr(tape), ptr(gh0), ptr(gcarry), B, T, A)
-    fn = lib().t2o_agent_unroll_bwd_range
+    nslab = ctypes.c_int32(0)
+    a = AgentBwdArgs(L=ctypes.pointer(L), pack=_p(pack), obs=_p(obs), obs_sb=obs.stride(0), obs_st=obs.stride(1),
+                     h0=_p(h0), h_seq=_p(h_seq), hmid=_p(hmid), h_ts=h_seq.shape[1], gq=_p(gq), gchosen=_p(gchosen),
+                     actions=_p(actions), act_sb=act_sb, act_st=act_st, gh=_p(gh), gslabs=_p(slabs), max_slabs=nmax,
+                     nslab=ctypes.pointer(nslab), tape=_p(tape), gh0=_p(gh0), gcarry=_p(gcarry), B=B, T=T, A=A)
+    fn = lib().t2o_agent_unroll_bwd
     fmt = int(lib().t2o_agent_bwd_tape_format(ctypes.byref(L), int(hmid is not None)))
 
     def go(t_lo, t_hi):
+        a.t_lo, a.t_hi = int(t_lo), int(t_hi)
         _mark(timer, "begin:agent_bwd")
-        check(fn(*args, t_lo, t_hi, stream_ptr()), "agent_unroll_bwd")
+        check(fn(ctypes.byref(a), stream_ptr()), "agent_unroll_bwd")
         _mark(timer, "end:agent_bwd")
         return DeferredContraction(shape, pack, tape, tiles, slabs, nslab.value, timer, "agent_dw", fmt)
     if launcher:  # go(t_lo, t_hi) per step range -> the (deferred) contraction
@@ -298,7 +308,7 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
     hid_* [B, >=T, A, E] (contiguous inner [A, E]); q_on/q_tg [B, q_ts, A, NA]
     contiguous; actions int64 [B, >=T, A]; avail int32 [B, >=T, A, NA].
     Returns dict of outputs per network: y [B,T], hw [B,T,3,E], qv [B,T,A], xout.
-    phase 1 / 2 (a decoupled mixer, t2o_mixer_unroll_fwd_split): the recurrence
+    phase 1 / 2 (a decoupled mixer, t2o_mixer_fwd_args.phase): the recurrence
     over steps=(t0, t1) / the parallel rows, into the given outs=(o_on, o_tg)."""
     _dev(pack_on, states, hid_on, qv_on, q_on, hw0_on, pack_tg, hid_tg, qv_tg, q_tg, hw0_tg)
     B = states.shape[0]
@@ -344,22 +354,22 @@ def mixer_unroll_fwd(shape: NetShape, pack_on, states, hid_on, *, qmode_on=0, qv
     n_actions = q_on.shape[3] if q_on is not None else 0
     act_sb, act_st = _mstrides(actions)
     av_sb, av_st = _mstrides(avail)
-    g = lambda d, k: ptr(d[k]) if d is not None else None  # noqa: E731
-    args = (ctypes.byref(L), ptr(pack_on), ptr(pack_tg), ptr(states), states.stride(0), states.stride(1),
-            ptr(hid_on), ptr(hid_tg), hid_on.stride(0), hid_on.stride(1), ptr(hw0_on), ptr(hw0_tg),
-            qmode_on, qmode_tg, ptr(qv_on), ptr(qv_tg), ptr(q_on), ptr(q_tg), q_ts, n_actions,
-            ptr(actions), act_sb, act_st, ptr(avail), av_sb, av_st,
-            g(o_on, "y"), g(o_on, "hw"), g(o_on, "qv"), g(o_on, "xout"), g(o_on, "xmid"),
-            g(o_tg, "y"), g(o_tg, "hw"), g(o_tg, "qv"), g(o_tg, "xout"), g(o_tg, "xmid"),
-            B, T_on, T_tg or 0)
-    fn_split, fn = lib().t2o_mixer_unroll_fwd_split, lib().t2o_mixer_unroll_fwd
+    g = lambda d, k: _p(d[k]) if d is not None else None  # noqa: E731
+    a = MixerFwdArgs(L=ctypes.pointer(L), pack_on=_p(pack_on), pack_tg=_p(pack_tg), states=_p(states),
+                     st_sb=states.stride(0), st_st=states.stride(1), hid_on=_p(hid_on), hid_tg=_p(hid_tg),
+                     hid_sb=hid_on.stride(0), hid_st=hid_on.stride(1), hw0_on=_p(hw0_on), hw0_tg=_p(hw0_tg),
+                     qmode_on=qmode_on, qmode_tg=qmode_tg, qv_on=_p(qv_on), qv_tg=_p(qv_tg), q_on=_p(q_on),
+                     q_tg=_p(q_tg), q_ts=q_ts, n_actions=n_actions, actions=_p(actions), act_sb=act_sb,
+                     act_st=act_st, avail=_p(avail), av_sb=av_sb, av_st=av_st,
+                     y_on=g(o_on, "y"), hw_on=g(o_on, "hw"), qvo_on=g(o_on, "qv"), xout_on=g(o_on, "xout"),
+                     xmid_on=g(o_on, "xmid"), y_tg=g(o_tg, "y"), hw_tg=g(o_tg, "hw"), qvo_tg=g(o_tg, "qv"),
+                     xout_tg=g(o_tg, "xout"), xmid_tg=g(o_tg, "xmid"), B=B, T_on=T_on, T_tg=T_tg or 0)
+    fn = lib().t2o_mixer_unroll_fwd
 
     def go(phase, t0=0, t1=0):
+        a.phase, a.t0, a.t1 = int(phase), int(t0), int(t1)
         _mark(timer, "begin:mixer_fwd")
-        if phase:
-            check(fn_split(*args, phase, t0, t1, stream_ptr()), "mixer_unroll_fwd_split")
-        else:
-            check(fn(*args, stream_ptr()), "mixer_unroll_fwd")
+        check(fn(ctypes.byref(a), stream_ptr()), "mixer_unroll_fwd")
         _mark(timer, "end:mixer_fwd")
     if launcher:  # go(phase, t0, t1) per phase / step range (pipelined learner)
         return go
@@ -374,8 +384,9 @@ def tape_contract(shape: NetShape, pack, tape, tiles, slabs, nslab, timer=None, 
     gradient block (on the current stream)."""
     L = shape.layout()
     _mark(timer, "begin:" + tag)
-    check(lib().t2o_bwd_tape_contract_ex(ctypes.byref(L), ptr(pack), ptr(tape), int(tiles), ptr(slabs), int(nslab),
-                                         int(fmt), stream_ptr()), "bwd_tape_contract")
+    a = TapeArgs(L=ctypes.pointer(L), pack=_p(pack), tape=_p(tape), tiles=int(tiles), gslabs=_p(slabs),
+                 nslab=int(nslab), rec_format=int(fmt))
+    check(lib().t2o_bwd_tape_contract(ctypes.byref(a), None, stream_ptr()), "bwd_tape_contract")
     _mark(timer, "end:" + tag)
     gpack = torch.empty(L.grad_total, device=slabs.device)
     reduce_slabs(slabs, nslab, gpack)
@@ -383,16 +394,17 @@ def tape_contract(shape: NetShape, pack, tape, tiles, slabs, nslab, timer=None, 
 
 
 def tape_contract_pair(dm: DeferredContraction, da: DeferredContraction, timer=None):
-    """Both backwards' tape contractions in one launch (t2o_bwd_tape_contract_pair;
+    """Both backwards' tape contractions in one launch (t2o_bwd_tape_contract with two tapes;
     dm the mixer's, da the agent's), then each slab sum.  Returns (gpack_m, gpack_a)."""
     Lm, La = dm.shape.layout(), da.shape.layout()
     dm.widen()
     da.widen()
     _mark(timer, "begin:dw_pair")
-    check(lib().t2o_bwd_tape_contract_pair(ctypes.byref(Lm), ptr(dm.pack), ptr(dm.tape), int(dm.tiles), ptr(dm.slabs),
-                                           int(dm.nslab), ctypes.byref(La), ptr(da.pack), ptr(da.tape), int(da.tiles),
-                                           ptr(da.slabs), int(da.nslab), int(da.fmt), stream_ptr()),
-          "bwd_tape_contract_pair")
+    am = TapeArgs(L=ctypes.pointer(Lm), pack=_p(dm.pack), tape=_p(dm.tape), tiles=int(dm.tiles), gslabs=_p(dm.slabs),
+                  nslab=int(dm.nslab), rec_format=0)
+    aa = TapeArgs(L=ctypes.pointer(La), pack=_p(da.pack), tape=_p(da.tape), tiles=int(da.tiles), gslabs=_p(da.slabs),
+                  nslab=int(da.nslab), rec_format=int(da.fmt))
+    check(lib().t2o_bwd_tape_contract(ctypes.byref(am), ctypes.byref(aa), stream_ptr()), "bwd_tape_contract (pair)")
     _mark(timer, "end:dw_pair")
     out = []
     for d, L in ((dm, Lm), (da, La)):
@@ -411,7 +423,7 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
     the tape contraction + slab sum (on whatever stream is current when called)
     and returns gpack.  work: optional float buffer for the decoupled multi-tile
     mixer (t2o_mixer_bwd_work_floats; allocated here when needed and not given).
-    phase 1 / 2 (a decoupled mixer, t2o_mixer_unroll_bwd_split): the parallel
+    phase 1 / 2 (a decoupled mixer, t2o_mixer_bwd_args.phase): the parallel
     part / the recurrence over steps=(t_lo, t_hi) (ranges from the last down,
     carry [B, 3, E] between them) into outs=(gqv, ghid), with the same slabs,
     tape and work every call; the contraction is then always deferred."""
@@ -435,19 +447,22 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
     ghw0 = torch.empty(B, 3, E, device=dev) if want_ghw0 else None
     tiles = mixer_tape_tiles(B, T, A, shape)
     tape = _tape(shape, tiles, tape, dev)
-    nslab = ctypes.c_int(0)
+    nslab = ctypes.c_int32(0)
     nwork = mixer_work_floats(shape, B, T)
     if nwork and (work is None or work.numel() < nwork):
         work = torch.empty(nwork, device=dev)
-    args = (ctypes.byref(L), ptr(pack), ptr(states), states.stride(0), states.stride(1), ptr(hid),
-            hid.stride(0), hid.stride(1), ptr(hw0), ptr(fwd["qv"]), ptr(fwd["hw"]), ptr(fwd["xout"]),
-            ptr(fwd.get("xmid")), ptr(gy), ptr(ghw_ext), ptr(gqv), ptr(ghid), ptr(ghw0), ptr(slabs), nmax,
-            ctypes.byref(nslab), ptr(tape), ptr(work) if nwork else None, nwork, ptr(carry))
-    fn = lib().t2o_mixer_unroll_bwd_split
+    a = MixerBwdArgs(L=ctypes.pointer(L), pack=_p(pack), states=_p(states), st_sb=states.stride(0),
+                     st_st=states.stride(1), hid=_p(hid), hid_sb=hid.stride(0), hid_st=hid.stride(1), hw0=_p(hw0),
+                     qv=_p(fwd["qv"]), hw=_p(fwd["hw"]), xout=_p(fwd["xout"]), xmid=_p(fwd.get("xmid")), gy=_p(gy),
+                     ghw_ext=_p(ghw_ext), gqv=_p(gqv), ghid=_p(ghid), ghw0=_p(ghw0), gslabs=_p(slabs), max_slabs=nmax,
+                     nslab=ctypes.pointer(nslab), tape=_p(tape), work=_p(work) if nwork else None, work_floats=nwork,
+                     ghw_carry=_p(carry), B=B, T=T)
+    fn = lib().t2o_mixer_unroll_bwd
 
     def go(phase, t_lo=0, t_hi=0):
+        a.phase, a.t_lo, a.t_hi = int(phase), int(t_lo), int(t_hi)
         _mark(timer, "begin:mixer_bwd")
-        check(fn(*args, phase, t_lo, t_hi, B, T, stream_ptr()), "mixer_unroll_bwd")
+        check(fn(ctypes.byref(a), stream_ptr()), "mixer_unroll_bwd")
         _mark(timer, "end:mixer_bwd")
         return DeferredContraction(shape, pack, tape, tiles, slabs, nslab.value, timer, "mixer_dw", 0)
     if launcher:  # go(phase, t_lo, t_hi) per phase / step range -> the (deferred) contraction
@@ -456,7 +471,7 @@ def mixer_unroll_bwd(shape: NetShape, pack, states, hid, fwd, gy, hw0=None, ghw_
     return (contract if defer_contract or phase else contract()), gqv, ghid, ghw0
 
 
-# t2o_td_loss_ex mask element types (include/t2omca.h T2O_DT_*)
+# TD loss mask element types (include/t2omca.h T2O_DT_*)
 _MASK_DT = {torch.float32: 0, torch.uint8: 1, torch.bool: 1, torch.int32: 2, torch.int64: 3}
 
 
@@ -491,16 +506,13 @@ def td_loss(qtot, qtot_tgt, reward, terminated=None, filled=None, per_weight=Non
     out = dict(gq=torch.empty(B, T, device=dev), targets=torch.empty(B, T, device=dev),
                prio=torch.empty(B, device=dev), loss=torch.empty(2, device=dev))
     rs, ts, fs = _mstrides(reward), _mstrides(terminated), _mstrides(filled)
-    args = (ptr(qtot), ptr(qtot_tgt), ptr(reward), rs[0], rs[1], ptr(terminated), _mask_dtype(terminated), ts[0],
-            ts[1], ptr(filled), _mask_dtype(filled), fs[0], fs[1], ptr(per_weight), float(gamma), float(td_lambda),
-            float(mask_sum), ptr(out["gq"]), ptr(out["targets"]), ptr(out["prio"]), ptr(out["loss"]))
-    if hasattr(lib(), "t2o_td_loss_ex2"):
-        check(lib().t2o_td_loss_ex2(*args, ptr(mask_sum_acc), TD_ALGOS[algo], B, T, stream_ptr()), "td_loss")
-    else:  # an older build under A/B timing (T2O_LIB)
-        assert algo == "auto"
-        check(lib().t2o_td_loss_ex(*args, B, T, stream_ptr()), "td_loss")
-        if mask_sum_acc is not None:
-            mask_sum_acc.add_(out["loss"][1:2])
+    a = TDArgs(qtot=_p(qtot), qtot_tgt=_p(qtot_tgt), reward=_p(reward), rw_sb=rs[0], rw_st=rs[1],
+               term=_p(terminated), tm_sb=ts[0], tm_st=ts[1], filled=_p(filled), fl_sb=fs[0], fl_st=fs[1],
+               per_weight=_p(per_weight), gq=_p(out["gq"]), targets=_p(out["targets"]), prio=_p(out["prio"]),
+               loss=_p(out["loss"]), mask_sum_acc=_p(mask_sum_acc), gamma=float(gamma), td_lambda=float(td_lambda),
+               mask_sum=float(mask_sum), term_dtype=_mask_dtype(terminated), filled_dtype=_mask_dtype(filled),
+               algo=TD_ALGOS[algo], B=B, T=T)
+    check(lib().t2o_td_loss(ctypes.byref(a), stream_ptr()), "td_loss")
     return out
 
 

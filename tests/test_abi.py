@@ -55,6 +55,23 @@ def test_layout_rejects_bad_shapes():
     assert _lib.lib().t2o_layout_init(ctypes.byref(L), 0, 32, 3, 2, 9, 5, 128, 8, 2) != 0  # precision
 
 
+def test_args_structs_match_c():
+    """The ctypes mirrors of the argument structs (ABI 6) have the C sizes, and a
+    misspelt field is an error, not a silently ignored attribute."""
+    from t2omca_amd import _lib
+    lib = _lib.lib()
+    for cls in _lib.ARGS_STRUCTS:
+        assert ctypes.sizeof(cls) == lib.t2o_args_sizeof(cls.WHICH), cls.__name__
+    assert lib.t2o_args_sizeof(99) == -1
+    a = _lib.TDArgs(B=3, T=4, gamma=0.99)
+    assert (a.B, a.T) == (3, 4) and abs(a.gamma - 0.99) < 1e-7 and a.qtot is None
+    with pytest.raises(AttributeError):
+        _lib.TDArgs(b=3)
+    assert lib.t2o_td_loss(None, None) == -1  # T2O_EINVAL, no launch
+    assert lib.t2o_bwd_tape_contract(None, None, None) == -1
+    assert lib.t2o_agent_unroll_fwd(None, None) == -1 and lib.t2o_mixer_unroll_bwd(None, None) == -1
+
+
 def test_layout_struct_matches_c():
     from t2omca_amd import _lib
     assert ctypes.sizeof(_lib.Layout) == _lib.lib().t2o_layout_sizeof()

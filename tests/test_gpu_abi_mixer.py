@@ -1,6 +1,7 @@
 """GPU: a C caller's view of the multi-tile mixer backward.  Every call goes
-straight through the C ABI (include/t2omca.h, no ops.* wrapper): layout, pack,
-forward, backward into a tape sized by t2o_bwd_tape_tiles, the tape contraction
+straight through the C ABI (include/t2omca.h, no ops.* wrapper; the unrolls, the
+BPTT and the contraction take their argument structs): layout, pack, forward,
+backward into a tape sized by t2o_bwd_tape_tiles, the tape contraction
 with that same tile count, the slab sum and the unfold into reference parameter
 order.  At 16 agents the mixer has A + 3 = 19 query rows, so the tuned kernel
 writes each block's records as one compact stream and the per-block stride is
@@ -62,11 +63,12 @@ def test_mixer_bwd_and_contraction_through_the_c_abi_A16(prec):
     qv_d, hid_d, st_d = qv.to(dev), hid.to(dev), states.to(dev)
     yo, hwo, qvo = torch.empty(B, T, device=dev), torch.empty(B, T, 3, E, device=dev), torch.empty(B, T, A, device=dev)
     xout, xmid = torch.empty(B, T, A + 3, E, device=dev), torch.empty(B, T, D - 1, A + 3, E, device=dev)
-    rc = lib.t2o_mixer_unroll_fwd(ctypes.byref(L), _p(pack), None, _p(st_d), st_d.stride(0), st_d.stride(1),
-                                  _p(hid_d), None, hid_d.stride(0), hid_d.stride(1), None, None, 0, 0,
-                                  _p(qv_d), None, None, None, 0, 0, None, 0, 0, None, 0, 0,
-                                  _p(yo), _p(hwo), _p(qvo), _p(xout), _p(xmid), None, None, None, None, None,
-                                  B, T, 0, s)
+    fa = _lib.MixerFwdArgs(L=ctypes.pointer(L), pack_on=pack.data_ptr(), states=st_d.data_ptr(),
+                           st_sb=st_d.stride(0), st_st=st_d.stride(1), hid_on=hid_d.data_ptr(),
+                           hid_sb=hid_d.stride(0), hid_st=hid_d.stride(1), qmode_on=0, qv_on=qv_d.data_ptr(),
+                           y_on=yo.data_ptr(), hw_on=hwo.data_ptr(), qvo_on=qvo.data_ptr(), xout_on=xout.data_ptr(),
+                           xmid_on=xmid.data_ptr(), B=B, T_on=T)
+    rc = lib.t2o_mixer_unroll_fwd(ctypes.byref(fa), s)
     assert rc == 0
     tiles = lib.t2o_bwd_tape_tiles(ctypes.byref(L), B, T, A)
     assert tiles == (B * T * (A + 3) + 15) // 16  # the compact stream, not B*T*ceil((A+3)/16)
@@ -76,13 +78,18 @@ def test_mixer_bwd_and_contraction_through_the_c_abi_A16(prec):
     slabs = torch.empty(nmax * L.grad_total, device=dev)
     gqv, ghid = torch.empty(B, T, A, device=dev), torch.empty(B, T, A, E, device=dev)
     cy_d, chw_d = cy.to(dev), chw.to(dev)
-    nslab = ctypes.c_int(0)
-    rc = lib.t2o_mixer_unroll_bwd(ctypes.byref(L), _p(pack), _p(st_d), st_d.stride(0), st_d.stride(1), _p(hid_d),
-                                  hid_d.stride(0), hid_d.stride(1), None, _p(qvo), _p(hwo), _p(xout), _p(xmid),
-                                  _p(cy_d), _p(chw_d), _p(gqv), _p(ghid), None, _p(slabs), nmax,
-                                  ctypes.byref(nslab), _p(tape), B, T, s)
+    nslab = ctypes.c_int32(0)
+    ba = _lib.MixerBwdArgs(L=ctypes.pointer(L), pack=pack.data_ptr(), states=st_d.data_ptr(), st_sb=st_d.stride(0),
+                           st_st=st_d.stride(1), hid=hid_d.data_ptr(), hid_sb=hid_d.stride(0), hid_st=hid_d.stride(1),
+                           qv=qvo.data_ptr(), hw=hwo.data_ptr(), xout=xout.data_ptr(), xmid=xmid.data_ptr(),
+                           gy=cy_d.data_ptr(), ghw_ext=chw_d.data_ptr(), gqv=gqv.data_ptr(), ghid=ghid.data_ptr(),
+                           gslabs=slabs.data_ptr(), max_slabs=nmax, nslab=ctypes.pointer(nslab), tape=tape.data_ptr(),
+                           B=B, T=T)
+    rc = lib.t2o_mixer_unroll_bwd(ctypes.byref(ba), s)
     assert rc == 0 and 1 <= nslab.value <= nmax
-    assert lib.t2o_bwd_tape_contract(ctypes.byref(L), _p(pack), _p(tape), tiles, _p(slabs), nslab.value, s) == 0
+    ta = _lib.TapeArgs(L=ctypes.pointer(L), pack=pack.data_ptr(), tape=tape.data_ptr(), tiles=tiles,
+                       gslabs=slabs.data_ptr(), nslab=nslab.value, rec_format=0)
+    assert lib.t2o_bwd_tape_contract(ctypes.byref(ta), None, s) == 0
     gpack = torch.empty(L.grad_total, device=dev)
     assert lib.t2o_reduce_slabs(_p(slabs), nslab.value, L.grad_total, _p(gpack), s) == 0
     grad = torch.zeros_like(params)

@@ -112,3 +112,35 @@ def test_other_heads_elementwise(name):
         ref_p, ref_d = x, torch.ones_like(x)
     assert torch.equal(p, ref_p) and torch.equal(p2, ref_p)
     assert torch.equal(d, ref_d) and torch.equal(d2, ref_d)
+
+
+def test_xdl_hand_off_wait_states():
+    """MFMA result hand-offs with a fixed number of wait states (t2o_probe.hip, inline
+    asm the compiler neither pads nor reorders), over 4096 waves.
+    32 states is past any MFMA's latency: the ground truth.  Asserted: what the
+    product's kernels rely on — a 16x16x4 f32 result stored to global memory from its
+    AGPRs 10 states on (hipcc's padding) and a same-opcode srcC chain back to back
+    hold the final value, as do the compiler-built references.  Reported (the
+    layout-sensitive failures): a 16x16x4 f32 result written to LDS 10 states on, and
+    a 16x16x32 bf16 result read as srcC by a 16x16x16 bf16 MFMA 0 / 4 states on —
+    hand-offs only the variant builds produced (tools/isa_hazards.py)."""
+    require_gpu()
+    from t2omca_amd._lib import check, lib, ptr, stream_ptr
+    W = 4096
+    x = torch.randn(W, 64, 12, generator=torch.Generator().manual_seed(3)).cuda()
+    out = torch.full((12, W, 64, 4), float("nan"), device="cuda")
+    check(lib().t2o_probe_xdl_hazards(ptr(x), ptr(out), W, stream_ptr()), "probe_xdl_hazards")
+    torch.cuda.synchronize()
+    o = out.cpu()
+    (lds10, lds32, glb10, glb32, mix0, mix4, mix32, same0, same32, ref_f32, ref_mix, ref_same) = o
+
+    def bad(a, b):  # waves with any lane differing
+        return int((a != b).any(dim=2).any(dim=1).sum())
+    rep = {"f32 -> LDS store @10": bad(lds10, lds32), "f32 -> global store @10": bad(glb10, glb32),
+           "f32 compiler ref": bad(ref_f32, lds32), "32x16 bf16 -> 16x16 srcC @0": bad(mix0, mix32),
+           "32x16 bf16 -> 16x16 srcC @4": bad(mix4, mix32), "mixed chain compiler ref": bad(ref_mix, mix32),
+           "32x16 bf16 -> 32x16 srcC @0": bad(same0, same32), "same chain compiler ref": bad(ref_same, same32)}
+    print(f"waves of {W} whose result differs from the 32-state hand-off:", rep)
+    assert torch.equal(lds32, glb32) and torch.isfinite(lds32).all()
+    assert rep["f32 -> global store @10"] == 0 and rep["f32 compiler ref"] == 0
+    assert rep["32x16 bf16 -> 32x16 srcC @0"] == 0 and rep["same chain compiler ref"] == 0

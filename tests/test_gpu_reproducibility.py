@@ -56,7 +56,7 @@ def test_td_update_bit_reproducible_across_runs(A, B, T, precision):
 @pytest.mark.parametrize("A,B,T,precision", [(8, 64, 12, "bf16"), (8, 6, 7, "fp32"), (16, 4, 6, "bf16"),
                                              (64, 2, 3, "bf16"), (5, 3, 4, "fp32")])
 def test_paired_contraction_equals_separate_launches(A, B, T, precision):
-    """t2o_bwd_tape_contract_pair (both tapes in one grid, TDLearner(contract="pair"))
+    """t2o_bwd_tape_contract with two tapes (both in one grid, TDLearner(contract="pair"))
     gives exactly the gradients of the two separate contractions (contract="side",
     the learner's default: the mixer's on the side stream):
     every workgroup runs the same code on the same tiles into the same slab."""

@@ -1,7 +1,7 @@
 """GPU: t2o_td_loss against the oracle's PyMARL2 TD(λ) semantics (oracle/ref_learner.py)
 on ragged episodes (filled tails of zeros, early termination), PER weights, both the local
 (mask_sum <= 0) and the externally supplied (data-parallel) normalisation, for both
-kernels (t2o_td_loss_ex2 algo: the sequential per-episode recursion in the oracle's
+kernels (t2o_td_args.algo: the sequential per-episode recursion in the oracle's
 order, and the one-wave-per-episode suffix scan, reassociated).  fp32, bar: 1e-5
 normwise."""
 import pytest
@@ -45,7 +45,7 @@ def _nw(a, b):
 @pytest.mark.parametrize("algo", ["sequential", "wave"])
 @pytest.mark.parametrize("B,T", [(1, 1), (7, 5), (5, 64), (3, 127), (300, 60), (1030, 150)])
 def test_td_loss_matches_oracle(B, T, algo):
-    """Both TD-loss kernels (t2o_td_loss_ex2: the sequential per-episode recursion and
+    """Both TD-loss kernels (t2o_td_args.algo: the sequential per-episode recursion and
     the one-wave-per-episode suffix scan; T = 64 / 127 put the scan's chunking on both
     sides of one step per lane)."""
     from t2omca_amd import ops
@@ -72,7 +72,7 @@ def test_td_loss_matches_oracle(B, T, algo):
 @pytest.mark.parametrize("algo", ["sequential", "wave"])
 @pytest.mark.parametrize("tdt,fdt", [(torch.uint8, torch.int64), (torch.bool, torch.int32)])
 def test_td_loss_native_mask_dtypes(tdt, fdt, algo):
-    """terminated / filled read in the EpisodeBatch's own storage types (t2o_td_loss_ex)
+    """terminated / filled read in the EpisodeBatch's own storage types (t2o_td_args.term_dtype / filled_dtype)
     give exactly the float-mask result (the masks are 0/1)."""
     from t2omca_amd import ops
     qtot, qtgt, reward, term, filled, w = _case(37, 23, 5)
