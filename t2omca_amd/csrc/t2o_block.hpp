@@ -30,19 +30,9 @@ struct PostCache {
 // instructions, block-1 BPTT wave 2466 -> 2247 with the paired key products.
 // fp32 (the reference-precision path, 1e-5 bar) keeps its summation order.
 // r2 (bf16: in = c2 + y) += W2 relu(f1)
-#ifndef T2O_RELU_BF16
-#define T2O_RELU_BF16 1
-#endif
 template <int ET, int FT, bool HOIST, typename WT>
 T2O_DEV void ffn_out_product(const Wts<WT>& P, int64_t off, int ld, const f4* f1, f4* r2) {
-  if constexpr (sizeof(WT) == 2 && !T2O_RELU_BF16) {  // fp32 ReLU, bias-first accumulation
-    f4 fr[FT];
-#pragma unroll
-    for (int t = 0; t < FT; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) fr[t][r] = fmaxf(f1[t][r], 0.f);
-    matvec<ET, FT, HOIST, true>(P.w + off, ld, fr, r2, P.vol);
-  } else if constexpr (sizeof(WT) == 2) {
+  if constexpr (sizeof(WT) == 2) {
     static_assert(FT % 2 == 0, "FFN tiles convert in pairs");
     bf4 fb[FT];
 #pragma unroll
@@ -62,14 +52,11 @@ T2O_DEV void ffn_out_product(const Wts<WT>& P, int64_t off, int ld, const f4* f1
   }
 }
 
-#ifndef T2O_BF_BACC
-#define T2O_BF_BACC 1
-#endif
 // r1 = N z + bu + x, y = LN1(r1), f1 = W1 y + c1 (bf16: bias-first accumulation)
 template <int ET, int HET, int FT, bool HOIST, typename WT>
 T2O_DEV void ffn_half(const Wts<WT>& P, const t2o_layout& L, int d, const f4* z, const f4* x, f4* r1, f4* y,
                       f4* xh1, float& rs1, f4* f1) {
-  constexpr bool BACC = sizeof(WT) == 2 && T2O_BF_BACC;
+  constexpr bool BACC = sizeof(WT) == 2;
   if constexpr (BACC) {
 #pragma unroll
     for (int t = 0; t < ET; ++t) r1[t] = vec_t(P.v + L.bu[d], t) + x[t];

@@ -85,7 +85,20 @@ __device__ long long t2o_prof_buf[128 * 8 * 4];  // [slot][wave][delta]
   } while (0)
 #endif
 
-// Debug builds only (python -m t2omca_amd.build --debug-poison): every kernel
+// Intra-wave LDS hand-off (one wave's lanes exchange rows through LDS): the
+// hardware keeps a wave's LDS operations in order, but __builtin_amdgcn_wave_barrier
+// alone is no memory barrier to the COMPILER, which may move a load of another
+// lane's row above this lane's store wherever it can prove the two addresses differ
+// for one lane.  The wavefront-scope fences make the hand-off an ordering point for
+// the optimiser; they emit no instructions.  (The bare barrier in the mixer kernels
+// let an edit elsewhere reorder such a pair: DESIGN §9.)
+T2O_DEV void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Debug builds only (tools/build_debug.sh, -DT2O_DEBUG_POISON=1): every kernel
 // first fills its launch's whole dynamic LDS allocation with 0xFFFFFFFF (a NaN
 // in fp32 and in both bf16 halves), so a read of LDS no code of the launch wrote
 // turns into a NaN in the results instead of whatever the previous workgroup on
@@ -274,6 +287,16 @@ T2O_DEV f4 mma_tile(const __bf16* __restrict__ W, int ldw, int o, int i, f4 x, f
   return mfma_b16(vol ? ldw4(p) : ldb4(p), to_bf4(x), acc);
 }
 
+// acc + A·B for a lone 16-wide K tail.  AFTER_B32: acc is a v_mfma_f32_16x16x32_bf16
+// result — chained in place, the 16x16x16 would read it stale (hipcc 7.2 issues the
+// pair with 0-4 wait states; t2o_probe_xdl_hazards), so the tail is
+// accumulated on its own and added by VALU (which hipcc pads correctly).
+template <bool AFTER_B32>
+T2O_DEV f4 chain_tail_b16(bf4 a, bf4 b, f4 acc) {
+  if constexpr (AFTER_B32) return acc + mfma_b16(a, b, zero4());
+  else return mfma_b16(a, b, acc);
+}
+
 // y[0..OT) = W · x[0..IT), bf16 weights and operands, fp32 accumulate
 template <int OT, int IT, bool HOIST = T2O_SWZ_HOIST, bool ACC = false>
 T2O_DEV void matvec_b(const __bf16* __restrict__ W, int ldw, const bf4* xb, f4* y, bool vol = true);
@@ -310,7 +333,7 @@ T2O_DEV void matvec_b(const __bf16* __restrict__ W, int ldw, const bf4* xb, f4* 
     }
     if constexpr (IT & 1) {
       const __bf16* p = row + ((16 * (IT - 1) + 4 * g) ^ xs);
-      acc = mfma_b16(vol ? ldw4(p) : ldb4(p), xb[IT - 1], acc);
+      acc = chain_tail_b16<(IT > 1)>(vol ? ldw4(p) : ldb4(p), xb[IT - 1], acc);
     }
     y[o] = acc;
   }
@@ -378,7 +401,7 @@ T2O_DEV void matvec_tr(const Wts<__bf16>& P, int64_t off, int ld, int64_t offT, 
     for (int i = 0; i + 1 < IT; i += 2)
       acc = mfma_b32(ld_tr_b16(W + (size_t)16 * i * ld + col), ld_tr_b16(W + (size_t)16 * (i + 1) * ld + col), xb[i],
                      xb[i + 1], acc);
-    if constexpr (IT & 1) acc = mfma_b16(ld_tr_b16(W + (size_t)16 * (IT - 1) * ld + col), xb[IT - 1], acc);
+    if constexpr (IT & 1) acc = chain_tail_b16<(IT > 1)>(ld_tr_b16(W + (size_t)16 * (IT - 1) * ld + col), xb[IT - 1], acc);
     y[o] = acc;
   }
 }

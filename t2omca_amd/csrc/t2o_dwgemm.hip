@@ -72,23 +72,12 @@ T2O_DEV void dw_vec_store(float* __restrict__ v, const float (&acc)[NT]) {
 
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 
-#ifndef T2O_DW_TG_A
-#define T2O_DW_TG_A 4
-#endif
-// bf16: contract tiles in pairs (K = 32 records per 16x16x32 MFMA; 0 = one tile
-// per 16x16x16 MFMA, the round-4 form).  The full (mixer) record's pair kernel
-// needs 256 VGPRs plus 12 B of scratch per lane, and one of four full GPU suites
-// on it failed the run-to-run reproducibility check (128 gradient elements, A=8,
-// 64 episodes, T=12; r5_final2) while ≥ 7 suites without it passed — so only the
-// lean agent record (223 VGPRs, no scratch) pairs by default (T2O_DW_PAIR_FULL=1
-// pairs both: mixer_dw 0.211 -> 0.197 ms alone, profiles/r5_dwp/).
-#ifndef T2O_DW_PAIR
-#define T2O_DW_PAIR 1
-#endif
-#ifndef T2O_DW_PAIR_FULL
-#define T2O_DW_PAIR_FULL 0
-#endif
-
+// bf16, the lean agent record: tiles are contracted in pairs (K = 32 records per
+// 16x16x32 MFMA).  The full (mixer) record keeps one tile per 16x16x16 MFMA: its
+// pair form needs 256 VGPRs plus 12 B of scratch, measured 14 us faster per update
+// alone (profiles/r5_dwp/), and one of four round-5 suites on it failed the
+// run-to-run reproducibility check (r5_final2; 87 later runs reproduced,
+// profiles/r6_hunt/x3_stress_pf.log, the cause unnamed): removed in round 6.
 template <typename TT> struct DwTraits;
 template <> struct DwTraits<__bf16> { static constexpr int TG = 2, PADC = 2; };  // tiles per group, pad chunks
 template <> struct DwTraits<float> { static constexpr int TG = 1, PADC = 1; };
@@ -103,7 +92,7 @@ struct DwDims {
   static constexpr bool BF = sizeof(TT) == 2;
   // tiles per group: the lean agent record is a third of the full one, so its
   // groups take more tiles (the same bytes in flight per workgroup)
-  static constexpr int TG = (FMT == 1 && BF) ? T2O_DW_TG_A : DwTraits<TT>::TG;
+  static constexpr int TG = (FMT == 1 && BF) ? 4 : DwTraits<TT>::TG;
   static constexpr int PER = 16 / (int)sizeof(TT);          // elements per 16-B chunk
   static constexpr int CPR = R::SIZE / PER;                  // chunks per record
   static constexpr int CPT = RT * CPR;                       // chunks per tile (HBM: RT records)
@@ -556,7 +545,7 @@ T2O_DEV void dw_run(const DwGemmArgs& a, int wg, int nwg, TT* buf0, TT* buf1, co
   DwRole<ROLE, E, H, FF, D, TT, FMT> st;
   st.init(a, d, wlds);
   auto compute = [&](const TT* buf) {
-    if constexpr (Dm::BF && Dm::TG % 2 == 0 && E == 32 && T2O_DW_PAIR && (FMT == 1 || T2O_DW_PAIR_FULL)) {
+    if constexpr (Dm::BF && Dm::TG % 2 == 0 && E == 32 && FMT == 1) {
 #pragma unroll
       for (int tt = 0; tt < Dm::TG; tt += 2) {
         st.tile2(buf + (d * Dm::TG + tt) * Dm::TSTR, buf + (d * Dm::TG + tt + 1) * Dm::TSTR);

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
     const float myq = mix_qv<E, A>(n, in, args.n_actions, args.avail != nullptr);
     __builtin_amdgcn_sched_barrier(0);  // every read of this step's inputs issued before they are reloaded
     if (t + 1 < n.T) mix_load<E, A>(args, n, b, t + 1, in, na);  // prefetch step t+1 (in is consumed)
-    __builtin_amdgcn_wave_barrier();
+    wave_sync();
     KeyFrags<E, Dm::KT, sizeof(WT) == 2> K;
     K.template load<Dm::LDX>(X0);
     T2O_MARK(1);
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft)
         x[ft] = q < nq ? ld4(X0 + (na + q) * Dm::LDX + 16 * ft + 4 * g) : zero4();
-      __builtin_amdgcn_wave_barrier();  // every X0 read done before OUT (may alias X0) is written
+      wave_sync();  // every X0 read done before OUT (may alias X0) is written
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         if (d > 0 && n.xmid && q < nq) {
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) st4(OUT + q * Dm::LDO + 16 * ft + 4 * g, x[ft]);
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_sync();
     float qv[A];
     bcast_agents<A>(myq, qv);
     float pre_h, pre2;
@@ -112,13 +112,13 @@ __global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
     if (n.xout) {
       for (int i = lane; i < nq * E; i += 64) n.xout[bt * nq * E + i] = OUT[(i / E) * Dm::LDO + i % E];
     }
-    __builtin_amdgcn_wave_barrier();  // OUT (may alias X0) fully read before the hyper rows change
+    wave_sync();  // OUT (may alias X0) fully read before the hyper rows change
 #pragma unroll
     for (int k = 0; k < (3 * E + 63) / 64; ++k) {
       const int i = lane + 64 * k;
       if (i < 3 * E) X0[(2 * na + i / E) * Dm::LDX + i % E] = hv[k];
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_sync();
     T2O_MARK(2 + D);
     if (blockIdx.y == 0) T2O_PROF_SAVE(t, 2 + D);
   }
@@ -244,7 +244,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
       if constexpr (!LEAN) {
         if (t > 0) mixb_load<E, A, D>(args, n, b, t - 1, nxt, na);  // prefetch step t-1
       }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       // ---- mixing head backward (lanes = features)
 #pragma unroll
       for (int k = 0; k < 3; ++k) ghw[k] += cur.ghx[k];
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
       mixer_head_bwd<E, A, WT, Bd::LDB>(P, L, OUT, GOUT, cur.m.qs[0], cur.gy, ghw, args.gqv + bt * na + lane, gWo, gbo, na,
                            RT ? L.pos_func : T2O_POS_ABS, RT ? L.pos_beta : 1.f);
       for (int i = nq * Bd::LDB + lane; i < Bd::OUTB; i += 64) GOUT[i] = 0.f;
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       // ---- blocks backward per query tile; gX0 accumulates in registers
       KeyFrags<E, KT, sizeof(WT) == 2> K;
       K.template load<Dm::LDX>(X0);
@@ -295,7 +295,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
             mixer_block_fwd_lean<E, H, KT, FF>(P, L, d, K, lk, x, cache, rec);
             mixer_block_bwd_lean<E, H, KT, FF>(P, L, gs, rec, stage, d, K, lk, gX0, cache, gx, ln2[d]);
           }
-          __builtin_amdgcn_wave_barrier();
+          wave_sync();
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft)
             st4(GOUT + (16 * qt + c) * Bd::LDB + 16 * ft + 4 * g, q < nq ? gx[ft] : zero4());
@@ -304,7 +304,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
       static_assert(LEAN || Dm::QT == 1, "the unrolled path runs one query tile");
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) gq0[0][ft] = ld4(GOUT + c * Bd::LDB + 16 * ft + 4 * g);
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       {
         const int q = c;
         f4 gx[ET];
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
             for (int r = 0; r < 4; ++r) gWe[ft] = mfma4(am[r], cur.stT[s][r], gWe[ft]);
           }
         }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       // ---- gX0 registers -> LDS rows [key][feature], plus the query path
       float* GX0 = stage;
 #pragma unroll
@@ -370,7 +370,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
         for (int ft = 0; ft < ET; ++ft)
 #pragma unroll
           for (int r = 0; r < 4; ++r) GX0[(16 * kt + 4 * g + r) * Bd::LDB + 16 * ft + c] = gX0[kt][ft][r];
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
 #pragma unroll
       for (int qt = 0; qt < Dm::QT; ++qt) {
         const int q = 16 * qt + c;
@@ -383,13 +383,13 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
           }
         }
       }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       // ---- key-token grads: agent hidden tokens out, hyper tokens carried
       for (int i = lane; i < na * E / 4; i += 64)
         st4(args.ghid + bt * na * E + 4 * i, ld4(GX0 + (na + 4 * i / E) * Bd::LDB + (4 * i) % E));
 #pragma unroll
       for (int k = 0; k < 3; ++k) ghw[k] = fv ? GX0[(2 * na + k) * Bd::LDB + f] : 0.f;
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       if constexpr (!LEAN) cur = nxt;
     }
     if (args.ghw0 && fv) {
@@ -441,10 +441,7 @@ struct MixPipeDims {
 // kernels' LDO) removes their T-layout bank conflicts here too, but measured slower
 // in this register-bound kernel: interleaved A/B, overlapped, 3 rounds
 // (profiles/r3_ab2/): mixer_bwd 0.618 ms at E vs 0.630 at E + 4.
-#ifndef T2O_MIXP_LDR
-#define T2O_MIXP_LDR E
-#endif
-  static constexpr int LDR = T2O_MIXP_LDR;
+  static constexpr int LDR = E;
   static constexpr int XCH = Dm::LKCAP * LDR;  // offset of the query-row grads in R
   static constexpr int R0 = Bd::W0 > Dm::KT * 16 * LDR ? Bd::W0 : Dm::KT * 16 * LDR;
   // (the hand-over needs R to hold the key grads and, past them, the query-row grads)
@@ -587,7 +584,7 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
         const int i = lane + 64 * k;
         if (i < 3 * E) X0[(2 * na + i / E) * Dm::LDX + i % E] = cur.hwp[k];
       }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       K.template load<Dm::LDX>(X0);
       f4 x[ET];
 #pragma unroll
@@ -600,30 +597,30 @@ T2O_DEV void mixp_block1(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
       float ghw[3];
 #pragma unroll
       for (int k = 0; k < 3; ++k) ghw[k] = (t < T - 1 && fv) ? R[(2 * na + k) * Pd::LDR + f] : 0.f;
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       float* OUT = R;  // forward final query rows, then their grads in place
 #pragma unroll
       for (int k = 0; k < In::XO; ++k) {
         const int i = lane + 64 * k;
         if (i < nq * E) OUT[(i / E) * Pd::LDR + i % E] = cur.xo[k];
       }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
 #pragma unroll
       for (int k = 0; k < 3; ++k) ghw[k] += cur.ghx[k];
       mixer_head_bwd<E, A, WT, Pd::LDR>(P, L, OUT, OUT, cur.qv, cur.gy, ghw, args.gqv + bt * na + lane, gWo, gbo, na,
                                         pf, pb);
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       f4 gx[ET];
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) gx[ft] = c < nq ? ld4(OUT + c * Pd::LDR + 16 * ft + 4 * g) : zero4();
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       f4 gX0[KT][ET];
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft) gX0[kt][ft] = zero4();
       mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, lk, gX0, cache, gx, ln2);
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       // hand-over to the block-0 wave
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
@@ -704,7 +701,7 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
           }
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) gx[ft] = c < nq ? ld4(R + Pd::XCH + c * Pd::LDR + 16 * ft + 4 * g) : zero4();
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, lk, gX0, cache, gx, ln2);
       // state embedding grads from the key-grad registers (as mixer_bwd_kernel)
 #pragma unroll
@@ -721,14 +718,14 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
             for (int r = 0; r < 4; ++r) gWe[ft] = mfma4(am[r], stT[s][r], gWe[ft]);
           }
         }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft)
 #pragma unroll
           for (int r = 0; r < 4; ++r) R[(16 * kt + 4 * g + r) * Pd::LDR + 16 * ft + c] = gX0[kt][ft][r];
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       if (c < nq) {  // the query path: block-0 input rows are X0's last na+3 rows
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft) {
@@ -736,7 +733,7 @@ T2O_DEV void mixp_block0(const MixerBwdArgs& args, const Wts<WT>& P0, const t2o_
           st4(dst, ld4(dst) + gx[ft]);
         }
       }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       for (int i = lane; i < na * E / 4; i += 64)
         st4(args.ghid + bt * na * E + 4 * i, ld4(R + (na + 4 * i / E) * Pd::LDR + (4 * i) % E));
       if (t == 0 && args.ghw0 && fv) {
@@ -811,10 +808,7 @@ T2O_DEV void mixer_bwd_pipe_body(const MixerBwdArgs& args, const t2o_layout& L, 
   // A/B, overlapped, 3 rounds: block 1 mixer_bwd 0.596 ms / update 2.556 ms,
   // block 0 0.634 / 2.602, none 0.637 / 2.586 (profiles/r2_pb/r2_prio_ovl/).
   // (Under workgroup barriers block 0 had measured better: 0.654 vs 0.665.)
-#ifndef T2O_MIXP_PRIO_BLOCK  // the block whose waves issue first on their SIMD (-1: none; A/B builds)
-#define T2O_MIXP_PRIO_BLOCK 1
-#endif
-  if (T2O_MIXP_PRIO_BLOCK >= 0 && d == T2O_MIXP_PRIO_BLOCK) __builtin_amdgcn_s_setprio(1);
+  if (d == 1) __builtin_amdgcn_s_setprio(1);  // the block-1 waves issue first on their SIMD
   if (d == 1)
     mixp_block1<E, H, A, FF, WT>(args, P0, L, G, gs, X0, R, b, pb, na, RT ? L.pos_func : T2O_POS_ABS,
                                  RT ? L.pos_beta : 1.f);

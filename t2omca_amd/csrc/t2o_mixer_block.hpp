@@ -39,20 +39,19 @@ struct MixerCache {
 // comb tile alone in comb1) — so each product takes half the MFMAs
 // and its B operand (u_h, gz_h; the probabilities) converts 8-wide, i.e. packed
 // (to_bf4: the 4-wide conversions of round 4 cost six VALU per tile).
-#ifndef T2O_KF_PAIR
-#define T2O_KF_PAIR 1
-#endif
-#ifndef T2O_KF_ODD_PAIR  // 1: an odd key-tile count pairs all but its last comb tile (A/B)
-#define T2O_KF_ODD_PAIR 0   // 2: ... the tail in its own accumulator, added by VALU
-#endif                      // 3: ... the tail chained after 16 wait states (diagnostic)
 template <int E, int KT, bool BF>
 struct KeyFrags {
-  // (an odd key-tile count keeps every comb tile unpaired: paired tiles plus a
-  // lone tail made the one-wave multi-tile BPTT disagree with the split kernels
-  // at 16 / 20 / 64 AGVs in bf16 — profiles/r5_bis/ — while 8, 13 and 40 AGVs,
-  // even counts, agree; the pairing's gain is at the headline's 2 key tiles)
-  static constexpr int ET = E / 16, EP = T2O_KF_PAIR ? ET / 2 : 0;
-  static constexpr int KP = !T2O_KF_PAIR || ((KT & 1) && !T2O_KF_ODD_PAIR) ? 0 : KT / 2;
+  // An odd key-tile count (16 / 20 / 64 AGVs) keeps every comb tile unpaired.  Paired
+  // tiles plus a lone tail chain a 16x16x16 MFMA onto a 16x16x32 result in place, and
+  // hipcc (ROCm 7.2) issues that pair with 0-4 wait states: on gfx950 the 16x16x16
+  // then reads a stale accumulator (t2o_probe_xdl_hazards: 3662 of 4096 waves wrong
+  // at 0 states, 3775 at 4; the same opcode back to back is exact).  That was round
+  // 5's run-to-run nondeterminism of the odd-pairing build (profiles/r5_bis/); with
+  // the tail padded or summed on its own it was exact and reproducible, and no faster
+  // (configs[0]-shape 3.640 / 3.663 vs 3.646 ms, 64 AGVs 40.41 / 40.45 vs 39.96 ms,
+  // profiles/r6_check/), so odd counts stay unpaired.
+  static constexpr int ET = E / 16, EP = ET / 2;
+  static constexpr int KP = (KT & 1) ? 0 : KT / 2;
   static constexpr bool EO = EP * 2 != ET, KO = KP * 2 != KT;
   // EU / KU unpaired feature / key tiles (the last ones: 2 EP .. ET-1, 2 KP .. KT-1)
   static constexpr int N_EP = EP > 0 ? EP : 1, N_KP = KP > 0 ? KP : 1, EU = ET - 2 * EP, KU = KT - 2 * KP;
@@ -122,7 +121,7 @@ T2O_DEV void keys_dot(const KeyFrags<E, KT, BF>& K, const f4* v, f4* out) {
       for (int p = 0; p < KF::EP; ++p) acc = mfma_b8(K.dot8[kt][p], vb[p], acc);
       if constexpr (KF::EO)
 #pragma unroll
-        for (int u = 0; u < KF::EU; ++u) acc = mfma_b16(K.dot1[kt][u], vt[u], acc);
+        for (int u = 0; u < KF::EU; ++u) acc = chain_tail_b16<(KF::EP > 0)>(K.dot1[kt][u], vt[u], acc);
       out[kt] = acc;
     }
   } else {
@@ -156,16 +155,10 @@ T2O_DEV void keys_combine(const KeyFrags<E, KT, BF>& K, const f4* w, f4* out) {
       f4 acc = zero4();
 #pragma unroll
       for (int p = 0; p < KF::KP; ++p) acc = mfma_b8(K.comb8[p][ft], wb[p], acc);
-      if constexpr (KF::KO && KF::KP > 0 && T2O_KF_ODD_PAIR == 2) {
-        f4 tail = zero4();
-#pragma unroll
-        for (int u = 0; u < KF::KU; ++u) tail = mfma_b16(K.comb1[u][ft], wt[u], tail);
-        acc += tail;
-      } else if constexpr (KF::KO) {
-        if constexpr (KF::KP > 0 && T2O_KF_ODD_PAIR == 3) asm volatile("s_nop 15" : "+v"(acc));
+      static_assert(!(KF::KO && KF::KP > 0), "a 16x16x16 chained onto a 16x16x32 accumulator (see KeyFrags)");
+      if constexpr (KF::KO)
 #pragma unroll
         for (int u = 0; u < KF::KU; ++u) acc = mfma_b16(K.comb1[u][ft], wt[u], acc);
-      }
       out[ft] = acc;
     }
   } else {

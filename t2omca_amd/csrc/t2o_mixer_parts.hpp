@@ -397,7 +397,7 @@ T2O_DEV void mixer_head_bwd(const Wts<WT>& P, const t2o_layout& L, const float* 
   gout[A + 2] = gpre2 * P.s(L.Wo + f) + ghw[2];
   gWo += gpre2 * x2;
   gbo += gpre2;
-  __builtin_amdgcn_wave_barrier();  // every OUT read done (GOUT may alias it)
+  wave_sync();  // every OUT read done (GOUT may alias it)
   if (fv) {
 #pragma unroll
     for (int q = 0; q < A + 3; ++q) {

@@ -114,7 +114,7 @@ __global__ __launch_bounds__(512) void mixs_fwd_rec_kernel(MixerFwdArgs args) {
     mix_keys<E, A>(P, L, in, X0, na);
     __builtin_amdgcn_sched_barrier(0);
     if (t + 1 < te) mixs_load_keys<E, A>(args, n, b, t + 1, in, na);
-    __builtin_amdgcn_wave_barrier();
+    wave_sync();
     KeyFrags<E, Dm::KT, sizeof(WT) == 2> K;
     K.template load<Dm::LDX>(X0);
     f4 x[ET];
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(512) void mixs_fwd_rec_kernel(MixerFwdArgs args) {
       st4(OUT + c * Dm::LDO + 16 * ft + 4 * g, x[ft]);
       st4(xo + 16 * ft + 4 * g, x[ft]);
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_sync();
     // the hyper rows na..na+2 are window rows 13..15: outputs, and step t+1's keys
     float hv[HW];
 #pragma unroll
@@ -145,13 +145,13 @@ __global__ __launch_bounds__(512) void mixs_fwd_rec_kernel(MixerFwdArgs args) {
       hv[k] = i < 3 * E ? OUT[(13 + i / E) * Dm::LDO + i % E] : 0.f;
       if (i < 3 * E) n.hw[bt * 3 * E + i] = hv[k];
     }
-    __builtin_amdgcn_wave_barrier();  // every X0 read of this step done (K, x) before the hyper rows change
+    wave_sync();  // every X0 read of this step done (K, x) before the hyper rows change
 #pragma unroll
     for (int k = 0; k < HW; ++k) {
       const int i = lane + 64 * k;
       if (i < 3 * E) X0[(2 * na + i / E) * Dm::LDX + i % E] = hv[k];
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_sync();
   }
 }
 
@@ -236,7 +236,7 @@ __global__ __launch_bounds__(512) void mixs_fwd_rows_kernel(MixerFwdArgs args) {
     const float myq = mix_qv<E, A>(n, in.m, args.n_actions, args.avail != nullptr);
     __builtin_amdgcn_sched_barrier(0);  // this item's inputs consumed before the next item's are loaded
     if (it + stride < items) mixs_rows_load<E, A>(args, n, (it + stride) / n.T, (it + stride) % n.T, in, na);
-    __builtin_amdgcn_wave_barrier();
+    wave_sync();
     KeyFrags<E, Dm::KT, sizeof(WT) == 2> K;
     K.template load<Dm::LDX>(X0);
     for (int qt = 0; qt < ntp; ++qt) {
@@ -263,14 +263,14 @@ __global__ __launch_bounds__(512) void mixs_fwd_rows_kernel(MixerFwdArgs args) {
         }
       }
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_sync();
     float qv[A];
     bcast_agents<A>(myq, qv);
     float pre_h, pre2;
     const float y = mixer_head<E, A>(P, L, OUT, qv, pre_h, pre2, na, pf, pb);
     if (lane == 0) n.y[bt] = y;
     if (n.qv && lane < na) n.qv[bt * na + lane] = myq;
-    __builtin_amdgcn_wave_barrier();  // OUT / X0 read before the next item writes them
+    wave_sync();  // OUT / X0 read before the next item writes them
   }
 }
 
@@ -350,13 +350,13 @@ __global__ __launch_bounds__(256) void mixs_bwd_rows_kernel(MixsBwdArgs sa) {
         const int i = lane + 64 * k;
         if (i < nq * E) OUT[(i / E) * Bd::LDB + i % E] = cur.xo[k];
       }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       // ---- mixing head backward without the carried hyper grads
       const float ghw0[3] = {0.f, 0.f, 0.f};
       mixer_head_bwd<E, A, WT, Bd::LDB>(P, L, OUT, GOUT, cur.m.qs[0], cur.gy, ghw0, args.gqv + bt * na + lane, gWo,
                                         gbo, na, RT ? L.pos_func : T2O_POS_ABS, RT ? L.pos_beta : 1.f);
       for (int i = nq * Bd::LDB + lane; i < Bd::OUTB; i += 64) GOUT[i] = 0.f;
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       // the window rows' grads for the recurrent kernel
       for (int i = lane; i < 16 * E; i += 64) sa.goutl[bt * 16 * E + i] = GOUT[(q0 + i / E) * Bd::LDB + i % E];
       KeyFrags<E, KT, sizeof(WT) == 2> K;
@@ -393,7 +393,7 @@ __global__ __launch_bounds__(256) void mixs_bwd_rows_kernel(MixsBwdArgs sa) {
           mixer_block_fwd_lean<E, H, KT, FF>(P, L, d, K, lk, x, cache, rec);
           mixer_block_bwd_lean<E, H, KT, FF>(P, L, gs, rec, stage, d, K, lk, gX0, cache, gx, ln2[d]);
         }
-        __builtin_amdgcn_wave_barrier();
+        wave_sync();
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft)
           if (qv_) st4(GOUT + q * Bd::LDB + 16 * ft + 4 * g, gx[ft]);
@@ -413,7 +413,7 @@ __global__ __launch_bounds__(256) void mixs_bwd_rows_kernel(MixsBwdArgs sa) {
             for (int r = 0; r < 4; ++r) gWe[ft] = mfma4(am[r], cur.stT[s][r], gWe[ft]);
           }
         }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       float* GX0 = stage;
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(256) void mixs_bwd_rows_kernel(MixsBwdArgs sa) {
         for (int ft = 0; ft < ET; ++ft)
 #pragma unroll
           for (int r = 0; r < 4; ++r) GX0[(16 * kt + 4 * g + r) * Bd::LDB + 16 * ft + c] = gX0[kt][ft][r];
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       // the query path of the rows before the window (all agents: q < q0 <= na)
       for (int qt = 0; qt < ntp; ++qt) {
         const int q = 16 * qt + c;
@@ -433,11 +433,11 @@ __global__ __launch_bounds__(256) void mixs_bwd_rows_kernel(MixsBwdArgs sa) {
           }
         }
       }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       for (int i = lane; i < na * E / 4; i += 64)
         st4(args.ghid + bt * na * E + 4 * i, ld4(GX0 + (na + 4 * i / E) * Bd::LDB + (4 * i) % E));
       for (int i = lane; i < 3 * E; i += 64) sa.pghw[bt * 3 * E + i] = GX0[(2 * na + i / E) * Bd::LDB + i % E];
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
     }
   }
   flush_in_wave_order([&] {
@@ -580,7 +580,7 @@ __global__ __launch_bounds__(256) void mixs_bwd_rec_kernel(MixsBwdArgs sa) {
         const int i = lane + 64 * k;
         GW[(i / E) * Bd::LDB + i % E] = cur.gl[k];
       }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       if (fv) {
 #pragma unroll
         for (int h = 0; h < 3; ++h) GW[(13 + h) * Bd::LDB + f] += ghw[h];
@@ -588,7 +588,7 @@ __global__ __launch_bounds__(256) void mixs_bwd_rec_kernel(MixsBwdArgs sa) {
       const MixsRecIn<E, A> now = cur;  // (the prefetch below overwrites cur)
       __builtin_amdgcn_sched_barrier(0);
       if (t > t_lo) mixs_rec_load<E, A>(sa, n, b, t - 1, cur, na);
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       KeyFrags<E, KT, sizeof(WT) == 2> K;
       K.template load<Dm::LDX>(X0);
       f4 gX0[KT][ET];
@@ -633,7 +633,7 @@ __global__ __launch_bounds__(256) void mixs_bwd_rec_kernel(MixsBwdArgs sa) {
             for (int r = 0; r < 4; ++r) gWe[ft] = mfma4(am[r], now.stT[s][r], gWe[ft]);
           }
         }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       float* GX0 = stage;
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
@@ -641,14 +641,14 @@ __global__ __launch_bounds__(256) void mixs_bwd_rec_kernel(MixsBwdArgs sa) {
         for (int ft = 0; ft < ET; ++ft)
 #pragma unroll
           for (int r = 0; r < 4; ++r) GX0[(16 * kt + 4 * g + r) * Bd::LDB + 16 * ft + c] = gX0[kt][ft][r];
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       // the window rows' query path
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) {
         float* dst = GX0 + (na + q) * Bd::LDB + 16 * ft + 4 * g;
         st4(dst, ld4(dst) + gx[ft]);
       }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       // agent hidden tokens: the parallel kernel's share + this one's
 #pragma unroll
       for (int k = 0; k < MixIn<E, A>::HV; ++k) {
@@ -659,7 +659,7 @@ __global__ __launch_bounds__(256) void mixs_bwd_rec_kernel(MixsBwdArgs sa) {
       // the hyper keys' total: the grad wrt the hyper outputs of step t - 1
 #pragma unroll
       for (int k = 0; k < 3; ++k) ghw[k] = fv ? GX0[(2 * na + k) * Bd::LDB + f] + now.ph[k] : 0.f;
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
     }
     float* const gout = t_lo > 0 ? sa.ghw_carry : args.ghw0;
     if (gout && fv) {
@@ -775,7 +775,7 @@ T2O_DEV void mixs_pipe_block1(const MixsBwdArgs& sa, const Wts<WT>& P0, const t2
         const int i = lane + 64 * k;
         if (i < 3 * E) X0[(2 * na + i / E) * Dm::LDX + i % E] = hwp[k];
       }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       K.template load<Dm::LDX>(X0);
       f4 x[ET];
 #pragma unroll
@@ -790,29 +790,29 @@ T2O_DEV void mixs_pipe_block1(const MixsBwdArgs& sa, const Wts<WT>& P0, const t2
       for (int k = 0; k < 3; ++k)
         ghw[k] = !fv ? 0.f : t < t_hi - 1 ? R[(2 * na + k) * Pd::LDR + f]
                            : t_hi < T ? sa.ghw_carry[((size_t)b * 3 + k) * E + f] : 0.f;
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
 #pragma unroll
       for (int k = 0; k < GL; ++k) {
         const int i = lane + 64 * k;
         R[(i / E) * Pd::LDR + i % E] = gl[k];
       }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       if (fv) {
 #pragma unroll
         for (int k = 0; k < 3; ++k) R[(13 + k) * Pd::LDR + f] += ghw[k] + ghx[k];
       }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       f4 gx[ET];
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) gx[ft] = ld4(R + c * Pd::LDR + 16 * ft + 4 * g);
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       f4 gX0[KT][ET];
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft) gX0[kt][ft] = zero4();
       mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, lk, gX0, cache, gx, ln2);
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       // hand-over to the block-0 wave
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
@@ -893,7 +893,7 @@ T2O_DEV void mixs_pipe_block0(const MixsBwdArgs& sa, const Wts<WT>& P0, const t2
           }
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) gx[ft] = ld4(R + Pd::XCH + c * Pd::LDR + 16 * ft + 4 * g);
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
       mixer_block_bwd_lean<E, H, KT, FF>(P, Lb, gs, rec, R, 0, K, lk, gX0, cache, gx, ln2);
 #pragma unroll
       for (int s = 0; s < Dm::ST; ++s)
@@ -909,20 +909,20 @@ T2O_DEV void mixs_pipe_block0(const MixsBwdArgs& sa, const Wts<WT>& P0, const t2
             for (int r = 0; r < 4; ++r) gWe[ft] = mfma4(am[r], stT[s][r], gWe[ft]);
           }
         }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
 #pragma unroll
         for (int ft = 0; ft < ET; ++ft)
 #pragma unroll
           for (int r = 0; r < 4; ++r) R[(16 * kt + 4 * g + r) * Pd::LDR + 16 * ft + c] = gX0[kt][ft][r];
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
 #pragma unroll
       for (int ft = 0; ft < ET; ++ft) {  // the window rows' query path
         float* dst = R + (na + q0 + c) * Pd::LDR + 16 * ft + 4 * g;
         st4(dst, ld4(dst) + gx[ft]);
       }
-      __builtin_amdgcn_wave_barrier();
+      wave_sync();
 #pragma unroll
       for (int k = 0; k < HV; ++k) {  // agent hidden tokens: the parallel kernel's share + the window's
         const int i = lane + 64 * k;

@@ -55,7 +55,7 @@ def parse(path, kre):
     funcs, cur, name = {}, None, None
     for line in open(path):
         m = re.match(r"^([\w.$]+):\s*(;.*)?$", line)
-        if m and not m.group(1).startswith("."):
+        if m and not m.group(1).startswith(".") and not m.group(1).isdigit():  # (digits: inline-asm local labels)
             name = m.group(1)
             if re.search(kre, name):
                 cur = funcs.setdefault(name, [])
@@ -64,7 +64,7 @@ def parse(path, kre):
             continue
         if cur is None:
             continue
-        if re.match(r"^\.LBB|^\.Ltmp|^\s*\.L", line):
+        if re.match(r"^\.LBB|^\.Ltmp|^\s*\.L|^\d+:", line):
             cur.append(("LABEL", [], set(), set()))
             continue
         s = line.split(";")[0].strip()
