@@ -23,8 +23,12 @@ namespace {
 // RT (t2o_dispatch.hpp RTM_): 0 exact agent count A + abs head; 1 runtime-agent
 // instance (A a capacity, args.na the agent count) + runtime head; 2 exact A +
 // runtime head (L.pos_func)
-template <int E, int H, int D, int A, int FF, int RT, bool WLDS, typename WT>
-__global__ __launch_bounds__(512) void mixer_fwd_kernel(MixerFwdArgs args) {
+// LB: the launch bound.  512 (8 waves, two per SIMD: 256 registers a wave); 256 for
+// the multi-tile mixers when the launch holds at most four waves per workgroup — the
+// LDS then admits one workgroup per CU, i.e. one wave per SIMD, and the wave may take
+// the whole register file (at 64 AGVs the 256-register build spilled 0.5-1.9 KB a lane)
+template <int E, int H, int D, int A, int FF, int RT, bool WLDS, typename WT, int LB = 512>
+__global__ __launch_bounds__(LB) void mixer_fwd_kernel(MixerFwdArgs args) {
   using Dm = MixDims<E, A>;
   constexpr int ET = E / 16;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -142,7 +146,10 @@ int launch_mixer_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
     lds = sizeof(float) * 4 * perw;
     if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
   }
-  auto kern = a.wlds ? mixer_fwd_kernel<E, H, D, A, FF, RT, true, WT> : mixer_fwd_kernel<E, H, D, A, FF, RT, false, WT>;
+  const bool wide = Dm::QT > 1 && a.waves <= 4 && 2 * lds > 160 * 1024;  // one wave per SIMD
+  auto kern = wide ? (a.wlds ? mixer_fwd_kernel<E, H, D, A, FF, RT, true, WT, Dm::QT == 1 ? 512 : 256>
+                             : mixer_fwd_kernel<E, H, D, A, FF, RT, false, WT, Dm::QT == 1 ? 512 : 256>)
+                   : (a.wlds ? mixer_fwd_kernel<E, H, D, A, FF, RT, true, WT> : mixer_fwd_kernel<E, H, D, A, FF, RT, false, WT>);
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid((args.B + a.waves - 1) / a.waves, nnet);
   hipLaunchKernelGGL(kern, grid, dim3(64 * a.waves), lds, stream, a);
@@ -165,7 +172,8 @@ int launch_mixer_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
 template <int E, int H, int D, int A, int FF, int RT, bool WLDS, typename WT>
 __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   using Dm = MixDims<E, A>;
-  using Bd = MixBwdDims<E, A>;
+  constexpr int KM = key_mode<Dm::KT, WT>();
+  using Bd = MixBwdDims<E, A, KM>;
   constexpr int ET = E / 16, KT = Dm::KT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   T2O_LDS_POISON(smem);
@@ -176,7 +184,8 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
   const int na = RT == 1 ? fa.na : A, nq = na + 3, lk = 2 * na + 3;
   const int w = wave_id();
   float* X0 = smem + args.lds_w + w * Bd::PERW;
-  float* WORK = X0 + Dm::X0F;
+  float* X0T = X0 + Dm::X0F;  // (KM 1: the transposed key block)
+  float* WORK = X0T + Bd::X0TF;
   float* GOUTB = Bd::GOUT ? WORK : WORK;        // head grads (rows of OUT layout)
   float* stage = WORK + Bd::GOUT;               // staging / gX0 region
   float* gs = args.slabs + (size_t)blockIdx.x * G.grad_total;
@@ -254,8 +263,8 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
       for (int i = nq * Bd::LDB + lane; i < Bd::OUTB; i += 64) GOUT[i] = 0.f;
       wave_sync();
       // ---- blocks backward per query tile; gX0 accumulates in registers
-      KeyFrags<E, KT, sizeof(WT) == 2> K;
-      K.template load<Dm::LDX>(X0);
+      KeyFrags<E, KT, sizeof(WT) == 2, KM> K;
+      load_keys<Dm::LDX>(K, X0, X0T);
       f4 gX0[KT][ET];
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
@@ -268,6 +277,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
         const int nqt = (nq + 15) / 16;
 #pragma unroll 1
         for (int qt = 0; qt < nqt; ++qt) {
+        const Wts<WT> Pq = step_view(P);  // (opaque per query tile: weight reads stay in the loop)
           const int q = 16 * qt + c;
           f4 gx[ET];
 #pragma unroll
@@ -284,7 +294,7 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
                   x[ft] = q < nq ? ld4(args.xmid + ((bt * (D - 1) + d - 1) * nq + q) * E + 16 * ft + 4 * g)
                                  : zero4();
               } else {
-                for (int dd = 0; dd < d; ++dd) mixer_block_fwd<E, H, KT, FF, false>(P, L, dd, K, lk, x, nullptr);
+                for (int dd = 0; dd < d; ++dd) mixer_block_fwd<E, H, KT, FF, false>(Pq, L, dd, K, lk, x, nullptr);
               }
             }
             // a tile's 16 records, or the nq - 16·qt real ones of the last
@@ -292,8 +302,8 @@ __global__ __launch_bounds__(256) void mixer_bwd_kernel(MixerBwdArgs args) {
                        ((size_t)d * ctiles * 16 + ((size_t)t * fa.B + b) * nq + 16 * qt) * Rec::SIZE;
             MixerCacheLean<E, H, KT, FF> cache;
             const MaskedRec<WT, 2> rec(tile, min(16, nq - 16 * qt), Rec::SIZE);  // non-temporal (MaskedRec)
-            mixer_block_fwd_lean<E, H, KT, FF>(P, L, d, K, lk, x, cache, rec);
-            mixer_block_bwd_lean<E, H, KT, FF>(P, L, gs, rec, stage, d, K, lk, gX0, cache, gx, ln2[d]);
+            mixer_block_fwd_lean<E, H, KT, FF>(Pq, L, d, K, lk, x, cache, rec);
+            mixer_block_bwd_lean<E, H, KT, FF>(Pq, L, gs, rec, stage, d, K, lk, gX0, cache, gx, ln2[d]);
           }
           wave_sync();
 #pragma unroll
@@ -834,7 +844,7 @@ __global__ __launch_bounds__(512) void mixer_bwd_pipe_kernel(MixerBwdArgs args) 
 template <int E, int H, int D, int A, int FF, int RT, typename WT>
 int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t stream) {
   if (!kernel_layout_matches<E, H, D, FF, WT>(args.f.L)) return T2O_EINVAL;  // (compile-time offsets)
-  constexpr int PERW = MixBwdDims<E, A>::PERW;
+  constexpr int PERW = MixBwdDims<E, A, key_mode<MixDims<E, A>::KT, WT>()>::PERW;
   const t2o_layout& L = args.f.L;
   args.lds_w = (int)((lds_weight_floats<WT>(L, L.fwd_total) + 15) / 16 * 16);
   if constexpr (D == 2 && MixPipeDims<E, A>::OK) {

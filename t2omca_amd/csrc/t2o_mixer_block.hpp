@@ -39,8 +39,20 @@ struct MixerCache {
 // comb tile alone in comb1) — so each product takes half the MFMAs
 // and its B operand (u_h, gz_h; the probabilities) converts 8-wide, i.e. packed
 // (to_bf4: the 4-wide conversions of round 4 cost six VALU per tile).
-template <int E, int KT, bool BF>
+// KM 1 (fp32 only): the fragments are read from LDS at each product instead of held
+// in registers — dot from the key block X0 itself, comb from a transposed copy X0T
+// ([feature][key], row stride 16 KT + 4) the kernel writes once per step.  The
+// one-wave BPTT kernels of the 32- / 64-agent capacity classes (KT >= 5) use it: their
+// 16·KT fragment registers beside KT·8 key-grad accumulators spilled 1-6 KB a lane.
+template <int KT, typename WT>
+constexpr int key_mode() { return sizeof(WT) == 4 && KT >= 5 ? 1 : 0; }
+
+template <int E, int KT, bool BF, int KM = 0>
 struct KeyFrags {
+  static_assert(KM == 0 || !BF, "LDS-read key fragments: fp32 only");
+  static constexpr bool IN_LDS = KM == 1;
+  static constexpr int LDXK = E + 4, LDT = 16 * KT + 4;  // X0 (MixDims::LDX) / X0T row strides
+  static constexpr int X0T_FLOATS = IN_LDS ? E * LDT : 0;
   // An odd key-tile count (16 / 20 / 64 AGVs) keeps every comb tile unpaired.  Paired
   // tiles plus a lone tail chain a 16x16x16 MFMA onto a 16x16x32 result in place, and
   // hipcc (ROCm 7.2) issues that pair with 0-4 wait states: on gfx950 the 16x16x16
@@ -56,12 +68,32 @@ struct KeyFrags {
   // EU / KU unpaired feature / key tiles (the last ones: 2 EP .. ET-1, 2 KP .. KT-1)
   static constexpr int N_EP = EP > 0 ? EP : 1, N_KP = KP > 0 ? KP : 1, EU = ET - 2 * EP, KU = KT - 2 * KP;
   // fp32
-  f4 dot[BF ? 1 : KT][BF ? 1 : ET], comb[BF ? 1 : KT][BF ? 1 : ET];
+  f4 dot[BF || IN_LDS ? 1 : KT][BF || IN_LDS ? 1 : ET], comb[BF || IN_LDS ? 1 : KT][BF || IN_LDS ? 1 : ET];
+  const float* x0 = nullptr;   // IN_LDS: the key block and its transposed copy
+  const float* x0t = nullptr;
   // bf16
   bf8 dot8[BF ? KT : 1][N_EP], comb8[BF ? N_KP : 1][ET];
   bf4 dot1[BF && EO ? KT : 1][EO ? EU : 1], comb1[BF && KO ? KU : 1][ET];
+  // IN_LDS: bind the block (X0T written by write_transposed, wave-synchronised)
+  T2O_DEV void bind(const float* X0, const float* X0T) {
+    x0 = X0;
+    x0t = X0T;
+  }
+  // X0T[f][k] = X0[k][f] for the KT·16 key rows (call after X0 is complete, then wave_sync)
+  static T2O_DEV void write_transposed(const float* X0, float* X0T) {
+    for (int i = threadIdx.x & 63; i < 16 * KT * E; i += 64) X0T[(i % E) * LDT + i / E] = X0[(i / E) * LDXK + i % E];
+  }
+  T2O_DEV f4 dotf(int kt, int ft) const {
+    if constexpr (IN_LDS) return ld4(x0 + (16 * kt + lane_c()) * LDXK + 16 * ft + 4 * lane_g());
+    else return dot[kt][ft];
+  }
+  T2O_DEV f4 combf(int kt, int ft) const {
+    if constexpr (IN_LDS) return ld4(x0t + (16 * ft + lane_c()) * LDT + 16 * kt + 4 * lane_g());
+    else return comb[kt][ft];
+  }
   template <int LDX>
   T2O_DEV void load(const float* __restrict__ X0) {
+    static_assert(!IN_LDS, "LDS-read fragments: bind()");
     const int c = lane_c(), g = lane_g();
     auto arow = [&](int kt, int ft) { return ld4(X0 + (16 * kt + c) * LDX + 16 * ft + 4 * g); };
     auto bcol = [&](int kt, int ft) {
@@ -99,12 +131,26 @@ struct KeyFrags {
   }
 };
 
+// The step's key fragments: into registers (KM 0), or X0T written and the LDS copy
+// bound (KM 1).  X0 must be complete and wave-synchronised; X0T's previous readers done.
+template <int LDX, int E, int KT, bool BF, int KM>
+T2O_DEV void load_keys(KeyFrags<E, KT, BF, KM>& K, const float* X0, float* X0T) {
+  if constexpr (KM == 1) {
+    KeyFrags<E, KT, BF, KM>::write_transposed(X0, X0T);
+    wave_sync();
+    K.bind(X0, X0T);
+  } else {
+    (void)X0T;
+    K.template load<LDX>(X0);
+  }
+}
+
 T2O_DEV f4 mfma_b8(bf8 a, bf8 b, f4 acc) { return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0); }
 
 // Sᵀ-style product: out[kt] (keys 16kt+4g+r, query c) = Σ_f X0[key][f] v[f]
-template <int E, int KT, bool BF>
-T2O_DEV void keys_dot(const KeyFrags<E, KT, BF>& K, const f4* v, f4* out) {
-  using KF = KeyFrags<E, KT, BF>;
+template <int E, int KT, bool BF, int KM>
+T2O_DEV void keys_dot(const KeyFrags<E, KT, BF, KM>& K, const f4* v, f4* out) {
+  using KF = KeyFrags<E, KT, BF, KM>;
   constexpr int ET = E / 16;
   if constexpr (BF) {
     bf8 vb[KF::N_EP];
@@ -129,18 +175,20 @@ T2O_DEV void keys_dot(const KeyFrags<E, KT, BF>& K, const f4* v, f4* out) {
     for (int kt = 0; kt < KT; ++kt) {
       f4 acc = zero4();
 #pragma unroll
-      for (int ft = 0; ft < ET; ++ft)
+      for (int ft = 0; ft < ET; ++ft) {
+        const f4 d = K.dotf(kt, ft);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc = mfma4(K.dot[kt][ft][s], v[ft][s], acc);
+        for (int s = 0; s < 4; ++s) acc = mfma4(d[s], v[ft][s], acc);
+      }
       out[kt] = acc;
     }
   }
 }
 
 // Zᵀ-style product: out[ft] (features 16ft+4g+r, query c) = Σ_key X0[key][f] w[key]
-template <int E, int KT, bool BF>
-T2O_DEV void keys_combine(const KeyFrags<E, KT, BF>& K, const f4* w, f4* out) {
-  using KF = KeyFrags<E, KT, BF>;
+template <int E, int KT, bool BF, int KM>
+T2O_DEV void keys_combine(const KeyFrags<E, KT, BF, KM>& K, const f4* w, f4* out) {
+  using KF = KeyFrags<E, KT, BF, KM>;
   constexpr int ET = E / 16;
   if constexpr (BF) {
     bf8 wb[KF::N_KP];
@@ -166,9 +214,11 @@ T2O_DEV void keys_combine(const KeyFrags<E, KT, BF>& K, const f4* w, f4* out) {
     for (int ft = 0; ft < ET; ++ft) {
       f4 acc = zero4();
 #pragma unroll
-      for (int kt = 0; kt < KT; ++kt)
+      for (int kt = 0; kt < KT; ++kt) {
+        const f4 b = K.combf(kt, ft);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc = mfma4(K.comb[kt][ft][s], w[kt][s], acc);
+        for (int s = 0; s < 4; ++s) acc = mfma4(b[s], w[kt][s], acc);
+      }
       out[ft] = acc;
     }
   }
@@ -196,9 +246,9 @@ T2O_DEV void key_mask(f4* s, int Lk, int g) {
 }
 
 // HOIST: matvec's swizzle hoisting (t2o_common.hpp), true from the forward kernel
-template <int E, int H, int KT, int FF, bool CACHE, typename WT, bool HOIST = T2O_SWZ_HOIST>
+template <int E, int H, int KT, int FF, bool CACHE, typename WT, bool HOIST = T2O_SWZ_HOIST, int KM = 0>
 T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
-                             const KeyFrags<E, KT, sizeof(WT) == 2>& K, int Lk, f4* x,
+                             const KeyFrags<E, KT, sizeof(WT) == 2, KM>& K, int Lk, f4* x,
                              MixerCache<E, H, KT, FF>* cache) {
   constexpr int ET = E / 16, HET = H * ET;
   constexpr bool BF = sizeof(WT) == 2;
@@ -209,7 +259,7 @@ T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
     f4 s[KT];
-    keys_dot<E, KT, BF>(K, &u[hh * ET], s);
+    keys_dot(K, &u[hh * ET], s);
     key_mask<KT, !BF && !(T2O_KM_FP32_FLAT & 1)>(s, Lk, g);
     float m = -INFINITY;
 #pragma unroll
@@ -228,7 +278,7 @@ T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
     const float il = rcp_fast(allsum4(l));
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) s[kt] *= il;
-    keys_combine<E, KT, BF>(K, s, &z[hh * ET]);
+    keys_combine(K, s, &z[hh * ET]);
     if constexpr (CACHE) {
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt) cache->p[hh][kt] = s[kt];
@@ -246,10 +296,10 @@ T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
 // holds gX0[key 16kt+4g+r][feature 16ft+c] — accumulates the grad wrt the key
 // tokens (a contraction over queries = rows, via the staging transposes).
 // Big-matrix operand pairs go to the query row's tape record (null = padding).
-template <int E, int H, int KT, int FF, typename WT>
+template <int E, int H, int KT, int FF, typename WT, int KM = 0>
 T2O_DEV void mixer_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_layout& G,
                              float* __restrict__ gs, WT* __restrict__ rec, float* __restrict__ stage, int d,
-                             const KeyFrags<E, KT, sizeof(WT) == 2>& K, f4 (&gX0)[KT][E / 16],
+                             const KeyFrags<E, KT, sizeof(WT) == 2, KM>& K, f4 (&gX0)[KT][E / 16],
                              const MixerCache<E, H, KT, FF>& c, f4* gx, f4* ln2) {
   constexpr int ET = E / 16, HET = H * ET;
   constexpr bool BF = sizeof(WT) == 2;
@@ -259,7 +309,7 @@ T2O_DEV void mixer_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_la
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
     f4 gp[KT];
-    keys_dot<E, KT, BF>(K, &gz[hh * ET], gp);
+    keys_dot(K, &gz[hh * ET], gp);
     float dot = 0.f;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt)
@@ -269,7 +319,7 @@ T2O_DEV void mixer_block_bwd(const Wts<WT>& P, const t2o_layout& L, const t2o_la
     f4 gsc[KT];
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) gsc[kt] = c.p[hh][kt] * (gp[kt] - dot);
-    keys_combine<E, KT, BF>(K, gsc, &gu[hh * ET]);
+    keys_combine(K, gsc, &gu[hh * ET]);
     dw_accumulate_regs<KT, ET, BF>(gX0, c.p[hh], &gz[hh * ET], stage);
     dw_accumulate_regs<KT, ET, BF>(gX0, gsc, &c.u[hh * ET], stage);
   }
@@ -298,10 +348,10 @@ struct MixerCacheLean {
 };
 
 // softmax over the Lk valid keys of one head's scores: s[kt] (keys 16kt+4g+r, query c)
-template <int E, int KT, bool BF>
-T2O_DEV void attn_probs(const KeyFrags<E, KT, BF>& K, const f4* u, int Lk, f4* s) {
+template <int E, int KT, bool BF, int KM>
+T2O_DEV void attn_probs(const KeyFrags<E, KT, BF, KM>& K, const f4* u, int Lk, f4* s) {
   const int g = lane_g();
-  keys_dot<E, KT, BF>(K, u, s);
+  keys_dot(K, u, s);
   key_mask<KT, !BF && !(T2O_KM_FP32_FLAT & 2)>(s, Lk, g);
   float m = -INFINITY;
 #pragma unroll
@@ -322,9 +372,9 @@ T2O_DEV void attn_probs(const KeyFrags<E, KT, BF>& K, const f4* u, int Lk, f4* s
   for (int kt = 0; kt < KT; ++kt) s[kt] *= il;
 }
 
-template <int E, int H, int KT, int FF, typename WT, int CP>
+template <int E, int H, int KT, int FF, typename WT, int CP, int KM = 0>
 T2O_DEV void mixer_block_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d,
-                                  const KeyFrags<E, KT, sizeof(WT) == 2>& K, int Lk, f4* x,
+                                  const KeyFrags<E, KT, sizeof(WT) == 2, KM>& K, int Lk, f4* x,
                                   MixerCacheLean<E, H, KT, FF>& cache, const MaskedRec<WT, CP>& rec) {
   constexpr int ET = E / 16, HET = H * ET;
   constexpr bool BF = sizeof(WT) == 2;
@@ -333,20 +383,20 @@ T2O_DEV void mixer_block_fwd_lean(const Wts<WT>& P, const t2o_layout& L, int d,
 #pragma unroll
   for (int hh = 0; hh < H; ++hh) {
     f4 s[KT];
-    attn_probs<E, KT, BF>(K, &cache.u[hh * ET], Lk, s);
+    attn_probs(K, &cache.u[hh * ET], Lk, s);
     if constexpr (MixerCacheLean<E, H, KT, FF>::PC) {
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt) cache.p[hh][kt] = s[kt];
     }
-    keys_combine<E, KT, BF>(K, s, &z[hh * ET]);
+    keys_combine(K, s, &z[hh * ET]);
   }
   post_fwd_lean<E, H, FF>(P, L, d, z, x, &cache.post, rec);
 }
 
-template <int E, int H, int KT, int FF, typename WT, int CP>
+template <int E, int H, int KT, int FF, typename WT, int CP, int KM = 0>
 T2O_DEV void mixer_block_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* __restrict__ gs,
                                   const MaskedRec<WT, CP>& rec, float* __restrict__ stage, int d,
-                                  const KeyFrags<E, KT, sizeof(WT) == 2>& K, int Lk, f4 (&gX0)[KT][E / 16],
+                                  const KeyFrags<E, KT, sizeof(WT) == 2, KM>& K, int Lk, f4 (&gX0)[KT][E / 16],
                                   const MixerCacheLean<E, H, KT, FF>& c, f4* gx, f4* ln2) {
   constexpr int ET = E / 16, HET = H * ET;
   constexpr bool BF = sizeof(WT) == 2;
@@ -360,10 +410,10 @@ T2O_DEV void mixer_block_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* 
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt) p[kt] = c.p[hh][kt];
     } else {
-      attn_probs<E, KT, BF>(K, &c.u[hh * ET], Lk, p);
+      attn_probs(K, &c.u[hh * ET], Lk, p);
     }
     f4 gp[KT];
-    keys_dot<E, KT, BF>(K, &gz[hh * ET], gp);
+    keys_dot(K, &gz[hh * ET], gp);
     float dot = 0.f;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt)
@@ -373,7 +423,7 @@ T2O_DEV void mixer_block_bwd_lean(const Wts<WT>& P, const t2o_layout& L, float* 
     f4 gsc[KT];
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) gsc[kt] = p[kt] * (gp[kt] - dot);
-    keys_combine<E, KT, BF>(K, gsc, &gu[hh * ET]);
+    keys_combine(K, gsc, &gu[hh * ET]);
     dw_accumulate_regs<KT, ET, BF>(gX0, p, &gz[hh * ET], stage);
     dw_accumulate_regs<KT, ET, BF>(gX0, gsc, &c.u[hh * ET], stage);
   }

@@ -332,9 +332,11 @@ T2O_DEV void mixb_load(const MixerBwdArgs& args, const MixerNet& n, int b, int t
     }
 }
 
-template <int E, int A>
+template <int E, int A, int KM = 0>
 struct MixBwdDims {
   using Dm = MixDims<E, A>;
+  // KM 1: the transposed key block X0T of LDS-read key fragments (KeyFrags) after X0
+  static constexpr int X0TF = KM ? E * (16 * Dm::KT + 4) : 0;
   static constexpr int ET = E / 16, KT = Dm::KT;
   static constexpr int NSTAGE = (KT < ET ? KT : ET) < 2 ? 2 : (KT < ET ? KT : ET);
   static constexpr int STAGE = StageDims<NSTAGE>::FLOATS;
@@ -351,7 +353,7 @@ struct MixBwdDims {
   static constexpr int GOUT = Dm::QT == 1 ? 0 : OUTB;
   static constexpr int W0 = OUTB > STAGE ? OUTB : STAGE;
   static constexpr int WORK = GOUT + (W0 > GX0B ? W0 : GX0B);
-  static constexpr int PERW = Dm::X0F + WORK;
+  static constexpr int PERW = Dm::X0F + X0TF + WORK;
 };
 
 // Mixing-head backward of one (episode, step), lanes = features

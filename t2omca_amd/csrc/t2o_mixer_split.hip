@@ -77,8 +77,9 @@ struct MixsFwdDims {
   static constexpr int PERW = Dm::X0F + 16 * Dm::LDO;  // key block + the window's final rows
 };
 
-template <int E, int H, int D, int A, int FF, int RT, bool WLDS, typename WT>
-__global__ __launch_bounds__(512) void mixs_fwd_rec_kernel(MixerFwdArgs args) {
+// LB: as mixer_fwd_kernel's (t2o_mixer.hip)
+template <int E, int H, int D, int A, int FF, int RT, bool WLDS, typename WT, int LB = 512>
+__global__ __launch_bounds__(LB) void mixs_fwd_rec_kernel(MixerFwdArgs args) {
   using Dm = MixDims<E, A>;
   constexpr int ET = E / 16, HW = mixs_hw<E>();
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -247,12 +248,13 @@ __global__ __launch_bounds__(512) void mixs_fwd_rows_kernel(MixerFwdArgs args) {
       for (int ft = 0; ft < ET; ++ft) x[ft] = qv_ ? ld4(X0 + (na + q) * Dm::LDX + 16 * ft + 4 * g) : zero4();
 #pragma unroll
       for (int d = 0; d < D; ++d) {
+        const Wts<WT> Pq = step_view(P);  // (opaque per query tile: weight reads stay in the loop)
         if (d > 0 && n.xmid && qv_) {
           float* xm = n.xmid + (((bt * (D - 1) + d - 1) * nq) + q) * E;
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft) st4(xm + 16 * ft + 4 * g, x[ft]);
         }
-        mixer_block_fwd<E, H, Dm::KT, FF, false>(P, L, d, K, lk, x, nullptr);
+        mixer_block_fwd<E, H, Dm::KT, FF, false>(Pq, L, d, K, lk, x, nullptr);
       }
       if (qv_) {
         float* xo = n.xout + (bt * nq + q) * E;
@@ -293,7 +295,8 @@ struct MixsBwdArgs {
 template <int E, int H, int D, int A, int FF, int RT, bool WLDS, typename WT>
 __global__ __launch_bounds__(256) void mixs_bwd_rows_kernel(MixsBwdArgs sa) {
   using Dm = MixDims<E, A>;
-  using Bd = MixBwdDims<E, A>;
+  constexpr int KM = key_mode<Dm::KT, WT>();
+  using Bd = MixBwdDims<E, A, KM>;
   constexpr int ET = E / 16, KT = Dm::KT;
   static_assert(Dm::QT > 1, "multi-tile mixers only");
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -306,7 +309,8 @@ __global__ __launch_bounds__(256) void mixs_bwd_rows_kernel(MixsBwdArgs sa) {
   const int na = RT == 1 ? fa.na : A, nq = na + 3, lk = 2 * na + 3, q0 = mixs_q0(nq);
   const int w = wave_id();
   float* X0 = smem + args.lds_w + w * Bd::PERW;
-  float* GOUT = X0 + Dm::X0F;       // head grads, rows of OUT layout (stride LDB)
+  float* X0T = X0 + Dm::X0F;        // (KM 1: the transposed key block)
+  float* GOUT = X0T + Bd::X0TF;     // head grads, rows of OUT layout (stride LDB)
   float* stage = GOUT + Bd::GOUT;   // final rows (head) / staging / gX0 region
   float* gs = args.slabs + (size_t)(sa.slab0 + blockIdx.x) * G.grad_total;
   Wts<WT> P0 = WLDS ? stage_weights(smem, n.pack, L, L.fwd_total, WT{}) : global_weights(n.pack, L, WT{});
@@ -359,8 +363,8 @@ __global__ __launch_bounds__(256) void mixs_bwd_rows_kernel(MixsBwdArgs sa) {
       wave_sync();
       // the window rows' grads for the recurrent kernel
       for (int i = lane; i < 16 * E; i += 64) sa.goutl[bt * 16 * E + i] = GOUT[(q0 + i / E) * Bd::LDB + i % E];
-      KeyFrags<E, KT, sizeof(WT) == 2> K;
-      K.template load<Dm::LDX>(X0);
+      KeyFrags<E, KT, sizeof(WT) == 2, KM> K;
+      load_keys<Dm::LDX>(K, X0, X0T);
       f4 gX0[KT][ET];
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
@@ -375,6 +379,7 @@ __global__ __launch_bounds__(256) void mixs_bwd_rows_kernel(MixsBwdArgs sa) {
         for (int ft = 0; ft < ET; ++ft) gx[ft] = qv_ ? ld4(GOUT + q * Bd::LDB + 16 * ft + 4 * g) : zero4();
 #pragma unroll
         for (int d = D - 1; d >= 0; --d) {
+        const Wts<WT> Pq = step_view(P);  // (opaque per query tile: weight reads stay in the loop)
           f4 x[ET];
 #pragma unroll
           for (int ft = 0; ft < ET; ++ft) x[ft] = qv_ ? ld4(X0 + (na + q) * Dm::LDX + 16 * ft + 4 * g) : zero4();
@@ -384,14 +389,14 @@ __global__ __launch_bounds__(256) void mixs_bwd_rows_kernel(MixsBwdArgs sa) {
               for (int ft = 0; ft < ET; ++ft)
                 x[ft] = qv_ ? ld4(args.xmid + ((bt * (D - 1) + d - 1) * nq + q) * E + 16 * ft + 4 * g) : zero4();
             } else {
-              for (int dd = 0; dd < d; ++dd) mixer_block_fwd<E, H, KT, FF, false>(P, L, dd, K, lk, x, nullptr);
+              for (int dd = 0; dd < d; ++dd) mixer_block_fwd<E, H, KT, FF, false>(Pq, L, dd, K, lk, x, nullptr);
             }
           }
           WT* tile = static_cast<WT*>(args.tape) + ((size_t)d * ctiles * 16 + ((size_t)t * fa.B + b) * nq + 16 * qt) * Rec::SIZE;
           MixerCacheLean<E, H, KT, FF> cache;
           const MaskedRec<WT, 2> rec(tile, min(16, q0 - 16 * qt), Rec::SIZE);
-          mixer_block_fwd_lean<E, H, KT, FF>(P, L, d, K, lk, x, cache, rec);
-          mixer_block_bwd_lean<E, H, KT, FF>(P, L, gs, rec, stage, d, K, lk, gX0, cache, gx, ln2[d]);
+          mixer_block_fwd_lean<E, H, KT, FF>(Pq, L, d, K, lk, x, cache, rec);
+          mixer_block_bwd_lean<E, H, KT, FF>(Pq, L, gs, rec, stage, d, K, lk, gX0, cache, gx, ln2[d]);
         }
         wave_sync();
 #pragma unroll
@@ -510,7 +515,8 @@ T2O_DEV void mixs_rec_load(const MixsBwdArgs& sa, const MixerNet& n, int b, int 
 template <int E, int H, int D, int A, int FF, int RT, bool WLDS, typename WT>
 __global__ __launch_bounds__(256) void mixs_bwd_rec_kernel(MixsBwdArgs sa) {
   using Dm = MixDims<E, A>;
-  using Bd = MixBwdDims<E, A>;
+  constexpr int KM = key_mode<Dm::KT, WT>();
+  using Bd = MixBwdDims<E, A, KM>;
   constexpr int ET = E / 16, KT = Dm::KT;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   T2O_LDS_POISON(smem);
@@ -522,7 +528,8 @@ __global__ __launch_bounds__(256) void mixs_bwd_rec_kernel(MixsBwdArgs sa) {
   const int na = RT == 1 ? fa.na : A, nq = na + 3, lk = 2 * na + 3, q0 = mixs_q0(nq);
   const int w = wave_id();
   float* X0 = smem + args.lds_w + w * Bd::PERW;
-  float* GW = X0 + Dm::X0F;  // the window rows' grads [16][LDB] (ghw staging first)
+  float* X0T = X0 + Dm::X0F;   // (KM 1: the transposed key block)
+  float* GW = X0T + Bd::X0TF;  // the window rows' grads [16][LDB] (ghw staging first)
   float* stage = GW + Bd::GOUT;
   float* gs = args.slabs + (size_t)(sa.slab0 + blockIdx.x) * G.grad_total;
   Wts<WT> P0 = WLDS ? stage_weights(smem, n.pack, L, L.fwd_total, WT{}) : global_weights(n.pack, L, WT{});
@@ -589,8 +596,8 @@ __global__ __launch_bounds__(256) void mixs_bwd_rec_kernel(MixsBwdArgs sa) {
       __builtin_amdgcn_sched_barrier(0);
       if (t > t_lo) mixs_rec_load<E, A>(sa, n, b, t - 1, cur, na);
       wave_sync();
-      KeyFrags<E, KT, sizeof(WT) == 2> K;
-      K.template load<Dm::LDX>(X0);
+      KeyFrags<E, KT, sizeof(WT) == 2, KM> K;
+      load_keys<Dm::LDX>(K, X0, X0T);
       f4 gX0[KT][ET];
 #pragma unroll
       for (int kt = 0; kt < KT; ++kt)
@@ -1056,7 +1063,11 @@ int mixs_launch_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream, int 
     while (a.waves > 1 && (args.B + a.waves - 1) / a.waves * nnet < 256) a.waves >>= 1;
     if (a.wlds) lds = sizeof(float) * (wfl + a.waves * perw);
     else lds = sizeof(float) * a.waves * perw;
-    auto kern = a.wlds ? mixs_fwd_rec_kernel<E, H, D, A, FF, RT, true, WT> : mixs_fwd_rec_kernel<E, H, D, A, FF, RT, false, WT>;
+    const bool wide = a.waves <= 4 && 2 * lds > 160 * 1024;  // one workgroup per CU: one wave per SIMD
+    auto kern = wide ? (a.wlds ? mixs_fwd_rec_kernel<E, H, D, A, FF, RT, true, WT, 256>
+                               : mixs_fwd_rec_kernel<E, H, D, A, FF, RT, false, WT, 256>)
+                     : (a.wlds ? mixs_fwd_rec_kernel<E, H, D, A, FF, RT, true, WT>
+                               : mixs_fwd_rec_kernel<E, H, D, A, FF, RT, false, WT>);
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kern, dim3((args.B + a.waves - 1) / a.waves, nnet), dim3(64 * a.waves), lds, stream, a);
     const int rc = (int)hipGetLastError();
@@ -1091,7 +1102,7 @@ int mixs_launch_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream, int 
 
 template <int E, int H, int D, int A, int FF, int RT, typename WT>
 int mixs_launch_bwd(MixsBwdArgs& sa, int max_slabs, int* nslab, hipStream_t stream, int phase) {
-  using Bd = MixBwdDims<E, A>;
+  using Bd = MixBwdDims<E, A, key_mode<MixDims<E, A>::KT, WT>()>;  // (the rows / one-wave kernels' buffers)
   MixerBwdArgs& args = sa.m;
   if (!kernel_layout_matches<E, H, D, FF, WT>(args.f.L)) return T2O_EINVAL;
   const t2o_layout& L = args.f.L;
