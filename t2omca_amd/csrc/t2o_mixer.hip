@@ -134,18 +134,12 @@ int launch_mixer_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
   using Dm = MixDims<E, A>;
   MixerFwdArgs a = args;
   const size_t wfl = (lds_weight_floats<WT>(args.L, args.L.fwd_total) + 15) / 16 * 16, perw = Dm::FWD_PERW;
-  size_t lds = 0;
-  // 8 (2 per SIMD) / 4 / 2 waves with LDS weights, else 4 waves reading weights from L2
-  for (a.waves = 8, a.wlds = 1; a.waves >= 2; a.waves >>= 1) {
-    lds = sizeof(float) * (wfl + a.waves * perw);
-    if (lds <= 160 * 1024) break;
-  }
-  if (a.waves < 2) {
-    a.waves = 4;
-    a.wlds = 0;
-    lds = sizeof(float) * 4 * perw;
-    if (lds > 160 * 1024) return T2O_EUNSUPPORTED;
-  }
+  // up to 8 waves (two per SIMD at the 512-thread bound's 256 registers)
+  const MixLaunch m = mix_pick(wfl, perw, 8, 2);
+  if (m.waves < 1) return T2O_EUNSUPPORTED;
+  a.waves = m.waves;
+  a.wlds = m.wlds;
+  const size_t lds = m.lds;
   const bool wide = Dm::QT > 1 && a.waves <= 4 && 2 * lds > 160 * 1024;  // one wave per SIMD
   auto kern = wide ? (a.wlds ? mixer_fwd_kernel<E, H, D, A, FF, RT, true, WT, Dm::QT == 1 ? 512 : 256>
                              : mixer_fwd_kernel<E, H, D, A, FF, RT, false, WT, Dm::QT == 1 ? 512 : 256>)
@@ -866,21 +860,13 @@ int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t 
       }
     }
   }
-  size_t lds = 0;
-  bool wlds = true;
-  for (args.waves = 4; args.waves >= 1; args.waves >>= 1) {
-    lds = sizeof(float) * ((size_t)args.lds_w + args.waves * PERW);
-    if (lds <= 160 * 1024) break;
-  }
-  if (args.waves < 1) {  // weights from L2, 4 or fewer waves of per-episode buffers
-    wlds = false;
-    args.lds_w = 0;
-    for (args.waves = 4; args.waves >= 1; args.waves >>= 1) {
-      lds = sizeof(float) * (size_t)args.waves * PERW;
-      if (lds <= 160 * 1024) break;
-    }
-    if (args.waves < 1) return T2O_EUNSUPPORTED;
-  }
+  // up to 4 waves (launch bound 256; the kernel takes the whole register file)
+  const MixLaunch m = mix_pick((size_t)args.lds_w, PERW, 4, 1);
+  if (m.waves < 1) return T2O_EUNSUPPORTED;
+  args.waves = m.waves;
+  const bool wlds = m.wlds;
+  if (!wlds) args.lds_w = 0;
+  const size_t lds = m.lds;
   const int grid = (args.f.B + args.waves - 1) / args.waves;
   if (grid > max_slabs) return T2O_EINVAL;
   auto kern = wlds ? mixer_bwd_kernel<E, H, D, A, FF, RT, true, WT> : mixer_bwd_kernel<E, H, D, A, FF, RT, false, WT>;

@@ -4,6 +4,9 @@
 // blocks, compile-time dims, the per-step input loads, the key block, and the
 // mixing head forward / backward.  Reference: n_transf_mixer.py:55-103.
 #pragma once
+#include <algorithm>
+#include <cstdlib>
+
 #include "t2o_layout.hpp"
 #include "t2o_mixer_block.hpp"
 
@@ -426,4 +429,36 @@ int mixer_split_bwd(const MixerBwdArgs& m, float* work, int64_t work_floats, int
 int64_t mixer_split_work_floats(const t2o_layout& L, int B, int T);
 bool mixer_split_taken(const t2o_layout& L, int B);
 int mixer_split_extra_slabs(int B);
+// Launch shape of a one-wave-per-episode mixer kernel: weights staged in LDS (wfl
+// floats) beside `waves` per-wave buffers (perw floats), or read through L2 beside
+// them alone — whichever keeps more waves resident per CU (LDS-limited workgroups x
+// waves, capped by the register budget: per_simd waves a SIMD holds), LDS weights on
+// a tie.  fp32 at 16 AGVs: its 121 KB of weights leave LDS room for two waves per CU,
+// half the SIMDs idle.  T2O_MIXER_WEIGHTS=lds / l2 forces the choice (A/B).
+struct MixLaunch {
+  int waves;
+  bool wlds;
+  size_t lds;  // bytes
+};
+inline MixLaunch mix_pick(size_t wfl, size_t perw, int wmax, int per_simd) {
+  constexpr size_t CAP = 160 * 1024;
+  auto fit = [&](bool wl, MixLaunch& m) {
+    for (m.waves = wmax; m.waves >= 1; m.waves >>= 1) {
+      m.lds = sizeof(float) * ((wl ? wfl : 0) + (size_t)m.waves * perw);
+      if (m.lds <= CAP) break;
+    }
+    m.wlds = wl;
+    return m.waves >= 1;
+  };
+  auto per_cu = [&](const MixLaunch& m) { return std::min((int)(CAP / m.lds) * m.waves, 4 * per_simd); };
+  MixLaunch l{}, g{};
+  const bool okl = fit(true, l), okg = fit(false, g);
+  const char* e = getenv("T2O_MIXER_WEIGHTS");
+  if (e && e[0] == 'l' && e[1] == 'd' && okl) return l;
+  if (e && e[0] == 'l' && e[1] == '2' && okg) return g;
+  if (okl && (!okg || per_cu(l) >= per_cu(g))) return l;
+  if (okg) return g;
+  return MixLaunch{0, false, 0};
+}
+
 }  // namespace t2o

@@ -1108,17 +1108,11 @@ int mixs_launch_bwd(MixsBwdArgs& sa, int max_slabs, int* nslab, hipStream_t stre
   const t2o_layout& L = args.f.L;
   const int lds_w = (int)((lds_weight_floats<WT>(L, L.fwd_total) + 15) / 16 * 16);
   auto pick = [&](int maxw, int& waves, bool& wlds, size_t& lds) {
-    wlds = true;
-    for (waves = maxw; waves >= 1; waves >>= 1) {
-      lds = sizeof(float) * ((size_t)lds_w + waves * Bd::PERW);
-      if (lds <= 160 * 1024) return true;
-    }
-    wlds = false;
-    for (waves = maxw; waves >= 1; waves >>= 1) {
-      lds = sizeof(float) * (size_t)waves * Bd::PERW;
-      if (lds <= 160 * 1024) return true;
-    }
-    return false;
+    const MixLaunch m = mix_pick((size_t)lds_w, Bd::PERW, maxw, 1);
+    waves = m.waves;
+    wlds = m.wlds;
+    lds = m.lds;
+    return m.waves >= 1;
   };
   const int B = args.f.B, T = args.f.net[0].T;
   // parallel part first: ghid partial, the window grads, the hyper keys' share
