@@ -98,6 +98,9 @@ def parse():
                          "~0.3%%; 0: never)")
     ap.add_argument("--no-fp32-companion", dest="fp32_companion", action="store_false",
                     help="skip the fp32-precision companion timing of the same workload (bf16 runs)")
+    ap.add_argument("--no-config-companions", dest="config_companions", action="store_false",
+                    help="skip the fp32 16-AGV TD update (1024 episodes x T=150) timed beside the "
+                         "headline (N=1, configs[2] runs only)")
     ap.add_argument("--print-workload-tag", action="store_true",
                     help="print the tag that keys profiles/hbm_traffic.json for these args and exit")
     a = ap.parse_args()
@@ -768,9 +771,9 @@ def main():
         return dropin_bench(args, world, rank, dev)
     if args.mode == "loop":
         return loop_bench(args, world, rank, dev)
-    def make_learner(precision):
+    def make_learner(precision, agents=A):
         torch.manual_seed(0)
-        margs = make_args(A, device=str(dev), qmix_pos_func=args.qmix_pos_func)
+        margs = make_args(agents, device=str(dev), qmix_pos_func=args.qmix_pos_func)
         agent = TransformerAgent(None, margs).to(dev)
         mixer = TransformerMixer(margs).to(dev)
         pipe = {"0": False, "1": True}.get(os.environ.get("T2O_PIPELINE", "auto"), "auto")
@@ -944,6 +947,24 @@ def main():
         out["fp32_companion"] = {"value": transitions / el32, "unit": "agent-transitions/s",
                                  "ms_per_step": el32 / args.steps * 1e3, "dtype": "fp32"}
         del lr32
+    if world == 1 and args.config_companions and (A, B, T) == (8, 1024, 60):
+        # an fp32 16-AGV TD update (the reference's precision at the
+        # 16-AGV scenario, 1024 episodes x T=150) in the same line; timed as above
+        A2, B2, T2, s2 = 16, 1024, 150, 3
+        lr16 = make_learner("fp32", agents=A2)
+        b16, w16 = make_batch(B2, T2, A2, seed=1 + rank, device=dev)
+        for i in range(1 + s2):
+            if i == 1:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+            lr16.train(b16, 0, i, per_weight=w16)
+        torch.cuda.synchronize()
+        el16 = time.perf_counter() - t0
+        out["configs"] = {"a16_fp32": {
+            "workload": f"TD update fwd+bwd+Adam, {A2} AGVs, batch {B2} episodes x T={T2}, fp32 MFMA operands",
+            "value": B2 * T2 * A2 * s2 / el16, "unit": "agent-transitions/s", "ms_per_step": el16 / s2 * 1e3,
+            "steps": s2, "warmup": 1, "kernels": {"agent": lr16.sa.instance, "mixer": lr16.sm.instance}}}
+        del lr16, b16, w16
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
     if rank == 0:

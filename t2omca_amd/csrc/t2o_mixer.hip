@@ -134,8 +134,9 @@ int launch_mixer_fwd(const MixerFwdArgs& args, int nnet, hipStream_t stream) {
   using Dm = MixDims<E, A>;
   MixerFwdArgs a = args;
   const size_t wfl = (lds_weight_floats<WT>(args.L, args.L.fwd_total) + 15) / 16 * 16, perw = Dm::FWD_PERW;
-  // up to 8 waves (two per SIMD at the 512-thread bound's 256 registers)
-  const MixLaunch m = mix_pick(wfl, perw, 8, 2);
+  // 8 (two per SIMD at the 512-thread bound's 256 registers) / 4 / 2 waves with LDS
+  // weights, else 4 waves reading weights from L2
+  const MixLaunch m = mix_pick(wfl, perw, 8, 2, 4, 4);
   if (m.waves < 1) return T2O_EUNSUPPORTED;
   a.waves = m.waves;
   a.wlds = m.wlds;
@@ -861,7 +862,7 @@ int launch_mixer_bwd(MixerBwdArgs& args, int max_slabs, int* nslab, hipStream_t 
     }
   }
   // up to 4 waves (launch bound 256; the kernel takes the whole register file)
-  const MixLaunch m = mix_pick((size_t)args.lds_w, PERW, 4, 1);
+  const MixLaunch m = mix_pick((size_t)args.lds_w, PERW, 4, 1, 4, 1);
   if (m.waves < 1) return T2O_EUNSUPPORTED;
   args.waves = m.waves;
   const bool wlds = m.wlds;

@@ -224,16 +224,12 @@ T2O_DEV void keys_combine(const KeyFrags<E, KT, BF, KM>& K, const f4* w, f4* out
   }
 }
 
-// scores of keys >= Lk (padding) to -inf. bf16: per element and branch-free: a
-// wave-uniform "does this tile reach Lk" test in front of each tile measured
-// slower where Lk is a run-time value (32 AGVs, five key tiles: mixer_bwd 7.49 vs
-// 6.56 ms, profiles/r5_km/) and equal at the exact 8-AGV instance. fp32 keeps the
-// per-tile test: its branch-free build returned wrong gradients from the
-// capacity-64 instances (40 / 63 AGVs, profiles/r5_final4/pytest.log) although the
-// two forms mask the same elements; not root-caused
-#ifndef T2O_KM_FP32_FLAT  // diagnostic: bit 0 flat fp32 mask in mixer_block_fwd, bit 1 in attn_probs
-#define T2O_KM_FP32_FLAT 0
-#endif
+// scores of keys >= Lk (padding) to -inf.  bf16: per element and branch-free (a
+// wave-uniform "does this tile reach Lk" test per tile measured slower where Lk is a
+// run-time value: 32 AGVs mixer_bwd 7.49 vs 6.56 ms, profiles/r5_km/).  fp32 keeps the
+// per-tile test: built branch-free, the capacity-64 split BPTT returned wrong
+// gradients although both forms mask the same elements; the cause is not named
+// (not an MFMA hand-off, not LDS ordering, not the frame size)
 template <int KT, bool TILE_TEST>
 T2O_DEV void key_mask(f4* s, int Lk, int g) {
 #pragma unroll
@@ -260,7 +256,7 @@ T2O_DEV void mixer_block_fwd(const Wts<WT>& P, const t2o_layout& L, int d,
   for (int hh = 0; hh < H; ++hh) {
     f4 s[KT];
     keys_dot(K, &u[hh * ET], s);
-    key_mask<KT, !BF && !(T2O_KM_FP32_FLAT & 1)>(s, Lk, g);
+    key_mask<KT, !BF>(s, Lk, g);
     float m = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt)
@@ -352,7 +348,7 @@ template <int E, int KT, bool BF, int KM>
 T2O_DEV void attn_probs(const KeyFrags<E, KT, BF, KM>& K, const f4* u, int Lk, f4* s) {
   const int g = lane_g();
   keys_dot(K, u, s);
-  key_mask<KT, !BF && !(T2O_KM_FP32_FLAT & 2)>(s, Lk, g);
+  key_mask<KT, !BF>(s, Lk, g);
   float m = -INFINITY;
 #pragma unroll
   for (int kt = 0; kt < KT; ++kt)

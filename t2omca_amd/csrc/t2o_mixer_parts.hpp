@@ -430,34 +430,27 @@ int64_t mixer_split_work_floats(const t2o_layout& L, int B, int T);
 bool mixer_split_taken(const t2o_layout& L, int B);
 int mixer_split_extra_slabs(int B);
 // Launch shape of a one-wave-per-episode mixer kernel: weights staged in LDS (wfl
-// floats) beside `waves` per-wave buffers (perw floats), or read through L2 beside
-// them alone — whichever keeps more waves resident per CU (LDS-limited workgroups x
-// waves, capped by the register budget: per_simd waves a SIMD holds), LDS weights on
-// a tie.  fp32 at 16 AGVs: its 121 KB of weights leave LDS room for two waves per CU,
-// half the SIMDs idle.  T2O_MIXER_WEIGHTS=lds / l2 forces the choice (A/B).
+// floats) beside wmax_lds .. min_lds per-wave buffers (perw floats, halving), else
+// read through L2 beside wmax_l2 .. min_l2 buffers alone; waves = 0 when neither
+// fits.  LDS weights first: the placement every parity test ran.  (fp32 at 16 AGVs:
+// 121 KB of weights leave room for two waves per CU, half the SIMDs idle — DESIGN §9
+// item 4 for the L2 alternative, not measured.)
 struct MixLaunch {
   int waves;
   bool wlds;
   size_t lds;  // bytes
 };
-inline MixLaunch mix_pick(size_t wfl, size_t perw, int wmax, int per_simd) {
+inline MixLaunch mix_pick(size_t wfl, size_t perw, int wmax_lds, int min_lds, int wmax_l2, int min_l2) {
   constexpr size_t CAP = 160 * 1024;
-  auto fit = [&](bool wl, MixLaunch& m) {
-    for (m.waves = wmax; m.waves >= 1; m.waves >>= 1) {
-      m.lds = sizeof(float) * ((wl ? wfl : 0) + (size_t)m.waves * perw);
-      if (m.lds <= CAP) break;
-    }
-    m.wlds = wl;
-    return m.waves >= 1;
-  };
-  auto per_cu = [&](const MixLaunch& m) { return std::min((int)(CAP / m.lds) * m.waves, 4 * per_simd); };
-  MixLaunch l{}, g{};
-  const bool okl = fit(true, l), okg = fit(false, g);
-  const char* e = getenv("T2O_MIXER_WEIGHTS");
-  if (e && e[0] == 'l' && e[1] == 'd' && okl) return l;
-  if (e && e[0] == 'l' && e[1] == '2' && okg) return g;
-  if (okl && (!okg || per_cu(l) >= per_cu(g))) return l;
-  if (okg) return g;
+  MixLaunch m{};
+  for (m.waves = wmax_lds, m.wlds = true; m.waves >= min_lds; m.waves >>= 1) {
+    m.lds = sizeof(float) * (wfl + (size_t)m.waves * perw);
+    if (m.lds <= CAP) return m;
+  }
+  for (m.waves = wmax_l2, m.wlds = false; m.waves >= min_l2; m.waves >>= 1) {
+    m.lds = sizeof(float) * (size_t)m.waves * perw;
+    if (m.lds <= CAP) return m;
+  }
   return MixLaunch{0, false, 0};
 }
 

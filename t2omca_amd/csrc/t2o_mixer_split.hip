@@ -1108,7 +1108,7 @@ int mixs_launch_bwd(MixsBwdArgs& sa, int max_slabs, int* nslab, hipStream_t stre
   const t2o_layout& L = args.f.L;
   const int lds_w = (int)((lds_weight_floats<WT>(L, L.fwd_total) + 15) / 16 * 16);
   auto pick = [&](int maxw, int& waves, bool& wlds, size_t& lds) {
-    const MixLaunch m = mix_pick((size_t)lds_w, Bd::PERW, maxw, 1);
+    const MixLaunch m = mix_pick((size_t)lds_w, Bd::PERW, maxw, 1, maxw, 1);
     waves = m.waves;
     wlds = m.wlds;
     lds = m.lds;
